@@ -1,0 +1,306 @@
+"""ctypes wrapper around oracle/liboracle.so — the CPU restatement of the hot path.
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg,
+always as the checker (or the reported CPU baseline), never as the product path.
+See qasr_oracle.c for what each function restates (reference file:line citations live there).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+QK = 32
+QBYTES = 34
+
+
+def build() -> str:
+    path = os.path.join(_HERE, "liboracle.so")
+    src = os.path.join(_HERE, "qasr_oracle.c")
+    if not os.path.exists(path) or os.path.getmtime(path) < os.path.getmtime(src):
+        subprocess.run(["make", "-C", _HERE, "-s"], check=True)
+    return path
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        L = C.CDLL(build())
+        P = C.c_void_p
+        i64 = C.c_int64
+        L.orc_set_mode.argtypes = [C.c_int, C.c_int]
+        L.orc_num_threads.restype = C.c_int
+        L.orc_set_num_threads.argtypes = [C.c_int]
+        L.orc_quantize_row_q8.argtypes = [P, i64, P]
+        L.orc_dequantize_row_q8.argtypes = [P, i64, P]
+        L.orc_q8_block_dots.argtypes = [P, P, i64, P]
+        L.orc_linear_q8.argtypes = [P, i64, i64, P, i64, P, P]
+        L.orc_name_id.argtypes = [C.c_char_p]
+        L.orc_name_id.restype = C.c_uint64
+        L.orc_synth_q8.argtypes = [C.c_uint64, C.c_char_p, i64, i64, C.c_float, P]
+        L.orc_synth_f32.argtypes = [C.c_uint64, C.c_char_p, i64, C.c_float, C.c_float, P]
+        L.orc_synth_f16.argtypes = [C.c_uint64, C.c_char_p, i64, C.c_float, P]
+        L.orc_kaldi_mel_banks.argtypes = [P]
+        L.orc_fbank.argtypes = [P, i64, P]
+        L.orc_fbank.restype = i64
+        L.orc_dfsmn.argtypes = [P, i64, P, P]
+        L.orc_vad_segments.argtypes = [P, i64, i64, C.c_float, C.c_int, C.c_int, C.c_int, C.c_int, P, i64]
+        L.orc_vad_segments.restype = i64
+        L.orc_mel_filters.argtypes = [C.c_int, P]
+        L.orc_mel_dims.argtypes = [i64, P, P]
+        L.orc_mel.argtypes = [P, i64, C.c_int, P]
+        L.orc_mel.restype = i64
+        L.orc_model_new.argtypes = [P, P]
+        L.orc_model_new.restype = P
+        L.orc_model_free.argtypes = [P]
+        L.orc_model_set.argtypes = [P, C.c_char_p, P]
+        L.orc_model_set.restype = C.c_int
+        L.orc_model_synth.argtypes = [P, C.c_uint64]
+        L.orc_audio_tokens.argtypes = [C.c_int]
+        L.orc_audio_tokens.restype = C.c_int
+        L.orc_encode.argtypes = [P, P, C.c_int, C.c_int, P, P]
+        L.orc_encode.restype = C.c_int
+        L.orc_kv_new.argtypes = [P, C.c_int]
+        L.orc_kv_new.restype = P
+        L.orc_kv_free.argtypes = [P]
+        L.orc_kv_reset.argtypes = [P]
+        L.orc_embed.argtypes = [P, P, C.c_int, P]
+        L.orc_forward.argtypes = [P, P, C.c_int, P, C.c_int]
+        L.orc_forward.restype = C.c_int
+        L.orc_generate.argtypes = [P, P, C.c_int, C.c_int, P, C.c_int, P, C.c_int, C.c_int, C.c_int, P, P]
+        L.orc_generate.restype = C.c_int
+        L.orc_f32_to_f16_array.argtypes = [P, P, i64]
+        L.orc_f16_to_f32_array.argtypes = [P, P, i64]
+        _LIB = L
+    return _LIB
+
+
+def _p(a: np.ndarray):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+def set_mode(engine: bool = True):
+    lib().orc_set_mode(1 if engine else 0, 1 if engine else 0)
+
+
+def set_threads(n: int):
+    lib().orc_set_num_threads(int(n))
+
+
+def num_threads() -> int:
+    return lib().orc_num_threads()
+
+
+# ------------------------------------------------------------------------------------------ Q8_0
+def quantize_q8(x: np.ndarray) -> np.ndarray:
+    """Q8_0 blocks of a [N][K] f32 matrix → uint8 [N][K/32*34] (ggml layout)."""
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    n, k = x.shape
+    out = np.empty((n, k // QK * QBYTES), dtype=np.uint8)
+    for r in range(n):
+        lib().orc_quantize_row_q8(_p(x[r]), k, _p(out[r]))
+    return out
+
+
+def dequantize_q8(blocks: np.ndarray, k: int) -> np.ndarray:
+    blocks = np.ascontiguousarray(blocks, dtype=np.uint8).reshape(-1, k // QK * QBYTES)
+    out = np.empty((blocks.shape[0], k), dtype=np.float32)
+    for r in range(blocks.shape[0]):
+        lib().orc_dequantize_row_q8(_p(blocks[r]), k, _p(out[r]))
+    return out
+
+
+def linear_q8(x: np.ndarray, w_blocks: np.ndarray, n: int, bias: np.ndarray | None = None) -> np.ndarray:
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    m, k = x.shape
+    y = np.empty((m, n), dtype=np.float32)
+    b = None if bias is None else np.ascontiguousarray(bias, dtype=np.float32)
+    lib().orc_linear_q8(_p(x), m, k, _p(np.ascontiguousarray(w_blocks)), n, None if b is None else _p(b), _p(y))
+    return y
+
+
+def synth_q8(seed: int, name: str, n: int, k: int, sigma: float) -> np.ndarray:
+    out = np.empty((n, k // QK * QBYTES), dtype=np.uint8)
+    lib().orc_synth_q8(seed, name.encode(), n, k, sigma, _p(out))
+    return out
+
+
+def f16_bits(x: np.ndarray) -> np.ndarray:
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    y = np.empty(x.shape, dtype=np.uint16)
+    lib().orc_f32_to_f16_array(_p(x), _p(y), x.size)
+    return y
+
+
+# ------------------------------------------------------------------------------------------ VAD
+def fbank(pcm_int16_scale: np.ndarray) -> np.ndarray:
+    x = np.ascontiguousarray(pcm_int16_scale, dtype=np.float32)
+    n = x.size
+    t = 1 + (n - 400) // 160 if n >= 400 else 0
+    out = np.empty((max(t, 0), 80), dtype=np.float32)
+    got = lib().orc_fbank(_p(x), n, _p(out))
+    assert got == t
+    return out
+
+
+def kaldi_mel_banks() -> np.ndarray:
+    out = np.empty((80, 256), dtype=np.float32)
+    lib().orc_kaldi_mel_banks(_p(out))
+    return out
+
+
+class VadWeights(C.Structure):
+    _fields_ = (
+        [("mean", C.c_void_p), ("istd", C.c_void_p), ("w1", C.c_void_p), ("b1", C.c_void_p), ("w2", C.c_void_p),
+         ("b2", C.c_void_p)]
+        + [("lb", C.c_void_p * 8), ("la", C.c_void_p * 8), ("wa", C.c_void_p * 7), ("ba", C.c_void_p * 7),
+           ("wb", C.c_void_p * 7)]
+        + [("wd", C.c_void_p), ("bd", C.c_void_p), ("wo", C.c_void_p), ("bo", C.c_float)]
+    )
+
+
+def vad_probabilities(feats: np.ndarray, w: dict) -> np.ndarray:
+    """DFSMN over raw log-fbank feats [T][80]; w = dict from assets/fireredvad (see qasr.vad_weights)."""
+    feats = np.ascontiguousarray(feats, dtype=np.float32)
+    t = feats.shape[0]
+    keep = {k: np.ascontiguousarray(v, dtype=np.float32) for k, v in w.items()}
+    s = VadWeights()
+    s.mean, s.istd = _p(keep["mean"]).value, _p(keep["istd"]).value
+    s.w1, s.b1, s.w2, s.b2 = (_p(keep[k]).value for k in ("w1", "b1", "w2", "b2"))
+    for i in range(8):
+        s.lb[i] = _p(keep[f"lb{i}"]).value
+        s.la[i] = _p(keep[f"la{i}"]).value
+    for i in range(7):
+        s.wa[i] = _p(keep[f"wa{i}"]).value
+        s.ba[i] = _p(keep[f"ba{i}"]).value
+        s.wb[i] = _p(keep[f"wb{i}"]).value
+    s.wd, s.bd, s.wo = _p(keep["wd"]).value, _p(keep["bd"]).value, _p(keep["wo"]).value
+    s.bo = float(keep["bo"].reshape(-1)[0])
+    out = np.empty(t, dtype=np.float32)
+    if t:
+        lib().orc_dfsmn(_p(feats), t, C.byref(s), _p(out))
+    return out
+
+
+def vad_segments(probs: np.ndarray, audio_len: int, threshold=0.5, smooth_window=5, min_speech_ms=150,
+                 min_silence_ms=300, pad_ms=120) -> list[dict]:
+    p = np.ascontiguousarray(probs, dtype=np.float32).reshape(-1)
+    cap = max(1, p.size)
+    out = np.empty(2 * cap, dtype=np.int64)
+    n = lib().orc_vad_segments(_p(p), p.size, int(audio_len), float(threshold), int(smooth_window),
+                               int(min_speech_ms), int(min_silence_ms), int(pad_ms), _p(out), cap)
+    return [{"start": int(out[2 * i]), "end": int(out[2 * i + 1])} for i in range(n)]
+
+
+# ------------------------------------------------------------------------------------------ mel
+def mel_filters(n_mels=128) -> np.ndarray:
+    out = np.empty((201, n_mels), dtype=np.float32)
+    lib().orc_mel_filters(n_mels, _p(out))
+    return out
+
+
+def mel_dims(n: int):
+    tv = np.zeros(1, np.int64)
+    tp = np.zeros(1, np.int64)
+    lib().orc_mel_dims(n, _p(tv), _p(tp))
+    return int(tv[0]), int(tp[0])
+
+
+def mel(pcm: np.ndarray, n_mels=128):
+    x = np.ascontiguousarray(pcm, dtype=np.float32)
+    tv, tp = mel_dims(x.size)
+    out = np.empty((n_mels, tp), dtype=np.float32)
+    got = lib().orc_mel(_p(x), x.size, n_mels, _p(out))
+    assert got == tv
+    return out, tv
+
+
+# ------------------------------------------------------------------------------------------ model
+CFG_INT_KEYS = ["n_mels", "conv_ch", "enc_d", "enc_layers", "enc_heads", "enc_ffn", "n_window", "n_window_infer",
+                "proj_out", "txt_h", "txt_layers", "txt_heads", "txt_kv_heads", "head_dim", "txt_ffn", "vocab"]
+CFG_FLOAT_KEYS = ["rope_theta", "rms_eps", "ln_eps"]
+
+
+class Model:
+    """Oracle model: either bound to numpy tensors (GGUF-style names) or synthetic (seeded)."""
+
+    def __init__(self, cfg: dict, tensors: dict | None = None, seed: int | None = None):
+        self.cfg = dict(cfg)
+        ints = np.array([cfg[k] for k in CFG_INT_KEYS], dtype=np.int32)
+        floats = np.array([cfg[k] for k in CFG_FLOAT_KEYS], dtype=np.float32)
+        self.h = lib().orc_model_new(_p(ints), _p(floats))
+        self._keep = []
+        if tensors is not None:
+            for name, arr in tensors.items():
+                a = np.ascontiguousarray(arr)
+                self._keep.append(a)
+                rc = lib().orc_model_set(self.h, name.encode(), _p(a))
+                if rc != 0:
+                    raise KeyError(name)
+        if seed is not None:
+            lib().orc_model_synth(self.h, int(seed))
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().orc_model_free(self.h)
+            self.h = None
+
+    def audio_tokens(self, t_valid: int) -> int:
+        return lib().orc_audio_tokens(int(t_valid))
+
+    def encode(self, mel: np.ndarray, t_valid: int, want_enc=False):
+        mel = np.ascontiguousarray(mel, dtype=np.float32)
+        t_pad = mel.shape[1]
+        n_tok = self.audio_tokens(t_valid)
+        out = np.empty((n_tok, self.cfg["proj_out"]), dtype=np.float32)
+        enc = np.empty((n_tok, self.cfg["enc_d"]), dtype=np.float32) if want_enc else None
+        got = lib().orc_encode(self.h, _p(mel), t_pad, t_valid, _p(out), None if enc is None else _p(enc))
+        assert got == n_tok
+        return (out, enc) if want_enc else out
+
+
+class KV:
+    def __init__(self, model: Model, n_ctx: int):
+        self.model = model
+        self.h = lib().orc_kv_new(model.h, int(n_ctx))
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().orc_kv_free(self.h)
+            self.h = None
+
+    def reset(self):
+        lib().orc_kv_reset(self.h)
+
+    def embed(self, ids) -> np.ndarray:
+        ids = np.ascontiguousarray(ids, dtype=np.int32)
+        out = np.empty((ids.size, self.model.cfg["txt_h"]), dtype=np.float32)
+        lib().orc_embed(self.model.h, _p(ids), ids.size, _p(out))
+        return out
+
+    def forward(self, x: np.ndarray, all_logits=False) -> np.ndarray:
+        x = np.ascontiguousarray(x, dtype=np.float32)
+        n = x.shape[0]
+        v = self.model.cfg["vocab"]
+        lg = np.empty((n if all_logits else 1, v), dtype=np.float32)
+        rc = lib().orc_forward(self.h, _p(x), n, _p(lg), 1 if all_logits else 0)
+        assert rc == 0
+        return lg
+
+    def generate(self, prompt, audio_pad: int, audio: np.ndarray, eos=(151645, 151643), max_new=64, force_len=0,
+                 want_logits=False):
+        prompt = np.ascontiguousarray(prompt, dtype=np.int32)
+        audio = np.ascontiguousarray(audio, dtype=np.float32)
+        eos = np.ascontiguousarray(eos, dtype=np.int32)
+        limit = force_len if force_len > 0 else max_new
+        out = np.empty(max(limit, 1), dtype=np.int32)
+        lg = np.empty((max(limit, 1), self.model.cfg["vocab"]), dtype=np.float32) if want_logits else None
+        n = lib().orc_generate(self.h, _p(prompt), prompt.size, int(audio_pad), _p(audio), audio.shape[0], _p(eos),
+                               eos.size, int(max_new), int(force_len), _p(out), None if lg is None else _p(lg))
+        assert n >= 0
+        return (out[:n].copy(), lg[:n].copy()) if want_logits else out[:n].copy()
