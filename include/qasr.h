@@ -1,0 +1,190 @@
+/*
+ * qasr.h — C ABI of libqasr, the MI355X-native (gfx950) Qwen3-ASR + FireRedVAD engine.
+ *
+ * This is the drop-in boundary for the light-whisper local ASR hot path.  Each entry point replaces one
+ * interface the reference binds (paths relative to sypsyp97/light-whisper):
+ *
+ *   qasr_model_open        ← transcribe_cpp.Model(path, backend=)          src-tauri/resources/qwen3_asr_server.py:122
+ *   qasr_session_open      ← Model.session(kv_type="f16", n_ctx=32768)     qwen3_asr_server.py:123
+ *   qasr_session_run       ← Session.run(audio, timestamps="none")         qwen3_asr_server.py:144,321
+ *                            (result.text / result.language, :326-327)
+ *   qasr_session_close /
+ *   qasr_model_close       ← Session.close() / Model.close()               qwen3_asr_server.py:100-112
+ *   qasr_run_batch         ← (new) VAD-split batch of utterances, one call
+ *   qasr_vad_open          ← FireRedVad.__init__ (knf fbank + ORT session) firered_vad.py:41-85
+ *   qasr_vad_probabilities ← FireRedVad.probabilities                      firered_vad.py:106-111
+ *   qasr_vad_speech_timestamps ← FireRedVad.speech_timestamps              firered_vad.py:116-119
+ *   qasr_vad_timestamps_from_probabilities ← FireRedVad._timestamps_from_probabilities firered_vad.py:121-191
+ *   qasr_decode_pcm_s16le  ← decode_inline_audio (pcm_s16le branch)        server_common.py:145-170
+ *   qasr_resample_linear   ← Qwen3ASRServer._resample                      qwen3_asr_server.py:230-243
+ *
+ * Conventions: every function returns an int status (0 = OK); on failure qasr_last_error() returns a
+ * thread-local UTF-8 message.  No C++ exception crosses the ABI.  Host buffers are plain pointers + sizes.
+ * The qasr_op_* functions are the kernel-level entry points used by the parity tests: their pointer
+ * arguments are DEVICE pointers and `stream` is a hipStream_t (NULL = default stream).
+ * Only backend "hip" (alias "auto") exists: there is no CPU or Vulkan fallback; other names fail with
+ * QASR_E_BACKEND, mirroring how transcribe_cpp rejects an unavailable backend (qwen3_asr_server.py:117-133).
+ */
+#ifndef QASR_H
+#define QASR_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define QASR_API __attribute__((visibility("default")))
+
+enum {
+    QASR_OK = 0,
+    QASR_E_INVALID = 1,
+    QASR_E_IO = 2,
+    QASR_E_FORMAT = 3,
+    QASR_E_BACKEND = 4,
+    QASR_E_HIP = 5,
+    QASR_E_CAPACITY = 6,
+    QASR_E_INTERNAL = 7,
+};
+
+typedef struct qasr_model qasr_model;
+typedef struct qasr_session qasr_session;
+typedef struct qasr_vad qasr_vad;
+
+/* Model hyper-parameters (GGUF metadata "qwen3-asr.*"; see DESIGN.md §tensor names). */
+typedef struct {
+    int32_t n_mels, conv_ch, enc_d, enc_layers, enc_heads, enc_ffn, n_window, n_window_infer, proj_out;
+    int32_t txt_h, txt_layers, txt_heads, txt_kv_heads, head_dim, txt_ffn, vocab;
+    float rope_theta, rms_eps, ln_eps;
+    /* special tokens of the chat prompt (defaults: Qwen2 tokenizer ids) */
+    int32_t tok_im_start, tok_im_end, tok_system, tok_user, tok_assistant, tok_newline;
+    int32_t tok_audio_start, tok_audio_end, tok_audio_pad, tok_eos0, tok_eos1, tok_asr_text;
+} qasr_hparams;
+
+typedef struct {
+    char* text;         /* UTF-8, after "<asr_text>" (reference applies .strip() itself) */
+    char* language;     /* the "language X" prefix, "" when absent */
+    char* raw;          /* full detokenised output */
+    int32_t* tokens;    /* generated ids (EOS excluded) */
+    int32_t n_tokens;
+    int32_t n_audio_tokens;
+    int32_t n_prompt;
+    double ms_mel, ms_encoder, ms_prefill, ms_decode;
+} qasr_result;
+
+typedef struct {
+    int32_t max_new_tokens;      /* 0 → default cap (DESIGN.md §decode length) */
+    int32_t force_tokens_per_s;  /* >0: throughput mode, exactly round(k·seconds)+1 tokens, EOS ignored */
+    int32_t return_logits;       /* reserved */
+} qasr_run_opts;
+
+/* -------------------------------------------------------------------------------------------- errors */
+QASR_API const char* qasr_last_error(void);
+QASR_API const char* qasr_version(void);
+QASR_API int qasr_device_info(char* name, size_t name_cap, double* mem_total_gb, int* n_devices);
+QASR_API int qasr_set_device(int device);
+
+/* -------------------------------------------------------------------------------------------- model */
+QASR_API int qasr_model_open(const char* gguf_path, const char* backend, qasr_model** out);
+/* Synthetic weights with the exact tensor shapes of `arch` ("qwen3-asr-0.6b" | "qwen3-asr-1.7b"), or of a
+   custom qasr_hparams when arch == NULL; generated on the device from `seed` by the generator shared with
+   the oracle.  Used when the GGUF weights are not provisioned. */
+QASR_API int qasr_model_open_synthetic(const char* arch, const qasr_hparams* hp, uint64_t seed, qasr_model** out);
+QASR_API int qasr_model_hparams(const qasr_model* m, qasr_hparams* out);
+QASR_API int64_t qasr_model_weight_bytes(const qasr_model* m);
+/* copy one tensor back to host in its GGUF storage form (Q8_0 blocks / f32 / f16) — for parity tests */
+QASR_API int qasr_model_export_tensor(const qasr_model* m, const char* name, void* dst, size_t cap, size_t* written);
+QASR_API void qasr_model_close(qasr_model* m);
+
+/* -------------------------------------------------------------------------------------------- session */
+QASR_API int qasr_session_open(qasr_model* m, const char* kv_type, int32_t n_ctx, qasr_session** out);
+QASR_API int qasr_session_run(qasr_session* s, const float* pcm16k, size_t n, int32_t timestamps, qasr_result* out);
+QASR_API int qasr_session_run_opts(qasr_session* s, const float* pcm16k, size_t n, const qasr_run_opts* opts,
+                                   qasr_result* out);
+/* Batched: `count` utterances (16 kHz f32 host buffers) encoded/prefilled/decoded together on this device. */
+QASR_API int qasr_run_batch(qasr_session* s, const float* const* pcm, const size_t* n, int32_t count,
+                            const qasr_run_opts* opts, qasr_result* out);
+/* Same, audio already resident on the device: one packed f32 buffer, per-utterance offsets/lengths (host
+   arrays).  This is the bench's timed entry point (inputs resident in HBM). */
+QASR_API int qasr_run_batch_device(qasr_session* s, const float* dev_pcm, const int64_t* offsets,
+                                   const int64_t* lengths, int32_t count, const qasr_run_opts* opts,
+                                   qasr_result* out);
+QASR_API void qasr_result_free(qasr_result* r);
+QASR_API void qasr_session_close(qasr_session* s);
+/* teacher-forced logits for parity tests: prompt (with audio placeholders) + forced continuation */
+QASR_API int qasr_session_forced_logits(qasr_session* s, const float* pcm16k, size_t n, const int32_t* forced,
+                                        int32_t n_forced, float* logits_out /* [n_forced+1][vocab] */);
+/* the stages of one utterance, for layer-level parity tests (host outputs) */
+QASR_API int qasr_session_mel(qasr_session* s, const float* pcm16k, size_t n, float* mel_out /*[n_mels][t_pad]*/,
+                              int32_t* t_valid, int32_t* t_pad);
+QASR_API int qasr_session_encode(qasr_session* s, const float* mel, int32_t t_pad, int32_t t_valid,
+                                 float* audio_emb /*[n_tok][proj_out]*/, float* enc_out /*[n_tok][enc_d] or NULL*/,
+                                 int32_t* n_tok);
+QASR_API int qasr_session_prefill_logits(qasr_session* s, const float* embeds, int32_t n, float* logits /*[n][V]*/);
+
+/* -------------------------------------------------------------------------------------------- VAD */
+typedef struct {
+    float threshold;               /* 0.5 */
+    int32_t smooth_window_frames;  /* 5 */
+    int32_t min_speech_duration_ms;  /* 150 */
+    int32_t min_silence_duration_ms; /* 300 */
+    int32_t speech_pad_ms;         /* 120 */
+} qasr_vad_options;
+
+typedef struct {
+    int64_t start, end;  /* samples */
+} qasr_segment;
+
+QASR_API void qasr_vad_default_options(qasr_vad_options* o);
+QASR_API int qasr_vad_open(const char* weights_path /* .qvad; NULL = bundled asset */, qasr_vad** out);
+/* pcm: f32 in [-1,1) at 16 kHz (scaled ×32768 and clipped internally, firered_vad.py:89) */
+QASR_API int qasr_vad_probabilities(qasr_vad* v, const float* pcm, size_t n, float* probs, size_t cap,
+                                    size_t* n_frames);
+QASR_API int qasr_vad_features(qasr_vad* v, const float* pcm, size_t n, float* feats /*[T][80] log-fbank*/,
+                               size_t cap_frames, size_t* n_frames);
+QASR_API int qasr_vad_speech_timestamps(qasr_vad* v, const float* pcm, size_t n, const qasr_vad_options* o,
+                                        qasr_segment* out, size_t cap, size_t* n_out);
+QASR_API int qasr_vad_timestamps_from_probabilities(const float* probs, size_t n_frames, int64_t audio_len,
+                                                    const qasr_vad_options* o, qasr_segment* out, size_t cap,
+                                                    size_t* n_out);
+QASR_API void qasr_vad_close(qasr_vad* v);
+
+/* -------------------------------------------------------------------------------------------- audio io */
+/* returns the f32 sample count; base64 of pcm_s16le → f32 = s/32768 (server_common.py:145-170) */
+QASR_API int qasr_decode_pcm_s16le(const char* b64, size_t len, float* out, size_t cap, size_t* n_out);
+QASR_API int qasr_resample_linear(const float* x, size_t n, int32_t source_rate, float* out, size_t cap,
+                                  size_t* n_out);
+
+/* -------------------------------------------------------------------------------------------- kernel ops */
+QASR_API int qasr_op_quant_rows(const float* x, int32_t M, int32_t K, int32_t ldx, int8_t* q, float* d, void* stream);
+QASR_API int qasr_op_repack_q8(const uint8_t* blocks, int64_t nblk, int8_t* qs, void* sc, void* stream);
+/* path: 0 auto, 1 GEMV, 2 MFMA GEMM; epi: 0 store, 1 residual, 2 gelu */
+QASR_API int qasr_op_linear_q8(const int8_t* xq, const float* xd, int32_t M, const int8_t* wqs, const void* wsc,
+                               int32_t N, int32_t K, const float* bias, const float* res, float* y, int32_t ldy,
+                               int32_t epi, int32_t path, void* stream);
+QASR_API int qasr_op_rmsnorm_q8(const float* x, int32_t M, int32_t H, const float* w, float eps, int8_t* q, float* d,
+                                void* stream);
+QASR_API int qasr_op_layernorm_q8(const float* x, int32_t M, int32_t H, const float* w, const float* b, float eps,
+                                  int8_t* q, float* d, float* y, void* stream);
+QASR_API int qasr_op_swiglu_q8(const float* gu, int32_t M, int32_t F, int8_t* q, float* d, void* stream);
+QASR_API int qasr_op_qk_norm_rope(const float* qkv, int32_t rows, int32_t nh, int32_t nkv, int32_t hd,
+                                  const int32_t* pos, const int32_t* slot, const float* qnw, const float* knw,
+                                  const float* rope_cs, float eps, void* qout, void* kc, void* vc, void* stream);
+QASR_API int qasr_op_attention(const void* q, int32_t ldq, const void* k, const void* v, int32_t ldkv,
+                               const int32_t* kv_start, const int32_t* kv_len, int32_t rows, int32_t nh, int32_t nkv,
+                               int32_t hd, float scale, float* o, int8_t* oq, float* od, void* stream);
+QASR_API int qasr_op_argmax(const float* x, int32_t M, int32_t V, int32_t* out, void* stream);
+QASR_API int qasr_op_embed_rows(const int32_t* ids, int32_t n, const int8_t* wqs, const void* wsc, int32_t K,
+                                const float* alt, float* out, void* stream);
+QASR_API int qasr_op_synth_q8(uint64_t seed, const char* name, int64_t N, int64_t K, float sigma, int8_t* qs, void* sc,
+                              void* stream);
+QASR_API int qasr_op_rope_table(int32_t n_ctx, int32_t head_dim, float theta, float* host_out /*[n_ctx][hd/2][2]*/);
+QASR_API int qasr_op_mel(const float* pcm, int64_t n, int32_t n_mels, float* mel /*[n_mels][t_pad]*/, void* stream);
+QASR_API int qasr_op_fbank(const float* pcm, int64_t n, float* feats /*[T][80]*/, void* stream);
+QASR_API int qasr_stream_sync(void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* QASR_H */

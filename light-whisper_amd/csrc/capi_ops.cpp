@@ -1,0 +1,143 @@
+// extern "C" kernel-level entry points (qasr_op_*) — see include/qasr.h.
+#include <math.h>
+#include <string.h>
+
+#include <string>
+
+#include "../../include/qasr.h"
+#include "capi_util.h"
+#include "kernels.h"
+
+using namespace qasr;
+
+namespace {
+inline hipStream_t S(void* s) { return (hipStream_t)s; }
+inline void launched() { QASR_HIP(hipGetLastError()); }
+}  // namespace
+
+extern "C" {
+
+QASR_API int qasr_op_quant_rows(const float* x, int32_t M, int32_t K, int32_t ldx, int8_t* q, float* d, void* stream) {
+    return guard([&] {
+        QASR_CHECK(K % QK == 0 && M >= 0 && ldx >= K, QASR_E_INVALID, "quant_rows: K must be a multiple of 32");
+        quant_rows(x, M, K, ldx, q, d, S(stream));
+        launched();
+    });
+}
+
+QASR_API int qasr_op_repack_q8(const uint8_t* blocks, int64_t nblk, int8_t* qs, void* sc, void* stream) {
+    return guard([&] {
+        repack_q8(blocks, nblk, qs, (__half*)sc, S(stream));
+        launched();
+    });
+}
+
+QASR_API int qasr_op_linear_q8(const int8_t* xq, const float* xd, int32_t M, const int8_t* wqs, const void* wsc,
+                               int32_t N, int32_t K, const float* bias, const float* res, float* y, int32_t ldy,
+                               int32_t epi, int32_t path, void* stream) {
+    return guard([&] {
+        QASR_CHECK(K % QK == 0 && N > 0 && M >= 0 && ldy >= N, QASR_E_INVALID, "linear_q8: bad shape");
+        QASR_CHECK(epi >= 0 && epi <= 2, QASR_E_INVALID, "linear_q8: bad epilogue");
+        QASR_CHECK(epi != EPI_RESID || res, QASR_E_INVALID, "linear_q8: residual epilogue needs res");
+        Q8Mat W;
+        W.qs = (int8_t*)wqs;
+        W.sc = (__half*)wsc;
+        W.N = N;
+        W.K = K;
+        if (path == 1) {
+            QASR_CHECK(M <= 8, QASR_E_INVALID, "linear_q8: GEMV path supports M <= 8");
+            gemv_q8(xq, xd, M, W, bias, res, y, ldy, epi, S(stream));
+        } else if (path == 2) {
+            gemm_q8(xq, xd, M, W, bias, res, y, ldy, epi, S(stream));
+        } else {
+            linear_q8(xq, xd, M, W, bias, res, y, ldy, epi, S(stream));
+        }
+        launched();
+    });
+}
+
+QASR_API int qasr_op_rmsnorm_q8(const float* x, int32_t M, int32_t H, const float* w, float eps, int8_t* q, float* d,
+                                void* stream) {
+    return guard([&] {
+        QASR_CHECK(H % QK == 0, QASR_E_INVALID, "rmsnorm_q8: H must be a multiple of 32");
+        rmsnorm_q8(x, M, H, H, w, eps, q, d, S(stream));
+        launched();
+    });
+}
+
+QASR_API int qasr_op_layernorm_q8(const float* x, int32_t M, int32_t H, const float* w, const float* b, float eps,
+                                  int8_t* q, float* d, float* y, void* stream) {
+    return guard([&] {
+        QASR_CHECK(H % QK == 0, QASR_E_INVALID, "layernorm_q8: H must be a multiple of 32");
+        layernorm_q8(x, M, H, w, b, eps, q, d, y, S(stream));
+        launched();
+    });
+}
+
+QASR_API int qasr_op_swiglu_q8(const float* gu, int32_t M, int32_t F, int8_t* q, float* d, void* stream) {
+    return guard([&] {
+        QASR_CHECK(F % QK == 0, QASR_E_INVALID, "swiglu_q8: F must be a multiple of 32");
+        swiglu_q8(gu, M, F, q, d, S(stream));
+        launched();
+    });
+}
+
+QASR_API int qasr_op_qk_norm_rope(const float* qkv, int32_t rows, int32_t nh, int32_t nkv, int32_t hd,
+                                  const int32_t* pos, const int32_t* slot, const float* qnw, const float* knw,
+                                  const float* rope_cs, float eps, void* qout, void* kc, void* vc, void* stream) {
+    return guard([&] {
+        QASR_CHECK(nkv > 0 && nh % nkv == 0, QASR_E_INVALID, "qk_norm_rope: bad head counts");
+        qk_norm_rope(qkv, rows, nh, nkv, hd, pos, slot, qnw, knw, rope_cs, eps, (__half*)qout, (__half*)kc,
+                     (__half*)vc, S(stream));
+        launched();
+    });
+}
+
+QASR_API int qasr_op_attention(const void* q, int32_t ldq, const void* k, const void* v, int32_t ldkv,
+                               const int32_t* kv_start, const int32_t* kv_len, int32_t rows, int32_t nh, int32_t nkv,
+                               int32_t hd, float scale, float* o, int8_t* oq, float* od, void* stream) {
+    return guard([&] {
+        QASR_CHECK(nkv > 0 && nh % nkv == 0, QASR_E_INVALID, "attention: bad head counts");
+        attention((const __half*)q, ldq, (const __half*)k, (const __half*)v, ldkv, kv_start, kv_len, rows, nh, nkv,
+                  hd, scale, o, oq, od, S(stream));
+        launched();
+    });
+}
+
+QASR_API int qasr_op_argmax(const float* x, int32_t M, int32_t V, int32_t* out, void* stream) {
+    return guard([&] {
+        argmax_rows(x, M, V, out, S(stream));
+        launched();
+    });
+}
+
+QASR_API int qasr_op_embed_rows(const int32_t* ids, int32_t n, const int8_t* wqs, const void* wsc, int32_t K,
+                                const float* alt, float* out, void* stream) {
+    return guard([&] {
+        Q8Mat W;
+        W.qs = (int8_t*)wqs;
+        W.sc = (__half*)wsc;
+        W.K = K;
+        embed_rows(ids, n, W, alt, out, S(stream));
+        launched();
+    });
+}
+
+QASR_API int qasr_op_synth_q8(uint64_t seed, const char* name, int64_t N, int64_t K, float sigma, int8_t* qs, void* sc,
+                              void* stream) {
+    return guard([&] {
+        QASR_CHECK(K % QK == 0, QASR_E_INVALID, "synth_q8: K must be a multiple of 32");
+        synth_q8(smix(seed ^ fnv1a(name)), N * (K / QK), sigma / 73.6f, qs, (__half*)sc, S(stream));
+        launched();
+    });
+}
+
+QASR_API int qasr_op_rope_table(int32_t n_ctx, int32_t head_dim, float theta, float* host_out) {
+    return guard([&] { rope_table(n_ctx, head_dim, theta, host_out); });
+}
+
+QASR_API int qasr_stream_sync(void* stream) {
+    return guard([&] { QASR_HIP(hipStreamSynchronize(S(stream))); });
+}
+
+}  // extern "C"

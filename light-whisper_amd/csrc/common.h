@@ -1,0 +1,75 @@
+// Shared host/device definitions for libqasr (MI355X / gfx950 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <hip/hip_fp16.h>
+#include <stdint.h>
+#include <stdio.h>
+
+#include <stdexcept>
+#include <string>
+
+#include "../../include/qasr.h"
+
+namespace qasr {
+
+// ------------------------------------------------------------------------------------------------ errors
+struct Error : std::runtime_error {
+    int code;
+    Error(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+#define QASR_HIP(expr)                                                                                   \
+    do {                                                                                                 \
+        hipError_t e_ = (expr);                                                                          \
+        if (e_ != hipSuccess)                                                                            \
+            throw ::qasr::Error(QASR_E_HIP, std::string("HIP error ") + hipGetErrorString(e_) + \
+                                                        " at " + __FILE__ + ":" + std::to_string(__LINE__)); \
+    } while (0)
+
+#define QASR_CHECK(cond, code, msg)                        \
+    do {                                                   \
+        if (!(cond)) throw ::qasr::Error((code), (msg));   \
+    } while (0)
+
+// ------------------------------------------------------------------------------------------------ Q8_0
+constexpr int QK = 32;       // ggml Q8_0 block length
+constexpr int QBYTES = 34;   // f16 scale + 32 int8 (GGUF on-disk block)
+
+// Device-resident Q8_0 matrix W[N][K], repacked structure-of-arrays so a wave streams 16-byte vectors:
+//   qs : int8 [N][K]      row-major
+//   sc : f16  [N][K/32]   per-block scale
+struct Q8Mat {
+    int8_t* qs = nullptr;
+    __half* sc = nullptr;
+    int N = 0, K = 0;
+};
+
+// Quantised activations X[M][K]: int8 values + per-32-block f16-rounded scale stored as f32.
+struct Q8Act {
+    int8_t* q = nullptr;
+    float* d = nullptr;
+    int M = 0, K = 0;  // capacity metadata only
+};
+
+// ------------------------------------------------------------------------------------------------ synth RNG
+// Same generator as oracle/qasr_oracle.c (orc_synth_*): splitmix64 over (seed ^ fnv1a(name)) + index.
+__host__ __device__ inline uint64_t smix(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+inline uint64_t fnv1a(const char* s) {
+    uint64_t h = 0xcbf29ce484222325ull;
+    for (const unsigned char* p = (const unsigned char*)s; *p; p++) {
+        h ^= *p;
+        h *= 0x100000001b3ull;
+    }
+    return h;
+}
+__host__ __device__ inline float unit_from(uint64_t h) { return (float)(h >> 40) * (1.0f / 16777216.0f); }
+
+inline int cdiv(int a, int b) { return (a + b - 1) / b; }
+inline int64_t cdiv64(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+}  // namespace qasr

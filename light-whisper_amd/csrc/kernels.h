@@ -1,0 +1,54 @@
+// Launch wrappers for the hand-written gfx950 kernels (definitions in kernels_*.hip).
+// Every wrapper takes device pointers and a stream; none allocates or synchronises (graph-capturable).
+#pragma once
+#include "common.h"
+
+namespace qasr {
+
+enum Epi : int {
+    EPI_STORE = 0,  // y = acc (+ bias)
+    EPI_RESID = 1,  // y = res + acc (+ bias)      (y may alias res)
+    EPI_GELU = 2,   // y = gelu_erf(acc + bias)
+};
+
+// ---- Q8_0 weights / activations (kernels_q8.hip)
+void repack_q8(const uint8_t* blocks, int64_t nblk, int8_t* qs, __half* sc, hipStream_t s);
+void synth_q8(uint64_t base, int64_t nblk, float dbase, int8_t* qs, __half* sc, hipStream_t s);
+void synth_f32(uint64_t base, int64_t n, float center, float scale, float* out, hipStream_t s);
+void synth_f16(uint64_t base, int64_t n, float scale, __half* out, hipStream_t s);
+// quantise rows of x (row stride ldx floats) into q [M][K] / d [M][K/32]
+void quant_rows(const float* x, int M, int K, int ldx, int8_t* q, float* d, hipStream_t s);
+// y[M][N] (row stride ldy) = epi(X·Wᵀ); dispatches GEMV (M ≤ 8) or the MFMA GEMM
+void linear_q8(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const float* bias, const float* res,
+               float* y, int ldy, int epi, hipStream_t s);
+void gemv_q8(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const float* bias, const float* res, float* y,
+             int ldy, int epi, hipStream_t s);
+void gemm_q8(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const float* bias, const float* res, float* y,
+             int ldy, int epi, hipStream_t s);
+// rows of a Q8 table (token embeddings), dequantised; ids < 0 take row -(id+1) of `alt` [*][K] f32 instead
+void embed_rows(const int* ids, int n, const Q8Mat& W, const float* alt, float* out, hipStream_t s);
+
+// ---- norms / elementwise (kernels_nn.hip)
+void rmsnorm_q8(const float* x, int M, int H, int ldx, const float* w, float eps, int8_t* q, float* d, hipStream_t s);
+void layernorm_q8(const float* x, int M, int H, const float* w, const float* b, float eps, int8_t* q, float* d,
+                  float* y_opt, hipStream_t s);
+void swiglu_q8(const float* gu, int M, int F, int8_t* q, float* d, hipStream_t s);
+void gelu_q8(const float* x, int M, int K, int8_t* q, float* d, hipStream_t s);
+// Qwen3 q/k RMSNorm + NeoX RoPE; Q → qout f16 [rows][nh*hd], K/V → cache slots (f16)
+void qk_norm_rope(const float* qkv, int rows, int nh, int nkv, int hd, const int* pos, const int* slot,
+                  const float* qnw, const float* knw, const float* rope_cs, float eps, __half* qout, __half* kc,
+                  __half* vc, hipStream_t s);
+// f32 [rows][ld_in] column range → f16 [rows][cols]
+void to_f16(const float* x, int rows, int cols, int ldx, __half* y, int ldy, hipStream_t s);
+void argmax_rows(const float* x, int M, int V, int* out, hipStream_t s);
+void add_posemb_gather(const float* proj, int n_chunks, int T, int d, const float* pe, const int* valid_idx,
+                       int n_out, float* out, hipStream_t s);
+
+// ---- attention (kernels_attn.hip)
+// one query row r: Q[r] (f16) against keys/values slots [kv_start[r], kv_start[r]+kv_len[r]) of K/V (f16);
+// output quantised (q/d, row stride nh*hd) and/or f32 (o)
+void attention(const __half* Q, int ldq, const __half* K, const __half* V, int ldkv, const int* kv_start,
+               const int* kv_len, int rows, int nh, int nkv, int hd, float scale, float* o, int8_t* oq, float* od,
+               hipStream_t s);
+
+}  // namespace qasr

@@ -1,0 +1,161 @@
+// Variable-length attention over f16 K/V (decoder KV cache slots or encoder window buffers), gfx950.
+//
+// One wave per (query row, head).  Keys are processed in LDS-resident chunks of 256 with an online softmax
+// (running max / sum, f32): QKᵀ uses 8 lanes per key (16-dim slices, 3 xor-shuffles to reduce), PV uses
+// one 4-byte (half2) V load per lane per key so each V row is read as one coalesced 256-byte segment.
+// Row r attends slots [kv_start[r], kv_start[r]+kv_len[r]) — causal prefill, single-token decode and the
+// encoder's bidirectional 104-token windows (modeling_qwen3_asr.py:276-315) are all expressed by the
+// per-row ranges.  The output is written as f32 and/or directly as Q8 blocks for the O-projection.
+#include "kernels.h"
+
+namespace qasr {
+
+__device__ __forceinline__ float wmax(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+    return v;
+}
+__device__ __forceinline__ float wsum_a(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+template <int HD>
+__global__ __launch_bounds__(256) void k_attention(const __half* __restrict__ Q, int ldq, const __half* __restrict__ K,
+                                                   const __half* __restrict__ V, int ldkv,
+                                                   const int* __restrict__ kv_start, const int* __restrict__ kv_len,
+                                                   int rows, int nh, int nkv, float scale, float* __restrict__ o,
+                                                   int8_t* __restrict__ oq, float* __restrict__ od) {
+    constexpr int CH = 256;
+    constexpr int QD = HD / 8;    // dims per lane in QKᵀ
+    constexpr int PD = HD / 64;   // dims per lane in PV / output
+    __shared__ float sp[4][CH];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int g = blockIdx.x * 4 + w;
+    if (g >= rows * nh) return;
+    const int r = g / nh, h = g % nh;
+    const int kvh = h / (nh / nkv);
+    const int s0 = kv_start[r], L = kv_len[r];
+    const int sub = lane & 7, kk = lane >> 3;
+
+    float qv[QD];
+    {
+        const __half* qp = Q + (size_t)r * ldq + h * HD + sub * QD;
+#pragma unroll
+        for (int j = 0; j < QD; j++) qv[j] = __half2float(qp[j]);
+    }
+    float acc[PD];
+#pragma unroll
+    for (int j = 0; j < PD; j++) acc[j] = 0.f;
+    float m = -INFINITY, lsum = 0.f;
+    float* spw = sp[w];
+
+    for (int c0 = 0; c0 < L; c0 += CH) {
+        const int n = min(CH, L - c0);
+        for (int j0 = 0; j0 < n; j0 += 8) {
+            const int j = j0 + kk;
+            float part = 0.f;
+            if (j < n) {
+                const __half* kr = K + (size_t)(s0 + c0 + j) * ldkv + kvh * HD + sub * QD;
+                if constexpr (QD == 16) {
+                    const int4 a = *(const int4*)kr, b = *(const int4*)(kr + 8);
+                    const __half2* ha = (const __half2*)&a;
+                    const __half2* hb = (const __half2*)&b;
+#pragma unroll
+                    for (int t = 0; t < 4; t++) {
+                        float2 fa = __half22float2(ha[t]), fb = __half22float2(hb[t]);
+                        part += qv[2 * t] * fa.x + qv[2 * t + 1] * fa.y;
+                        part += qv[8 + 2 * t] * fb.x + qv[8 + 2 * t + 1] * fb.y;
+                    }
+                } else {
+                    const int4 a = *(const int4*)kr;
+                    const __half2* ha = (const __half2*)&a;
+#pragma unroll
+                    for (int t = 0; t < 4; t++) {
+                        float2 fa = __half22float2(ha[t]);
+                        part += qv[2 * t] * fa.x + qv[2 * t + 1] * fa.y;
+                    }
+                }
+            }
+            part += __shfl_xor(part, 1);
+            part += __shfl_xor(part, 2);
+            part += __shfl_xor(part, 4);
+            if (sub == 0 && j < n) spw[j] = part * scale;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        float cm = -INFINITY;
+        for (int i = lane; i < n; i += 64) cm = fmaxf(cm, spw[i]);
+        cm = wmax(cm);
+        const float mnew = fmaxf(m, cm);
+        const float alpha = expf(m - mnew);
+#pragma unroll
+        for (int j = 0; j < PD; j++) acc[j] *= alpha;
+        float ps = 0.f;
+        for (int i = lane; i < n; i += 64) {
+            const float p = expf(spw[i] - mnew);
+            spw[i] = p;
+            ps += p;
+        }
+        lsum = lsum * alpha + wsum_a(ps);
+        m = mnew;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const __half* vb = V + (size_t)(s0 + c0) * ldkv + kvh * HD + lane * PD;
+        for (int j = 0; j < n; j++) {
+            const float p = spw[j];
+            if constexpr (PD == 2) {
+                const float2 vv = __half22float2(*(const __half2*)(vb + (size_t)j * ldkv));
+                acc[0] += p * vv.x;
+                acc[1] += p * vv.y;
+            } else {
+                acc[0] += p * __half2float(vb[(size_t)j * ldkv]);
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    const float inv = L > 0 ? 1.f / lsum : 0.f;
+    float out[PD];
+#pragma unroll
+    for (int j = 0; j < PD; j++) out[j] = acc[j] * inv;
+    const int D = nh * HD;
+    if (o) {
+#pragma unroll
+        for (int j = 0; j < PD; j++) o[(size_t)r * D + h * HD + lane * PD + j] = out[j];
+    }
+    if (oq) {
+        // a 32-dim block spans 32/PD lanes
+        float amax = 0.f;
+#pragma unroll
+        for (int j = 0; j < PD; j++) amax = fmaxf(amax, fabsf(out[j]));
+#pragma unroll
+        for (int off = 1; off < 32 / PD; off <<= 1) amax = fmaxf(amax, __shfl_xor(amax, off));
+        const float d = amax / 127.f;
+#pragma unroll
+        for (int j = 0; j < PD; j++) {
+            const int qv2 = amax == 0.f ? 0 : (int)roundf(out[j] / d);
+            oq[(size_t)r * D + h * HD + lane * PD + j] = (int8_t)qv2;
+        }
+        if ((lane & (32 / PD - 1)) == 0) od[(size_t)r * (D / 32) + (h * HD + lane * PD) / 32] = __half2float(__float2half(d));
+    }
+}
+
+void attention(const __half* Q, int ldq, const __half* K, const __half* V, int ldkv, const int* kv_start,
+               const int* kv_len, int rows, int nh, int nkv, int hd, float scale, float* o, int8_t* oq, float* od,
+               hipStream_t s) {
+    if (rows <= 0) return;
+    const int waves = rows * nh;
+    if (hd == 128)
+        k_attention<128><<<cdiv(waves, 4), 256, 0, s>>>(Q, ldq, K, V, ldkv, kv_start, kv_len, rows, nh, nkv, scale, o, oq, od);
+    else if (hd == 64)
+        k_attention<64><<<cdiv(waves, 4), 256, 0, s>>>(Q, ldq, K, V, ldkv, kv_start, kv_len, rows, nh, nkv, scale, o, oq, od);
+    else
+        throw Error(QASR_E_INVALID, "attention: head_dim must be 64 or 128");
+}
+
+}  // namespace qasr

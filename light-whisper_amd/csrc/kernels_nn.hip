@@ -1,0 +1,302 @@
+// Norm / activation / RoPE / reduction kernels for gfx950 (wave64).  Each fuses the Q8_0 activation
+// quantisation that feeds the next W8A8 matmul, so an activation row is written once as int8+scale.
+#include "kernels.h"
+
+namespace qasr {
+
+__device__ __forceinline__ float wsum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+__device__ __forceinline__ void quant32(const float* v, int8_t* q, float* dout) {
+    float amax = 0.f;
+#pragma unroll
+    for (int j = 0; j < 32; j++) amax = fmaxf(amax, fabsf(v[j]));
+    const float d = amax / 127.f;
+    int32_t packed[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        int32_t w = 0;
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+            int qv = amax == 0.f ? 0 : (int)roundf(v[4 * j + b] / d);
+            w |= (qv & 0xff) << (8 * b);
+        }
+        packed[j] = w;
+    }
+    int4* qo = (int4*)q;
+    qo[0] = make_int4(packed[0], packed[1], packed[2], packed[3]);
+    qo[1] = make_int4(packed[4], packed[5], packed[6], packed[7]);
+    *dout = __half2float(__float2half(d));
+}
+
+__device__ __forceinline__ void load32(const float* p, float* v) {
+    const float4* s = (const float4*)p;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        float4 t = s[j];
+        v[4 * j] = t.x; v[4 * j + 1] = t.y; v[4 * j + 2] = t.z; v[4 * j + 3] = t.w;
+    }
+}
+
+// ------------------------------------------------------------------------------------------------ RMSNorm
+// one wave per row; lane b handles 32-blocks b, b+64, ...
+__global__ __launch_bounds__(256) void k_rmsnorm_q8(const float* __restrict__ x, int M, int H, int ldx,
+                                                    const float* __restrict__ w, float eps, int8_t* __restrict__ q,
+                                                    float* __restrict__ d) {
+    const int lane = threadIdx.x & 63;
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= M) return;
+    const int nb = H / 32;
+    const float* xr = x + (size_t)row * ldx;
+    float ss = 0.f;
+    for (int b = lane; b < nb; b += 64) {
+        float v[32];
+        load32(xr + b * 32, v);
+#pragma unroll
+        for (int j = 0; j < 32; j++) ss += v[j] * v[j];
+    }
+    ss = wsum(ss);
+    const float inv = 1.0f / sqrtf(ss / (float)H + eps);
+    for (int b = lane; b < nb; b += 64) {
+        float v[32], g[32];
+        load32(xr + b * 32, v);
+        load32(w + b * 32, g);
+#pragma unroll
+        for (int j = 0; j < 32; j++) v[j] = v[j] * inv * g[j];
+        quant32(v, q + (size_t)row * H + b * 32, d + (size_t)row * nb + b);
+    }
+}
+
+void rmsnorm_q8(const float* x, int M, int H, int ldx, const float* w, float eps, int8_t* q, float* d, hipStream_t s) {
+    if (M <= 0) return;
+    k_rmsnorm_q8<<<cdiv(M, 4), 256, 0, s>>>(x, M, H, ldx, w, eps, q, d);
+}
+
+// ------------------------------------------------------------------------------------------------ LayerNorm
+__global__ __launch_bounds__(256) void k_layernorm_q8(const float* __restrict__ x, int M, int H,
+                                                      const float* __restrict__ w, const float* __restrict__ bb,
+                                                      float eps, int8_t* __restrict__ q, float* __restrict__ d,
+                                                      float* __restrict__ y) {
+    const int lane = threadIdx.x & 63;
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= M) return;
+    const int nb = H / 32;
+    const float* xr = x + (size_t)row * H;
+    float s1 = 0.f;
+    for (int b = lane; b < nb; b += 64) {
+        float v[32];
+        load32(xr + b * 32, v);
+#pragma unroll
+        for (int j = 0; j < 32; j++) s1 += v[j];
+    }
+    const float mean = wsum(s1) / (float)H;
+    float s2 = 0.f;
+    for (int b = lane; b < nb; b += 64) {
+        float v[32];
+        load32(xr + b * 32, v);
+#pragma unroll
+        for (int j = 0; j < 32; j++) {
+            float t = v[j] - mean;
+            s2 += t * t;
+        }
+    }
+    const float inv = 1.0f / sqrtf(wsum(s2) / (float)H + eps);
+    for (int b = lane; b < nb; b += 64) {
+        float v[32], g[32], c[32];
+        load32(xr + b * 32, v);
+        load32(w + b * 32, g);
+        load32(bb + b * 32, c);
+#pragma unroll
+        for (int j = 0; j < 32; j++) v[j] = (v[j] - mean) * inv * g[j] + c[j];
+        if (y) {
+            float4* yo = (float4*)(y + (size_t)row * H + b * 32);
+#pragma unroll
+            for (int j = 0; j < 8; j++) yo[j] = make_float4(v[4 * j], v[4 * j + 1], v[4 * j + 2], v[4 * j + 3]);
+        }
+        if (q) quant32(v, q + (size_t)row * H + b * 32, d + (size_t)row * nb + b);
+    }
+}
+
+void layernorm_q8(const float* x, int M, int H, const float* w, const float* b, float eps, int8_t* q, float* d,
+                  float* y_opt, hipStream_t s) {
+    if (M <= 0) return;
+    k_layernorm_q8<<<cdiv(M, 4), 256, 0, s>>>(x, M, H, w, b, eps, q, d, y_opt);
+}
+
+// ------------------------------------------------------------------------------------------------ SwiGLU / GELU
+__global__ void k_swiglu_q8(const float* __restrict__ gu, int M, int F, int8_t* __restrict__ q, float* __restrict__ d) {
+    const int nb = F / 32;
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)M * nb) return;
+    const int m = (int)(i / nb), b = (int)(i % nb);
+    float g[32], u[32];
+    load32(gu + (size_t)m * 2 * F + b * 32, g);
+    load32(gu + (size_t)m * 2 * F + F + b * 32, u);
+#pragma unroll
+    for (int j = 0; j < 32; j++) g[j] = g[j] / (1.f + expf(-g[j])) * u[j];
+    quant32(g, q + (size_t)m * F + b * 32, d + (size_t)m * nb + b);
+}
+
+void swiglu_q8(const float* gu, int M, int F, int8_t* q, float* d, hipStream_t s) {
+    int64_t n = (int64_t)M * (F / 32);
+    if (n <= 0) return;
+    k_swiglu_q8<<<(unsigned)cdiv64(n, 256), 256, 0, s>>>(gu, M, F, q, d);
+}
+
+__global__ void k_gelu_q8(const float* __restrict__ x, int M, int K, int8_t* __restrict__ q, float* __restrict__ d) {
+    const int nb = K / 32;
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)M * nb) return;
+    const int m = (int)(i / nb), b = (int)(i % nb);
+    float v[32];
+    load32(x + (size_t)m * K + b * 32, v);
+#pragma unroll
+    for (int j = 0; j < 32; j++) v[j] = 0.5f * v[j] * (1.f + erff(v[j] * 0.70710678118654752f));
+    quant32(v, q + (size_t)m * K + b * 32, d + (size_t)m * nb + b);
+}
+
+void gelu_q8(const float* x, int M, int K, int8_t* q, float* d, hipStream_t s) {
+    int64_t n = (int64_t)M * (K / 32);
+    if (n <= 0) return;
+    k_gelu_q8<<<(unsigned)cdiv64(n, 256), 256, 0, s>>>(x, M, K, q, d);
+}
+
+// ------------------------------------------------------------------------------------------------ q/k norm + RoPE
+// one wave per (row, head slot); slots [0,nh) = q heads, [nh,nh+nkv) = k heads, [nh+nkv, nh+2nkv) = v heads.
+// hd = 128 (2 dims per lane) or 64 (1 dim per lane); the RoPE partner of lane l is lane l^32.
+template <int HD>
+__global__ __launch_bounds__(256) void k_qk_norm_rope(const float* __restrict__ qkv, int rows, int nh, int nkv,
+                                                      const int* __restrict__ pos, const int* __restrict__ slot,
+                                                      const float* __restrict__ qnw, const float* __restrict__ knw,
+                                                      const float* __restrict__ rope_cs, float eps,
+                                                      __half* __restrict__ qout, __half* __restrict__ kc,
+                                                      __half* __restrict__ vc) {
+    constexpr int DPL = HD / 64;
+    const int lane = threadIdx.x & 63;
+    const int nslot = nh + 2 * nkv;
+    const int g = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (g >= rows * nslot) return;
+    const int r = g / nslot, h = g % nslot;
+    const int ld = nslot * HD;
+    const float* src = qkv + (size_t)r * ld + h * HD;
+    float v[DPL];
+#pragma unroll
+    for (int j = 0; j < DPL; j++) v[j] = src[lane * DPL + j];
+    const int kvd = nkv * HD;
+    if (h >= nh + nkv) {  // v head: copy to cache
+        __half* dst = vc + (size_t)slot[r] * kvd + (h - nh - nkv) * HD;
+#pragma unroll
+        for (int j = 0; j < DPL; j++) dst[lane * DPL + j] = __float2half(v[j]);
+        return;
+    }
+    const float* nw = h < nh ? qnw : knw;
+    float ss = 0.f;
+#pragma unroll
+    for (int j = 0; j < DPL; j++) ss += v[j] * v[j];
+    ss = wsum(ss);
+    const float inv = 1.0f / sqrtf(ss / (float)HD + eps);
+#pragma unroll
+    for (int j = 0; j < DPL; j++) v[j] = v[j] * inv * nw[lane * DPL + j];
+    const int p = pos[r];
+    const int half = HD / 2;
+    float o[DPL];
+#pragma unroll
+    for (int j = 0; j < DPL; j++) {
+        const float partner = __shfl_xor(v[j], 32);
+        const int dim = lane * DPL + j;
+        const int e = dim < half ? dim : dim - half;
+        const float c = rope_cs[((size_t)p * half + e) * 2], sn = rope_cs[((size_t)p * half + e) * 2 + 1];
+        o[j] = dim < half ? v[j] * c - partner * sn : v[j] * c + partner * sn;
+    }
+    if (h < nh) {
+        __half* dst = qout + (size_t)r * nh * HD + h * HD;
+#pragma unroll
+        for (int j = 0; j < DPL; j++) dst[lane * DPL + j] = __float2half(o[j]);
+    } else {
+        __half* dst = kc + (size_t)slot[r] * kvd + (h - nh) * HD;
+#pragma unroll
+        for (int j = 0; j < DPL; j++) dst[lane * DPL + j] = __float2half(o[j]);
+    }
+}
+
+void qk_norm_rope(const float* qkv, int rows, int nh, int nkv, int hd, const int* pos, const int* slot,
+                  const float* qnw, const float* knw, const float* rope_cs, float eps, __half* qout, __half* kc,
+                  __half* vc, hipStream_t s) {
+    if (rows <= 0) return;
+    const int waves = rows * (nh + 2 * nkv);
+    if (hd == 128)
+        k_qk_norm_rope<128><<<cdiv(waves, 4), 256, 0, s>>>(qkv, rows, nh, nkv, pos, slot, qnw, knw, rope_cs, eps, qout, kc, vc);
+    else if (hd == 64)
+        k_qk_norm_rope<64><<<cdiv(waves, 4), 256, 0, s>>>(qkv, rows, nh, nkv, pos, slot, qnw, knw, rope_cs, eps, qout, kc, vc);
+    else
+        throw Error(QASR_E_INVALID, "qk_norm_rope: head_dim must be 64 or 128");
+}
+
+// ------------------------------------------------------------------------------------------------ misc
+__global__ void k_to_f16(const float* __restrict__ x, int rows, int cols, int ldx, __half* __restrict__ y, int ldy) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)rows * cols) return;
+    const int r = (int)(i / cols), c = (int)(i % cols);
+    y[(size_t)r * ldy + c] = __float2half(x[(size_t)r * ldx + c]);
+}
+
+void to_f16(const float* x, int rows, int cols, int ldx, __half* y, int ldy, hipStream_t s) {
+    int64_t n = (int64_t)rows * cols;
+    if (n <= 0) return;
+    k_to_f16<<<(unsigned)cdiv64(n, 256), 256, 0, s>>>(x, rows, cols, ldx, y, ldy);
+}
+
+// first index of the maximum (ties → lowest index, like the oracle's strict '>' scan)
+__global__ __launch_bounds__(256) void k_argmax(const float* __restrict__ x, int V, int* __restrict__ out) {
+    const float* r = x + (size_t)blockIdx.x * V;
+    float best = -INFINITY;
+    int bi = 0x7fffffff;
+    for (int i = threadIdx.x; i < V; i += 256) {
+        float v = r[i];
+        if (v > best || (v == best && i < bi)) { best = v; bi = i; }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        float ov = __shfl_xor(best, o);
+        int oi = __shfl_xor(bi, o);
+        if (ov > best || (ov == best && oi < bi)) { best = ov; bi = oi; }
+    }
+    __shared__ float sv[4];
+    __shared__ int si[4];
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) { sv[w] = best; si[w] = bi; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int j = 1; j < 4; j++)
+            if (sv[j] > best || (sv[j] == best && si[j] < bi)) { best = sv[j]; bi = si[j]; }
+        out[blockIdx.x] = bi;
+    }
+}
+
+void argmax_rows(const float* x, int M, int V, int* out, hipStream_t s) {
+    if (M <= 0) return;
+    k_argmax<<<M, 256, 0, s>>>(x, V, out);
+}
+
+// audio encoder: gather the valid post-CNN positions of every chunk and add the sinusoid embedding
+__global__ void k_posemb_gather(const float* __restrict__ proj, int T, int d, const float* __restrict__ pe,
+                                const int* __restrict__ valid_idx, int n_out, float* __restrict__ out) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)n_out * d) return;
+    const int r = (int)(i / d), c = (int)(i % d);
+    const int src = valid_idx[r];
+    out[i] = proj[(size_t)src * d + c] + pe[(size_t)(src % T) * d + c];
+}
+
+void add_posemb_gather(const float* proj, int n_chunks, int T, int d, const float* pe, const int* valid_idx,
+                       int n_out, float* out, hipStream_t s) {
+    (void)n_chunks;
+    int64_t n = (int64_t)n_out * d;
+    if (n <= 0) return;
+    k_posemb_gather<<<(unsigned)cdiv64(n, 256), 256, 0, s>>>(proj, T, d, pe, valid_idx, n_out, out);
+}
+
+}  // namespace qasr

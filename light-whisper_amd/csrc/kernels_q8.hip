@@ -1,0 +1,368 @@
+// Q8_0 kernels for gfx950: weight repack / synthetic weights, activation quantisation, and the two
+// W8A8 matmul kernels (wave-per-row GEMV for decode, i8-MFMA GEMM for prefill / batched decode).
+//
+// Arithmetic contract (ggml Q8_0 conventions behind transcribe_cpp, qwen3_asr_server.py:321):
+//   activation block (32): d = amax/127 (f32), q = roundf(x/d) (IEEE division), d kept as f16
+//   block dot: exact int32 Σ q_w·q_x, contribution (float)sum · (d_w·d_x), f32 accumulation.
+#include "kernels.h"
+
+namespace qasr {
+
+// ------------------------------------------------------------------------------------------------ helpers
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
+
+__device__ __forceinline__ float epi_apply(int epi, float acc, int row, int col, const float* bias, const float* res,
+                                           int ldy) {
+    if (bias) acc += bias[col];
+    if (epi == EPI_RESID) acc += res[(size_t)row * ldy + col];
+    else if (epi == EPI_GELU) acc = gelu_erf(acc);
+    return acc;
+}
+
+// quantise one 32-block held by one thread
+__device__ __forceinline__ void quant_block32(const float* v, int8_t* q, float* dout) {
+    float amax = 0.f;
+#pragma unroll
+    for (int j = 0; j < 32; j++) amax = fmaxf(amax, fabsf(v[j]));
+    const float d = amax / 127.f;
+    int32_t packed[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        int32_t w = 0;
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+            int qv = amax == 0.f ? 0 : (int)roundf(v[4 * j + b] / d);
+            w |= (qv & 0xff) << (8 * b);
+        }
+        packed[j] = w;
+    }
+    int4* qo = (int4*)q;
+    qo[0] = make_int4(packed[0], packed[1], packed[2], packed[3]);
+    qo[1] = make_int4(packed[4], packed[5], packed[6], packed[7]);
+    *dout = __half2float(__float2half(d));
+}
+
+// ------------------------------------------------------------------------------------------------ repack / synth
+__global__ void k_repack_q8(const uint8_t* __restrict__ blocks, int64_t nblk, int8_t* __restrict__ qs,
+                            __half* __restrict__ sc) {
+    int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= nblk) return;
+    const uint8_t* p = blocks + b * QBYTES;
+    uint16_t h = (uint16_t)p[0] | ((uint16_t)p[1] << 8);
+    sc[b] = __ushort_as_half(h);
+    int32_t w[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++)
+        w[j] = (int32_t)p[2 + 4 * j] | ((int32_t)p[3 + 4 * j] << 8) | ((int32_t)p[4 + 4 * j] << 16) |
+               ((int32_t)p[5 + 4 * j] << 24);
+    int4* o = (int4*)(qs + b * QK);
+    o[0] = make_int4(w[0], w[1], w[2], w[3]);
+    o[1] = make_int4(w[4], w[5], w[6], w[7]);
+}
+
+void repack_q8(const uint8_t* blocks, int64_t nblk, int8_t* qs, __half* sc, hipStream_t s) {
+    if (nblk <= 0) return;
+    k_repack_q8<<<(unsigned)cdiv64(nblk, 256), 256, 0, s>>>(blocks, nblk, qs, sc);
+}
+
+__global__ void k_synth_q8(uint64_t base, int64_t nblk, float dbase, int8_t* __restrict__ qs, __half* __restrict__ sc) {
+    int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= nblk) return;
+    uint64_t h = smix(base + (uint64_t)b);
+    float d = dbase * (0.5f + unit_from(h));
+    sc[b] = __float2half(d);
+    int32_t w[8];
+#pragma unroll
+    for (int g = 0; g < 4; g++) {
+        uint64_t r = smix(h + (uint64_t)(g + 1));
+#pragma unroll
+        for (int half = 0; half < 2; half++) {
+            int32_t word = 0;
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                int v = (int)((r >> (8 * (4 * half + j))) & 0xff) - 128;
+                v = v < -127 ? -127 : v;
+                word |= (v & 0xff) << (8 * j);
+            }
+            w[2 * g + half] = word;
+        }
+    }
+    int4* o = (int4*)(qs + b * QK);
+    o[0] = make_int4(w[0], w[1], w[2], w[3]);
+    o[1] = make_int4(w[4], w[5], w[6], w[7]);
+}
+
+void synth_q8(uint64_t base, int64_t nblk, float dbase, int8_t* qs, __half* sc, hipStream_t s) {
+    if (nblk <= 0) return;
+    k_synth_q8<<<(unsigned)cdiv64(nblk, 256), 256, 0, s>>>(base, nblk, dbase, qs, sc);
+}
+
+__global__ void k_synth_f32(uint64_t base, int64_t n, float center, float scale, float* out) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    out[i] = fmaf(scale, 2.f * unit_from(smix(base + (uint64_t)i)) - 1.f, center);
+}
+void synth_f32(uint64_t base, int64_t n, float center, float scale, float* out, hipStream_t s) {
+    if (n <= 0) return;
+    k_synth_f32<<<(unsigned)cdiv64(n, 256), 256, 0, s>>>(base, n, center, scale, out);
+}
+
+__global__ void k_synth_f16(uint64_t base, int64_t n, float scale, __half* out) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    out[i] = __float2half(scale * (2.f * unit_from(smix(base + (uint64_t)i)) - 1.f));
+}
+void synth_f16(uint64_t base, int64_t n, float scale, __half* out, hipStream_t s) {
+    if (n <= 0) return;
+    k_synth_f16<<<(unsigned)cdiv64(n, 256), 256, 0, s>>>(base, n, scale, out);
+}
+
+// ------------------------------------------------------------------------------------------------ quant rows
+// one thread per 32-block; 8 × float4 loads
+__global__ void k_quant_rows(const float* __restrict__ x, int M, int K, int ldx, int8_t* __restrict__ q,
+                             float* __restrict__ d) {
+    const int nb = K / QK;
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)M * nb) return;
+    const int m = (int)(i / nb), b = (int)(i % nb);
+    const float4* src = (const float4*)(x + (size_t)m * ldx + b * QK);
+    float v[32];
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        float4 t = src[j];
+        v[4 * j] = t.x; v[4 * j + 1] = t.y; v[4 * j + 2] = t.z; v[4 * j + 3] = t.w;
+    }
+    quant_block32(v, q + (size_t)m * K + b * QK, d + (size_t)m * nb + b);
+}
+
+void quant_rows(const float* x, int M, int K, int ldx, int8_t* q, float* d, hipStream_t s) {
+    int64_t n = (int64_t)M * (K / QK);
+    if (n <= 0) return;
+    k_quant_rows<<<(unsigned)cdiv64(n, 256), 256, 0, s>>>(x, M, K, ldx, q, d);
+}
+
+typedef int v4i __attribute__((ext_vector_type(4)));
+
+// ------------------------------------------------------------------------------------------------ GEMV
+// One wave per output column n (= weight row).  Each lane streams 16 B of the weight row per step
+// (a half block); the two lanes of a block combine their sdot4 partials with one xor-shuffle so the block
+// sum is the exact int32 of the contract.  Activations (M ≤ 8 rows) are re-read from L1/L2.
+template <int MR>
+__global__ __launch_bounds__(256) void k_gemv_q8(const int8_t* __restrict__ W, const __half* __restrict__ Wsc, int N,
+                                                 int K, const int8_t* __restrict__ X, const float* __restrict__ Xd,
+                                                 int M, const float* __restrict__ bias, const float* res, float* y,
+                                                 int ldy, int epi) {
+    const int lane = threadIdx.x & 63;
+    const int n = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (n >= N) return;
+    const int nb = K / QK;
+    const int8_t* wr = W + (size_t)n * K;
+    const __half* sr = Wsc + (size_t)n * nb;
+    float acc[MR];
+#pragma unroll
+    for (int m = 0; m < MR; m++) acc[m] = 0.f;
+    const bool even = (lane & 1) == 0;
+    for (int k0 = lane * 16; k0 < K; k0 += 1024) {
+        const v4i wv = __builtin_nontemporal_load((const v4i*)(wr + k0));
+        const int4 w = make_int4(wv.x, wv.y, wv.z, wv.w);
+        const int blk = k0 >> 5;
+        const float dw = __half2float(sr[blk]);
+#pragma unroll
+        for (int m = 0; m < MR; m++) {
+            if (m < M) {
+                const int4 xv = *(const int4*)(X + (size_t)m * K + k0);
+                int p = __builtin_amdgcn_sdot4(w.x, xv.x, 0, false);
+                p = __builtin_amdgcn_sdot4(w.y, xv.y, p, false);
+                p = __builtin_amdgcn_sdot4(w.z, xv.z, p, false);
+                p = __builtin_amdgcn_sdot4(w.w, xv.w, p, false);
+                p += __shfl_xor(p, 1);
+                const float dx = Xd[(size_t)m * nb + blk];
+                acc[m] += even ? (float)p * (dw * dx) : 0.f;
+            }
+        }
+    }
+#pragma unroll
+    for (int m = 0; m < MR; m++) {
+        if (m < M) {
+            float v = wave_sum(acc[m]);
+            if (lane == 0) y[(size_t)m * ldy + n] = epi_apply(epi, v, m, n, bias, res, ldy);
+        }
+    }
+}
+
+void gemv_q8(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const float* bias, const float* res, float* y,
+             int ldy, int epi, hipStream_t s) {
+    dim3 grid(cdiv(W.N, 4));
+    if (M <= 1) k_gemv_q8<1><<<grid, 256, 0, s>>>(W.qs, W.sc, W.N, W.K, xq, xd, M, bias, res, y, ldy, epi);
+    else if (M <= 2) k_gemv_q8<2><<<grid, 256, 0, s>>>(W.qs, W.sc, W.N, W.K, xq, xd, M, bias, res, y, ldy, epi);
+    else if (M <= 4) k_gemv_q8<4><<<grid, 256, 0, s>>>(W.qs, W.sc, W.N, W.K, xq, xd, M, bias, res, y, ldy, epi);
+    else k_gemv_q8<8><<<grid, 256, 0, s>>>(W.qs, W.sc, W.N, W.K, xq, xd, M, bias, res, y, ldy, epi);
+}
+
+// ------------------------------------------------------------------------------------------------ GEMM (MFMA)
+// 64×64 output tile, 256 threads (4 waves, 2×2), each wave 32×32 = 2×2 v_mfma_i32_16x16x32_i8 tiles.
+// K step = 64 (two Q8 blocks); A (activations) and B (weights, stored [N][K]) staged in LDS with an 80-byte
+// row stride (conflict-free ds_read_b64 fragments); the next step is prefetched into registers while
+// the current one is consumed.  Each 16×16×32 MFMA produces the exact int32 block sum of one Q8 block,
+// rescaled into the f32 accumulator by d_x(row)·d_w(col).
+constexpr int GB = 64;       // tile M and N
+constexpr int GK = 64;       // K per step
+constexpr int GLDS = 80;     // LDS row stride (bytes)
+
+__global__ __launch_bounds__(256) void k_gemm_q8(const int8_t* __restrict__ X, const float* __restrict__ Xd, int M,
+                                                 const int8_t* __restrict__ W, const __half* __restrict__ Wsc, int N,
+                                                 int K, const float* __restrict__ bias, const float* res, float* y,
+                                                 int ldy, int epi) {
+    __shared__ __attribute__((aligned(16))) int8_t As[GB * GLDS];
+    __shared__ __attribute__((aligned(16))) int8_t Bs[GB * GLDS];
+    __shared__ float Asc[GB * 2];
+    __shared__ float Bsc[GB * 2];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wr = wave >> 1, wc = wave & 1;
+    const int n0 = blockIdx.x * GB, m0 = blockIdx.y * GB;
+    const int nb = K / QK;
+
+    // staging assignment: 16 B per thread for A and for B; 1 scale per thread (A: t<128, B: t>=128)
+    const int srow = tid >> 2, sseg = (tid & 3) * 16;
+    const int am = m0 + srow, bn = n0 + srow;
+    const int sc_row = (tid & 127) >> 1, sc_blk = tid & 1;
+
+    int4 ra, rb;
+    float rs;
+    auto gload = [&](int k0) {
+        const int k = k0 + sseg;
+        ra = (am < M && k < K) ? *(const int4*)(X + (size_t)am * K + k) : make_int4(0, 0, 0, 0);
+        rb = (bn < N && k < K) ? *(const int4*)(W + (size_t)bn * K + k) : make_int4(0, 0, 0, 0);
+        const int kb = (k0 >> 5) + sc_blk;
+        if (tid < 128) {
+            const int r = m0 + sc_row;
+            rs = (r < M && kb < nb) ? Xd[(size_t)r * nb + kb] : 0.f;
+        } else {
+            const int c = n0 + sc_row;
+            rs = (c < N && kb < nb) ? __half2float(Wsc[(size_t)c * nb + kb]) : 0.f;
+        }
+    };
+    auto lstore = [&]() {
+        *(int4*)(As + srow * GLDS + sseg) = ra;
+        *(int4*)(Bs + srow * GLDS + sseg) = rb;
+        if (tid < 128) Asc[sc_row * 2 + sc_blk] = rs;
+        else Bsc[sc_row * 2 + sc_blk] = rs;
+    };
+
+    float acc[2][2][4];
+#pragma unroll
+    for (int i = 0; i < 2; i++)
+#pragma unroll
+        for (int j = 0; j < 2; j++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) acc[i][j][r] = 0.f;
+
+    const int fr = lane & 15, fk = 8 * (lane >> 4);
+    gload(0);
+    lstore();
+    __syncthreads();
+    for (int k0 = 0; k0 < K; k0 += GK) {
+        const bool more = k0 + GK < K;
+        if (more) gload(k0 + GK);
+#pragma unroll
+        for (int kb = 0; kb < 2; kb++) {
+            long a[2], b[2];
+#pragma unroll
+            for (int i = 0; i < 2; i++) a[i] = *(const long*)(As + (wr * 32 + i * 16 + fr) * GLDS + kb * 32 + fk);
+#pragma unroll
+            for (int j = 0; j < 2; j++) b[j] = *(const long*)(Bs + (wc * 32 + j * 16 + fr) * GLDS + kb * 32 + fk);
+            float sa[2][4], sb[2];
+#pragma unroll
+            for (int i = 0; i < 2; i++)
+#pragma unroll
+                for (int r = 0; r < 4; r++) sa[i][r] = Asc[(wr * 32 + i * 16 + 4 * (lane >> 4) + r) * 2 + kb];
+#pragma unroll
+            for (int j = 0; j < 2; j++) sb[j] = Bsc[(wc * 32 + j * 16 + fr) * 2 + kb];
+#pragma unroll
+            for (int i = 0; i < 2; i++) {
+#pragma unroll
+                for (int j = 0; j < 2; j++) {
+                    v4i c = {0, 0, 0, 0};
+                    c = __builtin_amdgcn_mfma_i32_16x16x32_i8(a[i], b[j], c, 0, 0, 0);
+#pragma unroll
+                    for (int r = 0; r < 4; r++) acc[i][j][r] += (float)c[r] * (sa[i][r] * sb[j]);
+                }
+            }
+        }
+        __syncthreads();
+        if (more) {
+            lstore();
+            __syncthreads();
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 2; i++) {
+#pragma unroll
+        for (int j = 0; j < 2; j++) {
+            const int col = n0 + wc * 32 + j * 16 + fr;
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const int row = m0 + wr * 32 + i * 16 + 4 * (lane >> 4) + r;
+                if (row < M && col < N) y[(size_t)row * ldy + col] = epi_apply(epi, acc[i][j][r], row, col, bias, res, ldy);
+            }
+        }
+    }
+}
+
+void gemm_q8(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const float* bias, const float* res, float* y,
+             int ldy, int epi, hipStream_t s) {
+    dim3 grid(cdiv(W.N, GB), cdiv(M, GB));
+    k_gemm_q8<<<grid, 256, 0, s>>>(xq, xd, M, W.qs, W.sc, W.N, W.K, bias, res, y, ldy, epi);
+}
+
+void linear_q8(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const float* bias, const float* res,
+               float* y, int ldy, int epi, hipStream_t s) {
+    if (M <= 0) return;
+    if (M <= 8) gemv_q8(xq, xd, M, W, bias, res, y, ldy, epi, s);
+    else gemm_q8(xq, xd, M, W, bias, res, y, ldy, epi, s);
+}
+
+// ------------------------------------------------------------------------------------------------ embeddings
+__global__ void k_embed_rows(const int* __restrict__ ids, int n, const int8_t* __restrict__ qs,
+                             const __half* __restrict__ sc, int K, const float* __restrict__ alt,
+                             float* __restrict__ out) {
+    const int nb = K / QK;
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)n * nb) return;
+    const int r = (int)(i / nb), b = (int)(i % nb);
+    const int id = ids[r];
+    float4* dst = (float4*)(out + (size_t)r * K + b * QK);
+    if (id < 0) {
+        const float4* src = (const float4*)(alt + (size_t)(-(id + 1)) * K + b * QK);
+#pragma unroll
+        for (int j = 0; j < 8; j++) dst[j] = src[j];
+        return;
+    }
+    const float d = __half2float(sc[(size_t)id * nb + b]);
+    const int4* q4 = (const int4*)(qs + (size_t)id * K + b * QK);
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+        int4 v = q4[h];
+        int w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            dst[h * 4 + j] = make_float4(d * (float)(int8_t)(w[j] & 0xff), d * (float)(int8_t)((w[j] >> 8) & 0xff),
+                                         d * (float)(int8_t)((w[j] >> 16) & 0xff), d * (float)(int8_t)((w[j] >> 24) & 0xff));
+        }
+    }
+}
+
+void embed_rows(const int* ids, int n, const Q8Mat& W, const float* alt, float* out, hipStream_t s) {
+    int64_t total = (int64_t)n * (W.K / QK);
+    if (total <= 0) return;
+    k_embed_rows<<<(unsigned)cdiv64(total, 256), 256, 0, s>>>(ids, n, W.qs, W.sc, W.K, alt, out);
+}
+
+}  // namespace qasr

@@ -1,0 +1,314 @@
+"""Kernel-level parity: every qasr_op_* (HIP, through the C ABI) against the CPU oracle on seeded inputs.
+
+Bars: integer/byte work bit-exact (activation int8 + scales, synthetic weights, argmax, exact-int GEMM);
+fp32 math within the stated tolerances (sum-order differences only).
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import oracle
+from qasr import _lib
+
+pytestmark = pytest.mark.gpu
+
+
+def L():
+    return _lib.load()
+
+
+def dev(a, torch_dev):
+    import torch
+
+    return torch.from_numpy(np.ascontiguousarray(a)).to(torch_dev)
+
+
+def ptr(t):
+    return C.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def host(t):
+    import torch
+
+    torch.cuda.synchronize()
+    return t.cpu().numpy()
+
+
+def empty(shape, dtype, torch_dev):
+    import torch
+
+    return torch.empty(shape, dtype=dtype, device=torch_dev)
+
+
+def q8_split(blocks, n, k):
+    """GGUF Q8_0 blocks [N][K/32*34] → (qs int8 [N][K], sc f16-bits [N][K/32])"""
+    b = blocks.reshape(n, k // 32, 34)
+    sc = b[:, :, :2].copy().view(np.uint16).reshape(n, k // 32)
+    qs = b[:, :, 2:].copy().view(np.int8).reshape(n, k)
+    return qs, sc
+
+
+def quant_ref(x):
+    blocks = oracle.quantize_q8(x)
+    m, k = x.shape
+    qs, sc = q8_split(blocks, m, k)
+    return qs, sc.view(np.float16).astype(np.float32)
+
+
+@pytest.mark.parametrize("m,k", [(1, 32), (7, 256), (33, 2048)])
+def test_quant_rows_bit_exact(torch_dev, m, k):
+    import torch
+
+    rng = np.random.default_rng(m * 1000 + k)
+    x = (rng.standard_normal((m, k)) * rng.uniform(0.01, 100, size=(m, 1))).astype(np.float32)
+    x[0, :32] = 0.0                           # all-zero block → d = 0, q = 0
+    x[-1, -32:] = np.float32(127.0) * np.sign(rng.standard_normal(32)).astype(np.float32)  # amax exactly 127
+    x[-1, -31] = np.float32(63.5)             # a .5 tie: roundf rounds away from zero
+    xd = dev(x, torch_dev)
+    q = empty((m, k), torch.int8, torch_dev)
+    d = empty((m, k // 32), torch.float32, torch_dev)
+    _lib.check(L().qasr_op_quant_rows(ptr(xd), m, k, k, ptr(q), ptr(d), None))
+    qr, dr = quant_ref(x)
+    assert np.array_equal(host(q), qr)
+    assert np.array_equal(host(d), dr)
+
+
+def test_synth_q8_matches_oracle(torch_dev):
+    import torch
+
+    n, k = 96, 256
+    qs = empty((n, k), torch.int8, torch_dev)
+    sc = empty((n, k // 32), torch.float16, torch_dev)
+    _lib.check(L().qasr_op_synth_q8(1234, b"blk.3.attn_q.weight", n, k, 0.02, ptr(qs), ptr(sc), None))
+    ref = oracle.synth_q8(1234, "blk.3.attn_q.weight", n, k, 0.02)
+    rq, rs = q8_split(ref, n, k)
+    assert np.array_equal(host(qs), rq)
+    assert np.array_equal(host(sc).view(np.uint16), rs)
+
+
+def test_repack_q8(torch_dev):
+    import torch
+
+    n, k = 40, 128
+    blocks = oracle.synth_q8(7, "x", n, k, 1.0)
+    bd = dev(blocks.reshape(-1), torch_dev)
+    qs = empty((n, k), torch.int8, torch_dev)
+    sc = empty((n, k // 32), torch.float16, torch_dev)
+    _lib.check(L().qasr_op_repack_q8(ptr(bd), n * k // 32, ptr(qs), ptr(sc), None))
+    rq, rs = q8_split(blocks, n, k)
+    assert np.array_equal(host(qs), rq)
+    assert np.array_equal(host(sc).view(np.uint16), rs)
+
+
+def _linear_case(torch_dev, m, n, k, path, epi, seed=0, exact=False):
+    import torch
+
+    rng = np.random.default_rng(seed)
+    if exact:
+        # every block's amax = 127 → d_x = 1, weights with d_w = 1: results are exact integers in any order
+        x = rng.integers(-127, 128, size=(m, k)).astype(np.float32)
+        x[:, ::32] = 127.0
+        w = oracle.synth_q8(seed, "w", n, k, 1.0).reshape(n, k // 32, 34)
+        w[:, :, 0:2] = np.frombuffer(np.float16(1.0).tobytes(), np.uint8)
+        blocks = w.reshape(n, -1)
+    else:
+        x = rng.standard_normal((m, k)).astype(np.float32)
+        blocks = oracle.synth_q8(seed, "w", n, k, 0.05)
+    bias = rng.standard_normal(n).astype(np.float32) if epi != 1 else None
+    res = rng.standard_normal((m, n)).astype(np.float32)
+    oracle.set_mode(engine=True)
+    ref = oracle.linear_q8(x, blocks, n, bias)
+    if epi == 1:
+        ref = ref + res
+    elif epi == 2:
+        from scipy.special import erf
+
+        ref = 0.5 * ref * (1 + erf(ref / np.sqrt(2)))
+    qs, sc = q8_split(blocks, n, k)
+    xq = empty((m, k), torch.int8, torch_dev)
+    xdd = empty((m, k // 32), torch.float32, torch_dev)
+    xt = dev(x, torch_dev)
+    _lib.check(L().qasr_op_quant_rows(ptr(xt), m, k, k, ptr(xq), ptr(xdd), None))
+    wq, ws = dev(qs, torch_dev), dev(sc, torch_dev)
+    bt = dev(bias, torch_dev) if bias is not None else None
+    y = dev(res, torch_dev) if epi == 1 else empty((m, n), torch.float32, torch_dev)
+    _lib.check(L().qasr_op_linear_q8(ptr(xq), ptr(xdd), m, ptr(wq), ptr(ws), n, k, ptr(bt),
+                                     ptr(y) if epi == 1 else None, ptr(y), n, epi, path, None))
+    return host(y), ref.astype(np.float32)
+
+
+@pytest.mark.parametrize("path", [1, 2])
+@pytest.mark.parametrize("m,n,k", [(1, 64, 1024), (3, 130, 512), (8, 64, 1024), (9, 70, 96), (64, 128, 1024),
+                                   (100, 192, 512)])
+def test_linear_q8_exact_integer(torch_dev, path, m, n, k):
+    if path == 1 and m > 8:
+        pytest.skip("GEMV path is M<=8")
+    y, ref = _linear_case(torch_dev, m, n, k, path, 0, seed=m + n, exact=True)
+    assert np.array_equal(y, ref)
+
+
+@pytest.mark.parametrize("path", [1, 2])
+@pytest.mark.parametrize("epi", [0, 1, 2])
+@pytest.mark.parametrize("m,n,k", [(1, 2048, 2048), (5, 256, 6144), (37, 320, 2048), (130, 1024, 1024)])
+def test_linear_q8_vs_oracle(torch_dev, path, epi, m, n, k):
+    if path == 1 and m > 8:
+        pytest.skip("GEMV path is M<=8")
+    y, ref = _linear_case(torch_dev, m, n, k, path, epi, seed=k + epi)
+    scale = np.abs(ref).max() + 1e-6
+    assert np.abs(y - ref).max() <= 2e-5 * scale * np.sqrt(k / 256)
+
+
+def test_rmsnorm_q8(torch_dev):
+    import torch
+
+    rng = np.random.default_rng(3)
+    m, h = 9, 2048
+    x = (rng.standard_normal((m, h)) * 3).astype(np.float32)
+    w = (1 + 0.1 * rng.standard_normal(h)).astype(np.float32)
+    xt, wt = dev(x, torch_dev), dev(w, torch_dev)
+    q = empty((m, h), torch.int8, torch_dev)
+    d = empty((m, h // 32), torch.float32, torch_dev)
+    _lib.check(L().qasr_op_rmsnorm_q8(ptr(xt), m, h, ptr(wt), 1e-6, ptr(q), ptr(d), None))
+    y = x / np.sqrt((x.astype(np.float64) ** 2).mean(1, keepdims=True) + 1e-6) * w
+    qr, dr = quant_ref(y.astype(np.float32))
+    qh, dh = host(q), host(d)
+    assert np.allclose(dh, dr, rtol=1e-5)
+    assert (np.abs(qh.astype(int) - qr) <= 1).all() and (qh != qr).mean() < 1e-3
+
+
+def test_layernorm_q8(torch_dev):
+    import torch
+
+    rng = np.random.default_rng(4)
+    m, h = 5, 1024
+    x = (rng.standard_normal((m, h)) * 2 + 0.5).astype(np.float32)
+    w = (1 + 0.1 * rng.standard_normal(h)).astype(np.float32)
+    b = (0.1 * rng.standard_normal(h)).astype(np.float32)
+    xt, wt, bt = dev(x, torch_dev), dev(w, torch_dev), dev(b, torch_dev)
+    q = empty((m, h), torch.int8, torch_dev)
+    d = empty((m, h // 32), torch.float32, torch_dev)
+    y = empty((m, h), torch.float32, torch_dev)
+    _lib.check(L().qasr_op_layernorm_q8(ptr(xt), m, h, ptr(wt), ptr(bt), 1e-5, ptr(q), ptr(d), ptr(y), None))
+    x64 = x.astype(np.float64)
+    ref = (x64 - x64.mean(1, keepdims=True)) / np.sqrt(x64.var(1, keepdims=True) + 1e-5) * w + b
+    assert np.abs(host(y) - ref).max() < 1e-5 * np.abs(ref).max()
+
+
+def test_swiglu_q8(torch_dev):
+    import torch
+
+    rng = np.random.default_rng(5)
+    m, f = 4, 512
+    gu = rng.standard_normal((m, 2 * f)).astype(np.float32) * 3
+    gt = dev(gu, torch_dev)
+    q = empty((m, f), torch.int8, torch_dev)
+    d = empty((m, f // 32), torch.float32, torch_dev)
+    _lib.check(L().qasr_op_swiglu_q8(ptr(gt), m, f, ptr(q), ptr(d), None))
+    g, u = gu[:, :f], gu[:, f:]
+    y = (g / (1 + np.exp(-g)) * u).astype(np.float32)
+    qr, dr = quant_ref(y)
+    assert np.allclose(host(d), dr, rtol=1e-5)
+    assert (np.abs(host(q).astype(int) - qr) <= 1).all()
+
+
+def test_qk_norm_rope(torch_dev):
+    import torch
+
+    rng = np.random.default_rng(6)
+    rows, nh, nkv, hd = 3, 4, 2, 128
+    qkv = rng.standard_normal((rows, (nh + 2 * nkv) * hd)).astype(np.float32)
+    pos = np.array([0, 5, 77], np.int32)
+    slot = np.array([2, 0, 1], np.int32)
+    qnw = (1 + 0.1 * rng.standard_normal(hd)).astype(np.float32)
+    knw = (1 + 0.1 * rng.standard_normal(hd)).astype(np.float32)
+    tab = np.empty((128, hd // 2, 2), np.float32)
+    _lib.check(L().qasr_op_rope_table(128, hd, 1e6, tab.ctypes.data_as(C.c_void_p)))
+    qo = empty((rows, nh * hd), torch.float16, torch_dev)
+    kc = torch.zeros((4, nkv * hd), dtype=torch.float16, device=torch_dev)
+    vc = torch.zeros((4, nkv * hd), dtype=torch.float16, device=torch_dev)
+    # keep every device tensor referenced until the kernel has finished (a temporary would be freed and its
+    # block reused by the next allocation while the launch still reads it)
+    keep = [dev(a, torch_dev) for a in (qkv, pos, slot, qnw, knw, tab)]
+    _lib.check(L().qasr_op_qk_norm_rope(ptr(keep[0]), rows, nh, nkv, hd, ptr(keep[1]), ptr(keep[2]), ptr(keep[3]),
+                                        ptr(keep[4]), ptr(keep[5]), 1e-6, ptr(qo), ptr(kc), ptr(vc), None))
+
+    def norm_rope(v, w, p):
+        v = v / np.sqrt((v.astype(np.float64) ** 2).mean() + 1e-6) * w
+        c, s = tab[p, :, 0], tab[p, :, 1]
+        a, b = v[: hd // 2], v[hd // 2:]
+        return np.concatenate([a * c - b * s, b * c + a * s])
+
+    qh, kh, vh = host(qo).astype(np.float32), host(kc).astype(np.float32), host(vc).astype(np.float32)
+    for r in range(rows):
+        for h in range(nh):
+            ref = norm_rope(qkv[r, h * hd:(h + 1) * hd], qnw, pos[r])
+            assert np.abs(qh[r, h * hd:(h + 1) * hd] - ref).max() < 2e-3 * np.abs(ref).max()
+        for h in range(nkv):
+            ref = norm_rope(qkv[r, (nh + h) * hd:(nh + h + 1) * hd], knw, pos[r])
+            assert np.abs(kh[slot[r], h * hd:(h + 1) * hd] - ref).max() < 2e-3 * np.abs(ref).max()
+            vref = qkv[r, (nh + nkv + h) * hd:(nh + nkv + h + 1) * hd]
+            assert np.abs(vh[slot[r], h * hd:(h + 1) * hd] - vref).max() < 2e-3 * np.abs(vref).max()
+
+
+@pytest.mark.parametrize("hd,nh,nkv", [(128, 4, 2), (64, 3, 3)])
+def test_attention(torch_dev, hd, nh, nkv):
+    import torch
+
+    rng = np.random.default_rng(hd + nh)
+    slots = 700
+    k = rng.standard_normal((slots, nkv * hd)).astype(np.float16)
+    v = rng.standard_normal((slots, nkv * hd)).astype(np.float16)
+    starts = np.array([0, 10, 100, 0, 300], np.int32)
+    lens = np.array([1, 57, 300, 513, 104], np.int32)
+    rows = len(starts)
+    q = rng.standard_normal((rows, nh * hd)).astype(np.float16)
+    o = empty((rows, nh * hd), torch.float32, torch_dev)
+    oq = empty((rows, nh * hd), torch.int8, torch_dev)
+    od = empty((rows, nh * hd // 32), torch.float32, torch_dev)
+    scale = 1 / np.sqrt(hd)
+    keep = [dev(a, torch_dev) for a in (q, k, v, starts, lens)]
+    _lib.check(L().qasr_op_attention(ptr(keep[0]), nh * hd, ptr(keep[1]), ptr(keep[2]), nkv * hd, ptr(keep[3]),
+                                     ptr(keep[4]), rows, nh, nkv, hd, scale, ptr(o), ptr(oq), ptr(od), None))
+    oh = host(o)
+    ref = np.zeros((rows, nh * hd), np.float64)
+    for r in range(rows):
+        for h in range(nh):
+            g = h // (nh // nkv)
+            kk = k[starts[r]:starts[r] + lens[r], g * hd:(g + 1) * hd].astype(np.float64)
+            vv = v[starts[r]:starts[r] + lens[r], g * hd:(g + 1) * hd].astype(np.float64)
+            s = kk @ q[r, h * hd:(h + 1) * hd].astype(np.float64) * scale
+            p = np.exp(s - s.max())
+            ref[r, h * hd:(h + 1) * hd] = p @ vv / p.sum()
+    assert np.abs(oh - ref).max() < 1e-4
+    qr, dr = quant_ref(oh.astype(np.float32))
+    assert np.array_equal(host(oq), qr) and np.array_equal(host(od), dr)
+
+
+def test_argmax(torch_dev):
+    import torch
+
+    rng = np.random.default_rng(8)
+    x = rng.standard_normal((6, 151936)).astype(np.float32)
+    x[2, 1000] = x[2, 5000] = 99.0  # tie → lowest index
+    out = empty((6,), torch.int32, torch_dev)
+    xt = dev(x, torch_dev)
+    _lib.check(L().qasr_op_argmax(ptr(xt), 6, 151936, ptr(out), None))
+    assert np.array_equal(host(out), x.argmax(1))
+
+
+def test_embed_rows(torch_dev):
+    import torch
+
+    n, k = 50, 256
+    blocks = oracle.synth_q8(11, "token_embd.weight", n, k, 1.0)
+    qs, sc = q8_split(blocks, n, k)
+    alt = np.random.default_rng(0).standard_normal((3, k)).astype(np.float32)
+    ids = np.array([3, 0, -1, 49, -3, 3], np.int32)
+    out = empty((len(ids), k), torch.float32, torch_dev)
+    keep = [dev(a, torch_dev) for a in (ids, qs, sc, alt)]
+    _lib.check(L().qasr_op_embed_rows(ptr(keep[0]), len(ids), ptr(keep[1]), ptr(keep[2]), k, ptr(keep[3]), ptr(out),
+                                      None))
+    deq = oracle.dequantize_q8(blocks, k)
+    ref = np.stack([deq[i] if i >= 0 else alt[-(i + 1)] for i in ids])
+    assert np.array_equal(host(out), ref)
