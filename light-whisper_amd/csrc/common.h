@@ -69,6 +69,13 @@ inline uint64_t fnv1a(const char* s) {
 }
 __host__ __device__ inline float unit_from(uint64_t h) { return (float)(h >> 40) * (1.0f / 16777216.0f); }
 
+// f32 → f16 after the f32 value has been rounded (blocks hipcc's fused multiply/add → f16 single-rounding
+// v_fma_mix* forms, which would differ from the CPU's f32-then-f16 double rounding)
+__device__ __forceinline__ __half f2h(float v) {
+    asm volatile("" : "+v"(v));
+    return __float2half(v);
+}
+
 inline int cdiv(int a, int b) { return (a + b - 1) / b; }
 inline int64_t cdiv64(int64_t a, int64_t b) { return (a + b - 1) / b; }
 

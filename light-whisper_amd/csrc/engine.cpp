@@ -1,0 +1,594 @@
+// Host orchestration of the ASR hot path on one MI355X (see engine.h).  All compute is HIP kernels on
+// one stream; the host only builds index tables (prompt layout, window ranges, KV slots) and reads back
+// one int32 per active utterance per decode step.
+#include "engine.h"
+
+#include <math.h>
+#include <string.h>
+
+#include <algorithm>
+#include <chrono>
+
+#include "capi_util.h"
+#include "kernels.h"
+
+namespace qasr {
+
+namespace {
+enum SlotId {
+    S_UTTS, S_WORK, S_CHUNK_UTT, S_UMAX, S_LM, S_MELX, S_A1, S_A2, S_A3, S_XQ, S_XD, S_PROJ, S_VALID, S_HS,
+    S_QKV, S_QKVH, S_FF, S_KVS, S_KVL, S_EMB, S_IDS, S_POS, S_SLOT, S_X, S_QH, S_GU, S_LAST, S_XN, S_LOGITS,
+    S_TOK, S_PCM, S_ENC, S_COUNT
+};
+
+inline int post_cnn_len(int l) {
+    for (int i = 0; i < 3; i++) l = l > 0 ? (l - 1) / 2 + 1 : 0;
+    return l;
+}
+
+struct Timer {
+    hipEvent_t a, b;
+    hipStream_t s;
+    double* out;
+    Timer(hipStream_t st, double* o) : s(st), out(o) {
+        if (!out) return;
+        QASR_HIP(hipEventCreate(&a));
+        QASR_HIP(hipEventCreate(&b));
+        QASR_HIP(hipEventRecord(a, s));
+    }
+    ~Timer() {
+        if (!out) return;
+        (void)hipEventRecord(b, s);
+        (void)hipEventSynchronize(b);
+        float ms = 0;
+        (void)hipEventElapsedTime(&ms, a, b);
+        *out += ms;
+        (void)hipEventDestroy(a);
+        (void)hipEventDestroy(b);
+    }
+};
+
+__global__ void k_gather_rows(const float* __restrict__ x, const int* __restrict__ idx, int n, int H,
+                              float* __restrict__ y) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)n * H) return;
+    const int r = (int)(i / H), c = (int)(i % H);
+    y[i] = x[(size_t)idx[r] * H + c];
+}
+}  // namespace
+
+int audio_token_count(int t_valid) { return (t_valid / 100) * 13 + post_cnn_len(t_valid % 100); }
+
+void mel_dims(int64_t n, int& t_valid, int& t_pad) {
+    const int64_t nn = std::max<int64_t>(n, 8000);  // min_length (feature_extraction_qwen3_asr.py:192-196)
+    t_valid = (int)((nn + 159) / 160);
+    t_pad = (t_valid + 99) / 100 * 100;
+}
+
+std::vector<int32_t> build_prompt(const qasr_hparams& h, int n_audio, int audio_row0) {
+    std::vector<int32_t> p = {h.tok_im_start, h.tok_system, h.tok_newline, h.tok_im_end, h.tok_newline,
+                              h.tok_im_start, h.tok_user, h.tok_newline, h.tok_audio_start};
+    for (int i = 0; i < n_audio; i++) p.push_back(-(audio_row0 + i + 1));
+    const int32_t tail[] = {h.tok_audio_end, h.tok_im_end, h.tok_newline, h.tok_im_start, h.tok_assistant,
+                            h.tok_newline};
+    p.insert(p.end(), tail, tail + 6);
+    return p;
+}
+
+void* Scratch::get(int slot, size_t bytes) {
+    if ((int)bufs.size() <= slot) bufs.resize(slot + 1);
+    Buf& b = bufs[slot];
+    bytes = std::max<size_t>(bytes, 256);
+    if (b.cap < bytes) {
+        if (b.p) {
+            QASR_HIP(hipDeviceSynchronize());  // queued kernels may still use the old buffer
+            QASR_HIP(hipFree(b.p));
+        }
+        b.p = nullptr;
+        const size_t cap = bytes + bytes / 4;
+        QASR_HIP(hipMalloc(&b.p, cap));
+        b.cap = cap;
+    }
+    return b.p;
+}
+Scratch::~Scratch() {
+    for (auto& b : bufs)
+        if (b.p) (void)hipFree(b.p);
+}
+
+Session::Session(Model* m, int n_ctx) : m_(m), n_ctx_(n_ctx) {
+    QASR_CHECK(n_ctx > 32, QASR_E_INVALID, "n_ctx too small");
+    QASR_HIP(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking));
+    rope_n_ = n_ctx;
+    std::vector<float> tab((size_t)n_ctx * m->hp.head_dim);
+    rope_table(n_ctx, m->hp.head_dim, m->hp.rope_theta, tab.data());
+    QASR_HIP(hipMalloc(&rope_, tab.size() * sizeof(float)));
+    QASR_HIP(hipMemcpy(rope_, tab.data(), tab.size() * sizeof(float), hipMemcpyHostToDevice));
+    ensure_kv(n_ctx);  // the reference session reserves the full f16 KV for n_ctx (qwen3_asr_server.py:123)
+}
+
+Session::~Session() {
+    if (kc_) (void)hipFree(kc_);
+    if (vc_) (void)hipFree(vc_);
+    if (rope_) (void)hipFree(rope_);
+    if (pin_) (void)hipHostFree(pin_);
+    if (st_) (void)hipStreamDestroy(st_);
+}
+
+void* Session::pinned(size_t bytes) {
+    if (pin_cap_ < bytes) {
+        if (pin_) QASR_HIP(hipHostFree(pin_));
+        pin_cap_ = std::max<size_t>(bytes, 1 << 16);
+        QASR_HIP(hipHostMalloc(&pin_, pin_cap_, hipHostMallocDefault));
+    }
+    return pin_;
+}
+
+template <class T>
+T* Session::upload(int slot, const std::vector<T>& v) {
+    T* d = (T*)sc_.get(slot, v.size() * sizeof(T));
+    if (!v.empty()) {
+        // host vectors are transient: complete the copy before returning
+        QASR_HIP(hipMemcpyAsync(d, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, st_));
+        QASR_HIP(hipStreamSynchronize(st_));
+    }
+    return d;
+}
+
+void Session::ensure_kv(int64_t slots) {
+    if (slots <= kv_slots_) return;
+    QASR_HIP(hipStreamSynchronize(st_));
+    if (kc_) QASR_HIP(hipFree(kc_));
+    if (vc_) QASR_HIP(hipFree(vc_));
+    kc_ = vc_ = nullptr;
+    const qasr_hparams& h = m_->hp;
+    const size_t per = (size_t)h.txt_layers * (size_t)slots * h.txt_kv_heads * h.head_dim * sizeof(__half);
+    QASR_HIP(hipMalloc(&kc_, per));
+    QASR_HIP(hipMalloc(&vc_, per));
+    kv_slots_ = slots;
+}
+
+// ------------------------------------------------------------------------------------------ front end
+void Session::front_end(const float* dpcm, const std::vector<int64_t>& off, const std::vector<int64_t>& len,
+                        FrontEnd& fe, float* enc_out_dbg) {
+    (void)enc_out_dbg;
+    const qasr_hparams& h = m_->hp;
+    const int count = (int)len.size();
+    std::vector<MelUtt> utts(count);
+    std::vector<int2> work;
+    std::vector<int> chunk_utt;
+    int frames = 0, chunks = 0;
+    fe.n_tok.assign(count, 0);
+    fe.tok_base.assign(count, 0);
+    std::vector<int> valid_idx;
+    for (int u = 0; u < count; u++) {
+        MelUtt& U = utts[u];
+        U.pcm_off = off[u];
+        U.n = len[u];
+        const int64_t nn = std::max<int64_t>(len[u], 8000);
+        U.P = std::max<int64_t>(nn, 480000);
+        U.t_all = (int)(U.P / 160);
+        int tv, tp;
+        mel_dims(len[u], tv, tp);
+        U.t_valid = tv;
+        U.t_comp = std::min(tv + 3, U.t_all);
+        U.frame0 = frames;
+        U.chunk0 = chunks;
+        U.n_chunks = tp / 100;
+        for (int t0 = 0; t0 < U.t_comp; t0 += 16) work.push_back(make_int2(u, t0));
+        for (int c = 0; c < U.n_chunks; c++) {
+            chunk_utt.push_back(u);
+            const int clen = std::max(0, std::min(100, tv - c * 100));
+            const int v = post_cnn_len(clen);
+            for (int t = 0; t < v; t++) valid_idx.push_back((chunks + c) * 13 + t);
+        }
+        fe.tok_base[u] = fe.total_tokens;
+        fe.n_tok[u] = audio_token_count(tv);
+        fe.total_tokens += fe.n_tok[u];
+        frames += U.t_comp;
+        chunks += U.n_chunks;
+    }
+    QASR_CHECK((int)valid_idx.size() == fe.total_tokens, QASR_E_INTERNAL, "audio token count mismatch");
+    fe.total_chunks = chunks;
+    const int C = h.conv_ch, d = h.enc_d, nm = h.n_mels, F3 = m_->audio_F3();
+    MelUtt* d_utts = upload(S_UTTS, utts);
+    int2* d_work = upload(S_WORK, work);
+    int* d_cu = upload(S_CHUNK_UTT, chunk_utt);
+    unsigned* d_umax = (unsigned*)sc_.get(S_UMAX, count * sizeof(unsigned));
+    QASR_HIP(hipMemsetAsync(d_umax, 0, count * sizeof(unsigned), st_));
+    float* lm = (float*)sc_.get(S_LM, (size_t)frames * nm * sizeof(float));
+    float* melx = (float*)sc_.get(S_MELX, (size_t)chunks * nm * 100 * sizeof(float));
+    mel_frames(dpcm, d_utts, d_work, (int)work.size(), nm, m_->dft_basis, m_->mel_filters, lm, d_umax, st_);
+    mel_normalize(d_utts, count, chunks, d_cu, nm, lm, d_umax, melx, st_);
+    // conv stack
+    const int H1 = (nm + 1) / 2, W1 = 50, H2 = (H1 + 1) / 2, W2 = 25;
+    __half* a1 = (__half*)sc_.get(S_A1, (size_t)chunks * H1 * W1 * C * sizeof(__half));
+    __half* a2 = (__half*)sc_.get(S_A2, (size_t)chunks * H2 * W2 * C * sizeof(__half));
+    float* a3 = (float*)sc_.get(S_A3, (size_t)chunks * 13 * C * F3 * sizeof(float));
+    conv1_gelu(melx, chunks, nm, m_->conv_w[0], m_->conv_b[0], C, a1, st_);
+    conv3x3_gelu(a1, chunks, H1, W1, m_->conv_w[1], m_->conv_b[1], C, a2, 0, st_);
+    conv3x3_gelu(a2, chunks, H2, W2, m_->conv_w[2], m_->conv_b[2], C, a3, 1, st_);
+    const int rows = chunks * 13, K = C * F3;
+    int8_t* xq = (int8_t*)sc_.get(S_XQ, (size_t)rows * K);
+    float* xd = (float*)sc_.get(S_XD, (size_t)rows * (K / QK) * sizeof(float));
+    quant_rows(a3, rows, K, K, xq, xd, st_);
+    float* proj = (float*)sc_.get(S_PROJ, (size_t)rows * d * sizeof(float));
+    linear_q8(xq, xd, rows, m_->conv_out, nullptr, nullptr, proj, d, EPI_STORE, st_);
+    int* d_valid = upload(S_VALID, valid_idx);
+    float* hs = (float*)sc_.get(S_HS, (size_t)fe.total_tokens * d * sizeof(float));
+    add_posemb_gather(proj, chunks, 13, d, m_->pos_emb, d_valid, fe.total_tokens, hs, st_);
+    QASR_HIP(hipGetLastError());
+}
+
+// windowed bidirectional encoder + ln_post + projector → S_EMB [tokens][H]
+void Session::encoder(FrontEnd& fe, float* enc_out_dbg) {
+    const qasr_hparams& h = m_->hp;
+    const int N = fe.total_tokens, d = h.enc_d, F = h.enc_ffn, H = h.txt_h;
+    // attention windows (get_audio_cu_seqlens, modeling_qwen3_asr.py:276-315)
+    std::vector<int> kvs(N), kvl(N);
+    for (size_t u = 0; u < fe.n_tok.size(); u++) {
+        const int n = fe.n_tok[u];
+        // all chunks but the last are full → max post-CNN length is 13 unless the utterance is one partial chunk
+        const int maxlen = n >= 13 ? 13 : n;
+        const int window = maxlen * (h.n_window_infer / 100);
+        for (int i = 0; i < n; i++) {
+            const int w0 = (i / window) * window;
+            kvs[fe.tok_base[u] + i] = fe.tok_base[u] + w0;
+            kvl[fe.tok_base[u] + i] = std::min(window, n - w0);
+        }
+    }
+    int* d_kvs = upload(S_KVS, kvs);
+    int* d_kvl = upload(S_KVL, kvl);
+    float* hs = (float*)sc_.get(S_HS, (size_t)N * d * sizeof(float));
+    const int kmax = std::max(d, F);
+    int8_t* xq = (int8_t*)sc_.get(S_XQ, (size_t)N * kmax);
+    float* xd = (float*)sc_.get(S_XD, (size_t)N * (kmax / QK) * sizeof(float));
+    float* qkv = (float*)sc_.get(S_QKV, (size_t)N * 3 * d * sizeof(float));
+    __half* qkvh = (__half*)sc_.get(S_QKVH, (size_t)N * 3 * d * sizeof(__half));
+    float* ff = (float*)sc_.get(S_FF, (size_t)N * std::max(F, d) * sizeof(float));
+    const float scale = 1.0f / sqrtf((float)(d / h.enc_heads));
+    for (int l = 0; l < h.enc_layers; l++) {
+        const EncLayer& e = m_->enc[l];
+        layernorm_q8(hs, N, d, e.ln1_w, e.ln1_b, h.ln_eps, xq, xd, nullptr, st_);
+        linear_q8(xq, xd, N, e.qkv, e.qkv_b, nullptr, qkv, 3 * d, EPI_STORE, st_);
+        to_f16(qkv, N, 3 * d, 3 * d, qkvh, 3 * d, st_);
+        attention(qkvh, 3 * d, qkvh + d, qkvh + 2 * d, 3 * d, d_kvs, d_kvl, N, h.enc_heads, h.enc_heads, d / h.enc_heads,
+                  scale, nullptr, xq, xd, st_);
+        linear_q8(xq, xd, N, e.o, e.o_b, hs, hs, d, EPI_RESID, st_);
+        layernorm_q8(hs, N, d, e.ln2_w, e.ln2_b, h.ln_eps, xq, xd, nullptr, st_);
+        linear_q8(xq, xd, N, e.up, e.up_b, nullptr, ff, F, EPI_GELU, st_);
+        quant_rows(ff, N, F, F, xq, xd, st_);
+        linear_q8(xq, xd, N, e.down, e.down_b, hs, hs, d, EPI_RESID, st_);
+    }
+    layernorm_q8(hs, N, d, m_->ln_post_w, m_->ln_post_b, h.ln_eps, xq, xd, enc_out_dbg, st_);
+    linear_q8(xq, xd, N, m_->proj1, m_->proj1_b, nullptr, ff, d, EPI_GELU, st_);
+    quant_rows(ff, N, d, d, xq, xd, st_);
+    float* emb = (float*)sc_.get(S_EMB, (size_t)N * H * sizeof(float));
+    linear_q8(xq, xd, N, m_->proj2, m_->proj2_b, nullptr, emb, H, EPI_STORE, st_);
+    QASR_HIP(hipGetLastError());
+}
+
+// ------------------------------------------------------------------------------------------ decoder
+void Session::decoder_layers(float* x, int rows, const int* d_pos, const int* d_slot, const int* d_kvs,
+                             const int* d_kvl) {
+    const qasr_hparams& h = m_->hp;
+    const int H = h.txt_h, F = h.txt_ffn, nh = h.txt_heads, nkv = h.txt_kv_heads, hd = h.head_dim;
+    const int QD = nh * hd, KD = nkv * hd;
+    const int kmax = std::max(std::max(H, QD), F);
+    int8_t* xq = (int8_t*)sc_.get(S_XQ, (size_t)rows * kmax);
+    float* xd = (float*)sc_.get(S_XD, (size_t)rows * (kmax / QK) * sizeof(float));
+    float* qkv = (float*)sc_.get(S_QKV, (size_t)rows * (QD + 2 * KD) * sizeof(float));
+    __half* qh = (__half*)sc_.get(S_QH, (size_t)rows * QD * sizeof(__half));
+    float* gu = (float*)sc_.get(S_GU, (size_t)rows * 2 * F * sizeof(float));
+    const float scale = 1.0f / sqrtf((float)hd);
+    const size_t layer_kv = (size_t)kv_slots_ * KD;
+    for (int l = 0; l < h.txt_layers; l++) {
+        const DecLayer& L = m_->dec[l];
+        __half* kc = kc_ + (size_t)l * layer_kv;
+        __half* vc = vc_ + (size_t)l * layer_kv;
+        rmsnorm_q8(x, rows, H, H, L.attn_norm, h.rms_eps, xq, xd, st_);
+        linear_q8(xq, xd, rows, L.qkv, nullptr, nullptr, qkv, QD + 2 * KD, EPI_STORE, st_);
+        qk_norm_rope(qkv, rows, nh, nkv, hd, d_pos, d_slot, L.q_norm, L.k_norm, rope_, h.rms_eps, qh, kc, vc, st_);
+        attention(qh, QD, kc, vc, KD, d_kvs, d_kvl, rows, nh, nkv, hd, scale, nullptr, xq, xd, st_);
+        linear_q8(xq, xd, rows, L.o, nullptr, x, x, H, EPI_RESID, st_);
+        rmsnorm_q8(x, rows, H, H, L.ffn_norm, h.rms_eps, xq, xd, st_);
+        linear_q8(xq, xd, rows, L.gu, nullptr, nullptr, gu, 2 * F, EPI_STORE, st_);
+        swiglu_q8(gu, rows, F, xq, xd, st_);
+        linear_q8(xq, xd, rows, L.down, nullptr, x, x, H, EPI_RESID, st_);
+    }
+    QASR_HIP(hipGetLastError());
+}
+
+void Session::lm_head_rows(const float* x, int rows, int ldx, float* logits) {
+    const qasr_hparams& h = m_->hp;
+    int8_t* xq = (int8_t*)sc_.get(S_XQ, (size_t)std::max(rows, 1) * std::max(h.txt_h, std::max(h.txt_ffn, h.txt_heads * h.head_dim)));
+    float* xd = (float*)sc_.get(S_XD, (size_t)std::max(rows, 1) * (std::max(h.txt_h, std::max(h.txt_ffn, h.txt_heads * h.head_dim)) / QK) * sizeof(float));
+    rmsnorm_q8(x, rows, h.txt_h, ldx, m_->out_norm, h.rms_eps, xq, xd, st_);
+    linear_q8(xq, xd, rows, m_->lm_head, nullptr, nullptr, logits, h.vocab, EPI_STORE, st_);
+}
+
+// ------------------------------------------------------------------------------------------ batch run
+void Session::run_batch(const float* dpcm, const std::vector<int64_t>& off, const std::vector<int64_t>& len,
+                        int max_new, int force_tps, std::vector<UttResult>& out, StageTimes* times) {
+    const qasr_hparams& h = m_->hp;
+    const int count = (int)len.size();
+    out.assign(count, UttResult());
+    if (count == 0) return;
+    for (int u = 0; u < count; u++) QASR_CHECK(len[u] > 0, QASR_E_INVALID, "empty utterance");
+    FrontEnd fe;
+    {
+        Timer t(st_, times ? &times->mel : nullptr);
+        front_end(dpcm, off, len, fe, nullptr);
+    }
+    {
+        Timer t(st_, times ? &times->encoder : nullptr);
+        encoder(fe, nullptr);
+    }
+    // prompts, KV slots, generation budgets
+    std::vector<int> n_prompt(count), base(count), row0(count), budget(count);
+    std::vector<int32_t> ids;
+    int64_t slots = 0;
+    for (int u = 0; u < count; u++) {
+        std::vector<int32_t> p = build_prompt(h, fe.n_tok[u], fe.tok_base[u]);
+        n_prompt[u] = (int)p.size();
+        row0[u] = (int)ids.size();
+        ids.insert(ids.end(), p.begin(), p.end());
+        const double secs = (double)len[u] / 16000.0;
+        if (force_tps > 0) budget[u] = std::max(1, (int)lround(force_tps * secs) + 1);
+        else budget[u] = max_new > 0 ? max_new : 64 + (int)ceil(32.0 * secs);
+        budget[u] = std::min(budget[u], n_ctx_ - n_prompt[u]);
+        QASR_CHECK(budget[u] > 0, QASR_E_CAPACITY, "utterance exceeds n_ctx");
+        base[u] = (int)slots;
+        slots += n_prompt[u] + budget[u];
+        out[u].n_audio = fe.n_tok[u];
+        out[u].n_prompt = n_prompt[u];
+    }
+    ensure_kv(slots);
+    const int T = (int)ids.size(), H = h.txt_h, V = h.vocab;
+    std::vector<int> pos(T), slot(T), kvs(T), kvl(T), last(count);
+    for (int u = 0; u < count; u++) {
+        for (int i = 0; i < n_prompt[u]; i++) {
+            const int r = row0[u] + i;
+            pos[r] = i;
+            slot[r] = base[u] + i;
+            kvs[r] = base[u];
+            kvl[r] = i + 1;
+        }
+        last[u] = row0[u] + n_prompt[u] - 1;
+    }
+    std::vector<int32_t> next(count);
+    {
+        Timer t(st_, times ? &times->prefill : nullptr);
+        int* d_ids = upload(S_IDS, ids);
+        int* d_pos = upload(S_POS, pos);
+        int* d_slot = upload(S_SLOT, slot);
+        int* d_kvs = upload(S_KVS, kvs);
+        int* d_kvl = upload(S_KVL, kvl);
+        float* x = (float*)sc_.get(S_X, (size_t)T * H * sizeof(float));
+        float* emb = (float*)sc_.get(S_EMB, (size_t)fe.total_tokens * H * sizeof(float));
+        embed_rows(d_ids, T, m_->tok_embd, emb, x, st_);
+        decoder_layers(x, T, d_pos, d_slot, d_kvs, d_kvl);
+        int* d_last = upload(S_LAST, last);
+        float* xn = (float*)sc_.get(S_XN, (size_t)count * H * sizeof(float));
+        k_gather_rows<<<(unsigned)cdiv64((int64_t)count * H, 256), 256, 0, st_>>>(x, d_last, count, H, xn);
+        float* logits = (float*)sc_.get(S_LOGITS, (size_t)count * V * sizeof(float));
+        lm_head_rows(xn, count, H, logits);
+        int* d_tok = (int*)sc_.get(S_TOK, count * sizeof(int));
+        argmax_rows(logits, count, V, d_tok, st_);
+        int32_t* hp = (int32_t*)pinned(count * sizeof(int32_t));
+        QASR_HIP(hipMemcpyAsync(hp, d_tok, count * sizeof(int32_t), hipMemcpyDeviceToHost, st_));
+        QASR_HIP(hipStreamSynchronize(st_));
+        memcpy(next.data(), hp, count * sizeof(int32_t));
+    }
+    // continuous-batching greedy decode
+    Timer td(st_, times ? &times->decode : nullptr);
+    std::vector<int> active;
+    std::vector<int> gen(count, 0);
+    auto accept = [&](int u, int32_t tok) -> bool {  // returns true if u continues
+        const bool eos = tok == h.tok_eos0 || tok == h.tok_eos1;
+        if (force_tps <= 0 && eos) return false;
+        out[u].tokens.push_back(tok);
+        gen[u]++;
+        return gen[u] < budget[u];
+    };
+    for (int u = 0; u < count; u++)
+        if (accept(u, next[u])) active.push_back(u);
+    std::vector<int32_t> sids;
+    std::vector<int> spos, sslot, skvs, skvl;
+    while (!active.empty()) {
+        const int A = (int)active.size();
+        sids.resize(A); spos.resize(A); sslot.resize(A); skvs.resize(A); skvl.resize(A);
+        for (int i = 0; i < A; i++) {
+            const int u = active[i];
+            const int p = n_prompt[u] + gen[u] - 1;
+            sids[i] = out[u].tokens.back();
+            spos[i] = p;
+            sslot[i] = base[u] + p;
+            skvs[i] = base[u];
+            skvl[i] = p + 1;
+        }
+        // one pinned upload of the five per-row tables
+        int32_t* hp = (int32_t*)pinned((size_t)A * 5 * sizeof(int32_t));
+        memcpy(hp, sids.data(), A * 4);
+        memcpy(hp + A, spos.data(), A * 4);
+        memcpy(hp + 2 * A, sslot.data(), A * 4);
+        memcpy(hp + 3 * A, skvs.data(), A * 4);
+        memcpy(hp + 4 * A, skvl.data(), A * 4);
+        int* dt = (int*)sc_.get(S_IDS, (size_t)A * 5 * sizeof(int));
+        QASR_HIP(hipMemcpyAsync(dt, hp, (size_t)A * 5 * sizeof(int32_t), hipMemcpyHostToDevice, st_));
+        float* x = (float*)sc_.get(S_X, (size_t)A * H * sizeof(float));
+        embed_rows(dt, A, m_->tok_embd, nullptr, x, st_);
+        decoder_layers(x, A, dt + A, dt + 2 * A, dt + 3 * A, dt + 4 * A);
+        float* logits = (float*)sc_.get(S_LOGITS, (size_t)A * V * sizeof(float));
+        lm_head_rows(x, A, H, logits);
+        int* d_tok = (int*)sc_.get(S_TOK, A * sizeof(int));
+        argmax_rows(logits, A, V, d_tok, st_);
+        QASR_HIP(hipStreamSynchronize(st_));  // the upload above has been consumed before the pinned reuse
+        int32_t* hr = (int32_t*)pinned((size_t)A * 5 * sizeof(int32_t));
+        QASR_HIP(hipMemcpyAsync(hr, d_tok, A * sizeof(int32_t), hipMemcpyDeviceToHost, st_));
+        QASR_HIP(hipStreamSynchronize(st_));
+        std::vector<int> still;
+        still.reserve(A);
+        for (int i = 0; i < A; i++)
+            if (accept(active[i], hr[i])) still.push_back(active[i]);
+        active.swap(still);
+    }
+    for (int u = 0; u < count; u++) {
+        UttResult& r = out[u];
+        r.raw = m_->tok.decode(r.tokens.data(), (int)r.tokens.size());
+        Tokenizer::parse(r.raw, r.language, r.text);
+    }
+}
+
+void Session::run_host(const std::vector<const float*>& pcm, const std::vector<int64_t>& len, int max_new,
+                       int force_tps, std::vector<UttResult>& out, StageTimes* times) {
+    std::vector<int64_t> off(len.size());
+    int64_t total = 0;
+    for (size_t i = 0; i < len.size(); i++) {
+        off[i] = total;
+        total += len[i];
+    }
+    float* d = (float*)sc_.get(S_PCM, (size_t)std::max<int64_t>(total, 1) * sizeof(float));
+    for (size_t i = 0; i < len.size(); i++)
+        QASR_HIP(hipMemcpyAsync(d + off[i], pcm[i], (size_t)len[i] * sizeof(float), hipMemcpyHostToDevice, st_));
+    run_batch(d, off, len, max_new, force_tps, out, times);
+}
+
+// ------------------------------------------------------------------------------------------ test stages
+void Session::mel_host(const float* pcm, int64_t n, std::vector<float>& mel, int& t_valid, int& t_pad) {
+    const qasr_hparams& h = m_->hp;
+    float* d = (float*)sc_.get(S_PCM, (size_t)n * sizeof(float));
+    QASR_HIP(hipMemcpyAsync(d, pcm, (size_t)n * sizeof(float), hipMemcpyHostToDevice, st_));
+    FrontEnd fe;
+    std::vector<int64_t> off = {0}, len = {n};
+    front_end(d, off, len, fe, nullptr);
+    mel_dims(n, t_valid, t_pad);
+    std::vector<float> chunked((size_t)h.n_mels * t_pad);
+    QASR_HIP(hipMemcpyAsync(chunked.data(), sc_.get(S_MELX, 0), chunked.size() * sizeof(float), hipMemcpyDeviceToHost, st_));
+    QASR_HIP(hipStreamSynchronize(st_));
+    mel.assign(chunked.size(), 0.f);
+    const int nch = t_pad / 100;
+    for (int c = 0; c < nch; c++)
+        for (int m = 0; m < h.n_mels; m++)
+            for (int t = 0; t < 100; t++) mel[(size_t)m * t_pad + c * 100 + t] = chunked[((size_t)c * h.n_mels + m) * 100 + t];
+}
+
+void Session::encode_host(const float* mel, int t_pad, int t_valid, std::vector<float>& emb, std::vector<float>* enc,
+                          int& n_tok) {
+    // bypass the log-mel stage: feed the given mel into the conv stack
+    const qasr_hparams& h = m_->hp;
+    const int nch = t_pad / 100, nm = h.n_mels, C = h.conv_ch, d = h.enc_d, F3 = m_->audio_F3();
+    std::vector<float> chunked((size_t)nch * nm * 100);
+    for (int c = 0; c < nch; c++)
+        for (int m = 0; m < nm; m++)
+            for (int t = 0; t < 100; t++) chunked[((size_t)c * nm + m) * 100 + t] = mel[(size_t)m * t_pad + c * 100 + t];
+    float* melx = (float*)sc_.get(S_MELX, chunked.size() * sizeof(float));
+    QASR_HIP(hipMemcpyAsync(melx, chunked.data(), chunked.size() * sizeof(float), hipMemcpyHostToDevice, st_));
+    FrontEnd fe;
+    fe.total_chunks = nch;
+    fe.n_tok = {audio_token_count(t_valid)};
+    fe.tok_base = {0};
+    fe.total_tokens = fe.n_tok[0];
+    std::vector<int> valid_idx;
+    for (int c = 0; c < nch; c++) {
+        const int v = post_cnn_len(std::max(0, std::min(100, t_valid - c * 100)));
+        for (int t = 0; t < v; t++) valid_idx.push_back(c * 13 + t);
+    }
+    const int H1 = (nm + 1) / 2, H2 = (H1 + 1) / 2;
+    __half* a1 = (__half*)sc_.get(S_A1, (size_t)nch * H1 * 50 * C * sizeof(__half));
+    __half* a2 = (__half*)sc_.get(S_A2, (size_t)nch * H2 * 25 * C * sizeof(__half));
+    float* a3 = (float*)sc_.get(S_A3, (size_t)nch * 13 * C * F3 * sizeof(float));
+    conv1_gelu(melx, nch, nm, m_->conv_w[0], m_->conv_b[0], C, a1, st_);
+    conv3x3_gelu(a1, nch, H1, 50, m_->conv_w[1], m_->conv_b[1], C, a2, 0, st_);
+    conv3x3_gelu(a2, nch, H2, 25, m_->conv_w[2], m_->conv_b[2], C, a3, 1, st_);
+    const int rows = nch * 13, K = C * F3;
+    int8_t* xq = (int8_t*)sc_.get(S_XQ, (size_t)rows * K);
+    float* xd = (float*)sc_.get(S_XD, (size_t)rows * (K / QK) * sizeof(float));
+    quant_rows(a3, rows, K, K, xq, xd, st_);
+    float* proj = (float*)sc_.get(S_PROJ, (size_t)rows * d * sizeof(float));
+    linear_q8(xq, xd, rows, m_->conv_out, nullptr, nullptr, proj, d, EPI_STORE, st_);
+    int* d_valid = upload(S_VALID, valid_idx);
+    float* hs = (float*)sc_.get(S_HS, (size_t)fe.total_tokens * d * sizeof(float));
+    add_posemb_gather(proj, nch, 13, d, m_->pos_emb, d_valid, fe.total_tokens, hs, st_);
+    float* encd = enc ? (float*)sc_.get(S_ENC, (size_t)fe.total_tokens * d * sizeof(float)) : nullptr;
+    encoder(fe, encd);
+    n_tok = fe.total_tokens;
+    emb.resize((size_t)n_tok * h.txt_h);
+    QASR_HIP(hipMemcpyAsync(emb.data(), sc_.get(S_EMB, 0), emb.size() * sizeof(float), hipMemcpyDeviceToHost, st_));
+    if (enc) {
+        enc->resize((size_t)n_tok * d);
+        QASR_HIP(hipMemcpyAsync(enc->data(), encd, enc->size() * sizeof(float), hipMemcpyDeviceToHost, st_));
+    }
+    QASR_HIP(hipStreamSynchronize(st_));
+}
+
+void Session::prefill_logits_host(const float* embeds, int n, std::vector<float>& logits) {
+    const qasr_hparams& h = m_->hp;
+    QASR_CHECK(n > 0 && n <= n_ctx_, QASR_E_CAPACITY, "prefill length exceeds n_ctx");
+    ensure_kv(n);
+    std::vector<int> pos(n), slot(n), kvs(n, 0), kvl(n);
+    for (int i = 0; i < n; i++) {
+        pos[i] = i;
+        slot[i] = i;
+        kvl[i] = i + 1;
+    }
+    float* x = (float*)sc_.get(S_X, (size_t)n * h.txt_h * sizeof(float));
+    QASR_HIP(hipMemcpyAsync(x, embeds, (size_t)n * h.txt_h * sizeof(float), hipMemcpyHostToDevice, st_));
+    int* d_pos = upload(S_POS, pos);
+    int* d_slot = upload(S_SLOT, slot);
+    int* d_kvs = upload(S_KVS, kvs);
+    int* d_kvl = upload(S_KVL, kvl);
+    decoder_layers(x, n, d_pos, d_slot, d_kvs, d_kvl);
+    float* lg = (float*)sc_.get(S_LOGITS, (size_t)n * h.vocab * sizeof(float));
+    lm_head_rows(x, n, h.txt_h, lg);
+    logits.resize((size_t)n * h.vocab);
+    QASR_HIP(hipMemcpyAsync(logits.data(), lg, logits.size() * sizeof(float), hipMemcpyDeviceToHost, st_));
+    QASR_HIP(hipStreamSynchronize(st_));
+}
+
+// prompt from the audio, then the forced continuation one token per step (the decode path, M = 1):
+// logits [n_forced + 1][V]
+void Session::forced_logits_host(const float* pcm, int64_t n, const int32_t* forced, int n_forced,
+                                 std::vector<float>& logits) {
+    const qasr_hparams& h = m_->hp;
+    const int H = h.txt_h, V = h.vocab;
+    float* d = (float*)sc_.get(S_PCM, (size_t)n * sizeof(float));
+    QASR_HIP(hipMemcpyAsync(d, pcm, (size_t)n * sizeof(float), hipMemcpyHostToDevice, st_));
+    FrontEnd fe;
+    std::vector<int64_t> off = {0}, len = {n};
+    front_end(d, off, len, fe, nullptr);
+    encoder(fe, nullptr);
+    std::vector<int32_t> ids = build_prompt(h, fe.n_tok[0], 0);
+    const int P = (int)ids.size();
+    QASR_CHECK(P + n_forced <= n_ctx_, QASR_E_CAPACITY, "forced sequence exceeds n_ctx");
+    ensure_kv(P + n_forced + 1);
+    logits.assign((size_t)(n_forced + 1) * V, 0.f);
+    std::vector<int> pos(P), slot(P), kvs(P, 0), kvl(P);
+    for (int i = 0; i < P; i++) {
+        pos[i] = i;
+        slot[i] = i;
+        kvl[i] = i + 1;
+    }
+    int* d_ids = upload(S_IDS, ids);
+    float* x = (float*)sc_.get(S_X, (size_t)std::max(P, 1) * H * sizeof(float));
+    float* emb = (float*)sc_.get(S_EMB, (size_t)fe.total_tokens * H * sizeof(float));
+    embed_rows(d_ids, P, m_->tok_embd, emb, x, st_);
+    decoder_layers(x, P, upload(S_POS, pos), upload(S_SLOT, slot), upload(S_KVS, kvs), upload(S_KVL, kvl));
+    float* lg = (float*)sc_.get(S_LOGITS, (size_t)V * sizeof(float));
+    lm_head_rows(x + (size_t)(P - 1) * H, 1, H, lg);
+    QASR_HIP(hipMemcpyAsync(logits.data(), lg, (size_t)V * sizeof(float), hipMemcpyDeviceToHost, st_));
+    for (int i = 0; i < n_forced; i++) {
+        const int p = P + i;
+        std::vector<int> one_id = {forced[i]}, one_pos = {p}, one_slot = {p}, one_kvs = {0}, one_kvl = {p + 1};
+        int* di = upload(S_IDS, one_id);
+        embed_rows(di, 1, m_->tok_embd, nullptr, x, st_);
+        decoder_layers(x, 1, upload(S_POS, one_pos), upload(S_SLOT, one_slot), upload(S_KVS, one_kvs),
+                       upload(S_KVL, one_kvl));
+        lm_head_rows(x, 1, H, lg);
+        QASR_HIP(hipMemcpyAsync(logits.data() + (size_t)(i + 1) * V, lg, (size_t)V * sizeof(float),
+                                hipMemcpyDeviceToHost, st_));
+    }
+    QASR_HIP(hipStreamSynchronize(st_));
+}
+
+}  // namespace qasr

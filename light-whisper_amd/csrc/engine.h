@@ -1,0 +1,95 @@
+// Session: the ASR pipeline for one device — log-mel → conv stack → windowed encoder → projector →
+// prompt splice → packed prefill → continuous-batching greedy decode with an f16 KV cache → detokenise.
+#pragma once
+#include <string>
+#include <vector>
+
+#include "common.h"
+#include "kernels_audio.h"
+#include "model.h"
+
+namespace qasr {
+
+// grow-only device scratch buffers
+struct Scratch {
+    struct Buf {
+        void* p = nullptr;
+        size_t cap = 0;
+    };
+    std::vector<Buf> bufs;
+    void* get(int slot, size_t bytes);
+    ~Scratch();
+};
+
+struct UttResult {
+    std::vector<int32_t> tokens;
+    std::string raw, text, language;
+    int n_audio = 0, n_prompt = 0;
+};
+
+struct StageTimes {
+    double mel = 0, encoder = 0, prefill = 0, decode = 0;
+};
+
+class Session {
+   public:
+    Session(Model* m, int n_ctx);
+    ~Session();
+    Session(const Session&) = delete;
+    Session& operator=(const Session&) = delete;
+
+    // audio on the device, packed; per-utterance offsets/lengths on the host
+    void run_batch(const float* dpcm, const std::vector<int64_t>& off, const std::vector<int64_t>& len,
+                   int max_new, int force_tps, std::vector<UttResult>& out, StageTimes* times);
+    // host audio convenience
+    void run_host(const std::vector<const float*>& pcm, const std::vector<int64_t>& len, int max_new, int force_tps,
+                  std::vector<UttResult>& out, StageTimes* times);
+
+    // stages (parity tests)
+    void mel_host(const float* pcm, int64_t n, std::vector<float>& mel, int& t_valid, int& t_pad);
+    void encode_host(const float* mel, int t_pad, int t_valid, std::vector<float>& emb, std::vector<float>* enc,
+                     int& n_tok);
+    void prefill_logits_host(const float* embeds, int n, std::vector<float>& logits);
+    void forced_logits_host(const float* pcm, int64_t n, const int32_t* forced, int n_forced,
+                            std::vector<float>& logits);
+
+    Model& model() { return *m_; }
+    int n_ctx() const { return n_ctx_; }
+    hipStream_t stream() const { return st_; }
+
+   private:
+    struct FrontEnd {
+        int total_chunks = 0, total_tokens = 0;
+        std::vector<int> n_tok, tok_base;
+    };
+    void front_end(const float* dpcm, const std::vector<int64_t>& off, const std::vector<int64_t>& len, FrontEnd& fe,
+                   float* enc_out_dbg);
+    void encoder(FrontEnd& fe, float* enc_out_dbg);
+    void decoder_layers(float* x, int rows, const int* d_pos, const int* d_slot, const int* d_kvs, const int* d_kvl);
+    void ensure_kv(int64_t slots);
+    void lm_head_rows(const float* x, int rows, int ldx, float* logits);
+    template <class T>
+    T* upload(int slot, const std::vector<T>& v);
+
+    Model* m_;
+    int n_ctx_;
+    hipStream_t st_ = nullptr;
+    Scratch sc_;
+    __half* kc_ = nullptr;
+    __half* vc_ = nullptr;
+    int64_t kv_slots_ = 0;
+    float* rope_ = nullptr;
+    int rope_n_ = 0;
+    // pinned host staging for per-step uploads / downloads
+    void* pin_ = nullptr;
+    size_t pin_cap_ = 0;
+    void* pinned(size_t bytes);
+};
+
+// the chat prompt of one utterance (processing_qwen3_asr.py:534-553, empty system prompt); audio
+// placeholders are returned as -(audio_row + 1)
+std::vector<int32_t> build_prompt(const qasr_hparams& hp, int n_audio, int audio_row0);
+int audio_token_count(int t_valid);
+void mel_dims(int64_t n, int& t_valid, int& t_pad);
+
+}  // namespace qasr

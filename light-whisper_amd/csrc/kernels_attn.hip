@@ -141,7 +141,7 @@ __global__ __launch_bounds__(256) void k_attention(const __half* __restrict__ Q,
             const int qv2 = amax == 0.f ? 0 : (int)roundf(out[j] / d);
             oq[(size_t)r * D + h * HD + lane * PD + j] = (int8_t)qv2;
         }
-        if ((lane & (32 / PD - 1)) == 0) od[(size_t)r * (D / 32) + (h * HD + lane * PD) / 32] = __half2float(__float2half(d));
+        if ((lane & (32 / PD - 1)) == 0) od[(size_t)r * (D / 32) + (h * HD + lane * PD) / 32] = __half2float(f2h(d));
     }
 }
 

@@ -1,0 +1,564 @@
+// Audio front ends for gfx950:
+//   * Qwen3-ASR log-mel (feature_extraction_qwen3_asr.py:104-127 + the padding rules of __call__:189-228):
+//     windowed 400-point DFT per frame against an L2-resident basis (16 frames per workgroup share every
+//     basis load), |X|², Slaney mel, log10, per-utterance max via ordered-uint atomics, then clamp/normalise
+//     into the per-chunk conv1 layout.
+//   * encoder conv stack (modeling_qwen3_asr.py:344-346,407-409): conv1 direct (Cin = 1), conv2/conv3 as
+//     channel-last implicit GEMMs on v_mfma_f32_16x16x32_f16 (f16 operands — the ggml im2col convention —
+//     f32 accumulation) with fused bias + GELU.
+//   * FireRedVAD (firered_vad.py:87-111): Kaldi fbank with a per-wave LDS radix-2 FFT (512 points),
+//     DFSMN dense layers (f32), FSMN memory blocks and the sigmoid head.
+#include <math.h>
+
+#include "kernels_audio.h"
+
+namespace qasr {
+
+// ================================================================================================ tables
+static double slaney_h2m(double f) {
+    if (f >= 1000.0) return 15.0 + log(f / 1000.0) * (27.0 / log(6.4));
+    return 3.0 * f / 200.0;
+}
+static double slaney_m2h(double m) {
+    if (m >= 15.0) return 1000.0 * exp((log(6.4) / 27.0) * (m - 15.0));
+    return 200.0 * m / 3.0;
+}
+
+void mel_filter_table(int n_mels, float* out) {
+    std::vector<double> ff((size_t)n_mels + 2);
+    const double mmin = slaney_h2m(0.0), mmax = slaney_h2m(8000.0);
+    for (int i = 0; i < n_mels + 2; i++) {
+        double mel = mmin + (mmax - mmin) * (double)i / (double)(n_mels + 1);
+        if (i == n_mels + 1) mel = mmax;
+        ff[(size_t)i] = slaney_m2h(mel);
+    }
+    for (int k = 0; k < 201; k++) {
+        double fk = 8000.0 * (double)k / 200.0;
+        for (int m = 0; m < n_mels; m++) {
+            double down = -(ff[m] - fk) / (ff[m + 1] - ff[m]);
+            double up = (ff[m + 2] - fk) / (ff[m + 2] - ff[m + 1]);
+            double v = down < up ? down : up;
+            if (v < 0.0) v = 0.0;
+            v *= 2.0 / (ff[m + 2] - ff[m]);
+            out[k * n_mels + m] = (float)v;
+        }
+    }
+}
+
+void dft_basis_table(std::vector<float>& out) {
+    out.assign((size_t)400 * 402, 0.f);
+    for (int i = 0; i < 400; i++) {
+        const double w = 0.5 - 0.5 * cos(2.0 * M_PI * i / 400.0);  // periodic Hann (torch.hann_window)
+        for (int k = 0; k < 201; k++) {
+            const double a = -2.0 * M_PI * (double)((k * i) % 400) / 400.0;
+            out[(size_t)i * 402 + 2 * k] = (float)(w * cos(a));
+            out[(size_t)i * 402 + 2 * k + 1] = (float)(w * sin(a));
+        }
+    }
+}
+
+static double kaldi_mel(double f) { return 1127.0 * log(1.0 + f / 700.0); }
+
+void kaldi_mel_banks(float* banks) {
+    const double fft_bin_width = 16000.0 / 512;
+    const double mel_low = kaldi_mel(20.0), mel_high = kaldi_mel(8000.0);
+    const double delta = (mel_high - mel_low) / 81;
+    for (int b = 0; b < 80; b++) {
+        double left = mel_low + b * delta, center = left + delta, right = center + delta;
+        for (int i = 0; i < 256; i++) {
+            double mel = kaldi_mel(fft_bin_width * i);
+            float w = 0.f;
+            if (mel > left && mel < right)
+                w = (float)(mel <= center ? (mel - left) / (center - left) : (right - mel) / (right - center));
+            banks[b * 256 + i] = w;
+        }
+    }
+}
+
+void povey_window(float* out) {
+    for (int i = 0; i < 400; i++) out[i] = (float)pow(0.5 - 0.5 * cos(2.0 * M_PI * i / 399.0), 0.85);
+}
+
+// ================================================================================================ log-mel
+__device__ __forceinline__ unsigned f2ord(float f) {
+    unsigned u = __float_as_uint(f);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float ord2f(unsigned u) {
+    return __uint_as_float((u & 0x80000000u) ? (u & 0x7fffffffu) : ~u);
+}
+
+constexpr int MFR = 16;  // frames per workgroup
+
+__global__ __launch_bounds__(256) void k_mel_frames(const float* __restrict__ pcm, const MelUtt* __restrict__ utts,
+                                                    const int2* __restrict__ work, int n_mels,
+                                                    const float* __restrict__ basis, const float* __restrict__ filt,
+                                                    float* __restrict__ lm, unsigned* __restrict__ umax) {
+    __shared__ float xs[MFR][400];
+    __shared__ float ps[MFR][201];
+    const int2 wk = work[blockIdx.x];
+    const MelUtt U = utts[wk.x];
+    const int t0 = wk.y;
+    const int nf = min(MFR, U.t_comp - t0);
+    const float* x = pcm + U.pcm_off;
+    for (int idx = threadIdx.x; idx < MFR * 400; idx += 256) {
+        const int f = idx / 400, i = idx % 400;
+        float v = 0.f;
+        if (f < nf) {
+            int64_t sidx = (int64_t)(t0 + f) * 160 - 200 + i;
+            if (sidx < 0) sidx = -sidx;                         // reflect (center=True)
+            if (sidx >= U.P) sidx = 2 * U.P - 2 - sidx;
+            v = sidx < U.n ? x[sidx] : 0.f;                     // beyond the clip: zero padding
+        }
+        xs[f][i] = v;
+    }
+    __syncthreads();
+    const int k = threadIdx.x;
+    if (k < 201) {
+        float re[MFR], im[MFR];
+#pragma unroll
+        for (int f = 0; f < MFR; f++) re[f] = im[f] = 0.f;
+        const float2* b2 = (const float2*)basis;
+        for (int i = 0; i < 400; i++) {
+            const float2 b = b2[i * 201 + k];
+#pragma unroll
+            for (int f = 0; f < MFR; f++) {
+                const float xv = xs[f][i];
+                re[f] += xv * b.x;
+                im[f] += xv * b.y;
+            }
+        }
+#pragma unroll
+        for (int f = 0; f < MFR; f++) ps[f][k] = re[f] * re[f] + im[f] * im[f];
+    }
+    __syncthreads();
+    for (int m = threadIdx.x; m < n_mels; m += 256) {
+        float lmax = -INFINITY;
+        for (int f = 0; f < nf; f++) {
+            float acc = 0.f;
+            for (int kk = 0; kk < 201; kk++) acc += filt[kk * n_mels + m] * ps[f][kk];
+            const float l = log10f(fmaxf(acc, 1e-10f));
+            lm[(size_t)(U.frame0 + t0 + f) * n_mels + m] = l;
+            lmax = fmaxf(lmax, l);
+        }
+        if (nf > 0) atomicMax(umax + wk.x, f2ord(lmax));
+    }
+}
+
+void mel_frames(const float* pcm, const MelUtt* utts, const int2* work, int n_work, int n_mels, const float* basis,
+                const float* filt, float* lm, unsigned* umax, hipStream_t s) {
+    if (n_work <= 0) return;
+    k_mel_frames<<<n_work, 256, 0, s>>>(pcm, utts, work, n_mels, basis, filt, lm, umax);
+}
+
+__global__ void k_mel_normalize(const MelUtt* __restrict__ utts, int total_chunks, const int* __restrict__ chunk_utt,
+                                int n_mels, const float* __restrict__ lm, const unsigned* __restrict__ umax,
+                                float* __restrict__ x) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)total_chunks * n_mels * 100) return;
+    const int t = (int)(i % 100);
+    const int m = (int)((i / 100) % n_mels);
+    const int c = (int)(i / (100 * n_mels));
+    const int u = chunk_utt[c];
+    const MelUtt U = utts[u];
+    float gmax = ord2f(umax[u]);
+    if (U.t_all > U.t_comp) gmax = fmaxf(gmax, -10.f);  // pure zero-padding frames: log10(1e-10)
+    const int frame = (c - U.chunk0) * 100 + t;
+    float v = 0.f;                                      // np.pad of the mel axis
+    if (frame < U.t_all) {
+        float l = frame < U.t_comp ? lm[(size_t)(U.frame0 + frame) * n_mels + m] : -10.f;
+        l = fmaxf(l, gmax - 8.f);
+        v = (l + 4.f) / 4.f;
+    }
+    x[i] = v;
+}
+
+void mel_normalize(const MelUtt* utts, int n_utts, int total_chunks, const int* chunk_utt, int n_mels, const float* lm,
+                   const unsigned* umax, float* x, hipStream_t s) {
+    (void)n_utts;
+    const int64_t n = (int64_t)total_chunks * n_mels * 100;
+    if (n <= 0) return;
+    k_mel_normalize<<<(unsigned)cdiv64(n, 256), 256, 0, s>>>(utts, total_chunks, chunk_utt, n_mels, lm, umax, x);
+}
+
+// ================================================================================================ conv stack
+__device__ __forceinline__ float gelu_f(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
+
+__global__ void k_conv1_gelu(const float* __restrict__ x, int n_chunks, int H0, const __half* __restrict__ w,
+                             const float* __restrict__ b, int C, __half* __restrict__ y) {
+    const int W0 = 100, H1 = (H0 + 1) / 2, W1 = 50;
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)n_chunks * H1 * W1 * C) return;
+    const int co = (int)(i % C);
+    const int ox = (int)((i / C) % W1);
+    const int oy = (int)((i / ((int64_t)C * W1)) % H1);
+    const int ch = (int)(i / ((int64_t)C * W1 * H1));
+    const float* xc = x + (size_t)ch * H0 * W0;
+    float acc = 0.f;
+#pragma unroll
+    for (int ky = 0; ky < 3; ky++) {
+        const int iy = 2 * oy - 1 + ky;
+        if (iy < 0 || iy >= H0) continue;
+#pragma unroll
+        for (int kx = 0; kx < 3; kx++) {
+            const int ix = 2 * ox - 1 + kx;
+            if (ix < 0 || ix >= W0) continue;
+            acc += __half2float(w[co * 9 + ky * 3 + kx]) * __half2float(f2h(xc[iy * W0 + ix]));
+        }
+    }
+    y[i] = f2h(gelu_f(acc + b[co]));
+}
+
+void conv1_gelu(const float* x, int n_chunks, int n_mels, const __half* w, const float* b, int C, __half* y,
+                hipStream_t s) {
+    const int64_t n = (int64_t)n_chunks * ((n_mels + 1) / 2) * 50 * C;
+    if (n <= 0) return;
+    k_conv1_gelu<<<(unsigned)cdiv64(n, 256), 256, 0, s>>>(x, n_chunks, n_mels, w, b, C, y);
+}
+
+typedef _Float16 v8h __attribute__((ext_vector_type(8)));
+typedef float v4f __attribute__((ext_vector_type(4)));
+constexpr int CT = 64;     // output tile (positions × channels)
+constexpr int CLD = 40;    // LDS row stride in halves (80 B)
+
+__global__ __launch_bounds__(256) void k_conv3x3_gelu(const __half* __restrict__ in, int n_chunks, int Hi, int Wi,
+                                                      const __half* __restrict__ w, const float* __restrict__ bias,
+                                                      int C, void* __restrict__ out, int out_mode) {
+    __shared__ __attribute__((aligned(16))) _Float16 As[CT * CLD];
+    __shared__ __attribute__((aligned(16))) _Float16 Bs[CT * CLD];
+    const int Ho = (Hi + 1) / 2, Wo = (Wi + 1) / 2;
+    const int M = n_chunks * Ho * Wo;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wr = wave >> 1, wc = wave & 1;
+    const int n0 = blockIdx.x * CT, m0 = blockIdx.y * CT;
+    // staging: row t>>2, 8 halves at (t&3)*8
+    const int srow = tid >> 2, sseg = (tid & 3) * 8;
+    const int am = m0 + srow;
+    int a_ch = 0, a_oy = 0, a_ox = 0;
+    const bool a_ok = am < M;
+    if (a_ok) {
+        a_ch = am / (Ho * Wo);
+        const int rem = am % (Ho * Wo);
+        a_oy = rem / Wo;
+        a_ox = rem % Wo;
+    }
+    const int bn = n0 + srow;
+    const bool b_ok = bn < C;
+    const int cblk = C / 32;
+    const int steps = 9 * cblk;
+    v4f acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; i++)
+#pragma unroll
+        for (int j = 0; j < 2; j++) acc[i][j] = (v4f){0.f, 0.f, 0.f, 0.f};
+
+    int4 ra, rb;
+    auto gload = [&](int st) {
+        const int tap = st / cblk, ci0 = (st % cblk) * 32 + sseg;
+        const int ky = tap / 3, kx = tap % 3;
+        const int iy = 2 * a_oy - 1 + ky, ix = 2 * a_ox - 1 + kx;
+        ra = (a_ok && iy >= 0 && iy < Hi && ix >= 0 && ix < Wi)
+                 ? *(const int4*)(in + (((size_t)a_ch * Hi + iy) * Wi + ix) * C + ci0)
+                 : make_int4(0, 0, 0, 0);
+        rb = b_ok ? *(const int4*)(w + ((size_t)bn * 9 + tap) * C + ci0) : make_int4(0, 0, 0, 0);
+    };
+    auto lstore = [&]() {
+        *(int4*)(As + srow * CLD + sseg) = ra;
+        *(int4*)(Bs + srow * CLD + sseg) = rb;
+    };
+    const int fr = lane & 15, fk = 8 * (lane >> 4);
+    gload(0);
+    lstore();
+    __syncthreads();
+    for (int st = 0; st < steps; st++) {
+        const bool more = st + 1 < steps;
+        if (more) gload(st + 1);
+        v8h a[2], b[2];
+#pragma unroll
+        for (int i = 0; i < 2; i++) a[i] = *(const v8h*)(As + (wr * 32 + i * 16 + fr) * CLD + fk);
+#pragma unroll
+        for (int j = 0; j < 2; j++) b[j] = *(const v8h*)(Bs + (wc * 32 + j * 16 + fr) * CLD + fk);
+#pragma unroll
+        for (int i = 0; i < 2; i++)
+#pragma unroll
+            for (int j = 0; j < 2; j++) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[i], b[j], acc[i][j], 0, 0, 0);
+        __syncthreads();
+        if (more) {
+            lstore();
+            __syncthreads();
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 2; i++) {
+#pragma unroll
+        for (int j = 0; j < 2; j++) {
+            const int col = n0 + wc * 32 + j * 16 + fr;
+            if (col >= C) continue;
+            const float bv = bias[col];
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const int row = m0 + wr * 32 + i * 16 + 4 * (lane >> 4) + r;
+                if (row >= M) continue;
+                const float v = gelu_f(acc[i][j][r] + bv);
+                if (out_mode == 0) {
+                    ((__half*)out)[(size_t)row * C + col] = f2h(v);
+                } else {
+                    const int ch = row / (Ho * Wo), rem = row % (Ho * Wo), oy = rem / Wo, ox = rem % Wo;
+                    ((float*)out)[(((size_t)ch * Wo + ox) * C + col) * Ho + oy] = v;
+                }
+            }
+        }
+    }
+}
+
+void conv3x3_gelu(const __half* in, int n_chunks, int Hi, int Wi, const __half* w, const float* b, int C, void* out,
+                  int out_mode, hipStream_t s) {
+    const int M = n_chunks * ((Hi + 1) / 2) * ((Wi + 1) / 2);
+    if (M <= 0) return;
+    QASR_CHECK(C % 32 == 0, QASR_E_INVALID, "conv channels must be a multiple of 32");
+    dim3 grid(cdiv(C, CT), cdiv(M, CT));
+    k_conv3x3_gelu<<<grid, 256, 0, s>>>(in, n_chunks, Hi, Wi, w, b, C, out, out_mode);
+}
+
+__global__ void k_reorder_conv(const __half* __restrict__ src, int cout, int cin, __half* __restrict__ dst) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)cout * cin * 9) return;
+    const int ci = (int)(i % cin), k = (int)((i / cin) % 9), co = (int)(i / ((int64_t)cin * 9));
+    dst[i] = src[((size_t)co * cin + ci) * 9 + k];
+}
+
+void reorder_conv_weight(const __half* src, int cout, int cin, __half* dst, hipStream_t s) {
+    const int64_t n = (int64_t)cout * cin * 9;
+    k_reorder_conv<<<(unsigned)cdiv64(n, 256), 256, 0, s>>>(src, cout, cin, dst);
+}
+
+// ================================================================================================ FireRedVAD
+// One wave per 400-sample frame: DC removal, pre-emphasis 0.97, Povey window, zero-pad to 512, in-LDS
+// radix-2 FFT (bit-reversed load, 9 butterfly stages, 4 butterflies per lane), power, 80 Kaldi mel bins,
+// natural log floored at FLT_EPSILON (kaldi-native-fbank 1.22.3 defaults, firered_vad.py:65-72).
+__global__ __launch_bounds__(256) void k_kaldi_fbank(const float* __restrict__ pcm, int T,
+                                                     const float* __restrict__ win, const float* __restrict__ banks,
+                                                     float* __restrict__ feats) {
+    __shared__ float sre[4][512];
+    __shared__ float sim[4][512];
+    __shared__ float tw[2][256];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    for (int i = threadIdx.x; i < 256; i += 256) {
+        float sv, cv;
+        sincospif((float)i / 256.0f, &sv, &cv);   // exp(-2πi·i/512) = cos(π i/256) - i sin(π i/256)
+        tw[0][i] = cv;
+        tw[1][i] = -sv;
+    }
+    __syncthreads();
+    const int t = blockIdx.x * 4 + w;
+    if (t >= T) return;
+    float* re = sre[w];
+    float* im = sim[w];
+    const float* x = pcm + (size_t)t * 160;
+    float v[7];
+    float sum = 0.f;
+#pragma unroll
+    for (int j = 0; j < 7; j++) {
+        const int i = lane + 64 * j;
+        v[j] = i < 400 ? x[i] : 0.f;
+        sum += v[j];
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
+    const float mean = sum / 400.f;
+#pragma unroll
+    for (int j = 0; j < 7; j++) {
+        const int i = lane + 64 * j;
+        if (i < 400) re[i] = v[j] - mean;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    float y[7];
+#pragma unroll
+    for (int j = 0; j < 7; j++) {
+        const int i = lane + 64 * j;
+        if (i < 400) {
+            const float cur = re[i];
+            const float prev = i > 0 ? re[i - 1] : cur;
+            y[j] = (cur - 0.97f * prev) * win[i];
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        const int i = lane + 64 * j;
+        const int r = (int)(__brev((unsigned)i) >> 23);   // 9-bit reversal
+        re[r] = (j < 7 && i < 400) ? y[j] : 0.f;
+        im[r] = 0.f;
+    }
+    for (int half = 1; half < 512; half <<= 1) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const int tstride = 256 / half;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int bf = lane + 64 * j;              // butterfly 0..255
+            const int grp = bf / half, k = bf % half;
+            const int i0 = grp * 2 * half + k, i1 = i0 + half;
+            const float wr = tw[0][k * tstride], wi = tw[1][k * tstride];
+            const float xr = re[i1] * wr - im[i1] * wi;
+            const float xi = re[i1] * wi + im[i1] * wr;
+            const float ur = re[i0], ui = im[i0];
+            re[i0] = ur + xr; im[i0] = ui + xi;
+            re[i1] = ur - xr; im[i1] = ui - xi;
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    float pw[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const int i = lane + 64 * j;
+        pw[j] = re[i] * re[i] + im[i] * im[i];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int j = 0; j < 4; j++) re[lane + 64 * j] = pw[j];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (int m = lane; m < 80; m += 64) {
+        float e = 0.f;
+        const float* bk = banks + m * 256;
+        for (int i = 0; i < 256; i++) e += bk[i] * re[i];
+        feats[(size_t)t * 80 + m] = logf(fmaxf(e, 1.1920928955078125e-07f));
+    }
+}
+
+void kaldi_fbank(const float* pcm, int64_t n, int T, const float* window, const float* banks, float* feats,
+                 hipStream_t s) {
+    (void)n;
+    if (T <= 0) return;
+    k_kaldi_fbank<<<cdiv(T, 4), 256, 0, s>>>(pcm, T, window, banks, feats);
+}
+
+__global__ void k_cmvn(const float* __restrict__ x, int T, const float* __restrict__ mean,
+                       const float* __restrict__ istd, float* __restrict__ y) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)T * 80) return;
+    const int c = (int)(i % 80);
+    y[i] = (x[i] - mean[c]) * istd[c];
+}
+
+void cmvn(const float* x, int T, const float* mean, const float* istd, float* y, hipStream_t s) {
+    const int64_t n = (int64_t)T * 80;
+    if (n <= 0) return;
+    k_cmvn<<<(unsigned)cdiv64(n, 256), 256, 0, s>>>(x, T, mean, istd, y);
+}
+
+// y[T][N] = act(x[T][K]·W[K][N] + b): 64×64 tile, 16-deep K slabs in LDS, 4×4 outputs per thread
+__global__ __launch_bounds__(256) void k_dense_f32(const float* __restrict__ x, int T, int K,
+                                                   const float* __restrict__ W, const float* __restrict__ b, int N,
+                                                   int relu, float* __restrict__ y) {
+    __shared__ float xs[16][65];
+    __shared__ float ws[16][64];
+    const int tid = threadIdx.x;
+    const int t0 = blockIdx.y * 64, n0 = blockIdx.x * 64;
+    const int tr = (tid / 16) * 4, tc = (tid % 16) * 4;
+    float acc[4][4] = {};
+    for (int k0 = 0; k0 < K; k0 += 16) {
+        for (int i = tid; i < 16 * 64; i += 256) {
+            const int r = i / 16, kk = i % 16;   // x tile: 64 rows × 16 k
+            const int tt = t0 + r, k = k0 + kk;
+            xs[kk][r] = (tt < T && k < K) ? x[(size_t)tt * K + k] : 0.f;
+            const int kr = i / 64, nn = i % 64;  // W tile: 16 k × 64 n
+            ws[kr][nn] = (k0 + kr < K && n0 + nn < N) ? W[(size_t)(k0 + kr) * N + n0 + nn] : 0.f;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int kk = 0; kk < 16; kk++) {
+            float a[4], bb[4];
+#pragma unroll
+            for (int i = 0; i < 4; i++) a[i] = xs[kk][tr + i];
+#pragma unroll
+            for (int j = 0; j < 4; j++) bb[j] = ws[kk][tc + j];
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+#pragma unroll
+                for (int j = 0; j < 4; j++) acc[i][j] += a[i] * bb[j];
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const int tt = t0 + tr + i;
+        if (tt >= T) continue;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int nn = n0 + tc + j;
+            if (nn >= N) continue;
+            float v = acc[i][j] + (b ? b[nn] : 0.f);
+            if (relu) v = fmaxf(v, 0.f);
+            y[(size_t)tt * N + nn] = v;
+        }
+    }
+}
+
+void dense_f32(const float* x, int T, int K, const float* W, const float* b, int N, int relu, float* y, hipStream_t s) {
+    if (T <= 0) return;
+    dim3 grid(cdiv(N, 64), cdiv(T, 64));
+    k_dense_f32<<<grid, 256, 0, s>>>(x, T, K, W, b, N, relu, y);
+}
+
+__global__ void k_fsmn(const float* __restrict__ x, int T, const float* __restrict__ lb, const float* __restrict__ la,
+                       const float* __restrict__ skip, float* __restrict__ y) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)T * 128) return;
+    const int c = (int)(i % 128);
+    const int t = (int)(i / 128);
+    float ab = 0.f, aa = 0.f;
+#pragma unroll
+    for (int j = 0; j < 20; j++) {
+        const int k = t + j - 19;
+        if (k >= 0) ab += lb[c * 20 + j] * x[(size_t)k * 128 + c];
+    }
+    if (t < T - 1) {
+#pragma unroll
+        for (int j = 0; j < 20; j++) {
+            const int k = t + 1 + j;
+            if (k < T) aa += la[c * 20 + j] * x[(size_t)k * 128 + c];
+        }
+    }
+    float v = x[i] + ab;
+    v = v + aa;
+    if (skip) v += skip[i];
+    y[i] = v;
+}
+
+void fsmn_block(const float* x, int T, const float* lb, const float* la, const float* skip, float* y, hipStream_t s) {
+    const int64_t n = (int64_t)T * 128;
+    if (n <= 0) return;
+    k_fsmn<<<(unsigned)cdiv64(n, 256), 256, 0, s>>>(x, T, lb, la, skip, y);
+}
+
+__global__ __launch_bounds__(256) void k_vad_head(const float* __restrict__ h, int T, const float* __restrict__ wo,
+                                                  float bo, float* __restrict__ probs) {
+    const int lane = threadIdx.x & 63;
+    const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (t >= T) return;
+    float acc = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; j++) acc += h[(size_t)t * 256 + lane + 64 * j] * wo[lane + 64 * j];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+    if (lane == 0) probs[t] = 1.f / (1.f + expf(-(acc + bo)));
+}
+
+void vad_head(const float* h, int T, const float* wo, float bo, float* probs, hipStream_t s) {
+    if (T <= 0) return;
+    k_vad_head<<<cdiv(T, 4), 256, 0, s>>>(h, T, wo, bo, probs);
+}
+
+}  // namespace qasr

@@ -29,7 +29,7 @@ __device__ __forceinline__ void quant32(const float* v, int8_t* q, float* dout) 
     int4* qo = (int4*)q;
     qo[0] = make_int4(packed[0], packed[1], packed[2], packed[3]);
     qo[1] = make_int4(packed[4], packed[5], packed[6], packed[7]);
-    *dout = __half2float(__float2half(d));
+    *dout = __half2float(f2h(d));
 }
 
 __device__ __forceinline__ void load32(const float* p, float* v) {
@@ -189,7 +189,7 @@ __global__ __launch_bounds__(256) void k_qk_norm_rope(const float* __restrict__ 
     if (h >= nh + nkv) {  // v head: copy to cache
         __half* dst = vc + (size_t)slot[r] * kvd + (h - nh - nkv) * HD;
 #pragma unroll
-        for (int j = 0; j < DPL; j++) dst[lane * DPL + j] = __float2half(v[j]);
+        for (int j = 0; j < DPL; j++) dst[lane * DPL + j] = f2h(v[j]);
         return;
     }
     const float* nw = h < nh ? qnw : knw;
@@ -214,11 +214,11 @@ __global__ __launch_bounds__(256) void k_qk_norm_rope(const float* __restrict__ 
     if (h < nh) {
         __half* dst = qout + (size_t)r * nh * HD + h * HD;
 #pragma unroll
-        for (int j = 0; j < DPL; j++) dst[lane * DPL + j] = __float2half(o[j]);
+        for (int j = 0; j < DPL; j++) dst[lane * DPL + j] = f2h(o[j]);
     } else {
         __half* dst = kc + (size_t)slot[r] * kvd + (h - nh) * HD;
 #pragma unroll
-        for (int j = 0; j < DPL; j++) dst[lane * DPL + j] = __float2half(o[j]);
+        for (int j = 0; j < DPL; j++) dst[lane * DPL + j] = f2h(o[j]);
     }
 }
 
@@ -240,7 +240,7 @@ __global__ void k_to_f16(const float* __restrict__ x, int rows, int cols, int ld
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= (int64_t)rows * cols) return;
     const int r = (int)(i / cols), c = (int)(i % cols);
-    y[(size_t)r * ldy + c] = __float2half(x[(size_t)r * ldx + c]);
+    y[(size_t)r * ldy + c] = f2h(x[(size_t)r * ldx + c]);
 }
 
 void to_f16(const float* x, int rows, int cols, int ldx, __half* y, int ldy, hipStream_t s) {

@@ -45,7 +45,7 @@ __device__ __forceinline__ void quant_block32(const float* v, int8_t* q, float* 
     int4* qo = (int4*)q;
     qo[0] = make_int4(packed[0], packed[1], packed[2], packed[3]);
     qo[1] = make_int4(packed[4], packed[5], packed[6], packed[7]);
-    *dout = __half2float(__float2half(d));
+    *dout = __half2float(f2h(d));
 }
 
 // ------------------------------------------------------------------------------------------------ repack / synth
@@ -76,7 +76,7 @@ __global__ void k_synth_q8(uint64_t base, int64_t nblk, float dbase, int8_t* __r
     if (b >= nblk) return;
     uint64_t h = smix(base + (uint64_t)b);
     float d = dbase * (0.5f + unit_from(h));
-    sc[b] = __float2half(d);
+    sc[b] = f2h(d);
     int32_t w[8];
 #pragma unroll
     for (int g = 0; g < 4; g++) {
@@ -116,7 +116,7 @@ void synth_f32(uint64_t base, int64_t n, float center, float scale, float* out, 
 __global__ void k_synth_f16(uint64_t base, int64_t n, float scale, __half* out) {
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    out[i] = __float2half(scale * (2.f * unit_from(smix(base + (uint64_t)i)) - 1.f));
+    out[i] = f2h(scale * (2.f * unit_from(smix(base + (uint64_t)i)) - 1.f));
 }
 void synth_f16(uint64_t base, int64_t n, float scale, __half* out, hipStream_t s) {
     if (n <= 0) return;

@@ -1,0 +1,470 @@
+// Model construction: HBM layout, GGUF loading (tensor-name table validated by shape) and the on-device
+// synthetic weight generator (same values as oracle/qasr_oracle.c orc_model_synth).
+#include "model.h"
+
+#include <math.h>
+#include <string.h>
+
+#include "gguf.h"
+#include "kernels.h"
+#include "kernels_audio.h"
+
+namespace qasr {
+
+void* DevAlloc::alloc(size_t n) {
+    void* p = nullptr;
+    n = (n + 255) / 256 * 256;
+    QASR_HIP(hipMalloc(&p, n));
+    ptrs.push_back(p);
+    bytes += n;
+    return p;
+}
+DevAlloc::~DevAlloc() {
+    for (void* p : ptrs) (void)hipFree(p);
+}
+
+static void set_special_defaults(qasr_hparams* hp) {
+    hp->tok_im_start = 151644;
+    hp->tok_im_end = 151645;
+    hp->tok_system = 8948;
+    hp->tok_user = 872;
+    hp->tok_assistant = 77091;
+    hp->tok_newline = 198;
+    hp->tok_audio_start = 151669;
+    hp->tok_audio_end = 151670;
+    hp->tok_audio_pad = 151676;
+    hp->tok_eos0 = 151645;
+    hp->tok_eos1 = 151643;
+    hp->tok_asr_text = 151704;
+}
+
+// Dimensions of the two pinned checkpoints (hf_cache_utils.py:11-26).
+void default_hparams(const char* arch, qasr_hparams* hp) {
+    memset(hp, 0, sizeof(*hp));
+    const std::string a = arch ? arch : "qwen3-asr-1.7b";
+    hp->n_mels = 128;
+    hp->conv_ch = 480;
+    hp->n_window = 50;
+    hp->n_window_infer = 800;
+    hp->txt_layers = 28;
+    hp->txt_heads = 16;
+    hp->txt_kv_heads = 8;
+    hp->head_dim = 128;
+    hp->vocab = 151936;
+    hp->rope_theta = 1000000.0f;
+    hp->rms_eps = 1e-6f;
+    hp->ln_eps = 1e-5f;
+    if (a == "qwen3-asr-0.6b") {
+        hp->enc_d = 896; hp->enc_layers = 18; hp->enc_heads = 14; hp->enc_ffn = 3584;
+        hp->txt_h = 1024; hp->txt_ffn = 3072;
+    } else if (a == "qwen3-asr-1.7b") {
+        hp->enc_d = 1024; hp->enc_layers = 24; hp->enc_heads = 16; hp->enc_ffn = 4096;
+        hp->txt_h = 2048; hp->txt_ffn = 6144;
+    } else {
+        throw Error(QASR_E_INVALID, "unknown architecture: " + a);
+    }
+    hp->proj_out = hp->txt_h;
+    set_special_defaults(hp);
+}
+
+static void validate(const qasr_hparams& h) {
+    QASR_CHECK(h.n_mels == 128, QASR_E_FORMAT, "n_mels must be 128");
+    QASR_CHECK(h.conv_ch > 0 && h.conv_ch % 32 == 0, QASR_E_FORMAT, "conv channels must be a multiple of 32");
+    QASR_CHECK(h.enc_d % 64 == 0 && h.enc_heads > 0 && h.enc_d / h.enc_heads == 64, QASR_E_FORMAT,
+               "encoder head_dim must be 64");
+    QASR_CHECK(h.enc_ffn % 32 == 0 && h.txt_ffn % 32 == 0 && h.txt_h % 32 == 0, QASR_E_FORMAT, "dims % 32");
+    QASR_CHECK(h.head_dim == 128, QASR_E_FORMAT, "decoder head_dim must be 128");
+    QASR_CHECK(h.txt_kv_heads > 0 && h.txt_heads % h.txt_kv_heads == 0, QASR_E_FORMAT, "bad GQA head counts");
+    QASR_CHECK(h.proj_out == h.txt_h, QASR_E_FORMAT, "projector output must equal the text hidden size");
+    QASR_CHECK(h.n_window * 2 == 100 && h.n_window_infer % 100 == 0, QASR_E_FORMAT, "n_window must be 50");
+    QASR_CHECK(h.enc_layers > 0 && h.txt_layers > 0 && h.vocab > 0, QASR_E_FORMAT, "empty model");
+}
+
+// ----------------------------------------------------------------------------------------------- layout
+namespace {
+
+Q8Mat alloc_q8(Model& m, int N, int K) {
+    Q8Mat w;
+    w.N = N;
+    w.K = K;
+    w.qs = (int8_t*)m.mem.alloc((size_t)N * K);
+    w.sc = (__half*)m.mem.alloc((size_t)N * (K / QK) * sizeof(__half));
+    return w;
+}
+
+void reg_q8(Model& m, const std::string& name, const Q8Mat& w, int64_t row0, int64_t rows) {
+    TensorSlot s{};
+    s.type = 8;
+    s.base = w.qs;
+    s.sc = w.sc;
+    s.rows = rows;
+    s.cols = w.K;
+    s.row0 = row0;
+    s.ld = w.K;
+    m.slots[name] = s;
+}
+
+float* alloc_f32(Model& m, const std::string& name, int64_t n) {
+    float* p = (float*)m.mem.alloc((size_t)n * sizeof(float));
+    TensorSlot s{};
+    s.type = 0;
+    s.base = p;
+    s.rows = n;
+    s.cols = 1;
+    m.slots[name] = s;
+    return p;
+}
+
+__half* alloc_conv(Model& m, const std::string& name, int cout, int cin) {
+    __half* p = (__half*)m.mem.alloc((size_t)cout * cin * 9 * sizeof(__half));
+    TensorSlot s{};
+    s.type = 1;
+    s.base = p;
+    s.rows = (int64_t)cout * cin * 9;
+    s.cols = 1;
+    s.conv_cin = cin;
+    m.slots[name] = s;
+    return p;
+}
+
+std::string nm(const char* fmt, int l) {
+    char b[128];
+    snprintf(b, sizeof b, fmt, l);
+    return b;
+}
+
+void build_layout(Model& m) {
+    const qasr_hparams& h = m.hp;
+    const int C = h.conv_ch, d = h.enc_d, H = h.txt_h, F3 = m.audio_F3();
+    const int QD = h.txt_heads * h.head_dim, KD = h.txt_kv_heads * h.head_dim;
+    m.conv_w[0] = alloc_conv(m, "a.conv1.weight", C, 1);
+    m.conv_w[1] = alloc_conv(m, "a.conv2.weight", C, C);
+    m.conv_w[2] = alloc_conv(m, "a.conv3.weight", C, C);
+    for (int i = 0; i < 3; i++) m.conv_b[i] = alloc_f32(m, nm("a.conv%d.bias", i + 1), C);
+    m.conv_out = alloc_q8(m, d, C * F3);
+    reg_q8(m, "a.conv_out.weight", m.conv_out, 0, d);
+    m.enc.resize(h.enc_layers);
+    for (int l = 0; l < h.enc_layers; l++) {
+        EncLayer& e = m.enc[l];
+        e.ln1_w = alloc_f32(m, nm("a.blk.%d.ln1.weight", l), d);
+        e.ln1_b = alloc_f32(m, nm("a.blk.%d.ln1.bias", l), d);
+        e.ln2_w = alloc_f32(m, nm("a.blk.%d.ln2.weight", l), d);
+        e.ln2_b = alloc_f32(m, nm("a.blk.%d.ln2.bias", l), d);
+        e.qkv = alloc_q8(m, 3 * d, d);
+        reg_q8(m, nm("a.blk.%d.attn_q.weight", l), e.qkv, 0, d);
+        reg_q8(m, nm("a.blk.%d.attn_k.weight", l), e.qkv, d, d);
+        reg_q8(m, nm("a.blk.%d.attn_v.weight", l), e.qkv, 2 * d, d);
+        e.qkv_b = (float*)m.mem.alloc((size_t)3 * d * sizeof(float));
+        for (int j = 0; j < 3; j++) {
+            TensorSlot s{};
+            s.type = 0;
+            s.base = e.qkv_b + j * d;
+            s.rows = d;
+            s.cols = 1;
+            m.slots[nm(j == 0 ? "a.blk.%d.attn_q.bias" : j == 1 ? "a.blk.%d.attn_k.bias" : "a.blk.%d.attn_v.bias", l)] = s;
+        }
+        e.o = alloc_q8(m, d, d);
+        reg_q8(m, nm("a.blk.%d.attn_out.weight", l), e.o, 0, d);
+        e.o_b = alloc_f32(m, nm("a.blk.%d.attn_out.bias", l), d);
+        e.up = alloc_q8(m, h.enc_ffn, d);
+        reg_q8(m, nm("a.blk.%d.ffn_up.weight", l), e.up, 0, h.enc_ffn);
+        e.up_b = alloc_f32(m, nm("a.blk.%d.ffn_up.bias", l), h.enc_ffn);
+        e.down = alloc_q8(m, d, h.enc_ffn);
+        reg_q8(m, nm("a.blk.%d.ffn_down.weight", l), e.down, 0, d);
+        e.down_b = alloc_f32(m, nm("a.blk.%d.ffn_down.bias", l), d);
+    }
+    m.ln_post_w = alloc_f32(m, "a.ln_post.weight", d);
+    m.ln_post_b = alloc_f32(m, "a.ln_post.bias", d);
+    m.proj1 = alloc_q8(m, d, d);
+    reg_q8(m, "a.proj1.weight", m.proj1, 0, d);
+    m.proj1_b = alloc_f32(m, "a.proj1.bias", d);
+    m.proj2 = alloc_q8(m, h.proj_out, d);
+    reg_q8(m, "a.proj2.weight", m.proj2, 0, h.proj_out);
+    m.proj2_b = alloc_f32(m, "a.proj2.bias", h.proj_out);
+    m.tok_embd = alloc_q8(m, h.vocab, H);
+    reg_q8(m, "token_embd.weight", m.tok_embd, 0, h.vocab);
+    m.lm_head = m.tok_embd;  // tied (tie_word_embeddings); an "output.weight" in the GGUF replaces it
+    m.out_norm = alloc_f32(m, "output_norm.weight", H);
+    m.dec.resize(h.txt_layers);
+    for (int l = 0; l < h.txt_layers; l++) {
+        DecLayer& L = m.dec[l];
+        L.attn_norm = alloc_f32(m, nm("blk.%d.attn_norm.weight", l), H);
+        L.ffn_norm = alloc_f32(m, nm("blk.%d.ffn_norm.weight", l), H);
+        L.q_norm = alloc_f32(m, nm("blk.%d.attn_q_norm.weight", l), h.head_dim);
+        L.k_norm = alloc_f32(m, nm("blk.%d.attn_k_norm.weight", l), h.head_dim);
+        L.qkv = alloc_q8(m, QD + 2 * KD, H);
+        reg_q8(m, nm("blk.%d.attn_q.weight", l), L.qkv, 0, QD);
+        reg_q8(m, nm("blk.%d.attn_k.weight", l), L.qkv, QD, KD);
+        reg_q8(m, nm("blk.%d.attn_v.weight", l), L.qkv, QD + KD, KD);
+        L.o = alloc_q8(m, H, QD);
+        reg_q8(m, nm("blk.%d.attn_output.weight", l), L.o, 0, H);
+        L.gu = alloc_q8(m, 2 * h.txt_ffn, H);
+        reg_q8(m, nm("blk.%d.ffn_gate.weight", l), L.gu, 0, h.txt_ffn);
+        reg_q8(m, nm("blk.%d.ffn_up.weight", l), L.gu, h.txt_ffn, h.txt_ffn);
+        L.down = alloc_q8(m, H, h.txt_ffn);
+        reg_q8(m, nm("blk.%d.ffn_down.weight", l), L.down, 0, H);
+    }
+}
+
+// fixed tables: sinusoid position embedding (SinusoidsPositionEmbedding, modeling_qwen3_asr.py:245-263),
+// Slaney mel filters (feature_extraction_qwen3_asr.py:94-102) and the windowed DFT basis of the STFT
+void build_tables(Model& m, hipStream_t s) {
+    const int d = m.hp.enc_d, nmel = m.hp.n_mels;
+    std::vector<float> pe((size_t)13 * d);
+    const float inc = logf(10000.f) / (float)(d / 2 - 1);
+    for (int t = 0; t < 13; t++)
+        for (int i = 0; i < d / 2; i++) {
+            float st = (float)t * expf(-inc * (float)i);
+            pe[(size_t)t * d + i] = sinf(st);
+            pe[(size_t)t * d + d / 2 + i] = cosf(st);
+        }
+    m.pos_emb = (float*)m.mem.alloc(pe.size() * sizeof(float));
+    QASR_HIP(hipMemcpyAsync(m.pos_emb, pe.data(), pe.size() * sizeof(float), hipMemcpyHostToDevice, s));
+    std::vector<float> filt((size_t)201 * nmel), basis;
+    mel_filter_table(nmel, filt.data());
+    m.mel_filters = (float*)m.mem.alloc(filt.size() * sizeof(float));
+    QASR_HIP(hipMemcpyAsync(m.mel_filters, filt.data(), filt.size() * sizeof(float), hipMemcpyHostToDevice, s));
+    dft_basis_table(basis);
+    m.dft_basis = (float*)m.mem.alloc(basis.size() * sizeof(float));
+    QASR_HIP(hipMemcpyAsync(m.dft_basis, basis.data(), basis.size() * sizeof(float), hipMemcpyHostToDevice, s));
+    QASR_HIP(hipStreamSynchronize(s));
+}
+
+void make_tokenizer_synthetic(Model& m) {
+    const qasr_hparams& h = m.hp;
+    const int32_t ids[] = {h.tok_im_start, h.tok_im_end, h.tok_audio_start, h.tok_audio_end, h.tok_audio_pad,
+                           h.tok_eos1, h.tok_asr_text};
+    const char* txt[] = {"<|im_start|>", "<|im_end|>", "<|audio_start|>", "<|audio_end|>", "<|audio_pad|>",
+                         "<|endoftext|>", "<asr_text>"};
+    m.tok.make_synthetic(h.vocab, ids, txt, 7);
+}
+
+}  // namespace
+
+// ----------------------------------------------------------------------------------------------- synthetic
+// The per-tensor (sigma | center, scale) table mirrors orc_model_synth in oracle/qasr_oracle.c.
+std::unique_ptr<Model> make_synthetic_model(const qasr_hparams& hp, uint64_t seed, const std::string& arch) {
+    validate(hp);
+    auto mp = std::make_unique<Model>();
+    Model& m = *mp;
+    m.hp = hp;
+    m.arch = arch;
+    build_layout(m);
+    hipStream_t s = nullptr;
+    const int C = hp.conv_ch, d = hp.enc_d, H = hp.txt_h, F3 = m.audio_F3();
+    const int QD = hp.txt_heads * hp.head_dim;
+    auto base = [&](const std::string& name) { return smix(seed ^ fnv1a(name.c_str())); };
+    auto q8 = [&](const std::string& name, float sigma) {
+        const TensorSlot& t = m.slots.at(name);
+        synth_q8(base(name), t.rows * (t.cols / QK), sigma / 73.6f, (int8_t*)t.base + t.row0 * t.ld,
+                 t.sc + t.row0 * (t.ld / QK), s);
+    };
+    auto f32 = [&](const std::string& name, float center, float scale) {
+        const TensorSlot& t = m.slots.at(name);
+        synth_f32(base(name), t.rows, center, scale, (float*)t.base, s);
+    };
+    auto conv = [&](const std::string& name, float scale) {
+        const TensorSlot& t = m.slots.at(name);
+        __half* tmp = nullptr;
+        QASR_HIP(hipMalloc(&tmp, (size_t)t.rows * sizeof(__half)));
+        synth_f16(base(name), t.rows, scale, tmp, s);
+        reorder_conv_weight(tmp, C, t.conv_cin, (__half*)t.base, s);
+        QASR_HIP(hipStreamSynchronize(s));
+        QASR_HIP(hipFree(tmp));
+    };
+    conv("a.conv1.weight", 1.0f / 3.0f * 1.7320508f);
+    conv("a.conv2.weight", 1.7320508f / sqrtf((float)C * 9));
+    conv("a.conv3.weight", 1.7320508f / sqrtf((float)C * 9));
+    for (int i = 1; i <= 3; i++) f32(nm("a.conv%d.bias", i), 0.f, 0.05f);
+    q8("a.conv_out.weight", 1.0f / sqrtf((float)C * F3));
+    for (int l = 0; l < hp.enc_layers; l++) {
+        f32(nm("a.blk.%d.ln1.weight", l), 1.f, 0.1f);
+        f32(nm("a.blk.%d.ln1.bias", l), 0.f, 0.05f);
+        f32(nm("a.blk.%d.ln2.weight", l), 1.f, 0.1f);
+        f32(nm("a.blk.%d.ln2.bias", l), 0.f, 0.05f);
+        const char* lin[6] = {"attn_q", "attn_k", "attn_v", "attn_out", "ffn_up", "ffn_down"};
+        const int KK[6] = {d, d, d, d, d, hp.enc_ffn};
+        for (int i = 0; i < 6; i++) {
+            char b[128];
+            snprintf(b, sizeof b, "a.blk.%d.%s.weight", l, lin[i]);
+            q8(b, 0.5f / sqrtf((float)KK[i]));
+            snprintf(b, sizeof b, "a.blk.%d.%s.bias", l, lin[i]);
+            f32(b, 0.f, 0.02f);
+        }
+    }
+    f32("a.ln_post.weight", 1.f, 0.1f);
+    f32("a.ln_post.bias", 0.f, 0.05f);
+    q8("a.proj1.weight", 1.0f / sqrtf((float)d));
+    f32("a.proj1.bias", 0.f, 0.02f);
+    q8("a.proj2.weight", 1.0f / sqrtf((float)d));
+    f32("a.proj2.bias", 0.f, 0.02f);
+    q8("token_embd.weight", 1.0f);
+    f32("output_norm.weight", 1.f, 0.1f);
+    for (int l = 0; l < hp.txt_layers; l++) {
+        f32(nm("blk.%d.attn_norm.weight", l), 1.f, 0.1f);
+        f32(nm("blk.%d.ffn_norm.weight", l), 1.f, 0.1f);
+        f32(nm("blk.%d.attn_q_norm.weight", l), 1.f, 0.1f);
+        f32(nm("blk.%d.attn_k_norm.weight", l), 1.f, 0.1f);
+        q8(nm("blk.%d.attn_q.weight", l), 1.0f / sqrtf((float)H));
+        q8(nm("blk.%d.attn_k.weight", l), 1.0f / sqrtf((float)H));
+        q8(nm("blk.%d.attn_v.weight", l), 1.0f / sqrtf((float)H));
+        q8(nm("blk.%d.attn_output.weight", l), 0.5f / sqrtf((float)QD));
+        q8(nm("blk.%d.ffn_gate.weight", l), 1.0f / sqrtf((float)H));
+        q8(nm("blk.%d.ffn_up.weight", l), 1.0f / sqrtf((float)H));
+        q8(nm("blk.%d.ffn_down.weight", l), 0.5f / sqrtf((float)hp.txt_ffn));
+    }
+    QASR_HIP(hipGetLastError());
+    build_tables(m, s);
+    make_tokenizer_synthetic(m);
+    return mp;
+}
+
+// ----------------------------------------------------------------------------------------------- GGUF
+// Metadata keys and tensor names of this engine's GGUF convention (DESIGN.md §tensor names).  The text
+// decoder uses llama.cpp's qwen3 names; audio tensors use the "a." prefix.  Every tensor is validated
+// against the shape implied by the metadata before upload.
+std::unique_ptr<Model> load_gguf_model(const std::string& path) {
+    GgufFile f(path);
+    qasr_hparams hp;
+    default_hparams("qwen3-asr-1.7b", &hp);
+    const std::string A = f.get_str("general.architecture", "qwen3-asr");
+    auto gi = [&](const char* k, int def) { return (int)f.get_int(A + "." + k, def); };
+    auto gf = [&](const char* k, float def) { return (float)f.get_float(A + "." + k, def); };
+    hp.n_mels = gi("audio.n_mels", 128);
+    hp.conv_ch = gi("audio.conv_channels", 480);
+    hp.enc_d = gi("audio.embedding_length", hp.enc_d);
+    hp.enc_layers = gi("audio.block_count", hp.enc_layers);
+    hp.enc_heads = gi("audio.attention.head_count", hp.enc_heads);
+    hp.enc_ffn = gi("audio.feed_forward_length", hp.enc_ffn);
+    hp.n_window = gi("audio.n_window", 50);
+    hp.n_window_infer = gi("audio.n_window_infer", 800);
+    hp.txt_h = gi("embedding_length", hp.txt_h);
+    hp.proj_out = gi("audio.projection_dim", hp.txt_h);
+    hp.txt_layers = gi("block_count", hp.txt_layers);
+    hp.txt_heads = gi("attention.head_count", hp.txt_heads);
+    hp.txt_kv_heads = gi("attention.head_count_kv", hp.txt_kv_heads);
+    hp.head_dim = gi("attention.key_length", hp.head_dim);
+    hp.txt_ffn = gi("feed_forward_length", hp.txt_ffn);
+    hp.rope_theta = gf("rope.freq_base", hp.rope_theta);
+    hp.rms_eps = gf("attention.layer_norm_rms_epsilon", hp.rms_eps);
+    hp.ln_eps = gf("audio.attention.layer_norm_epsilon", hp.ln_eps);
+    const GgufValue* toks = f.get("tokenizer.ggml.tokens");
+    const GgufTensor* te = f.tensor("token_embd.weight");
+    QASR_CHECK(te, QASR_E_FORMAT, "GGUF has no token_embd.weight");
+    hp.vocab = (int)te->dims[1];
+    hp.tok_im_start = gi("token.im_start", hp.tok_im_start);
+    hp.tok_im_end = gi("token.im_end", hp.tok_im_end);
+    hp.tok_system = gi("token.system", hp.tok_system);
+    hp.tok_user = gi("token.user", hp.tok_user);
+    hp.tok_assistant = gi("token.assistant", hp.tok_assistant);
+    hp.tok_newline = gi("token.newline", hp.tok_newline);
+    hp.tok_audio_start = gi("token.audio_start", hp.tok_audio_start);
+    hp.tok_audio_end = gi("token.audio_end", hp.tok_audio_end);
+    hp.tok_audio_pad = gi("token.audio_pad", hp.tok_audio_pad);
+    hp.tok_eos0 = gi("token.eos0", hp.tok_eos0);
+    hp.tok_eos1 = gi("token.eos1", hp.tok_eos1);
+    hp.tok_asr_text = gi("token.asr_text", hp.tok_asr_text);
+    validate(hp);
+
+    auto mp = std::make_unique<Model>();
+    Model& m = *mp;
+    m.hp = hp;
+    m.arch = f.get_str("general.name", "qwen3-asr");
+    build_layout(m);
+    hipStream_t s = nullptr;
+    uint8_t* staging = nullptr;
+    size_t staging_cap = 0;
+    for (auto& kv : m.slots) {
+        const std::string& name = kv.first;
+        const TensorSlot& t = kv.second;
+        const GgufTensor* g = f.tensor(name);
+        QASR_CHECK(g, QASR_E_FORMAT, "GGUF is missing tensor " + name);
+        if (t.type == 8) {
+            QASR_CHECK(g->type == GGML_Q8_0, QASR_E_FORMAT, name + ": expected Q8_0");
+            QASR_CHECK(g->dims.size() == 2 && g->dims[0] == t.cols && g->dims[1] == t.rows, QASR_E_FORMAT,
+                       name + ": shape mismatch");
+            if (g->nbytes > staging_cap) {
+                if (staging) QASR_HIP(hipFree(staging));
+                staging_cap = g->nbytes;
+                QASR_HIP(hipMalloc(&staging, staging_cap));
+            }
+            QASR_HIP(hipMemcpy(staging, g->data, g->nbytes, hipMemcpyHostToDevice));
+            repack_q8(staging, t.rows * (t.cols / QK), (int8_t*)t.base + t.row0 * t.ld, t.sc + t.row0 * (t.ld / QK), s);
+            QASR_HIP(hipStreamSynchronize(s));
+        } else if (t.type == 0) {
+            QASR_CHECK(g->type == GGML_F32 && (int64_t)(g->nbytes / 4) == t.rows, QASR_E_FORMAT, name + ": expected f32");
+            QASR_HIP(hipMemcpy(t.base, g->data, g->nbytes, hipMemcpyHostToDevice));
+        } else {
+            QASR_CHECK(g->type == GGML_F16 && (int64_t)(g->nbytes / 2) == t.rows, QASR_E_FORMAT, name + ": expected f16");
+            __half* tmp = nullptr;
+            QASR_HIP(hipMalloc(&tmp, g->nbytes));
+            QASR_HIP(hipMemcpy(tmp, g->data, g->nbytes, hipMemcpyHostToDevice));
+            reorder_conv_weight(tmp, hp.conv_ch, t.conv_cin, (__half*)t.base, s);
+            QASR_HIP(hipStreamSynchronize(s));
+            QASR_HIP(hipFree(tmp));
+        }
+    }
+    if (staging) QASR_HIP(hipFree(staging));
+    if (const GgufTensor* out = f.tensor("output.weight")) {  // untied checkpoints
+        QASR_CHECK(out->type == GGML_Q8_0 && out->dims[0] == hp.txt_h && out->dims[1] == hp.vocab, QASR_E_FORMAT,
+                   "output.weight: shape mismatch");
+        m.lm_head = alloc_q8(m, hp.vocab, hp.txt_h);
+        reg_q8(m, "output.weight", m.lm_head, 0, hp.vocab);
+        uint8_t* tmp = nullptr;
+        QASR_HIP(hipMalloc(&tmp, out->nbytes));
+        QASR_HIP(hipMemcpy(tmp, out->data, out->nbytes, hipMemcpyHostToDevice));
+        repack_q8(tmp, (int64_t)hp.vocab * (hp.txt_h / QK), m.lm_head.qs, m.lm_head.sc, s);
+        QASR_HIP(hipStreamSynchronize(s));
+        QASR_HIP(hipFree(tmp));
+    }
+    build_tables(m, s);
+    if (toks && toks->arr_type == 8 && (int)toks->arr_s.size() >= hp.vocab) {
+        m.tok.pieces = toks->arr_s;
+        m.tok.is_special.assign(m.tok.pieces.size(), 0);
+        if (const GgufValue* tt = f.get("tokenizer.ggml.token_type"))
+            for (size_t i = 0; i < tt->arr_i.size() && i < m.tok.is_special.size(); i++)
+                m.tok.is_special[i] = tt->arr_i[i] == 3 || tt->arr_i[i] == 4;  // CONTROL / USER_DEFINED
+    } else {
+        make_tokenizer_synthetic(m);
+    }
+    return mp;
+}
+
+// ----------------------------------------------------------------------------------------------- export
+void export_tensor(const Model& m, const std::string& name, void* dst, size_t cap, size_t* written) {
+    auto it = m.slots.find(name);
+    QASR_CHECK(it != m.slots.end(), QASR_E_INVALID, "unknown tensor " + name);
+    const TensorSlot& t = it->second;
+    if (t.type == 8) {
+        const int64_t nb = t.cols / QK;
+        const size_t bytes = (size_t)(t.rows * nb * QBYTES);
+        QASR_CHECK(cap >= bytes, QASR_E_CAPACITY, "export buffer too small");
+        std::vector<int8_t> qs((size_t)(t.rows * t.cols));
+        std::vector<uint16_t> sc((size_t)(t.rows * nb));
+        QASR_HIP(hipMemcpy(qs.data(), (int8_t*)t.base + t.row0 * t.ld, qs.size(), hipMemcpyDeviceToHost));
+        QASR_HIP(hipMemcpy(sc.data(), t.sc + t.row0 * nb, sc.size() * 2, hipMemcpyDeviceToHost));
+        uint8_t* o = (uint8_t*)dst;
+        for (int64_t b = 0; b < t.rows * nb; b++) {
+            memcpy(o + b * QBYTES, &sc[(size_t)b], 2);
+            memcpy(o + b * QBYTES + 2, &qs[(size_t)b * QK], QK);
+        }
+        *written = bytes;
+    } else if (t.type == 0) {
+        QASR_CHECK(cap >= (size_t)t.rows * 4, QASR_E_CAPACITY, "export buffer too small");
+        QASR_HIP(hipMemcpy(dst, t.base, (size_t)t.rows * 4, hipMemcpyDeviceToHost));
+        *written = (size_t)t.rows * 4;
+    } else {
+        // conv weights back in GGUF order [Cout][Cin][3][3]
+        const int cin = t.conv_cin, cout = (int)(t.rows / (cin * 9));
+        QASR_CHECK(cap >= (size_t)t.rows * 2, QASR_E_CAPACITY, "export buffer too small");
+        std::vector<uint16_t> r((size_t)t.rows);
+        QASR_HIP(hipMemcpy(r.data(), t.base, r.size() * 2, hipMemcpyDeviceToHost));
+        uint16_t* o = (uint16_t*)dst;
+        for (int co = 0; co < cout; co++)
+            for (int k = 0; k < 9; k++)
+                for (int ci = 0; ci < cin; ci++) o[((size_t)co * cin + ci) * 9 + k] = r[((size_t)co * 9 + k) * cin + ci];
+        *written = (size_t)t.rows * 2;
+    }
+}
+
+}  // namespace qasr

@@ -1,0 +1,197 @@
+"""Drop-in for the `transcribe_cpp` Python API that the reference server binds, backed by libqasr (HIP).
+
+Reference call sites (sypsyp97/light-whisper src-tauri/resources/qwen3_asr_server.py):
+    model = transcribe_cpp.Model(model_path, backend=backend)          # :122
+    session = model.session(kv_type="f16", n_ctx=32768)                 # :123
+    result = session.run(audio_f32_16k, timestamps="none")             # :144, :321
+    result.text, result.language                                        # :326-327
+    session.close(); model.close()                                      # :100-112
+Backends: "hip" and "auto" select the MI355X engine; "cuda", "vulkan" and "cpu" raise (the reference's
+fallback loop then reports every backend's error, :117-133).  There is no CPU path.
+
+Extensions used by the bench and the parity tests: Model.synthetic(), Session.run_batch(),
+Session.forced_logits(), Session.mel(), Session.encode(), Session.prefill_logits().
+"""
+from __future__ import annotations
+
+import ctypes as C
+from types import SimpleNamespace
+
+import numpy as np
+
+from . import _lib
+from ._lib import HParams, Result, RunOpts, check
+
+__version__ = "0.1.3+mi355x"
+
+
+def _f32(a) -> np.ndarray:
+    return np.ascontiguousarray(np.asarray(a, dtype=np.float32).reshape(-1))
+
+
+def _take_result(r: Result) -> SimpleNamespace:
+    toks = [r.tokens[i] for i in range(r.n_tokens)]
+    out = SimpleNamespace(
+        text=(r.text or b"").decode("utf-8", "replace"),
+        language=(r.language or b"").decode("utf-8", "replace") or None,
+        raw=(r.raw or b"").decode("utf-8", "replace"),
+        tokens=toks,
+        n_audio_tokens=r.n_audio_tokens,
+        n_prompt=r.n_prompt,
+        timings_ms={"mel": r.ms_mel, "encoder": r.ms_encoder, "prefill": r.ms_prefill, "decode": r.ms_decode},
+    )
+    _lib.load().qasr_result_free(C.byref(r))
+    return out
+
+
+class Model:
+    def __init__(self, path: str, backend: str = "auto", _handle=None):
+        lib = _lib.load()
+        self._h = C.c_void_p()
+        if _handle is not None:
+            self._h = _handle
+        else:
+            check(lib.qasr_model_open(path.encode(), backend.encode(), C.byref(self._h)))
+        self.path = path
+        self.backend = "hip"
+
+    @classmethod
+    def synthetic(cls, arch: str | None = "qwen3-asr-1.7b", seed: int = 0, hparams: dict | None = None):
+        lib = _lib.load()
+        h = C.c_void_p()
+        hp = None
+        if hparams is not None:
+            hp = HParams()
+            for k, v in hparams.items():
+                setattr(hp, k, v)
+        check(lib.qasr_model_open_synthetic(arch.encode() if arch else None, C.byref(hp) if hp is not None else None,
+                                            int(seed), C.byref(h)))
+        return cls(f"synthetic:{arch or 'custom'}:{seed}", _handle=h)
+
+    @property
+    def hparams(self) -> dict:
+        hp = HParams()
+        check(_lib.load().qasr_model_hparams(self._h, C.byref(hp)))
+        return hp.to_dict()
+
+    def weight_bytes(self) -> int:
+        return int(_lib.load().qasr_model_weight_bytes(self._h))
+
+    def export_tensor(self, name: str, nbytes: int) -> np.ndarray:
+        buf = np.empty(nbytes, np.uint8)
+        written = C.c_size_t()
+        check(_lib.load().qasr_model_export_tensor(self._h, name.encode(), buf.ctypes.data_as(C.c_void_p), nbytes,
+                                                   C.byref(written)))
+        return buf[: written.value]
+
+    def session(self, kv_type: str = "f16", n_ctx: int = 32768) -> "Session":
+        return Session(self, kv_type, n_ctx)
+
+    def close(self):
+        if self._h:
+            _lib.load().qasr_model_close(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Session:
+    def __init__(self, model: Model, kv_type: str = "f16", n_ctx: int = 32768):
+        self.model = model
+        self._h = C.c_void_p()
+        check(_lib.load().qasr_session_open(model._h, kv_type.encode(), int(n_ctx), C.byref(self._h)))
+        self.n_ctx = n_ctx
+
+    def run(self, audio, timestamps: str = "none", max_new_tokens: int = 0, force_tokens_per_s: int = 0):
+        if timestamps not in ("none", None):
+            raise ValueError("only timestamps='none' is supported")
+        a = _f32(audio)
+        r = Result()
+        opts = RunOpts(int(max_new_tokens), int(force_tokens_per_s), 0)
+        check(_lib.load().qasr_session_run_opts(self._h, a.ctypes.data_as(C.c_void_p), a.size, C.byref(opts),
+                                                C.byref(r)))
+        return _take_result(r)
+
+    def run_batch(self, audios, max_new_tokens: int = 0, force_tokens_per_s: int = 0):
+        arrs = [_f32(a) for a in audios]
+        n = len(arrs)
+        ptrs = (C.c_void_p * n)(*[a.ctypes.data_as(C.c_void_p).value for a in arrs])
+        lens = (C.c_size_t * n)(*[a.size for a in arrs])
+        res = (Result * n)()
+        opts = RunOpts(int(max_new_tokens), int(force_tokens_per_s), 0)
+        check(_lib.load().qasr_run_batch(self._h, ptrs, lens, n, C.byref(opts), res))
+        return [_take_result(res[i]) for i in range(n)]
+
+    def run_batch_device(self, dev_ptr: int, offsets, lengths, max_new_tokens: int = 0, force_tokens_per_s: int = 0,
+                         want_results: bool = True):
+        n = len(lengths)
+        off = (C.c_int64 * n)(*[int(x) for x in offsets])
+        ln = (C.c_int64 * n)(*[int(x) for x in lengths])
+        res = (Result * n)() if want_results else None
+        opts = RunOpts(int(max_new_tokens), int(force_tokens_per_s), 0)
+        check(_lib.load().qasr_run_batch_device(self._h, C.c_void_p(dev_ptr), off, ln, n, C.byref(opts), res))
+        return [_take_result(res[i]) for i in range(n)] if want_results else None
+
+    def forced_logits(self, audio, forced) -> np.ndarray:
+        a = _f32(audio)
+        f = np.ascontiguousarray(forced, dtype=np.int32)
+        v = self.model.hparams["vocab"]
+        out = np.empty((f.size + 1, v), np.float32)
+        check(_lib.load().qasr_session_forced_logits(self._h, a.ctypes.data_as(C.c_void_p), a.size,
+                                                     f.ctypes.data_as(C.c_void_p), f.size,
+                                                     out.ctypes.data_as(C.c_void_p)))
+        return out
+
+    def mel(self, audio):
+        a = _f32(audio)
+        n = max(a.size, 8000)
+        tv = (n + 159) // 160
+        tp = (tv + 99) // 100 * 100
+        out = np.empty((self.model.hparams["n_mels"], tp), np.float32)
+        t_valid, t_pad = C.c_int32(), C.c_int32()
+        check(_lib.load().qasr_session_mel(self._h, a.ctypes.data_as(C.c_void_p), a.size,
+                                           out.ctypes.data_as(C.c_void_p), C.byref(t_valid), C.byref(t_pad)))
+        assert t_pad.value == tp
+        return out, t_valid.value
+
+    def encode(self, mel: np.ndarray, t_valid: int, want_enc: bool = False):
+        hp = self.model.hparams
+        mel = np.ascontiguousarray(mel, dtype=np.float32)
+        t_pad = mel.shape[1]
+        full, tail = divmod(t_valid, 100)
+        n = tail
+        for _ in range(3):
+            n = (n - 1) // 2 + 1 if n > 0 else 0
+        n_tok = full * 13 + n
+        emb = np.empty((n_tok, hp["txt_h"]), np.float32)
+        enc = np.empty((n_tok, hp["enc_d"]), np.float32) if want_enc else None
+        got = C.c_int32()
+        check(_lib.load().qasr_session_encode(self._h, mel.ctypes.data_as(C.c_void_p), t_pad, int(t_valid),
+                                              emb.ctypes.data_as(C.c_void_p),
+                                              enc.ctypes.data_as(C.c_void_p) if enc is not None else None,
+                                              C.byref(got)))
+        assert got.value == n_tok
+        return (emb, enc) if want_enc else emb
+
+    def prefill_logits(self, embeds: np.ndarray) -> np.ndarray:
+        e = np.ascontiguousarray(embeds, dtype=np.float32)
+        v = self.model.hparams["vocab"]
+        out = np.empty((e.shape[0], v), np.float32)
+        check(_lib.load().qasr_session_prefill_logits(self._h, e.ctypes.data_as(C.c_void_p), e.shape[0],
+                                                      out.ctypes.data_as(C.c_void_p)))
+        return out
+
+    def close(self):
+        if self._h:
+            _lib.load().qasr_session_close(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

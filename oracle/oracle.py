@@ -61,6 +61,8 @@ def lib():
         L.orc_model_set.argtypes = [P, C.c_char_p, P]
         L.orc_model_set.restype = C.c_int
         L.orc_model_synth.argtypes = [P, C.c_uint64]
+        L.orc_model_get.argtypes = [P, C.c_char_p]
+        L.orc_model_get.restype = P
         L.orc_audio_tokens.argtypes = [C.c_int]
         L.orc_audio_tokens.restype = C.c_int
         L.orc_encode.argtypes = [P, P, C.c_int, C.c_int, P, P]
@@ -249,6 +251,56 @@ class Model:
         if getattr(self, "h", None):
             lib().orc_model_free(self.h)
             self.h = None
+
+    def tensor_specs(self) -> dict:
+        """name → (kind, shape) of every tensor in this engine's GGUF convention (kind: q8 / f32 / f16)."""
+        c = self.cfg
+        C_, d, H = c["conv_ch"], c["enc_d"], c["txt_h"]
+        F3 = (((c["n_mels"] + 1) // 2 + 1) // 2 + 1) // 2
+        QD, KD = c["txt_heads"] * c["head_dim"], c["txt_kv_heads"] * c["head_dim"]
+        t = {"a.conv1.weight": ("f16", (C_, 1, 3, 3)), "a.conv2.weight": ("f16", (C_, C_, 3, 3)),
+             "a.conv3.weight": ("f16", (C_, C_, 3, 3)), "a.conv_out.weight": ("q8", (d, C_ * F3)),
+             "a.ln_post.weight": ("f32", (d,)), "a.ln_post.bias": ("f32", (d,)), "a.proj1.weight": ("q8", (d, d)),
+             "a.proj1.bias": ("f32", (d,)), "a.proj2.weight": ("q8", (c["proj_out"], d)),
+             "a.proj2.bias": ("f32", (c["proj_out"],)), "token_embd.weight": ("q8", (c["vocab"], H)),
+             "output_norm.weight": ("f32", (H,))}
+        for i in (1, 2, 3):
+            t[f"a.conv{i}.bias"] = ("f32", (C_,))
+        for l in range(c["enc_layers"]):
+            for n_ in ("ln1", "ln2"):
+                t[f"a.blk.{l}.{n_}.weight"] = ("f32", (d,))
+                t[f"a.blk.{l}.{n_}.bias"] = ("f32", (d,))
+            for n_, nn, kk in (("attn_q", d, d), ("attn_k", d, d), ("attn_v", d, d), ("attn_out", d, d),
+                               ("ffn_up", c["enc_ffn"], d), ("ffn_down", d, c["enc_ffn"])):
+                t[f"a.blk.{l}.{n_}.weight"] = ("q8", (nn, kk))
+                t[f"a.blk.{l}.{n_}.bias"] = ("f32", (nn,))
+        for l in range(c["txt_layers"]):
+            for n_ in ("attn_norm", "ffn_norm"):
+                t[f"blk.{l}.{n_}.weight"] = ("f32", (H,))
+            for n_ in ("attn_q_norm", "attn_k_norm"):
+                t[f"blk.{l}.{n_}.weight"] = ("f32", (c["head_dim"],))
+            for n_, nn, kk in (("attn_q", QD, H), ("attn_k", KD, H), ("attn_v", KD, H), ("attn_output", H, QD),
+                               ("ffn_gate", c["txt_ffn"], H), ("ffn_up", c["txt_ffn"], H),
+                               ("ffn_down", H, c["txt_ffn"])):
+                t[f"blk.{l}.{n_}.weight"] = ("q8", (nn, kk))
+        return t
+
+    def export(self) -> dict:
+        """copy every bound tensor out (Q8_0 as GGUF blocks [N][K/32*34] uint8, f16 as uint16 bits)."""
+        out = {}
+        for name, (kind, shape) in self.tensor_specs().items():
+            p = lib().orc_model_get(self.h, name.encode())
+            if not p:
+                continue
+            if kind == "q8":
+                nbytes = shape[0] * shape[1] // QK * QBYTES
+                a = np.ctypeslib.as_array((C.c_uint8 * nbytes).from_address(p)).copy().reshape(shape[0], -1)
+            elif kind == "f32":
+                a = np.ctypeslib.as_array((C.c_float * int(np.prod(shape))).from_address(p)).copy().reshape(shape)
+            else:
+                a = np.ctypeslib.as_array((C.c_uint16 * int(np.prod(shape))).from_address(p)).copy().reshape(shape)
+            out[name] = a
+        return out
 
     def audio_tokens(self, t_valid: int) -> int:
         return lib().orc_audio_tokens(int(t_valid))

@@ -291,64 +291,11 @@ TINY_SEED = 20260821
 
 
 def tiny_tensors(cfg=TINY, seed=TINY_SEED):
-    """Synthetic GGUF-style tensors from the shared generator (oracle.synth_*)."""
+    """Synthetic GGUF-style tensors from the oracle's generator (orc_model_synth) — the same values the
+    product's on-device generator produces (checked by tests/test_model_gpu.py)."""
     import oracle
 
-    L = oracle.lib()
-    import ctypes as C
-
-    def q8(name, n, k, sig):
-        return oracle.synth_q8(seed, name, n, k, sig)
-
-    def f32(name, n, ctr, sc):
-        a = np.empty(n, np.float32)
-        L.orc_synth_f32(seed, name.encode(), n, ctr, sc, a.ctypes.data_as(C.c_void_p))
-        return a
-
-    def f16(name, n, sc):
-        a = np.empty(n, np.uint16)
-        L.orc_synth_f16(seed, name.encode(), n, sc, a.ctypes.data_as(C.c_void_p))
-        return a
-
-    c = cfg
-    C_, d, H = c["conv_ch"], c["enc_d"], c["txt_h"]
-    t = {}
-    t["a.conv1.weight"] = f16("a.conv1.weight", C_ * 9, 1.0 / 3.0 * 1.7320508).reshape(C_, 1, 3, 3)
-    t["a.conv1.bias"] = f32("a.conv1.bias", C_, 0, 0.05)
-    for i in (2, 3):
-        t[f"a.conv{i}.weight"] = f16(f"a.conv{i}.weight", C_ * C_ * 9, 1.7320508 / np.sqrt(C_ * 9.0)).reshape(C_, C_, 3, 3)
-        t[f"a.conv{i}.bias"] = f32(f"a.conv{i}.bias", C_, 0, 0.05)
-    t["a.conv_out.weight"] = q8("a.conv_out.weight", d, C_ * 16, 1.0 / np.sqrt(C_ * 16.0))
-    for l in range(c["enc_layers"]):
-        for nm_ in ("ln1", "ln2"):
-            t[f"a.blk.{l}.{nm_}.weight"] = f32(f"a.blk.{l}.{nm_}.weight", d, 1, 0.1)
-            t[f"a.blk.{l}.{nm_}.bias"] = f32(f"a.blk.{l}.{nm_}.bias", d, 0, 0.05)
-        for nm_, n, k in (("attn_q", d, d), ("attn_k", d, d), ("attn_v", d, d), ("attn_out", d, d),
-                          ("ffn_up", c["enc_ffn"], d), ("ffn_down", d, c["enc_ffn"])):
-            t[f"a.blk.{l}.{nm_}.weight"] = q8(f"a.blk.{l}.{nm_}.weight", n, k, 0.5 / np.sqrt(k))
-            t[f"a.blk.{l}.{nm_}.bias"] = f32(f"a.blk.{l}.{nm_}.bias", n, 0, 0.02)
-    t["a.ln_post.weight"] = f32("a.ln_post.weight", d, 1, 0.1)
-    t["a.ln_post.bias"] = f32("a.ln_post.bias", d, 0, 0.05)
-    t["a.proj1.weight"] = q8("a.proj1.weight", d, d, 1.0 / np.sqrt(d))
-    t["a.proj1.bias"] = f32("a.proj1.bias", d, 0, 0.02)
-    t["a.proj2.weight"] = q8("a.proj2.weight", c["proj_out"], d, 1.0 / np.sqrt(d))
-    t["a.proj2.bias"] = f32("a.proj2.bias", c["proj_out"], 0, 0.02)
-    t["token_embd.weight"] = q8("token_embd.weight", c["vocab"], H, 1.0)
-    t["output_norm.weight"] = f32("output_norm.weight", H, 1, 0.1)
-    QD, KD = c["txt_heads"] * c["head_dim"], c["txt_kv_heads"] * c["head_dim"]
-    for l in range(c["txt_layers"]):
-        t[f"blk.{l}.attn_norm.weight"] = f32(f"blk.{l}.attn_norm.weight", H, 1, 0.1)
-        t[f"blk.{l}.ffn_norm.weight"] = f32(f"blk.{l}.ffn_norm.weight", H, 1, 0.1)
-        t[f"blk.{l}.attn_q_norm.weight"] = f32(f"blk.{l}.attn_q_norm.weight", c["head_dim"], 1, 0.1)
-        t[f"blk.{l}.attn_k_norm.weight"] = f32(f"blk.{l}.attn_k_norm.weight", c["head_dim"], 1, 0.1)
-        t[f"blk.{l}.attn_q.weight"] = q8(f"blk.{l}.attn_q.weight", QD, H, 1 / np.sqrt(H))
-        t[f"blk.{l}.attn_k.weight"] = q8(f"blk.{l}.attn_k.weight", KD, H, 1 / np.sqrt(H))
-        t[f"blk.{l}.attn_v.weight"] = q8(f"blk.{l}.attn_v.weight", KD, H, 1 / np.sqrt(H))
-        t[f"blk.{l}.attn_output.weight"] = q8(f"blk.{l}.attn_output.weight", H, QD, 0.5 / np.sqrt(QD))
-        t[f"blk.{l}.ffn_gate.weight"] = q8(f"blk.{l}.ffn_gate.weight", c["txt_ffn"], H, 1 / np.sqrt(H))
-        t[f"blk.{l}.ffn_up.weight"] = q8(f"blk.{l}.ffn_up.weight", c["txt_ffn"], H, 1 / np.sqrt(H))
-        t[f"blk.{l}.ffn_down.weight"] = q8(f"blk.{l}.ffn_down.weight", H, c["txt_ffn"], 0.5 / np.sqrt(c["txt_ffn"]))
-    return t
+    return oracle.Model(cfg, seed=seed).export()
 
 
 def make_hf_tiny():

@@ -1,0 +1,66 @@
+"""FireRedVAD on the GPU through the C ABI vs the golden ONNX-graph interpretation and the reference KAT.
+
+Pinned by: test_firered_vad.py:53-59 (1 s of zeros → 98 probabilities, no speech) and the DFSMN outputs of
+the reference ONNX graph interpreted in numpy (tests/golden/dfsmn.npz).  Fbank tolerance is in the log
+domain (FFT rounding differs from the numpy float64 restatement).
+"""
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+
+pytestmark = pytest.mark.gpu
+D = np.load(os.path.join(os.path.dirname(__file__), "golden", "dfsmn.npz"))
+NAMES = ["zeros_1s", "tone_bursts_3s", "noise_0p7s", "short_399", "one_frame_400"]
+
+
+@pytest.fixture(scope="module")
+def vad(torch_dev):
+    from qasr.firered_vad import FireRedVad
+
+    v = FireRedVad()
+    yield v
+    v.close()
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_fbank(vad, name):
+    f = vad.features(np.clip(D[f"{name}__audio"] * 32768.0, -32768, 32767) / 32768.0)
+    ref = D[f"{name}__feats"]
+    assert f.shape == ref.shape
+    if f.size:
+        assert np.abs(f - ref).max() < 2e-3
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_probabilities(vad, name):
+    p = vad.probabilities(D[f"{name}__audio"])
+    ref = D[f"{name}__probs"]
+    assert p.shape == ref.shape
+    if p.size:
+        assert np.abs(p - ref).max() < 1e-4
+
+
+def test_reference_kat_one_second_of_zeros(vad):
+    z = np.zeros(16000, np.float32)
+    assert vad.probabilities(z).shape == (98,)
+    assert vad.speech_timestamps(z) == []
+
+
+def test_speech_timestamps_match_oracle_pipeline(vad):
+    rng = np.random.default_rng(11)
+    t = np.arange(16000 * 6) / 16000.0
+    env = (np.sin(2 * np.pi * 0.4 * t) > 0).astype(np.float32)
+    voiced = sum(np.sin(2 * np.pi * 140 * k * t + rng.uniform(0, 6)) / k for k in range(1, 9))
+    audio = (0.25 * env * voiced * (1 + 0.5 * np.sin(2 * np.pi * 4 * t)) + 0.003 * rng.standard_normal(t.size))
+    audio = audio.astype(np.float32)
+    p = vad.probabilities(audio)
+    pcm = np.clip(audio * 32768.0, -32768, 32767).astype(np.float32)
+    from convert_vad import read_qvad
+
+    w = read_qvad(os.path.join(os.path.dirname(__file__), "..", "assets", "fireredvad_dfsmn.qvad"))
+    pr = oracle.vad_probabilities(oracle.fbank(pcm), w)
+    assert np.abs(p - pr).max() < 1e-3
+    assert vad.speech_timestamps(audio) == oracle.vad_segments(p, audio.size)
