@@ -1,0 +1,232 @@
+#!/usr/bin/env python3
+"""Throughput bench: audio-seconds per wall-second (RTF⁻¹) of Qwen3-ASR-1.7B Q8 on MI355X.
+
+Workload (BASELINE.json configs[3], "1.7B Q8, VAD-split segments batch-sharded"):
+  * 256 segments per rank, lengths U[2,12] s, seeded synthetic speech-like 16 kHz audio (f0 90-250 Hz with
+    jitter, 8 harmonics, 4 Hz syllabic AM, pink noise at -25 dB, peak -12 dBFS), VAD bypassed for ASR timing;
+    the global list of 256·N segments is LPT-sharded over the N ranks (weak scaling, no data-path collective);
+  * Qwen3-ASR-1.7B shapes with Q8_0 weights generated on the device from a seed (no checkpoint in the
+    container — DESIGN.md §synthetic), f16 KV cache;
+  * throughput mode: exactly round(8·seconds)+1 greedy tokens per segment (EOS ignored) so the work is fixed.
+A step = one qasr_run_batch_device call over the rank's resident segments: log-mel → conv stack → encoder →
+projector → prefill → continuous-batching decode → detokenise.
+
+Launch: python bench.py [--gpus N --steps K --warmup W]; N>1 via torch.distributed.run (RCCL only for the
+barrier and the max-over-ranks time).  Prints ONE JSON line (rank 0).
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "light-whisper_amd"))
+
+SEG_PER_RANK = 256
+FORCE_TPS = 8
+
+
+def speech_like(rng, n, sr=16000):
+    """Seeded speech-like signal (SURVEY §8(d) synthetic-audio recipe)."""
+    t = np.arange(n) / sr
+    f0 = rng.uniform(90, 250)
+    jitter = 1 + 0.03 * np.cumsum(rng.standard_normal(n)) / np.sqrt(np.arange(1, n + 1))
+    phase = 2 * np.pi * np.cumsum(f0 * jitter) / sr
+    voiced = sum(np.sin(k * phase + rng.uniform(0, 2 * np.pi)) / k for k in range(1, 9))
+    am = 0.55 + 0.45 * np.sin(2 * np.pi * 4.0 * t + rng.uniform(0, 2 * np.pi))
+    white = rng.standard_normal(n)
+    pink = np.fft.irfft(np.fft.rfft(white) / np.sqrt(np.maximum(np.arange(n // 2 + 1), 1)), n)
+    sig = voiced * am
+    sig = sig / (np.abs(sig).max() + 1e-9)
+    pink = pink / (np.sqrt((pink ** 2).mean()) + 1e-9) * np.sqrt((sig ** 2).mean()) * 10 ** (-25 / 20)
+    out = sig + pink
+    return (out / (np.abs(out).max() + 1e-9) * 10 ** (-12 / 20)).astype(np.float32)
+
+
+def lpt_shard(lengths, world):
+    """Longest-processing-time greedy assignment of segment indices to ranks."""
+    order = np.argsort(-np.asarray(lengths), kind="stable")
+    load = np.zeros(world)
+    shards = [[] for _ in range(world)]
+    for i in order:
+        r = int(np.argmin(load))
+        shards[r].append(int(i))
+        load[r] += lengths[i]
+    return shards
+
+
+def make_workload(world, rank, seed=1):
+    rng = np.random.default_rng(seed)
+    total = SEG_PER_RANK * world
+    secs = rng.uniform(2.0, 12.0, size=total)
+    lengths = [int(s * 16000) for s in secs]
+    mine = sorted(lpt_shard(lengths, world)[rank])
+    audio = [speech_like(np.random.default_rng(seed * 1_000_003 + i), lengths[i]) for i in mine]
+    return audio
+
+
+def cpu_baseline(seconds=5.0, seed=0, threads=None):
+    """Oracle (CPU restatement, same W8A8 semantics, OpenMP) on a bounded sample: one 5 s segment of the
+    same workload (1.7B, 8 tokens/s forced).  Returns audio-s per wall-s and the thread count."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+
+    if threads:
+        oracle.set_threads(threads)
+    oracle.set_mode(engine=True)
+    cfg = dict(n_mels=128, conv_ch=480, enc_d=1024, enc_layers=24, enc_heads=16, enc_ffn=4096, n_window=50,
+               n_window_infer=800, proj_out=2048, txt_h=2048, txt_layers=28, txt_heads=16, txt_kv_heads=8,
+               head_dim=128, txt_ffn=6144, vocab=151936, rope_theta=1e6, rms_eps=1e-6, ln_eps=1e-5)
+    model = oracle.Model(cfg, seed=seed)
+    audio = speech_like(np.random.default_rng(12345), int(seconds * 16000))
+    n_new = int(round(FORCE_TPS * seconds)) + 1
+    t0 = time.perf_counter()
+    mel, tv = oracle.mel(audio)
+    emb = model.encode(mel, tv)
+    n_audio = emb.shape[0]
+    prompt = ([151644, 8948, 198, 151645, 198, 151644, 872, 198, 151669] + [151676] * n_audio +
+              [151670, 151645, 198, 151644, 77091, 198])
+    kv = oracle.KV(model, len(prompt) + n_new + 8)
+    toks = kv.generate(prompt, 151676, emb, eos=(), max_new=n_new, force_len=n_new)
+    dt = time.perf_counter() - t0
+    assert len(toks) == n_new
+    return {"value": round(seconds / dt, 4), "unit": "audio-s/s", "cores": oracle.num_threads(), "kind": "port",
+            "sample": f"one {seconds:g} s segment, Qwen3-ASR-1.7B shapes (synthetic Q8_0), {n_new} forced tokens, "
+                      f"oracle/qasr_oracle.c W8A8 with OpenMP ({dt:.1f} s wall)"}
+
+
+def main():
+    global SEG_PER_RANK
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--arch", default="qwen3-asr-1.7b")
+    ap.add_argument("--segments", type=int, default=SEG_PER_RANK)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-prof", action="store_true")
+    args = ap.parse_args()
+
+    SEG_PER_RANK = args.segments
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import torch
+    import torch.distributed as dist
+
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from qasr import _lib
+    from qasr.transcribe_cpp import Model
+
+    lib = _lib.load()
+    _lib.check(lib.qasr_set_device(local))
+    audio = make_workload(world, rank)
+    lens = [a.size for a in audio]
+    offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int64)
+    dev = torch.from_numpy(np.concatenate(audio)).to(f"cuda:{local}")   # inputs resident in HBM
+    torch.cuda.synchronize()
+    audio_s = sum(lens) / 16000.0
+
+    model = Model.synthetic(args.arch, seed=0)
+    sess = model.session(kv_type="f16", n_ctx=32768)
+
+    def step():
+        sess.run_batch_device(dev.data_ptr(), offs, lens, force_tokens_per_s=FORCE_TPS, want_results=False)
+
+    for _ in range(args.warmup):
+        step()
+
+    def barrier():
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    if not args.no_prof:
+        _lib.check(lib.qasr_prof_reset())
+        _lib.check(lib.qasr_prof_enable(1))
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    prof = {}
+    if not args.no_prof:
+        _lib.check(lib.qasr_prof_enable(0))
+        need = C.c_size_t()
+        lib.qasr_prof_report(None, 0, C.byref(need))
+        buf = C.create_string_buffer(need.value)
+        _lib.check(lib.qasr_prof_report(buf, need.value, C.byref(need)))
+        prof = json.loads(buf.value.decode())
+    t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+    tot = torch.tensor([audio_s * args.steps], dtype=torch.float64, device=f"cuda:{local}")
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+    elapsed, total_audio = float(t.item()), float(tot.item())
+
+    if rank == 0:
+        # roofline of the dominant kernel class (most device time inside the timed region)
+        roof = None
+        if prof:
+            name, p = max(prof.items(), key=lambda kv: kv[1]["ms"])
+            avg_s = p["ms"] / p["count"] / 1e3
+            if name in ("gemm_q8", "conv3x3_f16", "mel_frames"):
+                peak = 5000.0 if name == "gemm_q8" else 2500.0   # dense i8 / f16 MFMA (MI355X_MICROARCH.md)
+                ach = p["flops"] / p["count"] / avg_s / 1e12
+                roof = {"bound": "mfma", "kernel": name, "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
+                        "frac": round(ach / peak, 4), "traffic": None,
+                        "avg_launch_us": round(avg_s * 1e6, 2), "launches": p["count"]}
+            else:
+                ach = p["bytes"] / p["count"] / avg_s / 1e9
+                roof = {"bound": "hbm", "kernel": name, "achieved": round(ach, 1), "peak": 8000.0, "unit": "GB/s",
+                        "frac": round(ach / 8000.0, 4), "traffic": None,
+                        "avg_launch_us": round(avg_s * 1e6, 2), "launches": p["count"]}
+            roof["breakdown_ms"] = {k: round(v["ms"], 3) for k, v in sorted(prof.items(), key=lambda kv: -kv[1]["ms"])}
+        cpu = None
+        if not args.no_cpu_baseline:
+            try:
+                cpu = cpu_baseline()
+            except Exception as e:  # noqa: BLE001 — reported, never fatal for the GPU number
+                cpu = {"value": None, "error": str(e)}
+        value = total_audio / elapsed
+        line = {
+            "metric": "audio-sec/wall-sec (RTF⁻¹) Qwen3-ASR-1.7B Q8",
+            "value": round(value, 2),
+            "unit": "audio-s/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 2),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "i8",
+            "data": "synthetic (seeded speech-like 16 kHz audio; seeded synthetic Q8_0 weights with 1.7B shapes)",
+            "config": {"workload": f"C4: {SEG_PER_RANK} VAD-split segments/rank, U[2,12] s, LPT-sharded, "
+                                   f"{FORCE_TPS} forced tokens/audio-s",
+                       "model": args.arch, "segments_per_rank": SEG_PER_RANK,
+                       "audio_s_per_rank": round(audio_s, 1), "parallelism": f"dp{world}"},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line, ensure_ascii=False), flush=True)
+    sess.close()
+    model.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -184,6 +184,13 @@ QASR_API int qasr_op_mel(const float* pcm, int64_t n, int32_t n_mels, float* mel
 QASR_API int qasr_op_fbank(const float* pcm, int64_t n, float* feats /*[T][80]*/, void* stream);
 QASR_API int qasr_stream_sync(void* stream);
 
+/* -------------------------------------------------------------------------------------------- profiling */
+/* live per-kernel-class timing (hipEvents on each instrumented launch's stream) + algorithmic FLOPs/bytes;
+   report = JSON {"gemm_q8": {"count", "ms", "flops", "bytes"}, ...}.  Used by bench.py for its roofline. */
+QASR_API int qasr_prof_enable(int on);
+QASR_API int qasr_prof_reset(void);
+QASR_API int qasr_prof_report(char* buf, size_t cap, size_t* needed);
+
 #ifdef __cplusplus
 }
 #endif

@@ -42,3 +42,26 @@ QASR_API int qasr_set_device(int device) {
 }
 
 }  // extern "C"
+
+#include "prof.h"
+
+extern "C" {
+
+QASR_API int qasr_prof_enable(int on) {
+    return guard([&] { qasr::prof_set(on != 0); });
+}
+
+QASR_API int qasr_prof_reset(void) {
+    return guard([&] { qasr::prof_reset(); });
+}
+
+QASR_API int qasr_prof_report(char* buf, size_t cap, size_t* needed) {
+    return guard([&] {
+        std::string r = qasr::prof_report();
+        if (needed) *needed = r.size() + 1;
+        QASR_CHECK(!buf || cap > r.size(), QASR_E_CAPACITY, "report buffer too small");
+        if (buf) memcpy(buf, r.c_str(), r.size() + 1);
+    });
+}
+
+}  // extern "C"

@@ -239,6 +239,8 @@ void Session::encoder(FrontEnd& fe, float* enc_out_dbg) {
     }
     int* d_kvs = upload(S_KVS, kvs);
     int* d_kvl = upload(S_KVL, kvl);
+    int64_t total_keys = 0;
+    for (int v : kvl) total_keys += v;
     float* hs = (float*)sc_.get(S_HS, (size_t)N * d * sizeof(float));
     const int kmax = std::max(d, F);
     int8_t* xq = (int8_t*)sc_.get(S_XQ, (size_t)N * kmax);
@@ -253,7 +255,7 @@ void Session::encoder(FrontEnd& fe, float* enc_out_dbg) {
         linear_q8(xq, xd, N, e.qkv, e.qkv_b, nullptr, qkv, 3 * d, EPI_STORE, st_);
         to_f16(qkv, N, 3 * d, 3 * d, qkvh, 3 * d, st_);
         attention(qkvh, 3 * d, qkvh + d, qkvh + 2 * d, 3 * d, d_kvs, d_kvl, N, h.enc_heads, h.enc_heads, d / h.enc_heads,
-                  scale, nullptr, xq, xd, st_);
+                  scale, nullptr, xq, xd, st_, total_keys);
         linear_q8(xq, xd, N, e.o, e.o_b, hs, hs, d, EPI_RESID, st_);
         layernorm_q8(hs, N, d, e.ln2_w, e.ln2_b, h.ln_eps, xq, xd, nullptr, st_);
         linear_q8(xq, xd, N, e.up, e.up_b, nullptr, ff, F, EPI_GELU, st_);
@@ -270,7 +272,7 @@ void Session::encoder(FrontEnd& fe, float* enc_out_dbg) {
 
 // ------------------------------------------------------------------------------------------ decoder
 void Session::decoder_layers(float* x, int rows, const int* d_pos, const int* d_slot, const int* d_kvs,
-                             const int* d_kvl) {
+                             const int* d_kvl, int64_t total_keys) {
     const qasr_hparams& h = m_->hp;
     const int H = h.txt_h, F = h.txt_ffn, nh = h.txt_heads, nkv = h.txt_kv_heads, hd = h.head_dim;
     const int QD = nh * hd, KD = nkv * hd;
@@ -289,7 +291,7 @@ void Session::decoder_layers(float* x, int rows, const int* d_pos, const int* d_
         rmsnorm_q8(x, rows, H, H, L.attn_norm, h.rms_eps, xq, xd, st_);
         linear_q8(xq, xd, rows, L.qkv, nullptr, nullptr, qkv, QD + 2 * KD, EPI_STORE, st_);
         qk_norm_rope(qkv, rows, nh, nkv, hd, d_pos, d_slot, L.q_norm, L.k_norm, rope_, h.rms_eps, qh, kc, vc, st_);
-        attention(qh, QD, kc, vc, KD, d_kvs, d_kvl, rows, nh, nkv, hd, scale, nullptr, xq, xd, st_);
+        attention(qh, QD, kc, vc, KD, d_kvs, d_kvl, rows, nh, nkv, hd, scale, nullptr, xq, xd, st_, total_keys);
         linear_q8(xq, xd, rows, L.o, nullptr, x, x, H, EPI_RESID, st_);
         rmsnorm_q8(x, rows, H, H, L.ffn_norm, h.rms_eps, xq, xd, st_);
         linear_q8(xq, xd, rows, L.gu, nullptr, nullptr, gu, 2 * F, EPI_STORE, st_);
@@ -367,7 +369,9 @@ void Session::run_batch(const float* dpcm, const std::vector<int64_t>& off, cons
         float* x = (float*)sc_.get(S_X, (size_t)T * H * sizeof(float));
         float* emb = (float*)sc_.get(S_EMB, (size_t)fe.total_tokens * H * sizeof(float));
         embed_rows(d_ids, T, m_->tok_embd, emb, x, st_);
-        decoder_layers(x, T, d_pos, d_slot, d_kvs, d_kvl);
+        int64_t keys = 0;
+        for (int v : kvl) keys += v;
+        decoder_layers(x, T, d_pos, d_slot, d_kvs, d_kvl, keys);
         int* d_last = upload(S_LAST, last);
         float* xn = (float*)sc_.get(S_XN, (size_t)count * H * sizeof(float));
         k_gather_rows<<<(unsigned)cdiv64((int64_t)count * H, 256), 256, 0, st_>>>(x, d_last, count, H, xn);
@@ -418,7 +422,9 @@ void Session::run_batch(const float* dpcm, const std::vector<int64_t>& off, cons
         QASR_HIP(hipMemcpyAsync(dt, hp, (size_t)A * 5 * sizeof(int32_t), hipMemcpyHostToDevice, st_));
         float* x = (float*)sc_.get(S_X, (size_t)A * H * sizeof(float));
         embed_rows(dt, A, m_->tok_embd, nullptr, x, st_);
-        decoder_layers(x, A, dt + A, dt + 2 * A, dt + 3 * A, dt + 4 * A);
+        int64_t keys = 0;
+        for (int v : skvl) keys += v;
+        decoder_layers(x, A, dt + A, dt + 2 * A, dt + 3 * A, dt + 4 * A, keys);
         float* logits = (float*)sc_.get(S_LOGITS, (size_t)A * V * sizeof(float));
         lm_head_rows(x, A, H, logits);
         int* d_tok = (int*)sc_.get(S_TOK, A * sizeof(int));
@@ -538,7 +544,7 @@ void Session::prefill_logits_host(const float* embeds, int n, std::vector<float>
     int* d_slot = upload(S_SLOT, slot);
     int* d_kvs = upload(S_KVS, kvs);
     int* d_kvl = upload(S_KVL, kvl);
-    decoder_layers(x, n, d_pos, d_slot, d_kvs, d_kvl);
+    decoder_layers(x, n, d_pos, d_slot, d_kvs, d_kvl, (int64_t)n * (n + 1) / 2);
     float* lg = (float*)sc_.get(S_LOGITS, (size_t)n * h.vocab * sizeof(float));
     lm_head_rows(x, n, h.txt_h, lg);
     logits.resize((size_t)n * h.vocab);
@@ -573,7 +579,8 @@ void Session::forced_logits_host(const float* pcm, int64_t n, const int32_t* for
     float* x = (float*)sc_.get(S_X, (size_t)std::max(P, 1) * H * sizeof(float));
     float* emb = (float*)sc_.get(S_EMB, (size_t)fe.total_tokens * H * sizeof(float));
     embed_rows(d_ids, P, m_->tok_embd, emb, x, st_);
-    decoder_layers(x, P, upload(S_POS, pos), upload(S_SLOT, slot), upload(S_KVS, kvs), upload(S_KVL, kvl));
+    decoder_layers(x, P, upload(S_POS, pos), upload(S_SLOT, slot), upload(S_KVS, kvs), upload(S_KVL, kvl),
+                   (int64_t)P * (P + 1) / 2);
     float* lg = (float*)sc_.get(S_LOGITS, (size_t)V * sizeof(float));
     lm_head_rows(x + (size_t)(P - 1) * H, 1, H, lg);
     QASR_HIP(hipMemcpyAsync(logits.data(), lg, (size_t)V * sizeof(float), hipMemcpyDeviceToHost, st_));
@@ -583,7 +590,7 @@ void Session::forced_logits_host(const float* pcm, int64_t n, const int32_t* for
         int* di = upload(S_IDS, one_id);
         embed_rows(di, 1, m_->tok_embd, nullptr, x, st_);
         decoder_layers(x, 1, upload(S_POS, one_pos), upload(S_SLOT, one_slot), upload(S_KVS, one_kvs),
-                       upload(S_KVL, one_kvl));
+                       upload(S_KVL, one_kvl), p + 1);
         lm_head_rows(x, 1, H, lg);
         QASR_HIP(hipMemcpyAsync(logits.data() + (size_t)(i + 1) * V, lg, (size_t)V * sizeof(float),
                                 hipMemcpyDeviceToHost, st_));

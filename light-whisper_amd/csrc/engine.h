@@ -65,7 +65,8 @@ class Session {
     void front_end(const float* dpcm, const std::vector<int64_t>& off, const std::vector<int64_t>& len, FrontEnd& fe,
                    float* enc_out_dbg);
     void encoder(FrontEnd& fe, float* enc_out_dbg);
-    void decoder_layers(float* x, int rows, const int* d_pos, const int* d_slot, const int* d_kvs, const int* d_kvl);
+    void decoder_layers(float* x, int rows, const int* d_pos, const int* d_slot, const int* d_kvs, const int* d_kvl,
+                        int64_t total_keys);
     void ensure_kv(int64_t slots);
     void lm_head_rows(const float* x, int rows, int ldx, float* logits);
     template <class T>

@@ -2,6 +2,7 @@
 // Every wrapper takes device pointers and a stream; none allocates or synchronises (graph-capturable).
 #pragma once
 #include "common.h"
+#include "prof.h"
 
 namespace qasr {
 
@@ -49,6 +50,6 @@ void add_posemb_gather(const float* proj, int n_chunks, int T, int d, const floa
 // output quantised (q/d, row stride nh*hd) and/or f32 (o)
 void attention(const __half* Q, int ldq, const __half* K, const __half* V, int ldkv, const int* kv_start,
                const int* kv_len, int rows, int nh, int nkv, int hd, float scale, float* o, int8_t* oq, float* od,
-               hipStream_t s);
+               hipStream_t s, int64_t total_keys = 0);
 
 }  // namespace qasr

@@ -147,8 +147,10 @@ __global__ __launch_bounds__(256) void k_attention(const __half* __restrict__ Q,
 
 void attention(const __half* Q, int ldq, const __half* K, const __half* V, int ldkv, const int* kv_start,
                const int* kv_len, int rows, int nh, int nkv, int hd, float scale, float* o, int8_t* oq, float* od,
-               hipStream_t s) {
+               hipStream_t s, int64_t total_keys) {
     if (rows <= 0) return;
+    // QKᵀ + PV: 4·hd flops per (query head, key); f16 K/V bytes read per (query head, key)
+    ProfScope ps(s, "attention", 4.0 * hd * nh * (double)total_keys, 4.0 * hd * nh * (double)total_keys);
     const int waves = rows * nh;
     if (hd == 128)
         k_attention<128><<<cdiv(waves, 4), 256, 0, s>>>(Q, ldq, K, V, ldkv, kv_start, kv_len, rows, nh, nkv, scale, o, oq, od);

@@ -3,6 +3,7 @@
 #include <vector>
 
 #include "common.h"
+#include "prof.h"
 
 namespace qasr {
 

@@ -148,6 +148,7 @@ __global__ __launch_bounds__(256) void k_mel_frames(const float* __restrict__ pc
 void mel_frames(const float* pcm, const MelUtt* utts, const int2* work, int n_work, int n_mels, const float* basis,
                 const float* filt, float* lm, unsigned* umax, hipStream_t s) {
     if (n_work <= 0) return;
+    ProfScope ps(s, "mel_frames", (double)n_work * 16 * (400.0 * 402 * 2 + 201.0 * n_mels * 2), (double)n_work * 16 * (640 + 4.0 * n_mels));
     k_mel_frames<<<n_work, 256, 0, s>>>(pcm, utts, work, n_mels, basis, filt, lm, umax);
 }
 
@@ -213,6 +214,7 @@ void conv1_gelu(const float* x, int n_chunks, int n_mels, const __half* w, const
                 hipStream_t s) {
     const int64_t n = (int64_t)n_chunks * ((n_mels + 1) / 2) * 50 * C;
     if (n <= 0) return;
+    ProfScope ps(s, "conv1", (double)n * 18, (double)n * 2);
     k_conv1_gelu<<<(unsigned)cdiv64(n, 256), 256, 0, s>>>(x, n_chunks, n_mels, w, b, C, y);
 }
 
@@ -316,6 +318,7 @@ void conv3x3_gelu(const __half* in, int n_chunks, int Hi, int Wi, const __half* 
     const int M = n_chunks * ((Hi + 1) / 2) * ((Wi + 1) / 2);
     if (M <= 0) return;
     QASR_CHECK(C % 32 == 0, QASR_E_INVALID, "conv channels must be a multiple of 32");
+    ProfScope ps(s, "conv3x3_f16", 2.0 * M * C * 9.0 * C, (double)M * 9 * C * 2 / 4 + (double)M * C * 2);
     dim3 grid(cdiv(C, CT), cdiv(M, CT));
     k_conv3x3_gelu<<<grid, 256, 0, s>>>(in, n_chunks, Hi, Wi, w, b, C, out, out_mode);
 }

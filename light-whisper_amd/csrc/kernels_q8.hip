@@ -196,8 +196,15 @@ __global__ __launch_bounds__(256) void k_gemv_q8(const int8_t* __restrict__ W, c
     }
 }
 
+static double q8_bytes(int M, const Q8Mat& W, int epi) {
+    // weights (int8 + f16 scale per 32) + activations (int8 + f32 scale per 32) + f32 output (+ residual read)
+    return (double)W.N * W.K * (1.0 + 2.0 / 32) + (double)M * W.K * (1.0 + 4.0 / 32) +
+           (double)M * W.N * 4.0 * (epi == EPI_RESID ? 2 : 1);
+}
+
 void gemv_q8(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const float* bias, const float* res, float* y,
              int ldy, int epi, hipStream_t s) {
+    ProfScope ps(s, "gemv_q8", 2.0 * M * W.N * W.K, q8_bytes(M, W, epi));
     dim3 grid(cdiv(W.N, 4));
     if (M <= 1) k_gemv_q8<1><<<grid, 256, 0, s>>>(W.qs, W.sc, W.N, W.K, xq, xd, M, bias, res, y, ldy, epi);
     else if (M <= 2) k_gemv_q8<2><<<grid, 256, 0, s>>>(W.qs, W.sc, W.N, W.K, xq, xd, M, bias, res, y, ldy, epi);
@@ -318,6 +325,7 @@ __global__ __launch_bounds__(256) void k_gemm_q8(const int8_t* __restrict__ X, c
 
 void gemm_q8(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const float* bias, const float* res, float* y,
              int ldy, int epi, hipStream_t s) {
+    ProfScope ps(s, "gemm_q8", 2.0 * M * W.N * W.K, q8_bytes(M, W, epi));
     dim3 grid(cdiv(W.N, GB), cdiv(M, GB));
     k_gemm_q8<<<grid, 256, 0, s>>>(xq, xd, M, W.qs, W.sc, W.N, W.K, bias, res, y, ldy, epi);
 }

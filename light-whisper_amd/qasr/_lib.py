@@ -109,6 +109,9 @@ SIGNATURES = {
     "qasr_op_mel": (C.c_int, [P, I64, I32, P, P]),
     "qasr_op_fbank": (C.c_int, [P, I64, P, P]),
     "qasr_stream_sync": (C.c_int, [P]),
+    "qasr_prof_enable": (C.c_int, [C.c_int]),
+    "qasr_prof_reset": (C.c_int, []),
+    "qasr_prof_report": (C.c_int, [C.c_char_p, SZ, C.POINTER(SZ)]),
 }
 
 _LIB = None

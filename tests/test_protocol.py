@@ -1,0 +1,82 @@
+"""The native `engine` speaks the reference's stdio JSON protocol byte-for-byte.
+
+Golden: the reference server loop (server_common.py:339-437 + qwen3_asr_server.py) driven with the reference
+tests' fake engine/VAD (test_qwen3_asr_server.py:15-57) — tests/golden/protocol.json.  The native engine is
+run with the same fakes (QASR_PROTOCOL_TEST_FAKE=1, no GPU needed); wall-clock fields are normalised.
+"""
+import json
+import os
+import re
+import subprocess
+
+import pytest
+
+from qasr import _lib
+
+G = os.path.join(os.path.dirname(__file__), "golden", "protocol.json")
+TIMING_KEYS = {"vad_ms", "inference_ms", "average_inference_ms", "average_vad_ms"}
+
+
+def _norm(obj):
+    if isinstance(obj, dict):
+        return {k: (type(v).__name__ if k in TIMING_KEYS else _norm(v)) for k, v in obj.items()}
+    if isinstance(obj, str):
+        return re.sub(r"耗时: [0-9.]+秒", "耗时: <t>秒", obj)
+    return obj
+
+
+def _run_engine(lines, env_extra, args=("serve", "--engine", "qwen3-asr-1.7b")):
+    env = dict(os.environ, QASR_PROTOCOL_TEST_FAKE="1", **env_extra)
+    return subprocess.run([_lib.ENGINE_PATH, *args], input="\n".join(lines) + "\n", capture_output=True, text=True,
+                          env=env, timeout=60)
+
+
+@pytest.fixture(scope="module")
+def golden():
+    return json.load(open(G, encoding="utf-8"))
+
+
+def test_transcript_matches_reference(golden, tmp_path):
+    res = _run_engine(golden["requests"], {"LIGHT_WHISPER_DATA_DIR": str(tmp_path), "HF_HUB_CACHE": str(tmp_path)})
+    assert res.returncode == 0, res.stderr
+    got = [ln for ln in res.stdout.splitlines() if ln.strip()]
+    want = golden["replies"]
+    # the reply after "exit" is never produced (the server stops reading)
+    assert len(got) == len(want)
+    for g, w in zip(got, want):
+        gj, wj = json.loads(g), json.loads(w)
+        assert _norm(gj) == _norm(wj), (g, w)
+        # key order and separators are part of the wire format (json.dumps(ensure_ascii=False))
+        assert list(gj) == list(wj)
+        if not (TIMING_KEYS & set(gj)) and "耗时" not in g and "stats" not in gj:
+            assert g == w
+    assert os.path.exists(os.path.join(tmp_path, "logs", "qwen3_asr_server.log"))
+
+
+def test_stdout_is_protocol_only(golden, tmp_path):
+    res = _run_engine(['{"action": "status", "request_id": 7}', '{"action": "exit"}'],
+                      {"LIGHT_WHISPER_DATA_DIR": str(tmp_path)})
+    lines = res.stdout.splitlines()
+    assert all(json.loads(ln) is not None for ln in lines)
+    assert json.loads(lines[1])["request_id"] == 7
+
+
+def test_eof_exits_cleanly(tmp_path):
+    res = _run_engine([], {"LIGHT_WHISPER_DATA_DIR": str(tmp_path)})
+    assert res.returncode == 0
+    assert json.loads(res.stdout.splitlines()[0])["success"] is True
+
+
+def test_cli_rejects_unknown_engine(tmp_path):
+    res = _run_engine([], {"LIGHT_WHISPER_DATA_DIR": str(tmp_path)}, args=("serve", "--engine", "whisper-large"))
+    assert res.returncode == 2
+
+
+def test_models_not_downloaded_without_fake(tmp_path):
+    env = {k: v for k, v in os.environ.items() if k not in ("QASR_PROTOCOL_TEST_FAKE", "QASR_SYNTHETIC")}
+    env.update(LIGHT_WHISPER_DATA_DIR=str(tmp_path), HF_HUB_CACHE=str(tmp_path))
+    res = subprocess.run([_lib.ENGINE_PATH, "serve", "--engine", "qwen3-asr-0.6b"], input="", capture_output=True,
+                         text=True, env=env, timeout=60)
+    first = json.loads(res.stdout.splitlines()[0])
+    assert first == {"success": False, "error": "Qwen3-ASR Q8 模型未下载: Qwen3-ASR-0.6B-Q8_0.gguf",
+                     "type": "models_not_downloaded", "engine": "qwen3-asr-0.6b"}
