@@ -159,7 +159,9 @@ QASR_API int qasr_resample_linear(const float* x, size_t n, int32_t source_rate,
 /* -------------------------------------------------------------------------------------------- kernel ops */
 QASR_API int qasr_op_quant_rows(const float* x, int32_t M, int32_t K, int32_t ldx, int8_t* q, float* d, void* stream);
 QASR_API int qasr_op_repack_q8(const uint8_t* blocks, int64_t nblk, int8_t* qs, void* sc, void* stream);
-/* path: 0 auto, 1 GEMV, 2 MFMA GEMM; epi: 0 store, 1 residual, 2 gelu */
+/* path: 0 auto, 1 GEMV, 2 MFMA GEMM; 16 + cfg + 8*splits: MFMA GEMM with a forced tile config (0 128x128,
+ * 1 64x128, 2 64x64, 3 32x64, 7 heuristic) and split-K count (0 heuristic) — tuning only.
+ * epi: 0 store, 1 residual, 2 gelu */
 QASR_API int qasr_op_linear_q8(const int8_t* xq, const float* xd, int32_t M, const int8_t* wqs, const void* wsc,
                                int32_t N, int32_t K, const float* bias, const float* res, float* y, int32_t ldy,
                                int32_t epi, int32_t path, void* stream);

@@ -49,6 +49,9 @@ QASR_API int qasr_op_linear_q8(const int8_t* xq, const float* xd, int32_t M, con
             gemv_q8(xq, xd, M, W, bias, res, y, ldy, epi, S(stream));
         } else if (path == 2) {
             gemm_q8(xq, xd, M, W, bias, res, y, ldy, epi, S(stream));
+        } else if (path >= 16) {
+            const int cfg = (path - 16) & 7, splits = (path - 16) >> 3;
+            gemm_q8(xq, xd, M, W, bias, res, y, ldy, epi, S(stream), cfg == 7 ? -1 : cfg, splits);
         } else {
             linear_q8(xq, xd, M, W, bias, res, y, ldy, epi, S(stream));
         }

@@ -1,11 +1,12 @@
 // Variable-length attention over f16 K/V (decoder KV cache slots or encoder window buffers), gfx950.
 //
 // One wave per (query row, head).  Keys are processed in LDS-resident chunks of 256 with an online softmax
-// (running max / sum, f32): QKᵀ uses 8 lanes per key (16-dim slices, 3 xor-shuffles to reduce), PV uses
-// one 4-byte (half2) V load per lane per key so each V row is read as one coalesced 256-byte segment.
-// Row r attends slots [kv_start[r], kv_start[r]+kv_len[r]) — causal prefill, single-token decode and the
-// encoder's bidirectional 104-token windows (modeling_qwen3_asr.py:276-315) are all expressed by the
-// per-row ranges.  The output is written as f32 and/or directly as Q8 blocks for the O-projection.
+// (running max / sum, f32).  QKᵀ: 8 lanes per key (16-dim slices, 3 xor-shuffles), 32 keys per unrolled
+// iteration so eight 16-byte K loads per lane are in flight together.  PV: each lane owns hd/64 dims and
+// walks the keys 8 at a time with eight independent 4-byte V loads in flight (each V row is one coalesced
+// 256-byte segment).  Row r attends slots [kv_start[r], kv_start[r]+kv_len[r]) — causal prefill, single-token
+// decode and the encoder's bidirectional 104-token windows (modeling_qwen3_asr.py:276-315) are all expressed
+// by the per-row ranges.  The output is written as f32 and/or directly as Q8 blocks for the O-projection.
 #include "kernels.h"
 
 namespace qasr {
@@ -20,6 +21,36 @@ __device__ __forceinline__ float wsum_a(float v) {
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
     return v;
 }
+__device__ __forceinline__ void wave_sync_lds() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <int QD>
+__device__ __forceinline__ float qk_dot(const float* qv, const __half* kr) {
+    float part = 0.f;
+    if constexpr (QD == 16) {
+        const int4 a = *(const int4*)kr, b = *(const int4*)(kr + 8);
+        const __half2* ha = (const __half2*)&a;
+        const __half2* hb = (const __half2*)&b;
+#pragma unroll
+        for (int t = 0; t < 4; t++) {
+            const float2 fa = __half22float2(ha[t]), fb = __half22float2(hb[t]);
+            part += qv[2 * t] * fa.x + qv[2 * t + 1] * fa.y;
+            part += qv[8 + 2 * t] * fb.x + qv[8 + 2 * t + 1] * fb.y;
+        }
+    } else {
+        const int4 a = *(const int4*)kr;
+        const __half2* ha = (const __half2*)&a;
+#pragma unroll
+        for (int t = 0; t < 4; t++) {
+            const float2 fa = __half22float2(ha[t]);
+            part += qv[2 * t] * fa.x + qv[2 * t + 1] * fa.y;
+        }
+    }
+    return part;
+}
 
 template <int HD>
 __global__ __launch_bounds__(256) void k_attention(const __half* __restrict__ Q, int ldq, const __half* __restrict__ K,
@@ -30,6 +61,8 @@ __global__ __launch_bounds__(256) void k_attention(const __half* __restrict__ Q,
     constexpr int CH = 256;
     constexpr int QD = HD / 8;    // dims per lane in QKᵀ
     constexpr int PD = HD / 64;   // dims per lane in PV / output
+    constexpr int KU = 4;         // 8-key groups per QKᵀ iteration
+    constexpr int VU = 8;         // keys per PV iteration
     __shared__ float sp[4][CH];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int g = blockIdx.x * 4 + w;
@@ -50,42 +83,30 @@ __global__ __launch_bounds__(256) void k_attention(const __half* __restrict__ Q,
     for (int j = 0; j < PD; j++) acc[j] = 0.f;
     float m = -INFINITY, lsum = 0.f;
     float* spw = sp[w];
+    const __half* kbase = K + (size_t)kvh * HD + sub * QD;
+    const __half* vbase = V + (size_t)kvh * HD + lane * PD;
 
     for (int c0 = 0; c0 < L; c0 += CH) {
         const int n = min(CH, L - c0);
-        for (int j0 = 0; j0 < n; j0 += 8) {
-            const int j = j0 + kk;
-            float part = 0.f;
-            if (j < n) {
-                const __half* kr = K + (size_t)(s0 + c0 + j) * ldkv + kvh * HD + sub * QD;
-                if constexpr (QD == 16) {
-                    const int4 a = *(const int4*)kr, b = *(const int4*)(kr + 8);
-                    const __half2* ha = (const __half2*)&a;
-                    const __half2* hb = (const __half2*)&b;
+        const __half* kc = kbase + (size_t)(s0 + c0) * ldkv;
+        for (int j0 = 0; j0 < n; j0 += 8 * KU) {
+            float part[KU];
 #pragma unroll
-                    for (int t = 0; t < 4; t++) {
-                        float2 fa = __half22float2(ha[t]), fb = __half22float2(hb[t]);
-                        part += qv[2 * t] * fa.x + qv[2 * t + 1] * fa.y;
-                        part += qv[8 + 2 * t] * fb.x + qv[8 + 2 * t + 1] * fb.y;
-                    }
-                } else {
-                    const int4 a = *(const int4*)kr;
-                    const __half2* ha = (const __half2*)&a;
-#pragma unroll
-                    for (int t = 0; t < 4; t++) {
-                        float2 fa = __half22float2(ha[t]);
-                        part += qv[2 * t] * fa.x + qv[2 * t + 1] * fa.y;
-                    }
-                }
+            for (int u = 0; u < KU; u++) {
+                const int j = j0 + u * 8 + kk;
+                part[u] = j < n ? qk_dot<QD>(qv, kc + (size_t)j * ldkv) : 0.f;
             }
-            part += __shfl_xor(part, 1);
-            part += __shfl_xor(part, 2);
-            part += __shfl_xor(part, 4);
-            if (sub == 0 && j < n) spw[j] = part * scale;
+#pragma unroll
+            for (int u = 0; u < KU; u++) {
+                float p = part[u];
+                p += __shfl_xor(p, 1);
+                p += __shfl_xor(p, 2);
+                p += __shfl_xor(p, 4);
+                const int j = j0 + u * 8 + kk;
+                if (sub == 0 && j < n) spw[j] = p * scale;
+            }
         }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        wave_sync_lds();
         float cm = -INFINITY;
         for (int i = lane; i < n; i += 64) cm = fmaxf(cm, spw[i]);
         cm = wmax(cm);
@@ -101,23 +122,40 @@ __global__ __launch_bounds__(256) void k_attention(const __half* __restrict__ Q,
         }
         lsum = lsum * alpha + wsum_a(ps);
         m = mnew;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        const __half* vb = V + (size_t)(s0 + c0) * ldkv + kvh * HD + lane * PD;
-        for (int j = 0; j < n; j++) {
+        wave_sync_lds();
+        const __half* vb = vbase + (size_t)(s0 + c0) * ldkv;
+        int j = 0;
+        for (; j + VU <= n; j += VU) {
+            if constexpr (PD == 2) {
+                __half2 vv[VU];
+#pragma unroll
+                for (int u = 0; u < VU; u++) vv[u] = *(const __half2*)(vb + (size_t)(j + u) * ldkv);
+#pragma unroll
+                for (int u = 0; u < VU; u++) {
+                    const float p = spw[j + u];
+                    const float2 f = __half22float2(vv[u]);
+                    acc[0] += p * f.x;
+                    acc[1] += p * f.y;
+                }
+            } else {
+                __half vv[VU];
+#pragma unroll
+                for (int u = 0; u < VU; u++) vv[u] = vb[(size_t)(j + u) * ldkv];
+#pragma unroll
+                for (int u = 0; u < VU; u++) acc[0] += spw[j + u] * __half2float(vv[u]);
+            }
+        }
+        for (; j < n; j++) {
             const float p = spw[j];
             if constexpr (PD == 2) {
-                const float2 vv = __half22float2(*(const __half2*)(vb + (size_t)j * ldkv));
-                acc[0] += p * vv.x;
-                acc[1] += p * vv.y;
+                const float2 f = __half22float2(*(const __half2*)(vb + (size_t)j * ldkv));
+                acc[0] += p * f.x;
+                acc[1] += p * f.y;
             } else {
                 acc[0] += p * __half2float(vb[(size_t)j * ldkv]);
             }
         }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        wave_sync_lds();
     }
     const float inv = L > 0 ? 1.f / lsum : 0.f;
     float out[PD];

@@ -4,6 +4,8 @@
 // Arithmetic contract (ggml Q8_0 conventions behind transcribe_cpp, qwen3_asr_server.py:321):
 //   activation block (32): d = amax/127 (f32), q = roundf(x/d) (IEEE division), d kept as f16
 //   block dot: exact int32 Σ q_w·q_x, contribution (float)sum · (d_w·d_x), f32 accumulation.
+#include <algorithm>
+
 #include "kernels.h"
 
 namespace qasr {
@@ -213,121 +215,205 @@ void gemv_q8(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const flo
 }
 
 // ------------------------------------------------------------------------------------------------ GEMM (MFMA)
-// 64×64 output tile, 256 threads (4 waves, 2×2), each wave 32×32 = 2×2 v_mfma_i32_16x16x32_i8 tiles.
-// K step = 64 (two Q8 blocks); A (activations) and B (weights, stored [N][K]) staged in LDS with an 80-byte
-// row stride (conflict-free ds_read_b64 fragments); the next step is prefetched into registers while
-// the current one is consumed.  Each 16×16×32 MFMA produces the exact int32 block sum of one Q8 block,
-// rescaled into the f32 accumulator by d_x(row)·d_w(col).
-constexpr int GB = 64;       // tile M and N
-constexpr int GK = 64;       // K per step
-constexpr int GLDS = 80;     // LDS row stride (bytes)
+// Tile (32·TI)×(32·TJ), 256 threads = 2×2 waves, each wave (16·TI)×(16·TJ) built from
+// v_mfma_i32_16x16x32_i8: one MFMA yields the exact int32 sum of one Q8 block for a 16×16 sub-tile, which is
+// rescaled into the f32 accumulator by d_x(row)·d_w(col) (3 VALU ops per output and block — with the MFMA
+// this is the whole inner loop).  K step = 128 (four Q8 blocks).  A (activations [M][K]) and B (weights
+// [N][K]) are staged through double-buffered LDS with a 144-byte row stride (conflict-free ds_read_b64
+// fragments); block scales are stored block-major and lane-permuted so each lane fetches its 4 row scales
+// and its TJ column scales with one ds_read_b128 each.  Step s+1 is loaded into registers while step s is
+// consumed, one barrier per step.
+// Split-K over grid.z fills the chip when M·N has few tiles (decode): partial sums are added with f32 atomics
+// (y pre-zeroed for a plain store; the residual already sits in y), the bias is added by split 0.
+constexpr int GBK = 128;     // K per step
+constexpr int GLD = 144;     // LDS row stride (bytes)
 
+template <int TI, int TJ>
 __global__ __launch_bounds__(256) void k_gemm_q8(const int8_t* __restrict__ X, const float* __restrict__ Xd, int M,
                                                  const int8_t* __restrict__ W, const __half* __restrict__ Wsc, int N,
                                                  int K, const float* __restrict__ bias, const float* res, float* y,
-                                                 int ldy, int epi) {
-    __shared__ __attribute__((aligned(16))) int8_t As[GB * GLDS];
-    __shared__ __attribute__((aligned(16))) int8_t Bs[GB * GLDS];
-    __shared__ float Asc[GB * 2];
-    __shared__ float Bsc[GB * 2];
+                                                 int ldy, int epi, int steps_per_split) {
+    constexpr int BM = 32 * TI, BN = 32 * TJ;
+    constexpr int ACH = BM * 8 / 256, BCH = BN * 8 / 256;     // 16-byte chunks per thread per step
+    constexpr int ASC = (BM * 4 + 255) / 256, BSC = (BN * 4 + 255) / 256;
+    __shared__ __attribute__((aligned(16))) int8_t As[2][BM * GLD];
+    __shared__ __attribute__((aligned(16))) int8_t Bs[2][BN * GLD];
+    __shared__ __attribute__((aligned(16))) float Asc[2][4 * BM];   // [kb][row]
+    __shared__ __attribute__((aligned(16))) float Bsc[2][4 * BN];   // [kb][wc][fr][j]
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wr = wave >> 1, wc = wave & 1;
-    const int n0 = blockIdx.x * GB, m0 = blockIdx.y * GB;
+    const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM;
     const int nb = K / QK;
+    const int k_begin = blockIdx.z * steps_per_split * GBK;
+    const int k_end = min(K, k_begin + steps_per_split * GBK);
+    const int nsteps = (k_end - k_begin + GBK - 1) / GBK;
 
-    // staging assignment: 16 B per thread for A and for B; 1 scale per thread (A: t<128, B: t>=128)
-    const int srow = tid >> 2, sseg = (tid & 3) * 16;
-    const int am = m0 + srow, bn = n0 + srow;
-    const int sc_row = (tid & 127) >> 1, sc_blk = tid & 1;
-
-    int4 ra, rb;
-    float rs;
+    int4 ra[ACH], rb[BCH];
+    float rsa[ASC], rsb[BSC];
     auto gload = [&](int k0) {
-        const int k = k0 + sseg;
-        ra = (am < M && k < K) ? *(const int4*)(X + (size_t)am * K + k) : make_int4(0, 0, 0, 0);
-        rb = (bn < N && k < K) ? *(const int4*)(W + (size_t)bn * K + k) : make_int4(0, 0, 0, 0);
-        const int kb = (k0 >> 5) + sc_blk;
-        if (tid < 128) {
-            const int r = m0 + sc_row;
-            rs = (r < M && kb < nb) ? Xd[(size_t)r * nb + kb] : 0.f;
-        } else {
-            const int c = n0 + sc_row;
-            rs = (c < N && kb < nb) ? __half2float(Wsc[(size_t)c * nb + kb]) : 0.f;
+#pragma unroll
+        for (int c = 0; c < ACH; c++) {
+            const int ch = tid + 256 * c, gm = m0 + (ch >> 3), k = k0 + (ch & 7) * 16;
+            ra[c] = (gm < M && k < k_end) ? *(const int4*)(X + (size_t)gm * K + k) : make_int4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int c = 0; c < BCH; c++) {
+            const int ch = tid + 256 * c, gn = n0 + (ch >> 3), k = k0 + (ch & 7) * 16;
+            rb[c] = (gn < N && k < k_end) ? *(const int4*)(W + (size_t)gn * K + k) : make_int4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int c = 0; c < ASC; c++) {
+            const int idx = tid + 256 * c, gm = m0 + (idx >> 2), kb = (k0 >> 5) + (idx & 3);
+            rsa[c] = (idx < BM * 4 && gm < M && kb * QK < k_end) ? Xd[(size_t)gm * nb + kb] : 0.f;
+        }
+#pragma unroll
+        for (int c = 0; c < BSC; c++) {
+            const int idx = tid + 256 * c, gn = n0 + (idx >> 2), kb = (k0 >> 5) + (idx & 3);
+            rsb[c] = (idx < BN * 4 && gn < N && kb * QK < k_end) ? __half2float(Wsc[(size_t)gn * nb + kb]) : 0.f;
         }
     };
-    auto lstore = [&]() {
-        *(int4*)(As + srow * GLDS + sseg) = ra;
-        *(int4*)(Bs + srow * GLDS + sseg) = rb;
-        if (tid < 128) Asc[sc_row * 2 + sc_blk] = rs;
-        else Bsc[sc_row * 2 + sc_blk] = rs;
+    auto lstore = [&](int buf) {
+#pragma unroll
+        for (int c = 0; c < ACH; c++) {
+            const int ch = tid + 256 * c;
+            *(int4*)(As[buf] + (ch >> 3) * GLD + (ch & 7) * 16) = ra[c];
+        }
+#pragma unroll
+        for (int c = 0; c < BCH; c++) {
+            const int ch = tid + 256 * c;
+            *(int4*)(Bs[buf] + (ch >> 3) * GLD + (ch & 7) * 16) = rb[c];
+        }
+#pragma unroll
+        for (int c = 0; c < ASC; c++) {
+            const int idx = tid + 256 * c;
+            if (idx < BM * 4) Asc[buf][(idx & 3) * BM + (idx >> 2)] = rsa[c];
+        }
+#pragma unroll
+        for (int c = 0; c < BSC; c++) {
+            const int idx = tid + 256 * c;
+            if (idx < BN * 4) {
+                const int n = idx >> 2, kb = idx & 3;
+                const int w = n / (16 * TJ), rem = n % (16 * TJ);
+                Bsc[buf][kb * BN + w * 16 * TJ + (rem & 15) * TJ + (rem >> 4)] = rsb[c];
+            }
+        }
     };
 
-    float acc[2][2][4];
+    float acc[TI][TJ][4];
 #pragma unroll
-    for (int i = 0; i < 2; i++)
+    for (int i = 0; i < TI; i++)
 #pragma unroll
-        for (int j = 0; j < 2; j++)
+        for (int j = 0; j < TJ; j++)
 #pragma unroll
             for (int r = 0; r < 4; r++) acc[i][j][r] = 0.f;
 
-    const int fr = lane & 15, fk = 8 * (lane >> 4);
-    gload(0);
-    lstore();
+    const int fr = lane & 15, fk = 8 * (lane >> 4), fq = 4 * (lane >> 4);
+    const int arow = wr * 16 * TI, bcol = wc * 16 * TJ;
+    if (nsteps > 0) {
+        gload(k_begin);
+        lstore(0);
+    }
     __syncthreads();
-    for (int k0 = 0; k0 < K; k0 += GK) {
-        const bool more = k0 + GK < K;
-        if (more) gload(k0 + GK);
+    for (int s = 0; s < nsteps; s++) {
+        const int cur = s & 1;
+        const bool more = s + 1 < nsteps;
+        if (more) gload(k_begin + (s + 1) * GBK);
+        const int8_t* as = As[cur];
+        const int8_t* bs = Bs[cur];
+#pragma unroll 1
+        for (int kb = 0; kb < 4; kb++) {
+            long a[TI], b[TJ];
+            float sa[TI][4], sb[TJ];
 #pragma unroll
-        for (int kb = 0; kb < 2; kb++) {
-            long a[2], b[2];
+            for (int i = 0; i < TI; i++) {
+                a[i] = *(const long*)(as + (arow + i * 16 + fr) * GLD + kb * 32 + fk);
+                const float4 v = *(const float4*)(&Asc[cur][kb * BM + arow + i * 16 + fq]);
+                sa[i][0] = v.x, sa[i][1] = v.y, sa[i][2] = v.z, sa[i][3] = v.w;
+            }
 #pragma unroll
-            for (int i = 0; i < 2; i++) a[i] = *(const long*)(As + (wr * 32 + i * 16 + fr) * GLDS + kb * 32 + fk);
+            for (int j = 0; j < TJ; j++) b[j] = *(const long*)(bs + (bcol + j * 16 + fr) * GLD + kb * 32 + fk);
+            if constexpr (TJ == 4) {
+                const float4 v = *(const float4*)(&Bsc[cur][kb * BN + bcol + fr * 4]);
+                sb[0] = v.x, sb[1] = v.y, sb[2] = v.z, sb[3] = v.w;
+            } else if constexpr (TJ == 2) {
+                const float2 v = *(const float2*)(&Bsc[cur][kb * BN + bcol + fr * 2]);
+                sb[0] = v.x, sb[1] = v.y;
+            } else {
 #pragma unroll
-            for (int j = 0; j < 2; j++) b[j] = *(const long*)(Bs + (wc * 32 + j * 16 + fr) * GLDS + kb * 32 + fk);
-            float sa[2][4], sb[2];
+                for (int j = 0; j < TJ; j++) sb[j] = Bsc[cur][kb * BN + bcol + fr * TJ + j];
+            }
 #pragma unroll
-            for (int i = 0; i < 2; i++)
+            for (int i = 0; i < TI; i++) {
 #pragma unroll
-                for (int r = 0; r < 4; r++) sa[i][r] = Asc[(wr * 32 + i * 16 + 4 * (lane >> 4) + r) * 2 + kb];
-#pragma unroll
-            for (int j = 0; j < 2; j++) sb[j] = Bsc[(wc * 32 + j * 16 + fr) * 2 + kb];
-#pragma unroll
-            for (int i = 0; i < 2; i++) {
-#pragma unroll
-                for (int j = 0; j < 2; j++) {
+                for (int j = 0; j < TJ; j++) {
                     v4i c = {0, 0, 0, 0};
                     c = __builtin_amdgcn_mfma_i32_16x16x32_i8(a[i], b[j], c, 0, 0, 0);
 #pragma unroll
-                    for (int r = 0; r < 4; r++) acc[i][j][r] += (float)c[r] * (sa[i][r] * sb[j]);
+                    for (int r = 0; r < 4; r++) acc[i][j][r] = fmaf((float)c[r], sa[i][r] * sb[j], acc[i][j][r]);
                 }
             }
         }
+        if (more) lstore(cur ^ 1);
         __syncthreads();
-        if (more) {
-            lstore();
-            __syncthreads();
-        }
     }
+    const bool split = gridDim.z > 1;
 #pragma unroll
-    for (int i = 0; i < 2; i++) {
+    for (int i = 0; i < TI; i++) {
 #pragma unroll
-        for (int j = 0; j < 2; j++) {
-            const int col = n0 + wc * 32 + j * 16 + fr;
+        for (int j = 0; j < TJ; j++) {
+            const int col = n0 + bcol + j * 16 + fr;
 #pragma unroll
             for (int r = 0; r < 4; r++) {
-                const int row = m0 + wr * 32 + i * 16 + 4 * (lane >> 4) + r;
-                if (row < M && col < N) y[(size_t)row * ldy + col] = epi_apply(epi, acc[i][j][r], row, col, bias, res, ldy);
+                const int row = m0 + arow + i * 16 + fq + r;
+                if (row >= M || col >= N) continue;
+                if (split) {
+                    float v = acc[i][j][r];
+                    if (bias && blockIdx.z == 0) v += bias[col];
+                    atomicAdd(y + (size_t)row * ldy + col, v);
+                } else {
+                    y[(size_t)row * ldy + col] = epi_apply(epi, acc[i][j][r], row, col, bias, res, ldy);
+                }
             }
         }
     }
 }
 
+template <int TI, int TJ>
+static void launch_gemm(dim3 grid, hipStream_t s, const int8_t* xq, const float* xd, int M, const Q8Mat& W,
+                        const float* bias, const float* res, float* y, int ldy, int epi, int sps) {
+    k_gemm_q8<TI, TJ><<<grid, 256, 0, s>>>(xq, xd, M, W.qs, W.sc, W.N, W.K, bias, res, y, ldy, epi, sps);
+}
+
 void gemm_q8(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const float* bias, const float* res, float* y,
-             int ldy, int epi, hipStream_t s) {
+             int ldy, int epi, hipStream_t s, int force_cfg, int force_splits) {
     ProfScope ps(s, "gemm_q8", 2.0 * M * W.N * W.K, q8_bytes(M, W, epi));
-    dim3 grid(cdiv(W.N, GB), cdiv(M, GB));
-    k_gemm_q8<<<grid, 256, 0, s>>>(xq, xd, M, W.qs, W.sc, W.N, W.K, bias, res, y, ldy, epi);
+    // tile choice: the largest tile that still gives >= 256 workgroups (one per CU), else the smallest allowed
+    // for this M, then split-K up to ~512 workgroups
+    struct Cfg { int ti, tj; };
+    static const Cfg cfgs[] = {{4, 4}, {2, 4}, {2, 2}, {1, 2}};
+    const int first = M <= 32 ? 3 : M <= 64 ? 1 : 0, last = M <= 32 ? 3 : 2;
+    int pick = last;
+    for (int c = first; c <= last; c++)
+        if ((long)cdiv(W.N, 32 * cfgs[c].tj) * cdiv(M, 32 * cfgs[c].ti) >= 256) { pick = c; break; }
+    if (force_cfg >= 0 && force_cfg < 4) pick = force_cfg;
+    const int BM = 32 * cfgs[pick].ti, BN = 32 * cfgs[pick].tj;
+    const int tiles = cdiv(W.N, BN) * cdiv(M, BM);
+    const int steps = cdiv(W.K, GBK);
+    const bool can_split = epi != EPI_GELU && ldy == W.N && (epi != EPI_RESID || res == y);
+    int splits = 1;
+    if (tiles < 256 && can_split) splits = std::max(1, std::min(std::min(cdiv(512, tiles), steps / 2), 8));
+    if (force_splits > 0) splits = can_split ? std::min(force_splits, steps) : 1;
+    const int sps = cdiv(steps, splits);
+    splits = cdiv(steps, sps);
+    if (splits > 1 && epi == EPI_STORE) QASR_HIP(hipMemsetAsync(y, 0, (size_t)M * ldy * sizeof(float), s));
+    dim3 grid(cdiv(W.N, BN), cdiv(M, BM), splits);
+    switch (pick) {
+        case 0: launch_gemm<4, 4>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps); break;
+        case 1: launch_gemm<2, 4>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps); break;
+        case 2: launch_gemm<2, 2>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps); break;
+        default: launch_gemm<1, 2>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps); break;
+    }
 }
 
 void linear_q8(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const float* bias, const float* res,

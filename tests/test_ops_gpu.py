@@ -115,7 +115,7 @@ def _linear_case(torch_dev, m, n, k, path, epi, seed=0, exact=False):
     else:
         x = rng.standard_normal((m, k)).astype(np.float32)
         blocks = oracle.synth_q8(seed, "w", n, k, 0.05)
-    bias = rng.standard_normal(n).astype(np.float32) if epi != 1 else None
+    bias = rng.standard_normal(n).astype(np.float32) if epi != 1 and not exact else None
     res = rng.standard_normal((m, n)).astype(np.float32)
     oracle.set_mode(engine=True)
     ref = oracle.linear_q8(x, blocks, n, bias)
@@ -140,7 +140,7 @@ def _linear_case(torch_dev, m, n, k, path, epi, seed=0, exact=False):
 
 @pytest.mark.parametrize("path", [1, 2])
 @pytest.mark.parametrize("m,n,k", [(1, 64, 1024), (3, 130, 512), (8, 64, 1024), (9, 70, 96), (64, 128, 1024),
-                                   (100, 192, 512)])
+                                   (100, 192, 512), (32, 2048, 2048), (300, 2048, 1024), (33, 96, 160)])
 def test_linear_q8_exact_integer(torch_dev, path, m, n, k):
     if path == 1 and m > 8:
         pytest.skip("GEMV path is M<=8")
@@ -150,7 +150,8 @@ def test_linear_q8_exact_integer(torch_dev, path, m, n, k):
 
 @pytest.mark.parametrize("path", [1, 2])
 @pytest.mark.parametrize("epi", [0, 1, 2])
-@pytest.mark.parametrize("m,n,k", [(1, 2048, 2048), (5, 256, 6144), (37, 320, 2048), (130, 1024, 1024)])
+@pytest.mark.parametrize("m,n,k", [(1, 2048, 2048), (5, 256, 6144), (37, 320, 2048), (130, 1024, 1024),
+                                   (24, 2048, 6144), (257, 2048, 2048)])
 def test_linear_q8_vs_oracle(torch_dev, path, epi, m, n, k):
     if path == 1 and m > 8:
         pytest.skip("GEMV path is M<=8")

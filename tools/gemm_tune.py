@@ -1,0 +1,59 @@
+#!/usr/bin/env python3
+"""Time the Q8 MFMA GEMM on the engine's shapes for every tile config / split-K choice (tuning aid, GPU)."""
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "light-whisper_amd"))
+from qasr import _lib  # noqa: E402
+
+SHAPES = [  # (tag, M, N, K, epi)
+    ("prefill gu", 27200, 12288, 2048, 0), ("prefill down", 27200, 2048, 6144, 1),
+    ("prefill qkv", 27200, 4096, 2048, 0), ("prefill o", 27200, 2048, 2048, 1),
+    ("enc fc1", 23360, 4096, 1024, 2), ("enc fc2", 23360, 1024, 4096, 1), ("enc qkv", 23360, 3072, 1024, 0),
+    ("dec256 qkv", 256, 4096, 2048, 0), ("dec256 o", 256, 2048, 2048, 1), ("dec256 gu", 256, 12288, 2048, 0),
+    ("dec256 down", 256, 2048, 6144, 1), ("dec256 lm", 256, 151936, 2048, 0),
+    ("dec64 qkv", 64, 4096, 2048, 0), ("dec64 o", 64, 2048, 2048, 1), ("dec64 gu", 64, 12288, 2048, 0),
+    ("dec64 down", 64, 2048, 6144, 1), ("dec64 lm", 64, 151936, 2048, 0),
+    ("dec16 gu", 16, 12288, 2048, 0), ("dec16 down", 16, 2048, 6144, 1), ("dec16 lm", 16, 151936, 2048, 0),
+]
+
+
+def main():
+    lib = _lib.load()
+    dev = torch.device("cuda:0")
+    only = sys.argv[1:] if len(sys.argv) > 1 else None
+    for tag, M, N, K, epi in SHAPES:
+        if only and not any(o in tag for o in only):
+            continue
+        xq = torch.randint(-127, 128, (M, K), dtype=torch.int8, device=dev)
+        xd = torch.rand(M, K // 32, device=dev) * 0.01
+        wq = torch.randint(-127, 128, (N, K), dtype=torch.int8, device=dev)
+        ws = (torch.rand(N, K // 32, device=dev) * 0.01).half()
+        y = torch.zeros(M, N, device=dev)
+        res = y if epi == 1 else None
+        flops = 2.0 * M * N * K
+        out = []
+        for path in [2] + [16 + c for c in range(4)] + [16 + c + 8 for c in range(4)]:
+            def run():
+                _lib.check(lib.qasr_op_linear_q8(xq.data_ptr(), xd.data_ptr(), M, wq.data_ptr(), ws.data_ptr(), N,
+                                                 K, None, res.data_ptr() if res is not None else None,
+                                                 y.data_ptr(), N, epi, path, None))
+            run()
+            torch.cuda.synchronize()
+            iters = max(3, min(50, int(2e12 / flops * 20)))
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(iters):
+                run()
+            e1.record()
+            torch.cuda.synchronize()
+            us = e0.elapsed_time(e1) / iters * 1e3
+            out.append(f"{path}:{us:8.1f}us {flops / us / 1e6:6.0f}TF")
+        print(f"{tag:14s} M={M:6d} N={N:6d} K={K:5d} | " + " ".join(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
