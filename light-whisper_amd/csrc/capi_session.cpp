@@ -470,7 +470,7 @@ QASR_API int qasr_op_mel(const float* pcm, int64_t n, int32_t n_mels, float* mel
             QASR_HIP(hipMemcpy2DAsync(mel + c * 100, (size_t)tp * 4, x + (size_t)c * n_mels * 100, 100 * 4, 100 * 4,
                                       (size_t)n_mels, hipMemcpyDeviceToDevice, s));
         QASR_HIP(hipStreamSynchronize(s));
-        hipFree(du); hipFree(dw); hipFree(dcu); hipFree(dmax); hipFree(lm); hipFree(x);
+        for (void* p : {(void*)du, (void*)dw, (void*)dcu, (void*)dmax, (void*)lm, (void*)x}) (void)hipFree(p);
     });
 }
 

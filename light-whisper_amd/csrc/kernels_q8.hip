@@ -5,6 +5,7 @@
 //   activation block (32): d = amax/127 (f32), q = roundf(x/d) (IEEE division), d kept as f16
 //   block dot: exact int32 Σ q_w·q_x, contribution (float)sum · (d_w·d_x), f32 accumulation.
 #include <algorithm>
+#include <type_traits>
 
 #include "kernels.h"
 
@@ -249,45 +250,49 @@ __global__ __launch_bounds__(256) void k_gemm_q8(const int8_t* __restrict__ X, c
     const int k_end = min(K, k_begin + steps_per_split * GBK);
     const int nsteps = (k_end - k_begin + GBK - 1) / GBK;
 
-    int4 ra[ACH], rb[BCH];
-    float rsa[ASC], rsb[BSC];
-    auto gload = [&](int k0) {
+    // global → register staging, two slots: step t's tiles are loaded at step t-2 and written to LDS at the end of
+    // step t-1, so each load has two steps of compute to land
+    int4 ra[2][ACH], rb[2][BCH];
+    float rsa[2][ASC], rsb[2][BSC];
+    auto gload = [&](auto slot_c, int k0) {
+        constexpr int sl = decltype(slot_c)::value;
 #pragma unroll
         for (int c = 0; c < ACH; c++) {
             const int ch = tid + 256 * c, gm = m0 + (ch >> 3), k = k0 + (ch & 7) * 16;
-            ra[c] = (gm < M && k < k_end) ? *(const int4*)(X + (size_t)gm * K + k) : make_int4(0, 0, 0, 0);
+            ra[sl][c] = (gm < M && k < k_end) ? *(const int4*)(X + (size_t)gm * K + k) : make_int4(0, 0, 0, 0);
         }
 #pragma unroll
         for (int c = 0; c < BCH; c++) {
             const int ch = tid + 256 * c, gn = n0 + (ch >> 3), k = k0 + (ch & 7) * 16;
-            rb[c] = (gn < N && k < k_end) ? *(const int4*)(W + (size_t)gn * K + k) : make_int4(0, 0, 0, 0);
+            rb[sl][c] = (gn < N && k < k_end) ? *(const int4*)(W + (size_t)gn * K + k) : make_int4(0, 0, 0, 0);
         }
 #pragma unroll
         for (int c = 0; c < ASC; c++) {
             const int idx = tid + 256 * c, gm = m0 + (idx >> 2), kb = (k0 >> 5) + (idx & 3);
-            rsa[c] = (idx < BM * 4 && gm < M && kb * QK < k_end) ? Xd[(size_t)gm * nb + kb] : 0.f;
+            rsa[sl][c] = (idx < BM * 4 && gm < M && kb * QK < k_end) ? Xd[(size_t)gm * nb + kb] : 0.f;
         }
 #pragma unroll
         for (int c = 0; c < BSC; c++) {
             const int idx = tid + 256 * c, gn = n0 + (idx >> 2), kb = (k0 >> 5) + (idx & 3);
-            rsb[c] = (idx < BN * 4 && gn < N && kb * QK < k_end) ? __half2float(Wsc[(size_t)gn * nb + kb]) : 0.f;
+            rsb[sl][c] = (idx < BN * 4 && gn < N && kb * QK < k_end) ? __half2float(Wsc[(size_t)gn * nb + kb]) : 0.f;
         }
     };
-    auto lstore = [&](int buf) {
+    auto lstore = [&](auto slot_c, int buf) {
+        constexpr int sl = decltype(slot_c)::value;
 #pragma unroll
         for (int c = 0; c < ACH; c++) {
             const int ch = tid + 256 * c;
-            *(int4*)(As[buf] + (ch >> 3) * GLD + (ch & 7) * 16) = ra[c];
+            *(int4*)(As[buf] + (ch >> 3) * GLD + (ch & 7) * 16) = ra[sl][c];
         }
 #pragma unroll
         for (int c = 0; c < BCH; c++) {
             const int ch = tid + 256 * c;
-            *(int4*)(Bs[buf] + (ch >> 3) * GLD + (ch & 7) * 16) = rb[c];
+            *(int4*)(Bs[buf] + (ch >> 3) * GLD + (ch & 7) * 16) = rb[sl][c];
         }
 #pragma unroll
         for (int c = 0; c < ASC; c++) {
             const int idx = tid + 256 * c;
-            if (idx < BM * 4) Asc[buf][(idx & 3) * BM + (idx >> 2)] = rsa[c];
+            if (idx < BM * 4) Asc[buf][(idx & 3) * BM + (idx >> 2)] = rsa[sl][c];
         }
 #pragma unroll
         for (int c = 0; c < BSC; c++) {
@@ -295,7 +300,7 @@ __global__ __launch_bounds__(256) void k_gemm_q8(const int8_t* __restrict__ X, c
             if (idx < BN * 4) {
                 const int n = idx >> 2, kb = idx & 3;
                 const int w = n / (16 * TJ), rem = n % (16 * TJ);
-                Bsc[buf][kb * BN + w * 16 * TJ + (rem & 15) * TJ + (rem >> 4)] = rsb[c];
+                Bsc[buf][kb * BN + w * 16 * TJ + (rem & 15) * TJ + (rem >> 4)] = rsb[sl][c];
             }
         }
     };
@@ -310,15 +315,17 @@ __global__ __launch_bounds__(256) void k_gemm_q8(const int8_t* __restrict__ X, c
 
     const int fr = lane & 15, fk = 8 * (lane >> 4), fq = 4 * (lane >> 4);
     const int arow = wr * 16 * TI, bcol = wc * 16 * TJ;
-    if (nsteps > 0) {
-        gload(k_begin);
-        lstore(0);
-    }
+    using S0 = std::integral_constant<int, 0>;
+    using S1 = std::integral_constant<int, 1>;
+    if (nsteps > 0) gload(S0{}, k_begin);
+    if (nsteps > 1) gload(S1{}, k_begin + GBK);
+    if (nsteps > 0) lstore(S0{}, 0);
     __syncthreads();
-    for (int s = 0; s < nsteps; s++) {
-        const int cur = s & 1;
-        const bool more = s + 1 < nsteps;
-        if (more) gload(k_begin + (s + 1) * GBK);
+    // step s computes from LDS buffer s&1 (= register slot s&1, already stored)
+    auto step = [&](auto slot_c, int s) {
+        constexpr int cur = decltype(slot_c)::value;
+        using Other = std::integral_constant<int, cur ^ 1>;
+        if (s + 2 < nsteps) gload(slot_c, k_begin + (s + 2) * GBK);
         const int8_t* as = As[cur];
         const int8_t* bs = Bs[cur];
 #pragma unroll 1
@@ -354,8 +361,12 @@ __global__ __launch_bounds__(256) void k_gemm_q8(const int8_t* __restrict__ X, c
                 }
             }
         }
-        if (more) lstore(cur ^ 1);
+        if (s + 1 < nsteps) lstore(Other{}, cur ^ 1);
         __syncthreads();
+    };
+    for (int s = 0; s < nsteps; s += 2) {
+        step(S0{}, s);
+        if (s + 1 < nsteps) step(S1{}, s + 1);
     }
     const bool split = gridDim.z > 1;
 #pragma unroll

@@ -22,7 +22,8 @@ SHAPES = [  # (tag, M, N, K, epi)
 
 
 def main():
-    lib = _lib.load()
+    lib = _lib.load(os.environ.get("QASR_LIB", _lib.LIB_PATH))
+    print("lib:", os.environ.get("QASR_LIB", _lib.LIB_PATH))
     dev = torch.device("cuda:0")
     only = sys.argv[1:] if len(sys.argv) > 1 else None
     for tag, M, N, K, epi in SHAPES:
