@@ -18,7 +18,7 @@ namespace {
 enum SlotId {
     S_UTTS, S_WORK, S_CHUNK_UTT, S_UMAX, S_LM, S_MELX, S_A1, S_A2, S_A3, S_XQ, S_XD, S_PROJ, S_VALID, S_HS,
     S_QKV, S_QKVH, S_FF, S_KVS, S_KVL, S_EMB, S_IDS, S_POS, S_SLOT, S_X, S_QH, S_GU, S_LAST, S_XN, S_LOGITS,
-    S_TOK, S_PCM, S_ENC, S_COUNT
+    S_TOK, S_PCM, S_ENC, S_DSTATE, S_DOUT, S_DTAB, S_ARGP, S_COUNT
 };
 
 inline int post_cnn_len(int l) {
@@ -85,6 +85,7 @@ void* Scratch::get(int slot, size_t bytes) {
             QASR_HIP(hipFree(b.p));
         }
         b.p = nullptr;
+        epoch++;
         const size_t cap = bytes + bytes / 4;
         QASR_HIP(hipMalloc(&b.p, cap));
         b.cap = cap;
@@ -99,6 +100,8 @@ Scratch::~Scratch() {
 Session::Session(Model* m, int n_ctx) : m_(m), n_ctx_(n_ctx) {
     QASR_CHECK(n_ctx > 32, QASR_E_INVALID, "n_ctx too small");
     QASR_HIP(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking));
+    QASR_HIP(hipHostMalloc(&pin_cnt_, 64, hipHostMallocDefault));
+    for (auto& e : step_ev_) QASR_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     rope_n_ = n_ctx;
     std::vector<float> tab((size_t)n_ctx * m->hp.head_dim);
     rope_table(n_ctx, m->hp.head_dim, m->hp.rope_theta, tab.data());
@@ -112,6 +115,10 @@ Session::~Session() {
     if (vc_) (void)hipFree(vc_);
     if (rope_) (void)hipFree(rope_);
     if (pin_) (void)hipHostFree(pin_);
+    for (auto& g : graphs_) (void)hipGraphExecDestroy(g.second);
+    for (auto& e : step_ev_)
+        if (e) (void)hipEventDestroy(e);
+    if (pin_cnt_) (void)hipHostFree(pin_cnt_);
     if (st_) (void)hipStreamDestroy(st_);
 }
 
@@ -146,6 +153,7 @@ void Session::ensure_kv(int64_t slots) {
     QASR_HIP(hipMalloc(&kc_, per));
     QASR_HIP(hipMalloc(&vc_, per));
     kv_slots_ = slots;
+    kv_epoch_++;
 }
 
 // ------------------------------------------------------------------------------------------ front end
@@ -309,6 +317,34 @@ void Session::lm_head_rows(const float* x, int rows, int ldx, float* logits) {
     linear_q8(xq, xd, rows, m_->lm_head, nullptr, nullptr, logits, h.vocab, EPI_STORE, st_);
 }
 
+// row bucket of a decode step: the GEMV path up to 8 rows, then steps of 16 / 32 / 64 / 128 rows
+int row_bucket(int m) {
+    if (m <= 8) return 8;
+    if (m <= 64) return (m + 15) / 16 * 16;
+    if (m <= 256) return (m + 31) / 32 * 32;
+    if (m <= 1024) return (m + 63) / 64 * 64;
+    return (m + 127) / 128 * 128;
+}
+
+// one decode step over B rows, fully on the device: plan → embed → 28 layers → lm_head → argmax → accept →
+// active count to the pinned host word.  Capturable (no allocation once the scratch is sized, no sync).
+void Session::decode_step(const DecState& ds, int B, bool sizing) {
+    (void)sizing;
+    const qasr_hparams& h = m_->hp;
+    const int H = h.txt_h, V = h.vocab;
+    int* tab = (int*)sc_.get(S_DTAB, (size_t)6 * B * sizeof(int));
+    dec_plan(ds, B, tab, tab + B, tab + 2 * B, tab + 3 * B, tab + 4 * B, tab + 5 * B, st_);
+    float* x = (float*)sc_.get(S_X, (size_t)B * H * sizeof(float));
+    embed_rows(tab, B, m_->tok_embd, nullptr, x, st_);
+    decoder_layers(x, B, tab + B, tab + 2 * B, tab + 3 * B, tab + 4 * B, 0);
+    float* logits = (float*)sc_.get(S_LOGITS, (size_t)B * V * sizeof(float));
+    lm_head_rows(x, B, H, logits);
+    int* d_tok = (int*)sc_.get(S_TOK, (size_t)B * sizeof(int));
+    argmax_rows(logits, B, V, d_tok, st_, sc_.get(S_ARGP, argmax_scratch_bytes(B)));
+    dec_accept(ds, B, tab + 5 * B, d_tok, st_);
+    QASR_HIP(hipMemcpyAsync(pin_cnt_, ds.counters, 4 * sizeof(int), hipMemcpyDeviceToHost, st_));
+}
+
 // ------------------------------------------------------------------------------------------ batch run
 void Session::run_batch(const float* dpcm, const std::vector<int64_t>& off, const std::vector<int64_t>& len,
                         int max_new, int force_tps, std::vector<UttResult>& out, StageTimes* times) {
@@ -345,7 +381,7 @@ void Session::run_batch(const float* dpcm, const std::vector<int64_t>& off, cons
         out[u].n_audio = fe.n_tok[u];
         out[u].n_prompt = n_prompt[u];
     }
-    ensure_kv(slots);
+    ensure_kv(slots + 1);  // + the dummy slot padding rows write to
     const int T = (int)ids.size(), H = h.txt_h, V = h.vocab;
     std::vector<int> pos(T), slot(T), kvs(T), kvl(T), last(count);
     for (int u = 0; u < count; u++) {
@@ -358,7 +394,43 @@ void Session::run_batch(const float* dpcm, const std::vector<int64_t>& off, cons
         }
         last[u] = row0[u] + n_prompt[u] - 1;
     }
-    std::vector<int32_t> next(count);
+    // device-resident decode state (kernels_decode.hip): one int32 block, laid out by a grow-only capacity so
+    // the pointers captured in the step graphs stay valid across calls
+    int ld = 1;
+    for (int u = 0; u < count; u++) ld = std::max(ld, budget[u]);
+    if (ucap_ < count) {
+        ucap_ = 64;
+        while (ucap_ < count) ucap_ *= 2;
+    }
+    int* blk = (int*)sc_.get(S_DSTATE, (size_t)(6 * ucap_ + 16) * sizeof(int));
+    DecState ds;
+    ds.last_tok = blk;
+    ds.gen = blk + ucap_;
+    ds.done = blk + 2 * ucap_;
+    ds.budget = blk + 3 * ucap_;
+    ds.n_prompt = blk + 4 * ucap_;
+    ds.base = blk + 5 * ucap_;
+    int* params = blk + 6 * ucap_;
+    ds.params = params;
+    ds.counters = params + 8;
+    ds.out = (int*)sc_.get(S_DOUT, (size_t)count * ld * sizeof(int));
+    {
+        std::vector<int> hb((size_t)6 * ucap_ + 16, 0);
+        for (int u = 0; u < count; u++) {
+            hb[3 * ucap_ + u] = budget[u];
+            hb[4 * ucap_ + u] = n_prompt[u];
+            hb[5 * ucap_ + u] = base[u];
+        }
+        int* hp = hb.data() + 6 * ucap_;
+        hp[0] = count;
+        hp[1] = (int)slots;  // the dummy KV slot (reserved by ensure_kv below)
+        hp[2] = force_tps > 0;
+        hp[3] = h.tok_eos0;
+        hp[4] = h.tok_eos1;
+        hp[5] = ld;
+        QASR_HIP(hipMemcpyAsync(blk, hb.data(), hb.size() * sizeof(int), hipMemcpyHostToDevice, st_));
+        QASR_HIP(hipStreamSynchronize(st_));
+    }
     {
         Timer t(st_, times ? &times->prefill : nullptr);
         int* d_ids = upload(S_IDS, ids);
@@ -378,66 +450,71 @@ void Session::run_batch(const float* dpcm, const std::vector<int64_t>& off, cons
         float* logits = (float*)sc_.get(S_LOGITS, (size_t)count * V * sizeof(float));
         lm_head_rows(xn, count, H, logits);
         int* d_tok = (int*)sc_.get(S_TOK, count * sizeof(int));
-        argmax_rows(logits, count, V, d_tok, st_);
-        int32_t* hp = (int32_t*)pinned(count * sizeof(int32_t));
-        QASR_HIP(hipMemcpyAsync(hp, d_tok, count * sizeof(int32_t), hipMemcpyDeviceToHost, st_));
+        argmax_rows(logits, count, V, d_tok, st_, sc_.get(S_ARGP, argmax_scratch_bytes(count)));
+        // the first generated token of every utterance: plan (identity rows) + accept on the device
+        int* tab = (int*)sc_.get(S_DTAB, (size_t)6 * count * sizeof(int));
+        dec_plan(ds, count, tab, tab + count, tab + 2 * count, tab + 3 * count, tab + 4 * count, tab + 5 * count, st_);
+        dec_accept(ds, count, tab + 5 * count, d_tok, st_);
+        QASR_HIP(hipMemcpyAsync(pin_cnt_, ds.counters, 4 * sizeof(int), hipMemcpyDeviceToHost, st_));
         QASR_HIP(hipStreamSynchronize(st_));
-        memcpy(next.data(), hp, count * sizeof(int32_t));
     }
-    // continuous-batching greedy decode
+    // continuous-batching greedy decode: rows = a bucket of the active count (padding rows are dummies); the
+    // bound is the active count read back one step late, which never undercounts because it only decreases
     Timer td(st_, times ? &times->decode : nullptr);
-    std::vector<int> active;
-    std::vector<int> gen(count, 0);
-    auto accept = [&](int u, int32_t tok) -> bool {  // returns true if u continues
-        const bool eos = tok == h.tok_eos0 || tok == h.tok_eos1;
-        if (force_tps <= 0 && eos) return false;
-        out[u].tokens.push_back(tok);
-        gen[u]++;
-        return gen[u] < budget[u];
-    };
-    for (int u = 0; u < count; u++)
-        if (accept(u, next[u])) active.push_back(u);
-    std::vector<int32_t> sids;
-    std::vector<int> spos, sslot, skvs, skvl;
-    while (!active.empty()) {
-        const int A = (int)active.size();
-        sids.resize(A); spos.resize(A); sslot.resize(A); skvs.resize(A); skvl.resize(A);
-        for (int i = 0; i < A; i++) {
-            const int u = active[i];
-            const int p = n_prompt[u] + gen[u] - 1;
-            sids[i] = out[u].tokens.back();
-            spos[i] = p;
-            sslot[i] = base[u] + p;
-            skvs[i] = base[u];
-            skvl[i] = p + 1;
+    int bound = ((volatile int*)pin_cnt_)[1];
+    const bool graphs = !prof_enabled() && !getenv("QASR_NO_GRAPH");
+    if (bound > 0) {
+        // size every scratch slot for the largest bucket eagerly, before any capture
+        const int bmax = row_bucket(bound);
+        sc_.get(S_DTAB, (size_t)6 * bmax * sizeof(int));
+        sc_.get(S_X, (size_t)bmax * H * sizeof(float));
+        sc_.get(S_LOGITS, (size_t)bmax * V * sizeof(float));
+        sc_.get(S_TOK, (size_t)bmax * sizeof(int));
+        sc_.get(S_ARGP, argmax_scratch_bytes(bmax));
+        decode_step(ds, bmax, true);  // also sizes the layer scratch
+        QASR_HIP(hipEventRecord(step_ev_[0], st_));
+    }
+    if (graph_epoch_ != sc_.epoch + kv_epoch_ * 1000003ull) {
+        for (auto& g : graphs_) (void)hipGraphExecDestroy(g.second);
+        graphs_.clear();
+        graph_epoch_ = sc_.epoch + kv_epoch_ * 1000003ull;
+    }
+    int step = 1;
+    while (bound > 0) {
+        const int B = row_bucket(bound);
+        if (graphs) {
+            auto it = graphs_.find(B);
+            if (it == graphs_.end()) {
+                hipGraph_t g;
+                QASR_HIP(hipStreamBeginCapture(st_, hipStreamCaptureModeRelaxed));
+                decode_step(ds, B, false);
+                QASR_HIP(hipStreamEndCapture(st_, &g));
+                hipGraphExec_t ex;
+                QASR_HIP(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
+                (void)hipGraphDestroy(g);
+                it = graphs_.emplace(B, ex).first;
+            }
+            QASR_HIP(hipGraphLaunch(it->second, st_));
+        } else {
+            decode_step(ds, B, false);
         }
-        // one pinned upload of the five per-row tables
-        int32_t* hp = (int32_t*)pinned((size_t)A * 5 * sizeof(int32_t));
-        memcpy(hp, sids.data(), A * 4);
-        memcpy(hp + A, spos.data(), A * 4);
-        memcpy(hp + 2 * A, sslot.data(), A * 4);
-        memcpy(hp + 3 * A, skvs.data(), A * 4);
-        memcpy(hp + 4 * A, skvl.data(), A * 4);
-        int* dt = (int*)sc_.get(S_IDS, (size_t)A * 5 * sizeof(int));
-        QASR_HIP(hipMemcpyAsync(dt, hp, (size_t)A * 5 * sizeof(int32_t), hipMemcpyHostToDevice, st_));
-        float* x = (float*)sc_.get(S_X, (size_t)A * H * sizeof(float));
-        embed_rows(dt, A, m_->tok_embd, nullptr, x, st_);
-        int64_t keys = 0;
-        for (int v : skvl) keys += v;
-        decoder_layers(x, A, dt + A, dt + 2 * A, dt + 3 * A, dt + 4 * A, keys);
-        float* logits = (float*)sc_.get(S_LOGITS, (size_t)A * V * sizeof(float));
-        lm_head_rows(x, A, H, logits);
-        int* d_tok = (int*)sc_.get(S_TOK, A * sizeof(int));
-        argmax_rows(logits, A, V, d_tok, st_);
-        QASR_HIP(hipStreamSynchronize(st_));  // the upload above has been consumed before the pinned reuse
-        int32_t* hr = (int32_t*)pinned((size_t)A * 5 * sizeof(int32_t));
-        QASR_HIP(hipMemcpyAsync(hr, d_tok, A * sizeof(int32_t), hipMemcpyDeviceToHost, st_));
+        QASR_HIP(hipEventRecord(step_ev_[step & 1], st_));
+        QASR_HIP(hipEventSynchronize(step_ev_[(step - 1) & 1]));
+        const int seen = ((volatile int*)pin_cnt_)[1];
+        bound = std::min(bound, seen);
+        step++;
+    }
+    QASR_HIP(hipStreamSynchronize(st_));
+    {
+        std::vector<int> hb((size_t)6 * ucap_ + 16), ho((size_t)count * ld);
+        QASR_HIP(hipMemcpyAsync(hb.data(), blk, hb.size() * sizeof(int), hipMemcpyDeviceToHost, st_));
+        QASR_HIP(hipMemcpyAsync(ho.data(), ds.out, ho.size() * sizeof(int), hipMemcpyDeviceToHost, st_));
         QASR_HIP(hipStreamSynchronize(st_));
-        std::vector<int> still;
-        still.reserve(A);
-        for (int i = 0; i < A; i++)
-            if (accept(active[i], hr[i])) still.push_back(active[i]);
-        active.swap(still);
+        QASR_CHECK(hb[6 * ucap_ + 8 + 2] == 0, QASR_E_INTERNAL, "decode: row bound violated");
+        for (int u = 0; u < count; u++) {
+            const int g = hb[ucap_ + u];
+            out[u].tokens.assign(ho.begin() + (size_t)u * ld, ho.begin() + (size_t)u * ld + g);
+        }
     }
     for (int u = 0; u < count; u++) {
         UttResult& r = out[u];

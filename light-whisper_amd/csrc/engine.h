@@ -1,10 +1,12 @@
 // Session: the ASR pipeline for one device — log-mel → conv stack → windowed encoder → projector →
 // prompt splice → packed prefill → continuous-batching greedy decode with an f16 KV cache → detokenise.
 #pragma once
+#include <map>
 #include <string>
 #include <vector>
 
 #include "common.h"
+#include "kernels.h"
 #include "kernels_audio.h"
 #include "model.h"
 
@@ -17,6 +19,7 @@ struct Scratch {
         size_t cap = 0;
     };
     std::vector<Buf> bufs;
+    uint64_t epoch = 0;  // bumped on every reallocation (captured graphs hold the old pointers)
     void* get(int slot, size_t bytes);
     ~Scratch();
 };
@@ -68,6 +71,7 @@ class Session {
     void decoder_layers(float* x, int rows, const int* d_pos, const int* d_slot, const int* d_kvs, const int* d_kvl,
                         int64_t total_keys);
     void ensure_kv(int64_t slots);
+    void decode_step(const DecState& ds, int B, bool sizing);
     void lm_head_rows(const float* x, int rows, int ldx, float* logits);
     template <class T>
     T* upload(int slot, const std::vector<T>& v);
@@ -85,7 +89,15 @@ class Session {
     void* pin_ = nullptr;
     size_t pin_cap_ = 0;
     void* pinned(size_t bytes);
+    // decode loop: pinned active-count word, per-step events, step graphs per row bucket
+    void* pin_cnt_ = nullptr;
+    hipEvent_t step_ev_[2] = {nullptr, nullptr};
+    std::map<int, hipGraphExec_t> graphs_;
+    uint64_t graph_epoch_ = ~0ull;
+    uint64_t kv_epoch_ = 0;
+    int ucap_ = 0;
 };
+int row_bucket(int m);
 
 // the chat prompt of one utterance (processing_qwen3_asr.py:534-553, empty system prompt); audio
 // placeholders are returned as -(audio_row + 1)

@@ -42,7 +42,9 @@ void qk_norm_rope(const float* qkv, int rows, int nh, int nkv, int hd, const int
                   __half* vc, hipStream_t s);
 // f32 [rows][ld_in] column range → f16 [rows][cols]
 void to_f16(const float* x, int rows, int cols, int ldx, __half* y, int ldy, hipStream_t s);
-void argmax_rows(const float* x, int M, int V, int* out, hipStream_t s);
+// argmax per row (lowest index on ties); scratch (argmax_scratch_bytes(M)) selects the two-stage kernel
+void argmax_rows(const float* x, int M, int V, int* out, hipStream_t s, void* scratch = nullptr);
+size_t argmax_scratch_bytes(int M);
 void add_posemb_gather(const float* proj, int n_chunks, int T, int d, const float* pe, const int* valid_idx,
                        int n_out, float* out, hipStream_t s);
 
@@ -52,5 +54,19 @@ void add_posemb_gather(const float* proj, int n_chunks, int T, int d, const floa
 void attention(const __half* Q, int ldq, const __half* K, const __half* V, int ldkv, const int* kv_start,
                const int* kv_len, int rows, int nh, int nkv, int hd, float scale, float* o, int8_t* oq, float* od,
                hipStream_t s, int64_t total_keys = 0);
+
+// ---- device-resident decode state (kernels_decode.hip)
+struct DecState {
+    int* last_tok;   // [U] token fed at the next step
+    int* gen;        // [U] tokens generated so far
+    int* done;       // [U]
+    const int* budget, *n_prompt, *base;  // [U]
+    int* out;        // [U][params[5]] generated tokens
+    const int* params;  // U, dummy KV slot, forced, eos0, eos1, ld_out
+    int* counters;   // rows this step, active after accept, bound violated
+};
+void dec_plan(const DecState& st, int M_max, int* ids, int* pos, int* slot, int* kvs, int* kvl, int* row_utt,
+              hipStream_t s);
+void dec_accept(const DecState& st, int M_max, const int* row_utt, const int* tok, hipStream_t s);
 
 }  // namespace qasr

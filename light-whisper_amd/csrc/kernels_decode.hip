@@ -1,0 +1,91 @@
+// Device-resident continuous-batching state for greedy decode.  Each step is planned, run and accepted on the
+// device, so the host only launches (one hipGraph per row bucket) and reads back the number of rows still
+// active, one step late, to pick the next bucket.  Mirrors the host loop of the reference server's
+// session.run (one utterance) for a batch: a row finishes at EOS (natural mode) or when its budget is spent.
+#include "kernels.h"
+
+namespace qasr {
+
+// one workgroup: compact the not-done utterances into rows [0, M), pad rows [M, M_max) with a harmless dummy
+// (token 0 at position 0 writing / reading only the dummy KV slot), zero the active counter for accept
+__global__ __launch_bounds__(1024) void k_dec_plan(DecState st, int M_max, int* __restrict__ ids,
+                                                   int* __restrict__ pos, int* __restrict__ slot,
+                                                   int* __restrict__ kvs, int* __restrict__ kvl,
+                                                   int* __restrict__ row_utt) {
+    __shared__ int part[1024];
+    const int U = st.params[0], dummy = st.params[1];
+    const int per = (U + 1023) / 1024;
+    const int u0 = threadIdx.x * per, u1 = min(U, u0 + per);
+    int c = 0;
+    for (int u = u0; u < u1; u++) c += st.done[u] ? 0 : 1;
+    part[threadIdx.x] = c;
+    __syncthreads();
+    // Hillis-Steele inclusive scan over 1024 partial counts
+    for (int o = 1; o < 1024; o <<= 1) {
+        const int v = threadIdx.x >= o ? part[threadIdx.x - o] : 0;
+        __syncthreads();
+        part[threadIdx.x] += v;
+        __syncthreads();
+    }
+    int r = part[threadIdx.x] - c;
+    for (int u = u0; u < u1; u++) {
+        if (st.done[u]) continue;
+        if (r < M_max) {
+            const int p = st.n_prompt[u] + st.gen[u] - 1;
+            ids[r] = st.last_tok[u];
+            pos[r] = p;
+            slot[r] = st.base[u] + p;
+            kvs[r] = st.base[u];
+            kvl[r] = p + 1;
+            row_utt[r] = u;
+        }
+        r++;
+    }
+    const int M = part[1023];
+    for (int i = M + threadIdx.x; i < M_max; i += 1024) {
+        ids[i] = 0;
+        pos[i] = 0;
+        slot[i] = dummy;
+        kvs[i] = dummy;
+        kvl[i] = 1;
+        row_utt[i] = -1;
+    }
+    if (threadIdx.x == 0) {
+        st.counters[0] = min(M, M_max);   // rows of this step
+        st.counters[1] = 0;               // active after accept
+        if (M > M_max) st.counters[2] = 1;  // bound violated (the host checks)
+    }
+}
+
+__global__ void k_dec_accept(DecState st, int M_max, const int* __restrict__ row_utt, const int* __restrict__ tok) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= M_max || i >= st.counters[0]) return;
+    const int u = row_utt[i];
+    if (u < 0) return;
+    const int t = tok[i];
+    const int forced = st.params[2], eos0 = st.params[3], eos1 = st.params[4], ld = st.params[5];
+    int still = 0;
+    if (!forced && (t == eos0 || t == eos1)) {
+        st.done[u] = 1;
+    } else {
+        const int g = st.gen[u];
+        st.out[(size_t)u * ld + g] = t;
+        st.gen[u] = g + 1;
+        st.last_tok[u] = t;
+        if (g + 1 >= st.budget[u]) st.done[u] = 1;
+        else still = 1;
+    }
+    if (still) atomicAdd(&st.counters[1], 1);
+}
+
+void dec_plan(const DecState& st, int M_max, int* ids, int* pos, int* slot, int* kvs, int* kvl, int* row_utt,
+              hipStream_t s) {
+    k_dec_plan<<<1, 1024, 0, s>>>(st, M_max, ids, pos, slot, kvs, kvl, row_utt);
+}
+
+void dec_accept(const DecState& st, int M_max, const int* row_utt, const int* tok, hipStream_t s) {
+    if (M_max <= 0) return;
+    k_dec_accept<<<cdiv(M_max, 256), 256, 0, s>>>(st, M_max, row_utt, tok);
+}
+
+}  // namespace qasr

@@ -1,5 +1,7 @@
 // Norm / activation / RoPE / reduction kernels for gfx950 (wave64).  Each fuses the Q8_0 activation
 // quantisation that feeds the next W8A8 matmul, so an activation row is written once as int8+scale.
+#include <algorithm>
+
 #include "kernels.h"
 
 namespace qasr {
@@ -276,9 +278,64 @@ __global__ __launch_bounds__(256) void k_argmax(const float* __restrict__ x, int
     }
 }
 
-void argmax_rows(const float* x, int M, int V, int* out, hipStream_t s) {
+// two-stage argmax: ARG_P workgroups per row each reduce a slice to one 64-bit key (order-preserving float bits
+// high, inverted index low, so the maximum key is the largest value at the lowest index), then one wave per row
+constexpr int ARG_P = 32;
+
+__device__ __forceinline__ unsigned long long argkey(float v, int i) {
+    unsigned u = __float_as_uint(v);
+    u = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+    return ((unsigned long long)u << 32) | (unsigned)(0xFFFFFFFFu - (unsigned)i);
+}
+
+__device__ __forceinline__ unsigned long long shfl_xor_u64(unsigned long long v, int o) {
+    const unsigned lo = __shfl_xor((unsigned)v, o), hi = __shfl_xor((unsigned)(v >> 32), o);
+    return ((unsigned long long)hi << 32) | lo;
+}
+
+__global__ __launch_bounds__(256) void k_argmax_part(const float* __restrict__ x, int V, int L,
+                                                     unsigned long long* __restrict__ part) {
+    const float* r = x + (size_t)blockIdx.y * V;
+    const int lo = blockIdx.x * L, hi = min(V, lo + L);
+    unsigned long long best = 0;
+    if ((V & 3) == 0) {
+        for (int i = lo + 4 * threadIdx.x; i < hi; i += 4 * 256) {
+            const float4 v = *(const float4*)(r + i);
+            best = max(best, argkey(v.x, i));
+            best = max(best, argkey(v.y, i + 1));
+            best = max(best, argkey(v.z, i + 2));
+            best = max(best, argkey(v.w, i + 3));
+        }
+    } else {
+        for (int i = lo + threadIdx.x; i < hi; i += 256) best = max(best, argkey(r[i], i));
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) best = max(best, shfl_xor_u64(best, o));
+    __shared__ unsigned long long sk[4];
+    if ((threadIdx.x & 63) == 0) sk[threadIdx.x >> 6] = best;
+    __syncthreads();
+    if (threadIdx.x == 0)
+        part[(size_t)blockIdx.y * ARG_P + blockIdx.x] = max(max(sk[0], sk[1]), max(sk[2], sk[3]));
+}
+
+__global__ __launch_bounds__(64) void k_argmax_final(const unsigned long long* __restrict__ part, int* __restrict__ out) {
+    unsigned long long k = threadIdx.x < ARG_P ? part[(size_t)blockIdx.x * ARG_P + threadIdx.x] : 0;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) k = max(k, shfl_xor_u64(k, o));
+    if (threadIdx.x == 0) out[blockIdx.x] = (int)(0xFFFFFFFFu - (unsigned)(k & 0xFFFFFFFFull));
+}
+
+size_t argmax_scratch_bytes(int M) { return (size_t)std::max(M, 1) * ARG_P * sizeof(unsigned long long); }
+
+void argmax_rows(const float* x, int M, int V, int* out, hipStream_t s, void* scratch) {
     if (M <= 0) return;
-    k_argmax<<<M, 256, 0, s>>>(x, V, out);
+    if (!scratch) {
+        k_argmax<<<M, 256, 0, s>>>(x, V, out);
+        return;
+    }
+    const int L = ((cdiv(V, ARG_P) + 3) / 4) * 4;
+    k_argmax_part<<<dim3(ARG_P, M), 256, 0, s>>>(x, V, L, (unsigned long long*)scratch);
+    k_argmax_final<<<M, 64, 0, s>>>((const unsigned long long*)scratch, out);
 }
 
 // audio encoder: gather the valid post-CNN positions of every chunk and add the sinusoid embedding
