@@ -170,6 +170,13 @@ QASR_API int qasr_op_rmsnorm_q8(const float* x, int32_t M, int32_t H, const floa
 QASR_API int qasr_op_layernorm_q8(const float* x, int32_t M, int32_t H, const float* w, const float* b, float eps,
                                   int8_t* q, float* d, float* y, void* stream);
 QASR_API int qasr_op_swiglu_q8(const float* gu, int32_t M, int32_t F, int8_t* q, float* d, void* stream);
+/* gate|up Q8 matrix [2F][K] (split planes) → rows interleaved by 16 in place (32j+t: t<16 gate 16j+t, else up
+ * 16j+t-16), the layout the fused SwiGLU GEMM and qasr_op_swiglu_q8_interleaved read */
+QASR_API int qasr_op_interleave_gate_up(int8_t* qs, void* sc, int32_t N, int32_t K, void* stream);
+/* h = silu(x·Wgᵀ)·(x·Wuᵀ) quantised to Q8 rows (hq [M][N/2], hd [M][N/64]) in the GEMM epilogue; W interleaved */
+QASR_API int qasr_op_gemm_swiglu_q8(const int8_t* xq, const float* xd, int32_t M, const int8_t* wqs, const void* wsc,
+                                    int32_t N, int32_t K, int8_t* hq, float* hd, void* stream);
+QASR_API int qasr_op_swiglu_q8_interleaved(const float* gu, int32_t M, int32_t F, int8_t* q, float* d, void* stream);
 QASR_API int qasr_op_qk_norm_rope(const float* qkv, int32_t rows, int32_t nh, int32_t nkv, int32_t hd,
                                   const int32_t* pos, const int32_t* slot, const float* qnw, const float* knw,
                                   const float* rope_cs, float eps, void* qout, void* kc, void* vc, void* stream);

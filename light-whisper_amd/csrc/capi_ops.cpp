@@ -85,6 +85,41 @@ QASR_API int qasr_op_swiglu_q8(const float* gu, int32_t M, int32_t F, int8_t* q,
     });
 }
 
+QASR_API int qasr_op_interleave_gate_up(int8_t* qs, void* sc, int32_t N, int32_t K, void* stream) {
+    return guard([&] {
+        QASR_CHECK(N % 32 == 0 && K % QK == 0, QASR_E_INVALID, "interleave_gate_up: bad shape");
+        Q8Mat W;
+        W.qs = qs;
+        W.sc = (__half*)sc;
+        W.N = N;
+        W.K = K;
+        interleave_gate_up(W, S(stream));
+        launched();
+    });
+}
+
+QASR_API int qasr_op_gemm_swiglu_q8(const int8_t* xq, const float* xd, int32_t M, const int8_t* wqs, const void* wsc,
+                                    int32_t N, int32_t K, int8_t* hq, float* hd, void* stream) {
+    return guard([&] {
+        QASR_CHECK(N % 64 == 0 && K % QK == 0 && M >= 0, QASR_E_INVALID, "gemm_swiglu_q8: bad shape");
+        Q8Mat W;
+        W.qs = (int8_t*)wqs;
+        W.sc = (__half*)wsc;
+        W.N = N;
+        W.K = K;
+        gemm_q8(xq, xd, M, W, nullptr, nullptr, nullptr, N, EPI_SWIGLU, S(stream), -1, 0, hq, hd);
+        launched();
+    });
+}
+
+QASR_API int qasr_op_swiglu_q8_interleaved(const float* gu, int32_t M, int32_t F, int8_t* q, float* d, void* stream) {
+    return guard([&] {
+        QASR_CHECK(F % QK == 0, QASR_E_INVALID, "swiglu_q8: F must be a multiple of 32");
+        swiglu_q8(gu, M, F, q, d, S(stream), true);
+        launched();
+    });
+}
+
 QASR_API int qasr_op_qk_norm_rope(const float* qkv, int32_t rows, int32_t nh, int32_t nkv, int32_t hd,
                                   const int32_t* pos, const int32_t* slot, const float* qnw, const float* knw,
                                   const float* rope_cs, float eps, void* qout, void* kc, void* vc, void* stream) {

@@ -18,7 +18,7 @@ namespace {
 enum SlotId {
     S_UTTS, S_WORK, S_CHUNK_UTT, S_UMAX, S_LM, S_MELX, S_A1, S_A2, S_A3, S_XQ, S_XD, S_PROJ, S_VALID, S_HS,
     S_QKV, S_QKVH, S_FF, S_KVS, S_KVL, S_EMB, S_IDS, S_POS, S_SLOT, S_X, S_QH, S_GU, S_LAST, S_XN, S_LOGITS,
-    S_TOK, S_PCM, S_ENC, S_DSTATE, S_DOUT, S_DTAB, S_ARGP, S_COUNT
+    S_TOK, S_PCM, S_ENC, S_DSTATE, S_DOUT, S_DTAB, S_ARGP, S_HQ, S_HD, S_COUNT
 };
 
 inline int post_cnn_len(int l) {
@@ -80,6 +80,7 @@ void* Scratch::get(int slot, size_t bytes) {
     Buf& b = bufs[slot];
     bytes = std::max<size_t>(bytes, 256);
     if (b.cap < bytes) {
+        QASR_CHECK(!capturing, QASR_E_INTERNAL, "scratch growth during graph capture");
         if (b.p) {
             QASR_HIP(hipDeviceSynchronize());  // queued kernels may still use the old buffer
             QASR_HIP(hipFree(b.p));
@@ -289,7 +290,10 @@ void Session::decoder_layers(float* x, int rows, const int* d_pos, const int* d_
     float* xd = (float*)sc_.get(S_XD, (size_t)rows * (kmax / QK) * sizeof(float));
     float* qkv = (float*)sc_.get(S_QKV, (size_t)rows * (QD + 2 * KD) * sizeof(float));
     __half* qh = (__half*)sc_.get(S_QH, (size_t)rows * QD * sizeof(__half));
-    float* gu = (float*)sc_.get(S_GU, (size_t)rows * 2 * F * sizeof(float));
+    float* gu = rows > 8 ? nullptr : (float*)sc_.get(S_GU, (size_t)rows * 2 * F * sizeof(float));
+    // the fused gate-up epilogue writes the SwiGLU rows into a second Q8 buffer (its input xq is still being read)
+    int8_t* hq = rows > 8 ? (int8_t*)sc_.get(S_HQ, (size_t)rows * F) : nullptr;
+    float* hd_ = rows > 8 ? (float*)sc_.get(S_HD, (size_t)rows * (F / QK) * sizeof(float)) : nullptr;
     const float scale = 1.0f / sqrtf((float)hd);
     const size_t layer_kv = (size_t)kv_slots_ * KD;
     for (int l = 0; l < h.txt_layers; l++) {
@@ -302,9 +306,19 @@ void Session::decoder_layers(float* x, int rows, const int* d_pos, const int* d_
         attention(qh, QD, kc, vc, KD, d_kvs, d_kvl, rows, nh, nkv, hd, scale, nullptr, xq, xd, st_, total_keys);
         linear_q8(xq, xd, rows, L.o, nullptr, x, x, H, EPI_RESID, st_);
         rmsnorm_q8(x, rows, H, H, L.ffn_norm, h.rms_eps, xq, xd, st_);
-        linear_q8(xq, xd, rows, L.gu, nullptr, nullptr, gu, 2 * F, EPI_STORE, st_);
-        swiglu_q8(gu, rows, F, xq, xd, st_);
+        if (rows > 8) {  // SwiGLU + Q8 in the gate-up GEMM epilogue (rows interleaved at load)
+            gemm_q8(xq, xd, rows, L.gu, nullptr, nullptr, nullptr, 2 * F, EPI_SWIGLU, st_, -1, 0, hq, hd_);
+            std::swap(xq, hq);
+            std::swap(xd, hd_);
+        } else {
+            linear_q8(xq, xd, rows, L.gu, nullptr, nullptr, gu, 2 * F, EPI_STORE, st_);
+            swiglu_q8(gu, rows, F, xq, xd, st_, true);
+        }
         linear_q8(xq, xd, rows, L.down, nullptr, x, x, H, EPI_RESID, st_);
+        if (rows > 8) {
+            std::swap(xq, hq);
+            std::swap(xd, hd_);
+        }
     }
     QASR_HIP(hipGetLastError());
 }
@@ -471,6 +485,7 @@ void Session::run_batch(const float* dpcm, const std::vector<int64_t>& off, cons
         sc_.get(S_LOGITS, (size_t)bmax * V * sizeof(float));
         sc_.get(S_TOK, (size_t)bmax * sizeof(int));
         sc_.get(S_ARGP, argmax_scratch_bytes(bmax));
+        sc_.get(S_GU, (size_t)8 * 2 * h.txt_ffn * sizeof(float));  // the unfused (GEMV) SwiGLU of buckets <= 8
         decode_step(ds, bmax, true);  // also sizes the layer scratch
         QASR_HIP(hipEventRecord(step_ev_[0], st_));
     }
@@ -487,7 +502,15 @@ void Session::run_batch(const float* dpcm, const std::vector<int64_t>& off, cons
             if (it == graphs_.end()) {
                 hipGraph_t g;
                 QASR_HIP(hipStreamBeginCapture(st_, hipStreamCaptureModeRelaxed));
-                decode_step(ds, B, false);
+                sc_.capturing = true;
+                try {
+                    decode_step(ds, B, false);
+                } catch (...) {
+                    sc_.capturing = false;
+                    (void)hipStreamEndCapture(st_, &g);
+                    throw;
+                }
+                sc_.capturing = false;
                 QASR_HIP(hipStreamEndCapture(st_, &g));
                 hipGraphExec_t ex;
                 QASR_HIP(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));

@@ -20,6 +20,7 @@ struct Scratch {
     };
     std::vector<Buf> bufs;
     uint64_t epoch = 0;  // bumped on every reallocation (captured graphs hold the old pointers)
+    bool capturing = false;  // a graph capture is in progress: growth would be a bug (throws)
     void* get(int slot, size_t bytes);
     ~Scratch();
 };

@@ -10,6 +10,7 @@ enum Epi : int {
     EPI_STORE = 0,  // y = acc (+ bias)
     EPI_RESID = 1,  // y = res + acc (+ bias)      (y may alias res)
     EPI_GELU = 2,   // y = gelu_erf(acc + bias)
+    EPI_SWIGLU = 3, // W rows gate/up interleaved by 16 (interleave_gate_up): h = silu(g)·u → Q8 rows (yq, yd)
 };
 
 // ---- Q8_0 weights / activations (kernels_q8.hip)
@@ -26,7 +27,11 @@ void gemv_q8(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const flo
              int ldy, int epi, hipStream_t s);
 // force_cfg: tile config 0 128×128, 1 64×128, 2 64×64, 3 32×64 (-1 = heuristic); force_splits: split-K (0 = heuristic)
 void gemm_q8(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const float* bias, const float* res, float* y,
-             int ldy, int epi, hipStream_t s, int force_cfg = -1, int force_splits = 0);
+             int ldy, int epi, hipStream_t s, int force_cfg = -1, int force_splits = 0, int8_t* yq = nullptr,
+             float* yd = nullptr);
+// rows of a [2F][K] gate|up matrix → interleaved by 16 (32j+t: t<16 gate 16j+t, else up 16j+t-16)
+int64_t gate_up_interleaved_row(int64_t r, int64_t F);
+void interleave_gate_up(Q8Mat& W, hipStream_t s);
 // rows of a Q8 table (token embeddings), dequantised; ids < 0 take row -(id+1) of `alt` [*][K] f32 instead
 void embed_rows(const int* ids, int n, const Q8Mat& W, const float* alt, float* out, hipStream_t s);
 
@@ -34,7 +39,8 @@ void embed_rows(const int* ids, int n, const Q8Mat& W, const float* alt, float* 
 void rmsnorm_q8(const float* x, int M, int H, int ldx, const float* w, float eps, int8_t* q, float* d, hipStream_t s);
 void layernorm_q8(const float* x, int M, int H, const float* w, const float* b, float eps, int8_t* q, float* d,
                   float* y_opt, hipStream_t s);
-void swiglu_q8(const float* gu, int M, int F, int8_t* q, float* d, hipStream_t s);
+// gu rows [gate F | up F], or interleaved by 16 (interleave_gate_up layout)
+void swiglu_q8(const float* gu, int M, int F, int8_t* q, float* d, hipStream_t s, bool interleaved = false);
 void gelu_q8(const float* x, int M, int K, int8_t* q, float* d, hipStream_t s);
 // Qwen3 q/k RMSNorm + NeoX RoPE; Q → qout f16 [rows][nh*hd], K/V → cache slots (f16)
 void qk_norm_rope(const float* qkv, int rows, int nh, int nkv, int hd, const int* pos, const int* slot,

@@ -185,29 +185,38 @@ void mel_normalize(const MelUtt* utts, int n_utts, int total_chunks, const int* 
 // ================================================================================================ conv stack
 __device__ __forceinline__ float gelu_f(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
 
-__global__ void k_conv1_gelu(const float* __restrict__ x, int n_chunks, int H0, const __half* __restrict__ w,
-                             const float* __restrict__ b, int C, __half* __restrict__ y) {
-    const int W0 = 100, H1 = (H0 + 1) / 2, W1 = 50;
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= (int64_t)n_chunks * H1 * W1 * C) return;
-    const int co = (int)(i % C);
-    const int ox = (int)((i / C) % W1);
-    const int oy = (int)((i / ((int64_t)C * W1)) % H1);
-    const int ch = (int)(i / ((int64_t)C * W1 * H1));
+// conv1 (Cin = 1, 3×3, stride 2, pad 1) + GELU: one workgroup per (chunk, output row).  The three input rows
+// (f16-rounded, zero-padded) sit in LDS and are read as broadcasts; each thread keeps one output channel's 9
+// taps and bias in registers and walks the 50 output columns, so every store instruction writes 256
+// consecutive channels of one position (channel-last f16 output).
+__global__ __launch_bounds__(256) void k_conv1_gelu(const float* __restrict__ x, int n_chunks, int H0,
+                                                    const __half* __restrict__ w, const float* __restrict__ b, int C,
+                                                    __half* __restrict__ y) {
+    constexpr int W0 = 100, W1 = 50;
+    const int H1 = (H0 + 1) / 2;
+    const int oy = blockIdx.x, ch = blockIdx.y;
+    __shared__ float xs[3][W0 + 2];
     const float* xc = x + (size_t)ch * H0 * W0;
-    float acc = 0.f;
+    for (int i = threadIdx.x; i < 3 * (W0 + 2); i += 256) {
+        const int ky = i / (W0 + 2), ix = i % (W0 + 2) - 1, iy = 2 * oy - 1 + ky;
+        xs[ky][ix + 1] = (iy >= 0 && iy < H0 && ix >= 0 && ix < W0) ? __half2float(f2h(xc[iy * W0 + ix])) : 0.f;
+    }
+    __syncthreads();
+    __half* yr = y + ((size_t)ch * H1 + oy) * W1 * C;
+    for (int co = threadIdx.x; co < C; co += 256) {
+        float k9[9];
 #pragma unroll
-    for (int ky = 0; ky < 3; ky++) {
-        const int iy = 2 * oy - 1 + ky;
-        if (iy < 0 || iy >= H0) continue;
+        for (int t = 0; t < 9; t++) k9[t] = __half2float(w[co * 9 + t]);
+        const float bias = b[co];
+        for (int ox = 0; ox < W1; ox++) {
+            float acc = 0.f;
 #pragma unroll
-        for (int kx = 0; kx < 3; kx++) {
-            const int ix = 2 * ox - 1 + kx;
-            if (ix < 0 || ix >= W0) continue;
-            acc += __half2float(w[co * 9 + ky * 3 + kx]) * __half2float(f2h(xc[iy * W0 + ix]));
+            for (int ky = 0; ky < 3; ky++)
+#pragma unroll
+                for (int kx = 0; kx < 3; kx++) acc += k9[ky * 3 + kx] * xs[ky][2 * ox + kx];
+            yr[(size_t)ox * C + co] = f2h(gelu_f(acc + bias));
         }
     }
-    y[i] = f2h(gelu_f(acc + b[co]));
 }
 
 void conv1_gelu(const float* x, int n_chunks, int n_mels, const __half* w, const float* b, int C, __half* y,
@@ -215,7 +224,7 @@ void conv1_gelu(const float* x, int n_chunks, int n_mels, const __half* w, const
     const int64_t n = (int64_t)n_chunks * ((n_mels + 1) / 2) * 50 * C;
     if (n <= 0) return;
     ProfScope ps(s, "conv1", (double)n * 18, (double)n * 2);
-    k_conv1_gelu<<<(unsigned)cdiv64(n, 256), 256, 0, s>>>(x, n_chunks, n_mels, w, b, C, y);
+    k_conv1_gelu<<<dim3((n_mels + 1) / 2, n_chunks), 256, 0, s>>>(x, n_chunks, n_mels, w, b, C, y);
 }
 
 typedef _Float16 v8h __attribute__((ext_vector_type(8)));

@@ -43,41 +43,74 @@ __device__ __forceinline__ void load32(const float* p, float* v) {
     }
 }
 
-// ------------------------------------------------------------------------------------------------ RMSNorm
-// one wave per row; lane b handles 32-blocks b, b+64, ...
+// Row kernels: one wave per row, the row held in registers as float4 chunks (lane + 64·k), one HBM pass.  A Q8
+// block is 8 consecutive lanes' chunks: its amax is three xor-shuffles, each lane packs its 4 int8 into one
+// dword (coalesced stores), the block's first lane writes the scale.  Rows up to RW_MAX·256 elements.
+constexpr int RW_MAX = 16;
+
+__device__ __forceinline__ float amax8(float v) {
+    v = fmaxf(v, __shfl_xor(v, 1));
+    v = fmaxf(v, __shfl_xor(v, 2));
+    return fmaxf(v, __shfl_xor(v, 4));
+}
+
+__device__ __forceinline__ void quant4_store(float4 v, int c, int lane, int8_t* qrow, float* drow) {
+    const float am = amax8(fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+    const float dd = am / 127.f;
+    int32_t w = 0;
+    if (am != 0.f) {
+        w = ((int)roundf(v.x / dd) & 0xff) | (((int)roundf(v.y / dd) & 0xff) << 8) |
+            (((int)roundf(v.z / dd) & 0xff) << 16) | (((int)roundf(v.w / dd) & 0xff) << 24);
+    }
+    ((int32_t*)qrow)[c] = w;
+    if ((lane & 7) == 0) drow[c >> 3] = __half2float(f2h(dd));
+}
+
+template <int KC>
 __global__ __launch_bounds__(256) void k_rmsnorm_q8(const float* __restrict__ x, int M, int H, int ldx,
                                                     const float* __restrict__ w, float eps, int8_t* __restrict__ q,
                                                     float* __restrict__ d) {
     const int lane = threadIdx.x & 63;
     const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (row >= M) return;
-    const int nb = H / 32;
-    const float* xr = x + (size_t)row * ldx;
+    const int nc = H / 4;
+    const float4* xr = (const float4*)(x + (size_t)row * ldx);
+    float4 v[KC];
     float ss = 0.f;
-    for (int b = lane; b < nb; b += 64) {
-        float v[32];
-        load32(xr + b * 32, v);
 #pragma unroll
-        for (int j = 0; j < 32; j++) ss += v[j] * v[j];
+    for (int k = 0; k < KC; k++) {
+        const int c = lane + 64 * k;
+        v[k] = c < nc ? xr[c] : make_float4(0.f, 0.f, 0.f, 0.f);
+        ss += v[k].x * v[k].x + v[k].y * v[k].y + v[k].z * v[k].z + v[k].w * v[k].w;
     }
     ss = wsum(ss);
     const float inv = 1.0f / sqrtf(ss / (float)H + eps);
-    for (int b = lane; b < nb; b += 64) {
-        float v[32], g[32];
-        load32(xr + b * 32, v);
-        load32(w + b * 32, g);
+    const float4* g4 = (const float4*)w;
 #pragma unroll
-        for (int j = 0; j < 32; j++) v[j] = v[j] * inv * g[j];
-        quant32(v, q + (size_t)row * H + b * 32, d + (size_t)row * nb + b);
+    for (int k = 0; k < KC; k++) {
+        const int c = lane + 64 * k;
+        if (64 * k >= nc) break;   // wave-uniform: every lane of a chunk row takes part in the shuffles
+        const float4 g = c < nc ? g4[c] : make_float4(0.f, 0.f, 0.f, 0.f);
+        const float4 y = make_float4(v[k].x * inv * g.x, v[k].y * inv * g.y, v[k].z * inv * g.z, v[k].w * inv * g.w);
+        if (c < nc) quant4_store(y, c, lane, q + (size_t)row * H, d + (size_t)row * (H / 32));
+        else amax8(0.f);
     }
 }
 
 void rmsnorm_q8(const float* x, int M, int H, int ldx, const float* w, float eps, int8_t* q, float* d, hipStream_t s) {
     if (M <= 0) return;
-    k_rmsnorm_q8<<<cdiv(M, 4), 256, 0, s>>>(x, M, H, ldx, w, eps, q, d);
+    QASR_CHECK(H % 32 == 0 && H <= RW_MAX * 256 && ldx % 4 == 0, QASR_E_INVALID, "rmsnorm_q8: unsupported width");
+    const int kc = cdiv(H, 256);
+    if (kc <= 4)
+        k_rmsnorm_q8<4><<<cdiv(M, 4), 256, 0, s>>>(x, M, H, ldx, w, eps, q, d);
+    else if (kc <= 8)
+        k_rmsnorm_q8<8><<<cdiv(M, 4), 256, 0, s>>>(x, M, H, ldx, w, eps, q, d);
+    else
+        k_rmsnorm_q8<RW_MAX><<<cdiv(M, 4), 256, 0, s>>>(x, M, H, ldx, w, eps, q, d);
 }
 
 // ------------------------------------------------------------------------------------------------ LayerNorm
+template <int KC>
 __global__ __launch_bounds__(256) void k_layernorm_q8(const float* __restrict__ x, int M, int H,
                                                       const float* __restrict__ w, const float* __restrict__ bb,
                                                       float eps, int8_t* __restrict__ q, float* __restrict__ d,
@@ -85,67 +118,89 @@ __global__ __launch_bounds__(256) void k_layernorm_q8(const float* __restrict__ 
     const int lane = threadIdx.x & 63;
     const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (row >= M) return;
-    const int nb = H / 32;
-    const float* xr = x + (size_t)row * H;
+    const int nc = H / 4;
+    const float4* xr = (const float4*)(x + (size_t)row * H);
+    float4 v[KC];
     float s1 = 0.f;
-    for (int b = lane; b < nb; b += 64) {
-        float v[32];
-        load32(xr + b * 32, v);
 #pragma unroll
-        for (int j = 0; j < 32; j++) s1 += v[j];
+    for (int k = 0; k < KC; k++) {
+        const int c = lane + 64 * k;
+        v[k] = c < nc ? xr[c] : make_float4(0.f, 0.f, 0.f, 0.f);
+        s1 += (v[k].x + v[k].y) + (v[k].z + v[k].w);
     }
     const float mean = wsum(s1) / (float)H;
     float s2 = 0.f;
-    for (int b = lane; b < nb; b += 64) {
-        float v[32];
-        load32(xr + b * 32, v);
 #pragma unroll
-        for (int j = 0; j < 32; j++) {
-            float t = v[j] - mean;
-            s2 += t * t;
+    for (int k = 0; k < KC; k++) {
+        if (lane + 64 * k < nc) {
+            const float a = v[k].x - mean, b = v[k].y - mean, c = v[k].z - mean, e = v[k].w - mean;
+            s2 += a * a + b * b + c * c + e * e;
         }
     }
     const float inv = 1.0f / sqrtf(wsum(s2) / (float)H + eps);
-    for (int b = lane; b < nb; b += 64) {
-        float v[32], g[32], c[32];
-        load32(xr + b * 32, v);
-        load32(w + b * 32, g);
-        load32(bb + b * 32, c);
+    const float4* g4 = (const float4*)w;
+    const float4* b4 = (const float4*)bb;
 #pragma unroll
-        for (int j = 0; j < 32; j++) v[j] = (v[j] - mean) * inv * g[j] + c[j];
-        if (y) {
-            float4* yo = (float4*)(y + (size_t)row * H + b * 32);
-#pragma unroll
-            for (int j = 0; j < 8; j++) yo[j] = make_float4(v[4 * j], v[4 * j + 1], v[4 * j + 2], v[4 * j + 3]);
+    for (int k = 0; k < KC; k++) {
+        const int c = lane + 64 * k;
+        if (64 * k >= nc) break;
+        float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (c < nc) {
+            const float4 g = g4[c], e = b4[c];
+            o = make_float4((v[k].x - mean) * inv * g.x + e.x, (v[k].y - mean) * inv * g.y + e.y,
+                            (v[k].z - mean) * inv * g.z + e.z, (v[k].w - mean) * inv * g.w + e.w);
+            if (y) ((float4*)(y + (size_t)row * H))[c] = o;
         }
-        if (q) quant32(v, q + (size_t)row * H + b * 32, d + (size_t)row * nb + b);
+        if (q) {
+            if (c < nc) quant4_store(o, c, lane, q + (size_t)row * H, d + (size_t)row * (H / 32));
+            else amax8(0.f);
+        }
     }
 }
 
 void layernorm_q8(const float* x, int M, int H, const float* w, const float* b, float eps, int8_t* q, float* d,
                   float* y_opt, hipStream_t s) {
     if (M <= 0) return;
-    k_layernorm_q8<<<cdiv(M, 4), 256, 0, s>>>(x, M, H, w, b, eps, q, d, y_opt);
+    QASR_CHECK(H % 32 == 0 && H <= RW_MAX * 256, QASR_E_INVALID, "layernorm_q8: unsupported width");
+    const int kc = cdiv(H, 256);
+    if (kc <= 4)
+        k_layernorm_q8<4><<<cdiv(M, 4), 256, 0, s>>>(x, M, H, w, b, eps, q, d, y_opt);
+    else if (kc <= 8)
+        k_layernorm_q8<8><<<cdiv(M, 4), 256, 0, s>>>(x, M, H, w, b, eps, q, d, y_opt);
+    else
+        k_layernorm_q8<RW_MAX><<<cdiv(M, 4), 256, 0, s>>>(x, M, H, w, b, eps, q, d, y_opt);
 }
 
 // ------------------------------------------------------------------------------------------------ SwiGLU / GELU
-__global__ void k_swiglu_q8(const float* __restrict__ gu, int M, int F, int8_t* __restrict__ q, float* __restrict__ d) {
+__global__ void k_swiglu_q8(const float* __restrict__ gu, int M, int F, int8_t* __restrict__ q, float* __restrict__ d,
+                            int interleaved) {
     const int nb = F / 32;
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= (int64_t)M * nb) return;
     const int m = (int)(i / nb), b = (int)(i % nb);
     float g[32], u[32];
-    load32(gu + (size_t)m * 2 * F + b * 32, g);
-    load32(gu + (size_t)m * 2 * F + F + b * 32, u);
+    const float* row = gu + (size_t)m * 2 * F;
+    if (interleaved) {   // h columns 32b..32b+31 = [g 16 | u 16 | g 16 | u 16] at 64b
+        float t[64];
+        load32(row + 64 * b, t);
+        load32(row + 64 * b + 32, t + 32);
+#pragma unroll
+        for (int j = 0; j < 16; j++) {
+            g[j] = t[j], u[j] = t[16 + j], g[16 + j] = t[32 + j], u[16 + j] = t[48 + j];
+        }
+    } else {
+        load32(row + b * 32, g);
+        load32(row + F + b * 32, u);
+    }
 #pragma unroll
     for (int j = 0; j < 32; j++) g[j] = g[j] / (1.f + expf(-g[j])) * u[j];
     quant32(g, q + (size_t)m * F + b * 32, d + (size_t)m * nb + b);
 }
 
-void swiglu_q8(const float* gu, int M, int F, int8_t* q, float* d, hipStream_t s) {
+void swiglu_q8(const float* gu, int M, int F, int8_t* q, float* d, hipStream_t s, bool interleaved) {
     int64_t n = (int64_t)M * (F / 32);
     if (n <= 0) return;
-    k_swiglu_q8<<<(unsigned)cdiv64(n, 256), 256, 0, s>>>(gu, M, F, q, d);
+    k_swiglu_q8<<<(unsigned)cdiv64(n, 256), 256, 0, s>>>(gu, M, F, q, d, interleaved ? 1 : 0);
 }
 
 __global__ void k_gelu_q8(const float* __restrict__ x, int M, int K, int8_t* __restrict__ q, float* __restrict__ d) {

@@ -233,7 +233,8 @@ template <int TI, int TJ>
 __global__ __launch_bounds__(256) void k_gemm_q8(const int8_t* __restrict__ X, const float* __restrict__ Xd, int M,
                                                  const int8_t* __restrict__ W, const __half* __restrict__ Wsc, int N,
                                                  int K, const float* __restrict__ bias, const float* res, float* y,
-                                                 int ldy, int epi, int steps_per_split) {
+                                                 int ldy, int epi, int steps_per_split, int8_t* __restrict__ yq,
+                                                 float* __restrict__ yd) {
     constexpr int BM = 32 * TI, BN = 32 * TJ;
     constexpr int ACH = BM * 8 / 256, BCH = BN * 8 / 256;     // 16-byte chunks per thread per step
     constexpr int ASC = (BM * 4 + 255) / 256, BSC = (BN * 4 + 255) / 256;
@@ -368,6 +369,35 @@ __global__ __launch_bounds__(256) void k_gemm_q8(const int8_t* __restrict__ X, c
         step(S0{}, s);
         if (s + 1 < nsteps) step(S1{}, s + 1);
     }
+    if constexpr (TJ == 4) {
+        if (epi == EPI_SWIGLU) {
+            // this wave's 64 columns = gate/up of 32 consecutive h columns = one Q8 block of the SwiGLU output
+            const int F = N / 2, hb = (n0 + bcol) / 2;
+#pragma unroll
+            for (int i = 0; i < TI; i++) {
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    const int row = m0 + arow + i * 16 + fq + r;
+                    const float g0 = acc[i][0][r], g1 = acc[i][2][r];
+                    const float h0 = g0 / (1.f + expf(-g0)) * acc[i][1][r];
+                    const float h1 = g1 / (1.f + expf(-g1)) * acc[i][3][r];
+                    float am = fmaxf(fabsf(h0), fabsf(h1));
+                    am = fmaxf(am, __shfl_xor(am, 1));
+                    am = fmaxf(am, __shfl_xor(am, 2));
+                    am = fmaxf(am, __shfl_xor(am, 4));
+                    am = fmaxf(am, __shfl_xor(am, 8));
+                    const float dd = am / 127.f;
+                    if (row < M && hb < F) {
+                        int8_t* qr = yq + (size_t)row * F + hb;
+                        qr[fr] = (int8_t)(am == 0.f ? 0 : (int)roundf(h0 / dd));
+                        qr[16 + fr] = (int8_t)(am == 0.f ? 0 : (int)roundf(h1 / dd));
+                        if (fr == 0) yd[(size_t)row * (F / QK) + hb / QK] = __half2float(f2h(dd));
+                    }
+                }
+            }
+            return;
+        }
+    }
     const bool split = gridDim.z > 1;
 #pragma unroll
     for (int i = 0; i < TI; i++) {
@@ -392,13 +422,24 @@ __global__ __launch_bounds__(256) void k_gemm_q8(const int8_t* __restrict__ X, c
 
 template <int TI, int TJ>
 static void launch_gemm(dim3 grid, hipStream_t s, const int8_t* xq, const float* xd, int M, const Q8Mat& W,
-                        const float* bias, const float* res, float* y, int ldy, int epi, int sps) {
-    k_gemm_q8<TI, TJ><<<grid, 256, 0, s>>>(xq, xd, M, W.qs, W.sc, W.N, W.K, bias, res, y, ldy, epi, sps);
+                        const float* bias, const float* res, float* y, int ldy, int epi, int sps, int8_t* yq,
+                        float* yd) {
+    k_gemm_q8<TI, TJ><<<grid, 256, 0, s>>>(xq, xd, M, W.qs, W.sc, W.N, W.K, bias, res, y, ldy, epi, sps, yq, yd);
 }
 
 void gemm_q8(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const float* bias, const float* res, float* y,
-             int ldy, int epi, hipStream_t s, int force_cfg, int force_splits) {
+             int ldy, int epi, hipStream_t s, int force_cfg, int force_splits, int8_t* yq, float* yd) {
     ProfScope ps(s, "gemm_q8", 2.0 * M * W.N * W.K, q8_bytes(M, W, epi));
+    if (epi == EPI_SWIGLU) {
+        QASR_CHECK(W.N % 64 == 0 && yq && yd, QASR_E_INVALID, "gemm_q8: SwiGLU epilogue needs N % 64 == 0");
+        const bool big = M > 64 && (long)cdiv(W.N, 128) * cdiv(M, 128) >= 256;
+        dim3 grid(cdiv(W.N, 128), cdiv(M, big ? 128 : 64), 1);
+        if (big)
+            launch_gemm<4, 4>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, cdiv(W.K, GBK), yq, yd);
+        else
+            launch_gemm<2, 4>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, cdiv(W.K, GBK), yq, yd);
+        return;
+    }
     // tile choice: the largest tile that still gives >= 256 workgroups (one per CU), else the smallest allowed
     // for this M, then split-K up to ~512 workgroups
     struct Cfg { int ti, tj; };
@@ -420,11 +461,37 @@ void gemm_q8(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const flo
     if (splits > 1 && epi == EPI_STORE) QASR_HIP(hipMemsetAsync(y, 0, (size_t)M * ldy * sizeof(float), s));
     dim3 grid(cdiv(W.N, BN), cdiv(M, BM), splits);
     switch (pick) {
-        case 0: launch_gemm<4, 4>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps); break;
-        case 1: launch_gemm<2, 4>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps); break;
-        case 2: launch_gemm<2, 2>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps); break;
-        default: launch_gemm<1, 2>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps); break;
+        case 0: launch_gemm<4, 4>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, nullptr, nullptr); break;
+        case 1: launch_gemm<2, 4>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, nullptr, nullptr); break;
+        case 2: launch_gemm<2, 2>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, nullptr, nullptr); break;
+        default: launch_gemm<1, 2>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, nullptr, nullptr); break;
     }
+}
+
+int64_t gate_up_interleaved_row(int64_t r, int64_t F) {
+    return r < F ? 32 * (r / 16) + r % 16 : 32 * ((r - F) / 16) + 16 + (r - F) % 16;
+}
+
+__global__ void k_gather_rows_q8(const int8_t* __restrict__ qs, const __half* __restrict__ sc, int64_t F, int K,
+                                 int8_t* __restrict__ qo, __half* __restrict__ so) {
+    const int64_t r = blockIdx.x;   // logical row
+    int64_t p = r < F ? 32 * (r / 16) + r % 16 : 32 * ((r - F) / 16) + 16 + (r - F) % 16;
+    for (int k = threadIdx.x; k < K; k += blockDim.x) qo[p * K + k] = qs[r * K + k];
+    for (int b = threadIdx.x; b < K / QK; b += blockDim.x) so[p * (K / QK) + b] = sc[r * (K / QK) + b];
+}
+
+void interleave_gate_up(Q8Mat& W, hipStream_t s) {
+    QASR_CHECK(W.N % 32 == 0, QASR_E_INVALID, "interleave_gate_up: N % 32 != 0");
+    int8_t* q2 = nullptr;
+    __half* s2 = nullptr;
+    QASR_HIP(hipMalloc(&q2, (size_t)W.N * W.K));
+    QASR_HIP(hipMalloc(&s2, (size_t)W.N * (W.K / QK) * sizeof(__half)));
+    k_gather_rows_q8<<<W.N, 256, 0, s>>>(W.qs, W.sc, W.N / 2, W.K, q2, s2);
+    QASR_HIP(hipMemcpyAsync(W.qs, q2, (size_t)W.N * W.K, hipMemcpyDeviceToDevice, s));
+    QASR_HIP(hipMemcpyAsync(W.sc, s2, (size_t)W.N * (W.K / QK) * sizeof(__half), hipMemcpyDeviceToDevice, s));
+    QASR_HIP(hipStreamSynchronize(s));
+    QASR_HIP(hipFree(q2));
+    QASR_HIP(hipFree(s2));
 }
 
 void linear_q8(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const float* bias, const float* res,

@@ -243,6 +243,15 @@ void make_tokenizer_synthetic(Model& m) {
 
 // ----------------------------------------------------------------------------------------------- synthetic
 // The per-tensor (sigma | center, scale) table mirrors orc_model_synth in oracle/qasr_oracle.c.
+// device layouts the kernels want, applied once after load: decoder gate|up rows interleaved by 16 so the
+// gate-up GEMM epilogue computes SwiGLU and its Q8 blocks in registers (kernels_q8.hip EPI_SWIGLU)
+void finalize_layout(Model& m, hipStream_t s) {
+    for (int l = 0; l < m.hp.txt_layers; l++) {
+        interleave_gate_up(m.dec[l].gu, s);
+        for (const char* n : {"blk.%d.ffn_gate.weight", "blk.%d.ffn_up.weight"}) m.slots.at(nm(n, l)).il16_F = m.hp.txt_ffn;
+    }
+}
+
 std::unique_ptr<Model> make_synthetic_model(const qasr_hparams& hp, uint64_t seed, const std::string& arch) {
     validate(hp);
     auto mp = std::make_unique<Model>();
@@ -314,6 +323,7 @@ std::unique_ptr<Model> make_synthetic_model(const qasr_hparams& hp, uint64_t see
         q8(nm("blk.%d.ffn_down.weight", l), 0.5f / sqrtf((float)hp.txt_ffn));
     }
     QASR_HIP(hipGetLastError());
+    finalize_layout(m, s);
     build_tables(m, s);
     make_tokenizer_synthetic(m);
     return mp;
@@ -417,6 +427,7 @@ std::unique_ptr<Model> load_gguf_model(const std::string& path) {
         QASR_HIP(hipStreamSynchronize(s));
         QASR_HIP(hipFree(tmp));
     }
+    finalize_layout(m, s);
     build_tables(m, s);
     if (toks && toks->arr_type == 8 && (int)toks->arr_s.size() >= hp.vocab) {
         m.tok.pieces = toks->arr_s;
@@ -441,8 +452,21 @@ void export_tensor(const Model& m, const std::string& name, void* dst, size_t ca
         QASR_CHECK(cap >= bytes, QASR_E_CAPACITY, "export buffer too small");
         std::vector<int8_t> qs((size_t)(t.rows * t.cols));
         std::vector<uint16_t> sc((size_t)(t.rows * nb));
-        QASR_HIP(hipMemcpy(qs.data(), (int8_t*)t.base + t.row0 * t.ld, qs.size(), hipMemcpyDeviceToHost));
-        QASR_HIP(hipMemcpy(sc.data(), t.sc + t.row0 * nb, sc.size() * 2, hipMemcpyDeviceToHost));
+        if (t.il16_F > 0) {
+            const int64_t N = 2 * t.il16_F;
+            std::vector<int8_t> aq((size_t)(N * t.cols));
+            std::vector<uint16_t> as((size_t)(N * nb));
+            QASR_HIP(hipMemcpy(aq.data(), t.base, aq.size(), hipMemcpyDeviceToHost));
+            QASR_HIP(hipMemcpy(as.data(), t.sc, as.size() * 2, hipMemcpyDeviceToHost));
+            for (int64_t r = 0; r < t.rows; r++) {
+                const int64_t p = gate_up_interleaved_row(t.row0 + r, t.il16_F);
+                memcpy(&qs[(size_t)(r * t.cols)], &aq[(size_t)(p * t.cols)], (size_t)t.cols);
+                memcpy(&sc[(size_t)(r * nb)], &as[(size_t)(p * nb)], (size_t)nb * 2);
+            }
+        } else {
+            QASR_HIP(hipMemcpy(qs.data(), (int8_t*)t.base + t.row0 * t.ld, qs.size(), hipMemcpyDeviceToHost));
+            QASR_HIP(hipMemcpy(sc.data(), t.sc + t.row0 * nb, sc.size() * 2, hipMemcpyDeviceToHost));
+        }
         uint8_t* o = (uint8_t*)dst;
         for (int64_t b = 0; b < t.rows * nb; b++) {
             memcpy(o + b * QBYTES, &sc[(size_t)b], 2);

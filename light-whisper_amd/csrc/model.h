@@ -42,6 +42,7 @@ struct TensorSlot {
     int64_t row0;
     int64_t ld;         // Q8: K
     int conv_cin;       // f16 conv weights stored reordered (0 = plain)
+    int64_t il16_F;     // Q8 gate|up rows stored interleaved by 16 (interleave_gate_up), F = half the rows
 };
 
 struct Model {

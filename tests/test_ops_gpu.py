@@ -196,6 +196,47 @@ def test_layernorm_q8(torch_dev):
     assert np.abs(host(y) - ref).max() < 1e-5 * np.abs(ref).max()
 
 
+def _il16(f):
+    """physical row of each logical gate|up row after qasr_op_interleave_gate_up"""
+    r = np.arange(2 * f)
+    return np.where(r < f, 32 * (r // 16) + r % 16, 32 * ((r - f) // 16) + 16 + (r - f) % 16)
+
+
+@pytest.mark.parametrize("m,f,k", [(3, 256, 512), (40, 512, 1024), (300, 1024, 512)])
+def test_gemm_swiglu_q8(torch_dev, m, f, k):
+    """fused gate-up GEMM + SwiGLU + Q8 epilogue vs the oracle's linear_q8 of gate and up"""
+    import torch
+
+    rng = np.random.default_rng(m + f)
+    x = rng.standard_normal((m, k)).astype(np.float32)
+    blocks = oracle.synth_q8(7, "gu", 2 * f, k, 0.05)
+    oracle.set_mode(engine=True)
+    gu = oracle.linear_q8(x, blocks, 2 * f, None)
+    g, u = gu[:, :f], gu[:, f:]
+    yref = (g / (1 + np.exp(-g)) * u).astype(np.float32)
+    qr, dr = quant_ref(yref)
+    qs, sc = q8_split(blocks, 2 * f, k)
+    wq, ws = dev(qs, torch_dev), dev(sc, torch_dev)
+    _lib.check(L().qasr_op_interleave_gate_up(ptr(wq), ptr(ws), 2 * f, k, None))
+    assert np.array_equal(host(wq)[_il16(f)], qs)
+    xq = empty((m, k), torch.int8, torch_dev)
+    xdd = empty((m, k // 32), torch.float32, torch_dev)
+    xt = dev(x, torch_dev)
+    _lib.check(L().qasr_op_quant_rows(ptr(xt), m, k, k, ptr(xq), ptr(xdd), None))
+    hq = empty((m, f), torch.int8, torch_dev)
+    hd = empty((m, f // 32), torch.float32, torch_dev)
+    _lib.check(L().qasr_op_gemm_swiglu_q8(ptr(xq), ptr(xdd), m, ptr(wq), ptr(ws), 2 * f, k, ptr(hq), ptr(hd), None))
+    assert np.allclose(host(hd), dr, rtol=2e-3)
+    assert (np.abs(host(hq).astype(int) - qr) <= 1).all()
+    # the unfused path (GEMV rows) on the interleaved layout
+    gut = dev(gu[:, np.argsort(_il16(f))], torch_dev)
+    q2 = empty((m, f), torch.int8, torch_dev)
+    d2 = empty((m, f // 32), torch.float32, torch_dev)
+    _lib.check(L().qasr_op_swiglu_q8_interleaved(ptr(gut), m, f, ptr(q2), ptr(d2), None))
+    assert np.allclose(host(d2), dr, rtol=1e-5)
+    assert (np.abs(host(q2).astype(int) - qr) <= 1).all()
+
+
 def test_swiglu_q8(torch_dev):
     import torch
 

@@ -1,0 +1,77 @@
+"""N>1 path of bench.py on CPU: world-size-2 gloo ranks shard the C4 segment list (LPT, no data-path collective)
+and reduce the step time with MAX and the audio-seconds with SUM, exactly as bench.py does over RCCL."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _rank(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    rng = np.random.default_rng(1)
+    secs = rng.uniform(2.0, 12.0, size=bench.SEG_PER_RANK * world)
+    lengths = [int(x * 16000) for x in secs]
+    mine = sorted(bench.lpt_shard(lengths, world)[rank])
+    audio_s = sum(lengths[i] for i in mine) / 16000.0
+    t = torch.tensor([0.5 + rank], dtype=torch.float64)
+    tot = torch.tensor([audio_s], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+    got = [None] * world
+    dist.all_gather_object(got, mine)
+    q.put((rank, float(t.item()), float(tot.item()), got, float(sum(lengths)) / 16000.0))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2])
+def test_lpt_sharding_gloo(world):
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, tmax, tot, shards, total in out:
+        assert tmax == 0.5 + (world - 1)            # max over ranks
+        assert abs(tot - total) < 1e-6               # every segment counted once
+        flat = sorted(i for s in shards for i in s)
+        assert flat == list(range(bench.SEG_PER_RANK * world))   # disjoint cover
+        assert min(len(s) for s in shards) > 0
+
+
+def test_lpt_balance():
+    rng = np.random.default_rng(1)
+    for world in (2, 4, 8):
+        secs = rng.uniform(2.0, 12.0, size=256 * world)
+        shards = bench.lpt_shard(list(secs), world)
+        loads = [sum(secs[i] for i in s) for s in shards]
+        assert max(loads) / min(loads) < 1.01
+
+
+def test_workload_deterministic():
+    a = bench.make_workload(2, 1)
+    b = bench.make_workload(2, 1)
+    assert len(a) == len(b) and all(np.array_equal(x, y) for x, y in zip(a, b))
+    assert all(x.dtype == np.float32 and np.abs(x).max() <= 1.0 for x in a)
