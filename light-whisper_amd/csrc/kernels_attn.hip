@@ -1,6 +1,6 @@
 // Variable-length attention over f16 K/V (decoder KV cache slots or encoder window buffers), gfx950.
 //
-// One wave per (query row, head).  Keys are processed in LDS-resident chunks of 256 with an online softmax
+// One wave per (query row, KV head), the G = n_heads/n_kv_heads query heads of the group sharing every K/V load.  Keys are processed in LDS-resident chunks of 256 with an online softmax
 // (running max / sum, f32).  QKᵀ: 8 lanes per key (16-dim slices, 3 xor-shuffles), 32 keys per unrolled
 // iteration so eight 16-byte K loads per lane are in flight together.  PV: each lane owns hd/64 dims and
 // walks the keys 8 at a time with eight independent 4-byte V loads in flight (each V row is one coalesced
@@ -52,7 +52,7 @@ __device__ __forceinline__ float qk_dot(const float* qv, const __half* kr) {
     return part;
 }
 
-template <int HD>
+template <int HD, int G>
 __global__ __launch_bounds__(256) void k_attention(const __half* __restrict__ Q, int ldq, const __half* __restrict__ K,
                                                    const __half* __restrict__ V, int ldkv,
                                                    const int* __restrict__ kv_start, const int* __restrict__ kv_len,
@@ -63,26 +63,34 @@ __global__ __launch_bounds__(256) void k_attention(const __half* __restrict__ Q,
     constexpr int PD = HD / 64;   // dims per lane in PV / output
     constexpr int KU = 4;         // 8-key groups per QKᵀ iteration
     constexpr int VU = 8;         // keys per PV iteration
-    __shared__ float sp[4][CH];
+    __shared__ float sp[4][G][CH];
+    __shared__ float cm_s[4][G], cl_s[4][G];
+    __shared__ float ca_s[4][G][HD];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int g = blockIdx.x * 4 + w;
-    if (g >= rows * nh) return;
-    const int r = g / nh, h = g % nh;
-    const int kvh = h / (nh / nkv);
-    const int s0 = kv_start[r], L = kv_len[r];
+    // one workgroup per (row, KV head); its 4 waves take contiguous quarters of the key range and merge their
+    // partial softmax states through LDS.  The G query heads of the group share every K/V load.
+    const int gw = blockIdx.x;
+    const int r = gw / nkv, kvh = gw % nkv;
+    const int Lr = kv_len[r], qn = (Lr + 3) / 4;
+    const int s0 = kv_start[r] + w * qn, L = max(0, min(qn, Lr - w * qn));
     const int sub = lane & 7, kk = lane >> 3;
 
-    float qv[QD];
-    {
-        const __half* qp = Q + (size_t)r * ldq + h * HD + sub * QD;
+    float qv[G][QD];
 #pragma unroll
-        for (int j = 0; j < QD; j++) qv[j] = __half2float(qp[j]);
+    for (int g = 0; g < G; g++) {
+        const __half* qp = Q + (size_t)r * ldq + (kvh * G + g) * HD + sub * QD;
+#pragma unroll
+        for (int j = 0; j < QD; j++) qv[g][j] = __half2float(qp[j]);
     }
-    float acc[PD];
+    float acc[G][PD];
+    float m[G], lsum[G];
 #pragma unroll
-    for (int j = 0; j < PD; j++) acc[j] = 0.f;
-    float m = -INFINITY, lsum = 0.f;
-    float* spw = sp[w];
+    for (int g = 0; g < G; g++) {
+        m[g] = -INFINITY;
+        lsum[g] = 0.f;
+#pragma unroll
+        for (int j = 0; j < PD; j++) acc[g][j] = 0.f;
+    }
     const __half* kbase = K + (size_t)kvh * HD + sub * QD;
     const __half* vbase = V + (size_t)kvh * HD + lane * PD;
 
@@ -90,38 +98,52 @@ __global__ __launch_bounds__(256) void k_attention(const __half* __restrict__ Q,
         const int n = min(CH, L - c0);
         const __half* kc = kbase + (size_t)(s0 + c0) * ldkv;
         for (int j0 = 0; j0 < n; j0 += 8 * KU) {
-            float part[KU];
+            float part[KU][G];
 #pragma unroll
             for (int u = 0; u < KU; u++) {
                 const int j = j0 + u * 8 + kk;
-                part[u] = j < n ? qk_dot<QD>(qv, kc + (size_t)j * ldkv) : 0.f;
+                if (j < n) {
+                    const __half* kr = kc + (size_t)j * ldkv;
+#pragma unroll
+                    for (int g = 0; g < G; g++) part[u][g] = qk_dot<QD>(qv[g], kr);
+                } else {
+#pragma unroll
+                    for (int g = 0; g < G; g++) part[u][g] = 0.f;
+                }
             }
 #pragma unroll
             for (int u = 0; u < KU; u++) {
-                float p = part[u];
-                p += __shfl_xor(p, 1);
-                p += __shfl_xor(p, 2);
-                p += __shfl_xor(p, 4);
                 const int j = j0 + u * 8 + kk;
-                if (sub == 0 && j < n) spw[j] = p * scale;
+#pragma unroll
+                for (int g = 0; g < G; g++) {
+                    float p = part[u][g];
+                    p += __shfl_xor(p, 1);
+                    p += __shfl_xor(p, 2);
+                    p += __shfl_xor(p, 4);
+                    if (sub == 0 && j < n) sp[w][g][j] = p * scale;
+                }
             }
         }
         wave_sync_lds();
-        float cm = -INFINITY;
-        for (int i = lane; i < n; i += 64) cm = fmaxf(cm, spw[i]);
-        cm = wmax(cm);
-        const float mnew = fmaxf(m, cm);
-        const float alpha = expf(m - mnew);
 #pragma unroll
-        for (int j = 0; j < PD; j++) acc[j] *= alpha;
-        float ps = 0.f;
-        for (int i = lane; i < n; i += 64) {
-            const float p = expf(spw[i] - mnew);
-            spw[i] = p;
-            ps += p;
+        for (int g = 0; g < G; g++) {
+            float* spw = sp[w][g];
+            float cm = -INFINITY;
+            for (int i = lane; i < n; i += 64) cm = fmaxf(cm, spw[i]);
+            cm = wmax(cm);
+            const float mnew = fmaxf(m[g], cm);
+            const float alpha = expf(m[g] - mnew);
+#pragma unroll
+            for (int j = 0; j < PD; j++) acc[g][j] *= alpha;
+            float ps = 0.f;
+            for (int i = lane; i < n; i += 64) {
+                const float p = expf(spw[i] - mnew);
+                spw[i] = p;
+                ps += p;
+            }
+            lsum[g] = lsum[g] * alpha + wsum_a(ps);
+            m[g] = mnew;
         }
-        lsum = lsum * alpha + wsum_a(ps);
-        m = mnew;
         wave_sync_lds();
         const __half* vb = vbase + (size_t)(s0 + c0) * ldkv;
         int j = 0;
@@ -132,54 +154,109 @@ __global__ __launch_bounds__(256) void k_attention(const __half* __restrict__ Q,
                 for (int u = 0; u < VU; u++) vv[u] = *(const __half2*)(vb + (size_t)(j + u) * ldkv);
 #pragma unroll
                 for (int u = 0; u < VU; u++) {
-                    const float p = spw[j + u];
                     const float2 f = __half22float2(vv[u]);
-                    acc[0] += p * f.x;
-                    acc[1] += p * f.y;
+#pragma unroll
+                    for (int g = 0; g < G; g++) {
+                        const float p = sp[w][g][j + u];
+                        acc[g][0] += p * f.x;
+                        acc[g][1] += p * f.y;
+                    }
                 }
             } else {
                 __half vv[VU];
 #pragma unroll
                 for (int u = 0; u < VU; u++) vv[u] = vb[(size_t)(j + u) * ldkv];
 #pragma unroll
-                for (int u = 0; u < VU; u++) acc[0] += spw[j + u] * __half2float(vv[u]);
+                for (int u = 0; u < VU; u++) {
+                    const float f = __half2float(vv[u]);
+#pragma unroll
+                    for (int g = 0; g < G; g++) acc[g][0] += sp[w][g][j + u] * f;
+                }
             }
         }
         for (; j < n; j++) {
-            const float p = spw[j];
             if constexpr (PD == 2) {
                 const float2 f = __half22float2(*(const __half2*)(vb + (size_t)j * ldkv));
-                acc[0] += p * f.x;
-                acc[1] += p * f.y;
+#pragma unroll
+                for (int g = 0; g < G; g++) {
+                    const float p = sp[w][g][j];
+                    acc[g][0] += p * f.x;
+                    acc[g][1] += p * f.y;
+                }
             } else {
-                acc[0] += p * __half2float(vb[(size_t)j * ldkv]);
+                const float f = __half2float(vb[(size_t)j * ldkv]);
+#pragma unroll
+                for (int g = 0; g < G; g++) acc[g][0] += sp[w][g][j] * f;
             }
         }
         wave_sync_lds();
     }
-    const float inv = L > 0 ? 1.f / lsum : 0.f;
-    float out[PD];
+    // merge the 4 partial states (m, l, acc) of this row's key quarters
 #pragma unroll
-    for (int j = 0; j < PD; j++) out[j] = acc[j] * inv;
-    const int D = nh * HD;
-    if (o) {
+    for (int g = 0; g < G; g++) {
+        if (lane == 0) {
+            cm_s[w][g] = m[g];
+            cl_s[w][g] = lsum[g];
+        }
 #pragma unroll
-        for (int j = 0; j < PD; j++) o[(size_t)r * D + h * HD + lane * PD + j] = out[j];
+        for (int j = 0; j < PD; j++) ca_s[w][g][lane * PD + j] = acc[g][j];
     }
-    if (oq) {
-        // a 32-dim block spans 32/PD lanes
-        float amax = 0.f;
+    __syncthreads();
+    if (w != 0) return;
+    const int D = nh * HD;
 #pragma unroll
-        for (int j = 0; j < PD; j++) amax = fmaxf(amax, fabsf(out[j]));
+    for (int g = 0; g < G; g++) {
+        const int h = kvh * G + g;
+        float mt = -INFINITY;
 #pragma unroll
-        for (int off = 1; off < 32 / PD; off <<= 1) amax = fmaxf(amax, __shfl_xor(amax, off));
-        const float d = amax / 127.f;
+        for (int u = 0; u < 4; u++) mt = fmaxf(mt, cm_s[u][g]);
+        float lt = 0.f, sc[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            sc[u] = cm_s[u][g] == -INFINITY ? 0.f : expf(cm_s[u][g] - mt);
+            lt += cl_s[u][g] * sc[u];
+        }
+        const float inv = Lr > 0 ? 1.f / lt : 0.f;
+        float out[PD];
 #pragma unroll
         for (int j = 0; j < PD; j++) {
-            const int qv2 = amax == 0.f ? 0 : (int)roundf(out[j] / d);
-            oq[(size_t)r * D + h * HD + lane * PD + j] = (int8_t)qv2;
+            float a = 0.f;
+#pragma unroll
+            for (int u = 0; u < 4; u++) a += ca_s[u][g][lane * PD + j] * sc[u];
+            out[j] = a * inv;
         }
-        if ((lane & (32 / PD - 1)) == 0) od[(size_t)r * (D / 32) + (h * HD + lane * PD) / 32] = __half2float(f2h(d));
+        if (o) {
+#pragma unroll
+            for (int j = 0; j < PD; j++) o[(size_t)r * D + h * HD + lane * PD + j] = out[j];
+        }
+        if (oq) {
+            // a 32-dim block spans 32/PD lanes
+            float amax = 0.f;
+#pragma unroll
+            for (int j = 0; j < PD; j++) amax = fmaxf(amax, fabsf(out[j]));
+#pragma unroll
+            for (int off = 1; off < 32 / PD; off <<= 1) amax = fmaxf(amax, __shfl_xor(amax, off));
+            const float d = amax / 127.f;
+#pragma unroll
+            for (int j = 0; j < PD; j++) {
+                const int qv2 = amax == 0.f ? 0 : (int)roundf(out[j] / d);
+                oq[(size_t)r * D + h * HD + lane * PD + j] = (int8_t)qv2;
+            }
+            if ((lane & (32 / PD - 1)) == 0)
+                od[(size_t)r * (D / 32) + (h * HD + lane * PD) / 32] = __half2float(f2h(d));
+        }
+    }
+}
+
+template <int HD>
+static void launch_attention(int G, unsigned blocks, hipStream_t s, const __half* Q, int ldq, const __half* K,
+                             const __half* V, int ldkv, const int* kv_start, const int* kv_len, int rows, int nh,
+                             int nkv, float scale, float* o, int8_t* oq, float* od) {
+    switch (G) {
+        case 1: k_attention<HD, 1><<<blocks, 256, 0, s>>>(Q, ldq, K, V, ldkv, kv_start, kv_len, rows, nh, nkv, scale, o, oq, od); break;
+        case 2: k_attention<HD, 2><<<blocks, 256, 0, s>>>(Q, ldq, K, V, ldkv, kv_start, kv_len, rows, nh, nkv, scale, o, oq, od); break;
+        case 4: k_attention<HD, 4><<<blocks, 256, 0, s>>>(Q, ldq, K, V, ldkv, kv_start, kv_len, rows, nh, nkv, scale, o, oq, od); break;
+        default: throw Error(QASR_E_INVALID, "attention: query heads per KV head must be 1, 2 or 4");
     }
 }
 
@@ -189,11 +266,13 @@ void attention(const __half* Q, int ldq, const __half* K, const __half* V, int l
     if (rows <= 0) return;
     // QKᵀ + PV: 4·hd flops per (query head, key); f16 K/V bytes read per (query head, key)
     ProfScope ps(s, "attention", 4.0 * hd * nh * (double)total_keys, 4.0 * hd * nh * (double)total_keys);
-    const int waves = rows * nh;
+    QASR_CHECK(nkv > 0 && nh % nkv == 0, QASR_E_INVALID, "attention: bad head counts");
+    const int G = nh / nkv;
+    const unsigned blocks = (unsigned)(rows * nkv);
     if (hd == 128)
-        k_attention<128><<<cdiv(waves, 4), 256, 0, s>>>(Q, ldq, K, V, ldkv, kv_start, kv_len, rows, nh, nkv, scale, o, oq, od);
+        launch_attention<128>(G, blocks, s, Q, ldq, K, V, ldkv, kv_start, kv_len, rows, nh, nkv, scale, o, oq, od);
     else if (hd == 64)
-        k_attention<64><<<cdiv(waves, 4), 256, 0, s>>>(Q, ldq, K, V, ldkv, kv_start, kv_len, rows, nh, nkv, scale, o, oq, od);
+        launch_attention<64>(G, blocks, s, Q, ldq, K, V, ldkv, kv_start, kv_len, rows, nh, nkv, scale, o, oq, od);
     else
         throw Error(QASR_E_INVALID, "attention: head_dim must be 64 or 128");
 }

@@ -75,25 +75,28 @@ __global__ __launch_bounds__(256) void k_rmsnorm_q8(const float* __restrict__ x,
     if (row >= M) return;
     const int nc = H / 4;
     const float4* xr = (const float4*)(x + (size_t)row * ldx);
-    float4 v[KC];
-    float ss = 0.f;
+    const float4* g4 = (const float4*)w;
+    // every load of the row and of the weights is issued before the first use (one memory round trip)
+    float4 v[KC], gw[KC];
 #pragma unroll
     for (int k = 0; k < KC; k++) {
         const int c = lane + 64 * k;
         v[k] = c < nc ? xr[c] : make_float4(0.f, 0.f, 0.f, 0.f);
-        ss += v[k].x * v[k].x + v[k].y * v[k].y + v[k].z * v[k].z + v[k].w * v[k].w;
+        gw[k] = c < nc ? g4[c] : make_float4(0.f, 0.f, 0.f, 0.f);
     }
+    float ss = 0.f;
+#pragma unroll
+    for (int k = 0; k < KC; k++) ss += v[k].x * v[k].x + v[k].y * v[k].y + v[k].z * v[k].z + v[k].w * v[k].w;
     ss = wsum(ss);
     const float inv = 1.0f / sqrtf(ss / (float)H + eps);
-    const float4* g4 = (const float4*)w;
 #pragma unroll
     for (int k = 0; k < KC; k++) {
         const int c = lane + 64 * k;
-        if (64 * k >= nc) break;   // wave-uniform: every lane of a chunk row takes part in the shuffles
-        const float4 g = c < nc ? g4[c] : make_float4(0.f, 0.f, 0.f, 0.f);
-        const float4 y = make_float4(v[k].x * inv * g.x, v[k].y * inv * g.y, v[k].z * inv * g.z, v[k].w * inv * g.w);
-        if (c < nc) quant4_store(y, c, lane, q + (size_t)row * H, d + (size_t)row * (H / 32));
-        else amax8(0.f);
+        if (64 * k < nc && c < nc) {   // 8-lane blocks are all in or all out (nc % 8 == 0)
+            const float4 g = gw[k];
+            const float4 y = make_float4(v[k].x * inv * g.x, v[k].y * inv * g.y, v[k].z * inv * g.z, v[k].w * inv * g.w);
+            quant4_store(y, c, lane, q + (size_t)row * H, d + (size_t)row * (H / 32));
+        }
     }
 }
 
@@ -239,41 +242,52 @@ __global__ __launch_bounds__(256) void k_qk_norm_rope(const float* __restrict__ 
     const int r = g / nslot, h = g % nslot;
     const int ld = nslot * HD;
     const float* src = qkv + (size_t)r * ld + h * HD;
-    float v[DPL];
+    // issue the independent loads first: row data, position, slot, norm weights, then the RoPE pair
+    const int p = pos[r], sl = slot[r];
+    float v[DPL], nwv[DPL];
+    const float* nw = h < nh ? qnw : knw;
 #pragma unroll
-    for (int j = 0; j < DPL; j++) v[j] = src[lane * DPL + j];
+    for (int j = 0; j < DPL; j++) {
+        v[j] = src[lane * DPL + j];
+        nwv[j] = nw[lane * DPL + j];
+    }
+    const int half = HD / 2;
+    float cs[DPL], sn[DPL];
+#pragma unroll
+    for (int j = 0; j < DPL; j++) {
+        const int dim = lane * DPL + j;
+        const int e = dim < half ? dim : dim - half;
+        const float2 t = *(const float2*)(rope_cs + ((size_t)p * half + e) * 2);
+        cs[j] = t.x;
+        sn[j] = t.y;
+    }
     const int kvd = nkv * HD;
     if (h >= nh + nkv) {  // v head: copy to cache
-        __half* dst = vc + (size_t)slot[r] * kvd + (h - nh - nkv) * HD;
+        __half* dst = vc + (size_t)sl * kvd + (h - nh - nkv) * HD;
 #pragma unroll
         for (int j = 0; j < DPL; j++) dst[lane * DPL + j] = f2h(v[j]);
         return;
     }
-    const float* nw = h < nh ? qnw : knw;
     float ss = 0.f;
 #pragma unroll
     for (int j = 0; j < DPL; j++) ss += v[j] * v[j];
     ss = wsum(ss);
     const float inv = 1.0f / sqrtf(ss / (float)HD + eps);
 #pragma unroll
-    for (int j = 0; j < DPL; j++) v[j] = v[j] * inv * nw[lane * DPL + j];
-    const int p = pos[r];
-    const int half = HD / 2;
+    for (int j = 0; j < DPL; j++) v[j] = v[j] * inv * nwv[j];
     float o[DPL];
 #pragma unroll
     for (int j = 0; j < DPL; j++) {
         const float partner = __shfl_xor(v[j], 32);
         const int dim = lane * DPL + j;
-        const int e = dim < half ? dim : dim - half;
-        const float c = rope_cs[((size_t)p * half + e) * 2], sn = rope_cs[((size_t)p * half + e) * 2 + 1];
-        o[j] = dim < half ? v[j] * c - partner * sn : v[j] * c + partner * sn;
+        o[j] = dim < half ? v[j] * cs[j] - partner * sn[j] : v[j] * cs[j] + partner * sn[j];
     }
     if (h < nh) {
         __half* dst = qout + (size_t)r * nh * HD + h * HD;
 #pragma unroll
         for (int j = 0; j < DPL; j++) dst[lane * DPL + j] = f2h(o[j]);
     } else {
-        __half* dst = kc + (size_t)slot[r] * kvd + (h - nh) * HD;
+        __half* dst = kc + (size_t)sl * kvd + (h - nh) * HD;
 #pragma unroll
         for (int j = 0; j < DPL; j++) dst[lane * DPL + j] = f2h(o[j]);
     }

@@ -252,48 +252,65 @@ __global__ __launch_bounds__(256) void k_gemm_q8(const int8_t* __restrict__ X, c
     const int nsteps = (k_end - k_begin + GBK - 1) / GBK;
 
     // global → register staging, two slots: step t's tiles are loaded at step t-2 and written to LDS at the end of
-    // step t-1, so each load has two steps of compute to land
+    // step t-1, so each load has two steps of compute to land.  The loads are unconditional (addresses clamped
+    // into the matrices, out-of-range data zeroed when written to LDS) and the f16 scales stay raw until then:
+    // no branch or conversion touches a load result early, so the compiler's vmcnt waits stay counted instead of
+    // draining every load in flight.
     int4 ra[2][ACH], rb[2][BCH];
-    float rsa[2][ASC], rsb[2][BSC];
+    float rsa[2][ASC];
+    unsigned short rsb[2][BSC];
+    unsigned ok_a[2], ok_b[2];
+    const int kmax = K - 16;
     auto gload = [&](auto slot_c, int k0) {
         constexpr int sl = decltype(slot_c)::value;
+        unsigned oa = 0, ob = 0;
 #pragma unroll
         for (int c = 0; c < ACH; c++) {
             const int ch = tid + 256 * c, gm = m0 + (ch >> 3), k = k0 + (ch & 7) * 16;
-            ra[sl][c] = (gm < M && k < k_end) ? *(const int4*)(X + (size_t)gm * K + k) : make_int4(0, 0, 0, 0);
+            oa |= (unsigned)(gm < M && k < k_end) << c;
+            ra[sl][c] = *(const int4*)(X + (size_t)min(gm, M - 1) * K + min(k, kmax));
         }
 #pragma unroll
         for (int c = 0; c < BCH; c++) {
             const int ch = tid + 256 * c, gn = n0 + (ch >> 3), k = k0 + (ch & 7) * 16;
-            rb[sl][c] = (gn < N && k < k_end) ? *(const int4*)(W + (size_t)gn * K + k) : make_int4(0, 0, 0, 0);
+            ob |= (unsigned)(gn < N && k < k_end) << c;
+            rb[sl][c] = *(const int4*)(W + (size_t)min(gn, N - 1) * K + min(k, kmax));
         }
 #pragma unroll
         for (int c = 0; c < ASC; c++) {
             const int idx = tid + 256 * c, gm = m0 + (idx >> 2), kb = (k0 >> 5) + (idx & 3);
-            rsa[sl][c] = (idx < BM * 4 && gm < M && kb * QK < k_end) ? Xd[(size_t)gm * nb + kb] : 0.f;
+            oa |= (unsigned)(idx < BM * 4 && gm < M && kb * QK < k_end) << (8 + c);
+            rsa[sl][c] = Xd[(size_t)min(gm, M - 1) * nb + min(kb, nb - 1)];
         }
 #pragma unroll
         for (int c = 0; c < BSC; c++) {
             const int idx = tid + 256 * c, gn = n0 + (idx >> 2), kb = (k0 >> 5) + (idx & 3);
-            rsb[sl][c] = (idx < BN * 4 && gn < N && kb * QK < k_end) ? __half2float(Wsc[(size_t)gn * nb + kb]) : 0.f;
+            ob |= (unsigned)(idx < BN * 4 && gn < N && kb * QK < k_end) << (8 + c);
+            rsb[sl][c] = ((const unsigned short*)Wsc)[(size_t)min(gn, N - 1) * nb + min(kb, nb - 1)];
         }
+        ok_a[sl] = oa;
+        ok_b[sl] = ob;
     };
     auto lstore = [&](auto slot_c, int buf) {
         constexpr int sl = decltype(slot_c)::value;
+        auto masked = [](int4 v, unsigned ok) {   // bitwise: a select on the aggregate makes it a memory object
+            const int mk = -(int)(ok & 1u);
+            return make_int4(v.x & mk, v.y & mk, v.z & mk, v.w & mk);
+        };
 #pragma unroll
         for (int c = 0; c < ACH; c++) {
             const int ch = tid + 256 * c;
-            *(int4*)(As[buf] + (ch >> 3) * GLD + (ch & 7) * 16) = ra[sl][c];
+            *(int4*)(As[buf] + (ch >> 3) * GLD + (ch & 7) * 16) = masked(ra[sl][c], ok_a[sl] >> c);
         }
 #pragma unroll
         for (int c = 0; c < BCH; c++) {
             const int ch = tid + 256 * c;
-            *(int4*)(Bs[buf] + (ch >> 3) * GLD + (ch & 7) * 16) = rb[sl][c];
+            *(int4*)(Bs[buf] + (ch >> 3) * GLD + (ch & 7) * 16) = masked(rb[sl][c], ok_b[sl] >> c);
         }
 #pragma unroll
         for (int c = 0; c < ASC; c++) {
             const int idx = tid + 256 * c;
-            if (idx < BM * 4) Asc[buf][(idx & 3) * BM + (idx >> 2)] = rsa[sl][c];
+            if (idx < BM * 4) Asc[buf][(idx & 3) * BM + (idx >> 2)] = (ok_a[sl] >> (8 + c)) & 1 ? rsa[sl][c] : 0.f;
         }
 #pragma unroll
         for (int c = 0; c < BSC; c++) {
@@ -301,7 +318,8 @@ __global__ __launch_bounds__(256) void k_gemm_q8(const int8_t* __restrict__ X, c
             if (idx < BN * 4) {
                 const int n = idx >> 2, kb = idx & 3;
                 const int w = n / (16 * TJ), rem = n % (16 * TJ);
-                Bsc[buf][kb * BN + w * 16 * TJ + (rem & 15) * TJ + (rem >> 4)] = rsb[sl][c];
+                const float v = __half2float(__ushort_as_half(rsb[sl][c]));
+                Bsc[buf][kb * BN + w * 16 * TJ + (rem & 15) * TJ + (rem >> 4)] = (ok_b[sl] >> (8 + c)) & 1 ? v : 0.f;
             }
         }
     };
@@ -326,7 +344,7 @@ __global__ __launch_bounds__(256) void k_gemm_q8(const int8_t* __restrict__ X, c
     auto step = [&](auto slot_c, int s) {
         constexpr int cur = decltype(slot_c)::value;
         using Other = std::integral_constant<int, cur ^ 1>;
-        if (s + 2 < nsteps) gload(slot_c, k_begin + (s + 2) * GBK);
+        gload(slot_c, k_begin + (s + 2) * GBK);   // unconditional (clamped) so the vmcnt waits stay counted
         const int8_t* as = As[cur];
         const int8_t* bs = Bs[cur];
 #pragma unroll 1
