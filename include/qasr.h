@@ -190,6 +190,10 @@ QASR_API int qasr_op_synth_q8(uint64_t seed, const char* name, int64_t N, int64_
                               void* stream);
 QASR_API int qasr_op_rope_table(int32_t n_ctx, int32_t head_dim, float theta, float* host_out /*[n_ctx][hd/2][2]*/);
 QASR_API int qasr_op_mel(const float* pcm, int64_t n, int32_t n_mels, float* mel /*[n_mels][t_pad]*/, void* stream);
+/* conv 3×3 stride 2 pad 1 + GELU (audio encoder conv2/conv3): in f16 [n_chunks][Hi][Wi][C] channel-last, w f16
+ * [Cout=C][9][Cin=C] (tap-major), out_mode 0: f16 [chunk][Ho][Wo][C]; 1: f32 [chunk][Wo][C][Ho] */
+QASR_API int qasr_op_conv3x3_gelu(const void* in, int32_t n_chunks, int32_t Hi, int32_t Wi, const void* w,
+                                  const float* bias, int32_t C, void* out, int32_t out_mode, void* stream);
 QASR_API int qasr_op_fbank(const float* pcm, int64_t n, float* feats /*[T][80]*/, void* stream);
 QASR_API int qasr_stream_sync(void* stream);
 

@@ -474,6 +474,17 @@ QASR_API int qasr_op_mel(const float* pcm, int64_t n, int32_t n_mels, float* mel
     });
 }
 
+QASR_API int qasr_op_conv3x3_gelu(const void* in, int32_t n_chunks, int32_t Hi, int32_t Wi, const void* w,
+                                  const float* bias, int32_t C, void* out, int32_t out_mode, void* stream) {
+    return guard([&] {
+        QASR_CHECK(n_chunks >= 0 && Hi > 0 && Wi > 0 && C % 32 == 0 && (out_mode == 0 || out_mode == 1),
+                   QASR_E_INVALID, "conv3x3_gelu: bad arguments");
+        conv3x3_gelu((const __half*)in, n_chunks, Hi, Wi, (const __half*)w, bias, C, out, out_mode,
+                     (hipStream_t)stream);
+        QASR_HIP(hipGetLastError());
+    });
+}
+
 QASR_API int qasr_op_fbank(const float* pcm, int64_t n, float* feats, void* stream) {
     return guard([&] {
         ensure_tables(128);

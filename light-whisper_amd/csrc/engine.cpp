@@ -65,6 +65,8 @@ void mel_dims(int64_t n, int& t_valid, int& t_pad) {
     t_pad = (t_valid + 99) / 100 * 100;
 }
 
+const int kPromptPrefix = 9;
+
 std::vector<int32_t> build_prompt(const qasr_hparams& h, int n_audio, int audio_row0) {
     std::vector<int32_t> p = {h.tok_im_start, h.tok_system, h.tok_newline, h.tok_im_end, h.tok_newline,
                               h.tok_im_start, h.tok_user, h.tok_newline, h.tok_audio_start};
@@ -379,12 +381,17 @@ void Session::run_batch(const float* dpcm, const std::vector<int64_t>& off, cons
     // prompts, KV slots, generation budgets
     std::vector<int> n_prompt(count), base(count), row0(count), budget(count);
     std::vector<int32_t> ids;
+    // the prompt prefix before the audio (im_start system \n im_end \n im_start user \n audio_start) is the same
+    // tokens at the same positions for every utterance, so its K/V is computed once and copied into each
+    // utterance's slots; the packed prefill then starts at position P0
+    const int P0 = kPromptPrefix;
+    const int skip = count >= 4 ? P0 : 0;
     int64_t slots = 0;
     for (int u = 0; u < count; u++) {
         std::vector<int32_t> p = build_prompt(h, fe.n_tok[u], fe.tok_base[u]);
         n_prompt[u] = (int)p.size();
         row0[u] = (int)ids.size();
-        ids.insert(ids.end(), p.begin(), p.end());
+        ids.insert(ids.end(), p.begin() + skip, p.end());
         const double secs = (double)len[u] / 16000.0;
         if (force_tps > 0) budget[u] = std::max(1, (int)lround(force_tps * secs) + 1);
         else budget[u] = max_new > 0 ? max_new : 64 + (int)ceil(32.0 * secs);
@@ -395,18 +402,19 @@ void Session::run_batch(const float* dpcm, const std::vector<int64_t>& off, cons
         out[u].n_audio = fe.n_tok[u];
         out[u].n_prompt = n_prompt[u];
     }
-    ensure_kv(slots + 1);  // + the dummy slot padding rows write to
+    const int64_t pref = slots + 1;          // slots: utterances, the dummy slot, the shared prefix
+    ensure_kv(slots + 1 + (skip ? P0 : 0));
     const int T = (int)ids.size(), H = h.txt_h, V = h.vocab;
     std::vector<int> pos(T), slot(T), kvs(T), kvl(T), last(count);
     for (int u = 0; u < count; u++) {
-        for (int i = 0; i < n_prompt[u]; i++) {
-            const int r = row0[u] + i;
+        for (int i = skip; i < n_prompt[u]; i++) {
+            const int r = row0[u] + i - skip;
             pos[r] = i;
             slot[r] = base[u] + i;
             kvs[r] = base[u];
             kvl[r] = i + 1;
         }
-        last[u] = row0[u] + n_prompt[u] - 1;
+        last[u] = row0[u] + n_prompt[u] - skip - 1;
     }
     // device-resident decode state (kernels_decode.hip): one int32 block, laid out by a grow-only capacity so
     // the pointers captured in the step graphs stay valid across calls
@@ -447,6 +455,25 @@ void Session::run_batch(const float* dpcm, const std::vector<int64_t>& off, cons
     }
     {
         Timer t(st_, times ? &times->prefill : nullptr);
+        sc_.get(S_X, (size_t)std::max(T, P0) * H * sizeof(float));
+        if (skip) {
+            const std::vector<int32_t> full = build_prompt(h, 0, 0);
+            std::vector<int32_t> pid(full.begin(), full.begin() + P0);
+            std::vector<int> ppos(P0), pslot(P0), pkvs(P0, (int)pref), pkvl(P0);
+            for (int i = 0; i < P0; i++) {
+                ppos[i] = i;
+                pslot[i] = (int)pref + i;
+                pkvl[i] = i + 1;
+            }
+            float* xp = (float*)sc_.get(S_X, (size_t)P0 * H * sizeof(float));
+            int* dpi = upload(S_IDS, pid);
+            embed_rows(dpi, P0, m_->tok_embd, nullptr, xp, st_);
+            decoder_layers(xp, P0, upload(S_POS, ppos), upload(S_SLOT, pslot), upload(S_KVS, pkvs),
+                           upload(S_KVL, pkvl), (int64_t)P0 * (P0 + 1) / 2);
+            copy_kv_prefix(kc_, vc_, h.txt_layers, kv_slots_, h.txt_kv_heads * h.head_dim, pref, P0,
+                           upload(S_LAST, base), count, st_);
+            QASR_HIP(hipStreamSynchronize(st_));   // the small tables above are reused by the main prefill
+        }
         int* d_ids = upload(S_IDS, ids);
         int* d_pos = upload(S_POS, pos);
         int* d_slot = upload(S_SLOT, slot);

@@ -103,6 +103,7 @@ int row_bucket(int m);
 // the chat prompt of one utterance (processing_qwen3_asr.py:534-553, empty system prompt); audio
 // placeholders are returned as -(audio_row + 1)
 std::vector<int32_t> build_prompt(const qasr_hparams& hp, int n_audio, int audio_row0);
+extern const int kPromptPrefix;   // prompt tokens before the audio, shared by every utterance
 int audio_token_count(int t_valid);
 void mel_dims(int64_t n, int& t_valid, int& t_pad);
 

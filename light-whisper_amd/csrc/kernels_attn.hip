@@ -7,6 +7,8 @@
 // 256-byte segment).  Row r attends slots [kv_start[r], kv_start[r]+kv_len[r]) — causal prefill, single-token
 // decode and the encoder's bidirectional 104-token windows (modeling_qwen3_asr.py:276-315) are all expressed
 // by the per-row ranges.  The output is written as f32 and/or directly as Q8 blocks for the O-projection.
+#include <type_traits>
+
 #include "kernels.h"
 
 namespace qasr {
@@ -52,7 +54,7 @@ __device__ __forceinline__ float qk_dot(const float* qv, const __half* kr) {
     return part;
 }
 
-template <int HD, int G>
+template <int HD, int G, int NW>
 __global__ __launch_bounds__(256) void k_attention(const __half* __restrict__ Q, int ldq, const __half* __restrict__ K,
                                                    const __half* __restrict__ V, int ldkv,
                                                    const int* __restrict__ kv_start, const int* __restrict__ kv_len,
@@ -67,12 +69,15 @@ __global__ __launch_bounds__(256) void k_attention(const __half* __restrict__ Q,
     __shared__ float cm_s[4][G], cl_s[4][G];
     __shared__ float ca_s[4][G][HD];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    // one workgroup per (row, KV head); its 4 waves take contiguous quarters of the key range and merge their
-    // partial softmax states through LDS.  The G query heads of the group share every K/V load.
-    const int gw = blockIdx.x;
+    // NW = 4: one workgroup per (row, KV head), its 4 waves take contiguous quarters of the key range and merge
+    // their partial softmax states through LDS (long decoder KV ranges).  NW = 1: one wave per (row, KV head)
+    // (the encoder's 104-key windows).  The G query heads of a KV group share every K/V load.
+    const int gw = NW == 4 ? blockIdx.x : blockIdx.x * 4 + w;
+    if (NW == 1 && gw >= rows * nkv) return;
+    const int part = NW == 4 ? w : 0;
     const int r = gw / nkv, kvh = gw % nkv;
-    const int Lr = kv_len[r], qn = (Lr + 3) / 4;
-    const int s0 = kv_start[r] + w * qn, L = max(0, min(qn, Lr - w * qn));
+    const int Lr = kv_len[r], qn = (Lr + NW - 1) / NW;
+    const int s0 = kv_start[r] + part * qn, L = max(0, min(qn, Lr - part * qn));
     const int sub = lane & 7, kk = lane >> 3;
 
     float qv[G][QD];
@@ -97,6 +102,7 @@ __global__ __launch_bounds__(256) void k_attention(const __half* __restrict__ Q,
     for (int c0 = 0; c0 < L; c0 += CH) {
         const int n = min(CH, L - c0);
         const __half* kc = kbase + (size_t)(s0 + c0) * ldkv;
+        const __half* vb = vbase + (size_t)(s0 + c0) * ldkv;
         for (int j0 = 0; j0 < n; j0 += 8 * KU) {
             float part[KU][G];
 #pragma unroll
@@ -145,7 +151,6 @@ __global__ __launch_bounds__(256) void k_attention(const __half* __restrict__ Q,
             m[g] = mnew;
         }
         wave_sync_lds();
-        const __half* vb = vbase + (size_t)(s0 + c0) * ldkv;
         int j = 0;
         for (; j + VU <= n; j += VU) {
             if constexpr (PD == 2) {
@@ -191,30 +196,44 @@ __global__ __launch_bounds__(256) void k_attention(const __half* __restrict__ Q,
         }
         wave_sync_lds();
     }
-    // merge the 4 partial states (m, l, acc) of this row's key quarters
+    // merge the NW partial states (m, l, acc) of this row's key ranges
+    if constexpr (NW == 1) {
 #pragma unroll
-    for (int g = 0; g < G; g++) {
-        if (lane == 0) {
-            cm_s[w][g] = m[g];
-            cl_s[w][g] = lsum[g];
+        for (int g = 0; g < G; g++) {
+            if (lane == 0) {
+                cm_s[w][g] = m[g];
+                cl_s[w][g] = lsum[g];
+            }
+#pragma unroll
+            for (int j = 0; j < PD; j++) ca_s[w][g][lane * PD + j] = acc[g][j];
         }
+        wave_sync_lds();
+    } else {
 #pragma unroll
-        for (int j = 0; j < PD; j++) ca_s[w][g][lane * PD + j] = acc[g][j];
+        for (int g = 0; g < G; g++) {
+            if (lane == 0) {
+                cm_s[w][g] = m[g];
+                cl_s[w][g] = lsum[g];
+            }
+#pragma unroll
+            for (int j = 0; j < PD; j++) ca_s[w][g][lane * PD + j] = acc[g][j];
+        }
+        __syncthreads();
+        if (w != 0) return;
     }
-    __syncthreads();
-    if (w != 0) return;
+    const int wb = NW == 1 ? w : 0;   // first partial state of this item
     const int D = nh * HD;
 #pragma unroll
     for (int g = 0; g < G; g++) {
         const int h = kvh * G + g;
         float mt = -INFINITY;
 #pragma unroll
-        for (int u = 0; u < 4; u++) mt = fmaxf(mt, cm_s[u][g]);
-        float lt = 0.f, sc[4];
+        for (int u = 0; u < NW; u++) mt = fmaxf(mt, cm_s[wb + u][g]);
+        float lt = 0.f, sc[NW];
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
-            sc[u] = cm_s[u][g] == -INFINITY ? 0.f : expf(cm_s[u][g] - mt);
-            lt += cl_s[u][g] * sc[u];
+        for (int u = 0; u < NW; u++) {
+            sc[u] = cm_s[wb + u][g] == -INFINITY ? 0.f : expf(cm_s[wb + u][g] - mt);
+            lt += cl_s[wb + u][g] * sc[u];
         }
         const float inv = Lr > 0 ? 1.f / lt : 0.f;
         float out[PD];
@@ -222,7 +241,7 @@ __global__ __launch_bounds__(256) void k_attention(const __half* __restrict__ Q,
         for (int j = 0; j < PD; j++) {
             float a = 0.f;
 #pragma unroll
-            for (int u = 0; u < 4; u++) a += ca_s[u][g][lane * PD + j] * sc[u];
+            for (int u = 0; u < NW; u++) a += ca_s[wb + u][g][lane * PD + j] * sc[u];
             out[j] = a * inv;
         }
         if (o) {
@@ -249,13 +268,14 @@ __global__ __launch_bounds__(256) void k_attention(const __half* __restrict__ Q,
 }
 
 template <int HD>
-static void launch_attention(int G, unsigned blocks, hipStream_t s, const __half* Q, int ldq, const __half* K,
-                             const __half* V, int ldkv, const int* kv_start, const int* kv_len, int rows, int nh,
-                             int nkv, float scale, float* o, int8_t* oq, float* od) {
+static void launch_attention(int G, int rows, hipStream_t s, const __half* Q, int ldq, const __half* K,
+                             const __half* V, int ldkv, const int* kv_start, const int* kv_len, int nh, int nkv,
+                             float scale, float* o, int8_t* oq, float* od) {
+    const unsigned b4 = (unsigned)(rows * nkv), b1 = (unsigned)cdiv(rows * nkv, 4);
     switch (G) {
-        case 1: k_attention<HD, 1><<<blocks, 256, 0, s>>>(Q, ldq, K, V, ldkv, kv_start, kv_len, rows, nh, nkv, scale, o, oq, od); break;
-        case 2: k_attention<HD, 2><<<blocks, 256, 0, s>>>(Q, ldq, K, V, ldkv, kv_start, kv_len, rows, nh, nkv, scale, o, oq, od); break;
-        case 4: k_attention<HD, 4><<<blocks, 256, 0, s>>>(Q, ldq, K, V, ldkv, kv_start, kv_len, rows, nh, nkv, scale, o, oq, od); break;
+        case 1: k_attention<HD, 1, 1><<<b1, 256, 0, s>>>(Q, ldq, K, V, ldkv, kv_start, kv_len, rows, nh, nkv, scale, o, oq, od); break;
+        case 2: k_attention<HD, 2, 4><<<b4, 256, 0, s>>>(Q, ldq, K, V, ldkv, kv_start, kv_len, rows, nh, nkv, scale, o, oq, od); break;
+        case 4: k_attention<HD, 4, 4><<<b4, 256, 0, s>>>(Q, ldq, K, V, ldkv, kv_start, kv_len, rows, nh, nkv, scale, o, oq, od); break;
         default: throw Error(QASR_E_INVALID, "attention: query heads per KV head must be 1, 2 or 4");
     }
 }
@@ -268,11 +288,10 @@ void attention(const __half* Q, int ldq, const __half* K, const __half* V, int l
     ProfScope ps(s, "attention", 4.0 * hd * nh * (double)total_keys, 4.0 * hd * nh * (double)total_keys);
     QASR_CHECK(nkv > 0 && nh % nkv == 0, QASR_E_INVALID, "attention: bad head counts");
     const int G = nh / nkv;
-    const unsigned blocks = (unsigned)(rows * nkv);
     if (hd == 128)
-        launch_attention<128>(G, blocks, s, Q, ldq, K, V, ldkv, kv_start, kv_len, rows, nh, nkv, scale, o, oq, od);
+        launch_attention<128>(G, rows, s, Q, ldq, K, V, ldkv, kv_start, kv_len, nh, nkv, scale, o, oq, od);
     else if (hd == 64)
-        launch_attention<64>(G, blocks, s, Q, ldq, K, V, ldkv, kv_start, kv_len, rows, nh, nkv, scale, o, oq, od);
+        launch_attention<64>(G, rows, s, Q, ldq, K, V, ldkv, kv_start, kv_len, nh, nkv, scale, o, oq, od);
     else
         throw Error(QASR_E_INVALID, "attention: head_dim must be 64 or 128");
 }

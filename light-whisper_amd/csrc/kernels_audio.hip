@@ -229,10 +229,12 @@ void conv1_gelu(const float* x, int n_chunks, int n_mels, const __half* w, const
 
 typedef _Float16 v8h __attribute__((ext_vector_type(8)));
 typedef float v4f __attribute__((ext_vector_type(4)));
+
+// generic-width fallback (channels a multiple of 32, e.g. the tiny test configs): 64×64 tiles, K step 32
 constexpr int CT = 64;     // output tile (positions × channels)
 constexpr int CLD = 40;    // LDS row stride in halves (80 B)
 
-__global__ __launch_bounds__(256) void k_conv3x3_gelu(const __half* __restrict__ in, int n_chunks, int Hi, int Wi,
+__global__ __launch_bounds__(256) void k_conv3x3_gelu_c32(const __half* __restrict__ in, int n_chunks, int Hi, int Wi,
                                                       const __half* __restrict__ w, const float* __restrict__ bias,
                                                       int C, void* __restrict__ out, int out_mode) {
     __shared__ __attribute__((aligned(16))) _Float16 As[CT * CLD];
@@ -322,14 +324,151 @@ __global__ __launch_bounds__(256) void k_conv3x3_gelu(const __half* __restrict__
     }
 }
 
+// conv 3×3 stride 2 pad 1 as an implicit GEMM on v_mfma_f32_16x16x32_f16: rows = output positions (chunk, oy, ox),
+// columns = output channels, K = (tap, input channel) with channel-last f16 activations so each (position, tap)
+// contributes one contiguous 2·BK-byte run.  Tile 128 positions × 96 channels, 4 waves of 64×48, K step 96
+// (three 32-deep MFMA slices), one LDS buffer (row stride 104 halves: conflict-free b128 fragments; 47 KB so
+// two workgroups share a CU) refilled from a register prefetch of the next step between two barriers, and
+// unconditional clamped staging loads (padding taps and tails zeroed by masks at the LDS write).
+constexpr int CV_BM = 128, CV_BN = 96, CV_BK = 96, CV_LD = CV_BK + 8;
+constexpr int CV_ACH = CV_BM * (CV_BK / 8) / 256;                    // 6 A chunks of 16 B per thread
+constexpr int CV_BCH = (CV_BN * (CV_BK / 8) + 255) / 256;            // 5 B chunks (last partial)
+
+__global__ __launch_bounds__(256) void k_conv3x3_gelu(const __half* __restrict__ in, int n_chunks, int Hi, int Wi,
+                                                      const __half* __restrict__ w, const float* __restrict__ bias,
+                                                      int C, void* __restrict__ out, int out_mode) {
+    __shared__ __attribute__((aligned(16))) _Float16 As[1][CV_BM * CV_LD];
+    __shared__ __attribute__((aligned(16))) _Float16 Bs[1][CV_BN * CV_LD];
+    const int Ho = (Hi + 1) / 2, Wo = (Wi + 1) / 2;
+    const int M = n_chunks * Ho * Wo;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wr = wave >> 1, wc = wave & 1;
+    const int n0 = blockIdx.x * CV_BN, m0 = blockIdx.y * CV_BM;
+    constexpr int SEG = CV_BK / 8;   // 16-byte chunks per row per step
+    // per staged A chunk: its output position, decoded once
+    int a_base[CV_ACH], a_oy[CV_ACH], a_ox[CV_ACH];
+    bool a_in[CV_ACH];
+#pragma unroll
+    for (int c = 0; c < CV_ACH; c++) {
+        const int ch = tid + 256 * c, row = m0 + ch / SEG;
+        a_in[c] = row < M;
+        const int rr = min(row, M - 1);
+        const int chn = rr / (Ho * Wo), rem = rr % (Ho * Wo);
+        a_oy[c] = rem / Wo;
+        a_ox[c] = rem % Wo;
+        a_base[c] = chn * Hi;
+    }
+    const int kper = C / CV_BK, steps = 9 * kper;
+    v4f acc[4][3];
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+#pragma unroll
+        for (int j = 0; j < 3; j++) acc[i][j] = (v4f){0.f, 0.f, 0.f, 0.f};
+
+    int4 ra[CV_ACH], rb[CV_BCH];
+    unsigned oka = 0, okb = 0;
+    auto gload = [&](int st) {
+        const int tap = st / kper, ci0 = (st % kper) * CV_BK;
+        const int ky = tap / 3, kx = tap % 3;
+        oka = 0;
+#pragma unroll
+        for (int c = 0; c < CV_ACH; c++) {
+            const int ch = tid + 256 * c, seg = ch % SEG;
+            const int iy = 2 * a_oy[c] - 1 + ky, ix = 2 * a_ox[c] - 1 + kx;
+            const bool ok = a_in[c] && iy >= 0 && iy < Hi && ix >= 0 && ix < Wi;
+            oka |= (unsigned)ok << c;
+            const int iyc = min(max(iy, 0), Hi - 1), ixc = min(max(ix, 0), Wi - 1);
+            ra[c] = *(const int4*)(in + (((size_t)a_base[c] + iyc) * Wi + ixc) * C + ci0 + seg * 8);
+        }
+        okb = 0;
+#pragma unroll
+        for (int c = 0; c < CV_BCH; c++) {
+            const int ch = tid + 256 * c, row = ch / SEG, seg = ch % SEG;
+            const bool ok = ch < CV_BN * SEG && n0 + row < C;
+            okb |= (unsigned)ok << c;
+            const int co = min(n0 + row, C - 1);
+            rb[c] = *(const int4*)(w + ((size_t)co * 9 + tap) * C + ci0 + seg * 8);
+        }
+    };
+    auto masked = [](int4 v, unsigned ok) {
+        const int mk = -(int)(ok & 1u);
+        return make_int4(v.x & mk, v.y & mk, v.z & mk, v.w & mk);
+    };
+    auto lstore = [&](int buf) {
+#pragma unroll
+        for (int c = 0; c < CV_ACH; c++) {
+            const int ch = tid + 256 * c;
+            *(int4*)(&As[buf][(ch / SEG) * CV_LD + (ch % SEG) * 8]) = masked(ra[c], oka >> c);
+        }
+#pragma unroll
+        for (int c = 0; c < CV_BCH; c++) {
+            const int ch = tid + 256 * c;
+            if (ch < CV_BN * SEG) *(int4*)(&Bs[buf][(ch / SEG) * CV_LD + (ch % SEG) * 8]) = masked(rb[c], okb >> c);
+        }
+    };
+    const int fr = lane & 15, fk = 8 * (lane >> 4);
+    gload(0);
+    lstore(0);
+    __syncthreads();
+    for (int st = 0; st < steps; st++) {
+        gload(min(st + 1, steps - 1));   // unconditional (the last one is a harmless repeat)
+        const _Float16* as = As[0];
+        const _Float16* bs = Bs[0];
+#pragma unroll
+        for (int ks = 0; ks < CV_BK / 32; ks++) {
+            v8h a[4], b[3];
+#pragma unroll
+            for (int i = 0; i < 4; i++) a[i] = *(const v8h*)(as + (wr * 64 + i * 16 + fr) * CV_LD + ks * 32 + fk);
+#pragma unroll
+            for (int j = 0; j < 3; j++) b[j] = *(const v8h*)(bs + (wc * 48 + j * 16 + fr) * CV_LD + ks * 32 + fk);
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+#pragma unroll
+                for (int j = 0; j < 3; j++)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[i], b[j], acc[i][j], 0, 0, 0);
+        }
+        __syncthreads();
+        if (st + 1 < steps) {
+            lstore(0);
+            __syncthreads();
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+#pragma unroll
+        for (int j = 0; j < 3; j++) {
+            const int col = n0 + wc * 48 + j * 16 + fr;
+            if (col >= C) continue;
+            const float bv = bias[col];
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const int row = m0 + wr * 64 + i * 16 + 4 * (lane >> 4) + r;
+                if (row >= M) continue;
+                const float v = gelu_f(acc[i][j][r] + bv);
+                if (out_mode == 0) {
+                    ((__half*)out)[(size_t)row * C + col] = f2h(v);
+                } else {
+                    const int ch = row / (Ho * Wo), rem = row % (Ho * Wo), oy = rem / Wo, ox = rem % Wo;
+                    ((float*)out)[(((size_t)ch * Wo + ox) * C + col) * Ho + oy] = v;
+                }
+            }
+        }
+    }
+}
+
 void conv3x3_gelu(const __half* in, int n_chunks, int Hi, int Wi, const __half* w, const float* b, int C, void* out,
                   int out_mode, hipStream_t s) {
     const int M = n_chunks * ((Hi + 1) / 2) * ((Wi + 1) / 2);
     if (M <= 0) return;
     QASR_CHECK(C % 32 == 0, QASR_E_INVALID, "conv channels must be a multiple of 32");
     ProfScope ps(s, "conv3x3_f16", 2.0 * M * C * 9.0 * C, (double)M * 9 * C * 2 / 4 + (double)M * C * 2);
-    dim3 grid(cdiv(C, CT), cdiv(M, CT));
-    k_conv3x3_gelu<<<grid, 256, 0, s>>>(in, n_chunks, Hi, Wi, w, b, C, out, out_mode);
+    if (C % CV_BK == 0) {
+        dim3 grid(cdiv(C, CV_BN), cdiv(M, CV_BM));
+        k_conv3x3_gelu<<<grid, 256, 0, s>>>(in, n_chunks, Hi, Wi, w, b, C, out, out_mode);
+    } else {
+        dim3 grid(cdiv(C, CT), cdiv(M, CT));
+        k_conv3x3_gelu_c32<<<grid, 256, 0, s>>>(in, n_chunks, Hi, Wi, w, b, C, out, out_mode);
+    }
 }
 
 __global__ void k_reorder_conv(const __half* __restrict__ src, int cout, int cin, __half* __restrict__ dst) {

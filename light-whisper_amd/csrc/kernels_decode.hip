@@ -88,4 +88,27 @@ void dec_accept(const DecState& st, int M_max, const int* row_utt, const int* to
     k_dec_accept<<<cdiv(M_max, 256), 256, 0, s>>>(st, M_max, row_utt, tok);
 }
 
+// copy the shared prompt prefix's K/V (P0 slots from `src`, every layer) into each utterance's first slots
+__global__ void k_copy_kv_prefix(__half* __restrict__ kc, __half* __restrict__ vc, int64_t kv_slots, int kvd,
+                                 int64_t src, int P0, const int* __restrict__ bases) {
+    const int u = blockIdx.x, l = blockIdx.y;
+    const size_t n = (size_t)P0 * kvd / 8;   // int4 units
+    const size_t so = ((size_t)l * kv_slots + src) * kvd, dso = ((size_t)l * kv_slots + bases[u]) * kvd;
+    const int4* ks = (const int4*)(kc + so);
+    const int4* vs = (const int4*)(vc + so);
+    int4* kd = (int4*)(kc + dso);
+    int4* vd = (int4*)(vc + dso);
+    for (size_t i = threadIdx.x; i < n; i += blockDim.x) {
+        kd[i] = ks[i];
+        vd[i] = vs[i];
+    }
+}
+
+void copy_kv_prefix(__half* kc, __half* vc, int layers, int64_t kv_slots, int kvd, int64_t src, int P0,
+                    const int* bases, int count, hipStream_t s) {
+    if (count <= 0 || P0 <= 0) return;
+    QASR_CHECK(kvd % 8 == 0, QASR_E_INVALID, "copy_kv_prefix: kv width must be a multiple of 8");
+    k_copy_kv_prefix<<<dim3(count, layers), 256, 0, s>>>(kc, vc, kv_slots, kvd, src, P0, bases);
+}
+
 }  // namespace qasr

@@ -110,6 +110,7 @@ SIGNATURES = {
     "qasr_op_synth_q8": (C.c_int, [C.c_uint64, C.c_char_p, I64, I64, F32, P, P, P]),
     "qasr_op_rope_table": (C.c_int, [I32, I32, F32, P]),
     "qasr_op_mel": (C.c_int, [P, I64, I32, P, P]),
+    "qasr_op_conv3x3_gelu": (C.c_int, [P, I32, I32, I32, P, P, I32, P, I32, P]),
     "qasr_op_fbank": (C.c_int, [P, I64, P, P]),
     "qasr_stream_sync": (C.c_int, [P]),
     "qasr_prof_enable": (C.c_int, [C.c_int]),

@@ -354,3 +354,33 @@ def test_embed_rows(torch_dev):
     deq = oracle.dequantize_q8(blocks, k)
     ref = np.stack([deq[i] if i >= 0 else alt[-(i + 1)] for i in ids])
     assert np.array_equal(host(out), ref)
+
+
+@pytest.mark.parametrize("c,hi,wi,mode", [(480, 64, 50, 0), (480, 32, 25, 1), (64, 64, 50, 0), (64, 32, 25, 1)])
+def test_conv3x3_gelu(torch_dev, c, hi, wi, mode):
+    """conv 3×3 s2 p1 + erf-GELU implicit GEMM (f16 MFMA) vs an f64 numpy convolution of the same f16 data"""
+    import torch
+    from scipy.special import erf
+
+    rng = np.random.default_rng(c + hi + mode)
+    n = 2
+    x = (rng.standard_normal((n, hi, wi, c)) * 0.5).astype(np.float16)
+    w = (rng.standard_normal((c, c, 3, 3)) / np.sqrt(9 * c)).astype(np.float16)
+    b = (rng.standard_normal(c) * 0.1).astype(np.float32)
+    ho, wo = (hi + 1) // 2, (wi + 1) // 2
+    xp = np.zeros((n, hi + 2, wi + 2, c), np.float64)
+    xp[:, 1:-1, 1:-1] = x
+    cols = np.stack([xp[:, ky:ky + 2 * ho:2, kx:kx + 2 * wo:2, :] for ky in range(3) for kx in range(3)], 3)
+    ref = cols.reshape(n * ho * wo, 9 * c) @ w.astype(np.float64).transpose(2, 3, 1, 0).reshape(9 * c, c) + b
+    ref = 0.5 * ref * (1 + erf(ref / np.sqrt(2)))
+    wt = np.ascontiguousarray(w.transpose(0, 2, 3, 1).reshape(c, 9, c))    # [Cout][tap][Cin]
+    xt, wd, bd = dev(x, torch_dev), dev(wt, torch_dev), dev(b, torch_dev)
+    out = empty((n * ho * wo * c,), torch.float16 if mode == 0 else torch.float32, torch_dev)
+    _lib.check(L().qasr_op_conv3x3_gelu(ptr(xt), n, hi, wi, ptr(wd), ptr(bd), c, ptr(out), mode, None))
+    got = host(out).astype(np.float64)
+    if mode == 0:
+        got = got.reshape(n * ho * wo, c)
+    else:  # [chunk][Wo][C][Ho] → rows (chunk, oy, ox)
+        got = got.reshape(n, wo, c, ho).transpose(0, 3, 1, 2).reshape(n * ho * wo, c)
+    tol = (2e-3 if mode == 0 else 1e-4) * np.abs(ref).max() + 1e-3 * np.abs(ref)
+    assert (np.abs(got - ref) <= tol).all(), np.abs(got - ref).max()
