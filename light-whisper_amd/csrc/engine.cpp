@@ -333,8 +333,11 @@ void Session::lm_head_rows(const float* x, int rows, int ldx, float* logits) {
     linear_q8(xq, xd, rows, m_->lm_head, nullptr, nullptr, logits, h.vocab, EPI_STORE, st_);
 }
 
-// row bucket of a decode step: the GEMV path up to 8 rows, then steps of 16 / 32 / 64 / 128 rows
+// row bucket of a decode step: 1/2/4/8 rows on the GEMV path, then steps of 16 / 32 / 64 / 128 rows
 int row_bucket(int m) {
+    if (m <= 1) return 1;
+    if (m <= 2) return 2;
+    if (m <= 4) return 4;
     if (m <= 8) return 8;
     if (m <= 64) return (m + 15) / 16 * 16;
     if (m <= 256) return (m + 31) / 32 * 32;

@@ -153,48 +153,72 @@ void quant_rows(const float* x, int M, int K, int ldx, int8_t* q, float* d, hipS
 typedef int v4i __attribute__((ext_vector_type(4)));
 
 // ------------------------------------------------------------------------------------------------ GEMV
-// One wave per output column n (= weight row).  Each lane streams 16 B of the weight row per step
-// (a half block); the two lanes of a block combine their sdot4 partials with one xor-shuffle so the block
-// sum is the exact int32 of the contract.  Activations (M ≤ 8 rows) are re-read from L1/L2.
-template <int MR>
+// Weight streaming for M ≤ 8 rows.  One wave per 4 output columns (weight rows): per 2 KB K-segment each lane
+// owns two 16-byte chunks (lane, lane+64) of every column, so 8 weight loads per lane are in flight at once and
+// the activation chunks it loads are reused for all 4 columns.  The two lanes of a Q8 block (adjacent chunks)
+// combine their sdot4 partials with one xor-shuffle, so the block sum is the exact int32 of the contract.
+// Every load is unconditional (rows past M are clamped and their results dropped), keeping waits counted.
+template <int MR, int GV_COLS>
 __global__ __launch_bounds__(256) void k_gemv_q8(const int8_t* __restrict__ W, const __half* __restrict__ Wsc, int N,
                                                  int K, const int8_t* __restrict__ X, const float* __restrict__ Xd,
                                                  int M, const float* __restrict__ bias, const float* res, float* y,
                                                  int ldy, int epi) {
     const int lane = threadIdx.x & 63;
-    const int n = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (n >= N) return;
+    const int n0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * GV_COLS;
+    if (n0 >= N) return;
     const int nb = K / QK;
-    const int8_t* wr = W + (size_t)n * K;
-    const __half* sr = Wsc + (size_t)n * nb;
-    float acc[MR];
-#pragma unroll
-    for (int m = 0; m < MR; m++) acc[m] = 0.f;
     const bool even = (lane & 1) == 0;
-    for (int k0 = lane * 16; k0 < K; k0 += 1024) {
-        const v4i wv = __builtin_nontemporal_load((const v4i*)(wr + k0));
-        const int4 w = make_int4(wv.x, wv.y, wv.z, wv.w);
-        const int blk = k0 >> 5;
-        const float dw = __half2float(sr[blk]);
+    float acc[GV_COLS][MR];
 #pragma unroll
-        for (int m = 0; m < MR; m++) {
-            if (m < M) {
-                const int4 xv = *(const int4*)(X + (size_t)m * K + k0);
-                int p = __builtin_amdgcn_sdot4(w.x, xv.x, 0, false);
-                p = __builtin_amdgcn_sdot4(w.y, xv.y, p, false);
-                p = __builtin_amdgcn_sdot4(w.z, xv.z, p, false);
-                p = __builtin_amdgcn_sdot4(w.w, xv.w, p, false);
-                p += __shfl_xor(p, 1);
-                const float dx = Xd[(size_t)m * nb + blk];
-                acc[m] += even ? (float)p * (dw * dx) : 0.f;
+    for (int c = 0; c < GV_COLS; c++)
+#pragma unroll
+        for (int m = 0; m < MR; m++) acc[c][m] = 0.f;
+    for (int seg = 0; seg < K; seg += 2048) {
+        int4 w[GV_COLS][2], x[MR][2];
+        float dw[GV_COLS][2], dx[MR][2];
+        bool in[2];
+#pragma unroll
+        for (int t = 0; t < 2; t++) {
+            const int k = seg + 16 * (lane + 64 * t);
+            in[t] = k < K;
+            const int kc = min(k, K - 16), blk = kc >> 5;
+#pragma unroll
+            for (int c = 0; c < GV_COLS; c++) {
+                const int n = min(n0 + c, N - 1);
+                const v4i wv = __builtin_nontemporal_load((const v4i*)(W + (size_t)n * K + kc));
+                w[c][t] = make_int4(wv.x, wv.y, wv.z, wv.w);
+                dw[c][t] = __half2float(Wsc[(size_t)n * nb + blk]);
+            }
+#pragma unroll
+            for (int m = 0; m < MR; m++) {
+                const int mm = min(m, M - 1);
+                x[m][t] = *(const int4*)(X + (size_t)mm * K + kc);
+                dx[m][t] = Xd[(size_t)mm * nb + blk];
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < 2; t++) {
+#pragma unroll
+            for (int c = 0; c < GV_COLS; c++) {
+#pragma unroll
+                for (int m = 0; m < MR; m++) {
+                    int p = __builtin_amdgcn_sdot4(w[c][t].x, x[m][t].x, 0, false);
+                    p = __builtin_amdgcn_sdot4(w[c][t].y, x[m][t].y, p, false);
+                    p = __builtin_amdgcn_sdot4(w[c][t].z, x[m][t].z, p, false);
+                    p = __builtin_amdgcn_sdot4(w[c][t].w, x[m][t].w, p, false);
+                    p += __shfl_xor(p, 1);
+                    acc[c][m] += (even && in[t]) ? (float)p * (dw[c][t] * dx[m][t]) : 0.f;
+                }
             }
         }
     }
 #pragma unroll
-    for (int m = 0; m < MR; m++) {
-        if (m < M) {
-            float v = wave_sum(acc[m]);
-            if (lane == 0) y[(size_t)m * ldy + n] = epi_apply(epi, v, m, n, bias, res, ldy);
+    for (int c = 0; c < GV_COLS; c++) {
+#pragma unroll
+        for (int m = 0; m < MR; m++) {
+            const float v = wave_sum(acc[c][m]);
+            const int n = n0 + c;
+            if (lane == 0 && m < M && n < N) y[(size_t)m * ldy + n] = epi_apply(epi, v, m, n, bias, res, ldy);
         }
     }
 }
@@ -208,11 +232,12 @@ static double q8_bytes(int M, const Q8Mat& W, int epi) {
 void gemv_q8(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const float* bias, const float* res, float* y,
              int ldy, int epi, hipStream_t s) {
     ProfScope ps(s, "gemv_q8", 2.0 * M * W.N * W.K, q8_bytes(M, W, epi));
-    dim3 grid(cdiv(W.N, 4));
-    if (M <= 1) k_gemv_q8<1><<<grid, 256, 0, s>>>(W.qs, W.sc, W.N, W.K, xq, xd, M, bias, res, y, ldy, epi);
-    else if (M <= 2) k_gemv_q8<2><<<grid, 256, 0, s>>>(W.qs, W.sc, W.N, W.K, xq, xd, M, bias, res, y, ldy, epi);
-    else if (M <= 4) k_gemv_q8<4><<<grid, 256, 0, s>>>(W.qs, W.sc, W.N, W.K, xq, xd, M, bias, res, y, ldy, epi);
-    else k_gemv_q8<8><<<grid, 256, 0, s>>>(W.qs, W.sc, W.N, W.K, xq, xd, M, bias, res, y, ldy, epi);
+    QASR_CHECK(W.K % 32 == 0 && W.K >= 32, QASR_E_INVALID, "gemv_q8: K must be a multiple of 32");
+    const dim3 g4(cdiv(W.N, 16)), g2(cdiv(W.N, 8));
+    if (M <= 1) k_gemv_q8<1, 4><<<g4, 256, 0, s>>>(W.qs, W.sc, W.N, W.K, xq, xd, M, bias, res, y, ldy, epi);
+    else if (M <= 2) k_gemv_q8<2, 4><<<g4, 256, 0, s>>>(W.qs, W.sc, W.N, W.K, xq, xd, M, bias, res, y, ldy, epi);
+    else if (M <= 4) k_gemv_q8<4, 4><<<g4, 256, 0, s>>>(W.qs, W.sc, W.N, W.K, xq, xd, M, bias, res, y, ldy, epi);
+    else k_gemv_q8<8, 2><<<g2, 256, 0, s>>>(W.qs, W.sc, W.N, W.K, xq, xd, M, bias, res, y, ldy, epi);
 }
 
 // ------------------------------------------------------------------------------------------------ GEMM (MFMA)
