@@ -101,6 +101,18 @@ def cpu_baseline(seconds=5.0, seed=0, threads=None):
                       f"oracle/qasr_oracle.c W8A8 with OpenMP ({dt:.1f} s wall)"}
 
 
+def traffic_per_launch(kernel):
+    """HBM-side bytes per launch of `kernel` from the committed PMC passes of this same bench command
+    (profiles/*_traffic_<kernel>.json, written by tools/pmc_traffic.py), or None."""
+    import glob
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_traffic_{kernel}.json")))
+    if not files:
+        return None
+    with open(files[-1]) as f:
+        return round(json.load(f)["per_launch_bytes"])
+
+
 def main():
     global SEG_PER_RANK
     ap = argparse.ArgumentParser()
@@ -189,7 +201,8 @@ def main():
                 peak = 5000.0 if name == "gemm_q8" else 2500.0   # dense i8 / f16 MFMA (MI355X_MICROARCH.md)
                 ach = p["flops"] / p["count"] / avg_s / 1e12
                 roof = {"bound": "mfma", "kernel": name, "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
-                        "frac": round(ach / peak, 4), "traffic": None,
+                        "frac": round(ach / peak, 4), "traffic": traffic_per_launch(name),
+                        "algorithmic_bytes_per_launch": round(p["bytes"] / p["count"]),
                         "avg_launch_us": round(avg_s * 1e6, 2), "launches": p["count"],
                         "measured_on": "one instrumented step after the timed region (HIP events per launch)"}
             else:
