@@ -50,8 +50,8 @@ QASR_API int qasr_op_linear_q8(const int8_t* xq, const float* xd, int32_t M, con
         } else if (path == 2) {
             gemm_q8(xq, xd, M, W, bias, res, y, ldy, epi, S(stream));
         } else if (path >= 16) {
-            const int cfg = (path - 16) & 7, splits = (path - 16) >> 3;
-            gemm_q8(xq, xd, M, W, bias, res, y, ldy, epi, S(stream), cfg == 7 ? -1 : cfg, splits);
+            const int cfg = (path - 16) % 16, splits = (path - 16) / 16;
+            gemm_q8(xq, xd, M, W, bias, res, y, ldy, epi, S(stream), cfg == 15 ? -1 : cfg, splits);
         } else {
             linear_q8(xq, xd, M, W, bias, res, y, ldy, epi, S(stream));
         }

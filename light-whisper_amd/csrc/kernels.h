@@ -25,7 +25,7 @@ void linear_q8(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const f
                float* y, int ldy, int epi, hipStream_t s);
 void gemv_q8(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const float* bias, const float* res, float* y,
              int ldy, int epi, hipStream_t s);
-// force_cfg: tile config 0 128×128, 1 64×128, 2 64×64, 3 32×64 (-1 = heuristic); force_splits: split-K (0 = heuristic)
+// force_cfg: index into kernels_q8.hip kGemmCfgs (-1 = heuristic); force_splits: split-K (0 = heuristic)
 void gemm_q8(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const float* bias, const float* res, float* y,
              int ldy, int epi, hipStream_t s, int force_cfg = -1, int force_splits = 0, int8_t* yq = nullptr,
              float* yd = nullptr);

@@ -251,6 +251,65 @@ void gemv_q8(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const flo
 // consumed, one barrier per step.
 // Split-K over grid.z fills the chip when M·N has few tiles (decode): partial sums are added with f32 atomics
 // (y pre-zeroed for a plain store; the residual already sits in y), the bias is added by split 0.
+// Shared GEMM epilogue: the wave's (16·TI)×(16·TJ) f32 accumulators (lane: rows fq..fq+3 of each 16-row
+// fragment, column fr of each 16-column fragment) → bias / residual / GELU store, split-K f32 atomics, or the fused
+// SwiGLU + Q8 quantisation of interleaved gate/up columns.
+template <int TI, int TJ>
+__device__ __forceinline__ void gemm_epilogue(const float (&acc)[TI][TJ][4], int M, int N, int m0, int n0, int arow,
+                                              int bcol, int fr, int fq, const float* __restrict__ bias,
+                                              const float* res, float* y, int ldy, int epi, int8_t* __restrict__ yq,
+                                              float* __restrict__ yd) {
+    if constexpr (TJ == 4) {
+        if (epi == EPI_SWIGLU) {
+            // this wave's 64 columns = gate/up of 32 consecutive h columns = one Q8 block of the SwiGLU output
+            const int F = N / 2, hb = (n0 + bcol) / 2;
+#pragma unroll
+            for (int i = 0; i < TI; i++) {
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    const int row = m0 + arow + i * 16 + fq + r;
+                    const float g0 = acc[i][0][r], g1 = acc[i][2][r];
+                    const float h0 = g0 / (1.f + expf(-g0)) * acc[i][1][r];
+                    const float h1 = g1 / (1.f + expf(-g1)) * acc[i][3][r];
+                    float am = fmaxf(fabsf(h0), fabsf(h1));
+                    am = fmaxf(am, __shfl_xor(am, 1));
+                    am = fmaxf(am, __shfl_xor(am, 2));
+                    am = fmaxf(am, __shfl_xor(am, 4));
+                    am = fmaxf(am, __shfl_xor(am, 8));
+                    const float dd = am / 127.f;
+                    if (row < M && hb < F) {
+                        int8_t* qr = yq + (size_t)row * F + hb;
+                        qr[fr] = (int8_t)(am == 0.f ? 0 : (int)roundf(h0 / dd));
+                        qr[16 + fr] = (int8_t)(am == 0.f ? 0 : (int)roundf(h1 / dd));
+                        if (fr == 0) yd[(size_t)row * (F / QK) + hb / QK] = __half2float(f2h(dd));
+                    }
+                }
+            }
+            return;
+        }
+    }
+    const bool split = gridDim.z > 1;
+#pragma unroll
+    for (int i = 0; i < TI; i++) {
+#pragma unroll
+        for (int j = 0; j < TJ; j++) {
+            const int col = n0 + bcol + j * 16 + fr;
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const int row = m0 + arow + i * 16 + fq + r;
+                if (row >= M || col >= N) continue;
+                if (split) {
+                    float v = acc[i][j][r];
+                    if (bias && blockIdx.z == 0) v += bias[col];
+                    atomicAdd(y + (size_t)row * ldy + col, v);
+                } else {
+                    y[(size_t)row * ldy + col] = epi_apply(epi, acc[i][j][r], row, col, bias, res, ldy);
+                }
+            }
+        }
+    }
+}
+
 constexpr int GBK = 128;     // K per step
 constexpr int GLD = 144;     // LDS row stride (bytes)
 
@@ -412,55 +471,207 @@ __global__ __launch_bounds__(256) void k_gemm_q8(const int8_t* __restrict__ X, c
         step(S0{}, s);
         if (s + 1 < nsteps) step(S1{}, s + 1);
     }
-    if constexpr (TJ == 4) {
-        if (epi == EPI_SWIGLU) {
-            // this wave's 64 columns = gate/up of 32 consecutive h columns = one Q8 block of the SwiGLU output
-            const int F = N / 2, hb = (n0 + bcol) / 2;
-#pragma unroll
-            for (int i = 0; i < TI; i++) {
-#pragma unroll
-                for (int r = 0; r < 4; r++) {
-                    const int row = m0 + arow + i * 16 + fq + r;
-                    const float g0 = acc[i][0][r], g1 = acc[i][2][r];
-                    const float h0 = g0 / (1.f + expf(-g0)) * acc[i][1][r];
-                    const float h1 = g1 / (1.f + expf(-g1)) * acc[i][3][r];
-                    float am = fmaxf(fabsf(h0), fabsf(h1));
-                    am = fmaxf(am, __shfl_xor(am, 1));
-                    am = fmaxf(am, __shfl_xor(am, 2));
-                    am = fmaxf(am, __shfl_xor(am, 4));
-                    am = fmaxf(am, __shfl_xor(am, 8));
-                    const float dd = am / 127.f;
-                    if (row < M && hb < F) {
-                        int8_t* qr = yq + (size_t)row * F + hb;
-                        qr[fr] = (int8_t)(am == 0.f ? 0 : (int)roundf(h0 / dd));
-                        qr[16 + fr] = (int8_t)(am == 0.f ? 0 : (int)roundf(h1 / dd));
-                        if (fr == 0) yd[(size_t)row * (F / QK) + hb / QK] = __half2float(f2h(dd));
-                    }
-                }
-            }
-            return;
-        }
+    gemm_epilogue<TI, TJ>(acc, M, N, m0, n0, arow, bcol, fr, fq, bias, res, y, ldy, epi, yq, yd);
+}
+
+
+// LDS-DMA (global_load_lds): lane i's 16 (4) bytes from its own global address land at LDS byte m0 + 16·i (4·i).
+// Issued from inline asm so the compiler does not treat the in-flight DMA as a pending LDS write and drain it
+// (vmcnt(0)) before the next ds_read; the kernels count these loads in their own s_waitcnt vmcnt(N).
+__device__ __forceinline__ void dma_lds16(const void* g, uint32_t lds) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(g), "s"(lds) : "memory");
+}
+__device__ __forceinline__ void dma_lds4(const void* g, uint32_t lds) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(g), "s"(lds) : "memory");
+}
+
+// ------------------------------------------------------------------------------------------------ GEMM (LDS-DMA)
+// The main Q8 W8A8 GEMM (K % 64 == 0).  256 threads = WM×WN waves, wave tile (16·TI)×(16·TJ) of
+// v_mfma_i32_16x16x32_i8 (one MFMA = the exact int32 sum of one Q8 block for a 16×16 sub-tile), workgroup tile
+// BM×BN = (WM·16·TI)×(WN·16·TJ).  2×2 waves of 64×64 (128×128) serve prefill / encoder shapes; 4×1 waves
+// (256×64, 128×64) serve batched decode, where the whole active row set shares every weight panel so the
+// weights stream from HBM once per step.
+//  * Staging: every operand byte goes global → LDS by `global_load_lds` (LDS-DMA, no VGPR staging, no ds_write):
+//    a stage is K = 64 (two Q8 blocks) of A [BM][64 B] and B [BN][64 B], A block scales [2][BM] f32 and B scales
+//    [BN] × (2 × f16); an NBUF-stage ring keeps stages s+1 … s+NBUF-1 in flight while stage s is consumed (deep
+//    rings for the small decode tiles, whose K loop is latency-bound), with one raw barrier per stage and a
+//    counted `vmcnt`.
+//  * LDS image: 64-B rows, 16-B chunk c of row r stored at chunk c ^ ((r >> 2) & 3) (the DMA is lane-linear, so the
+//    swizzle is applied to each lane's SOURCE address); single ds_read_b64 fragment reads (2 × 32 lanes, 64 banks)
+//    are then bank-conflict free.  Fragment addresses are made opaque so the compiler cannot pair two of them
+//    into ds_read2st64_b64, whose 16-lane / 32-bank groups would conflict 2-way on this image.
+//  * Compute: MFMA q is issued LAG MFMAs before its int32 result is rescaled into the f32 accumulator
+//    (cvt, d_x·d_w, fma: 3 VALU per output and block); sched_group_barrier pins the MFMA/VALU interleave.  Waves
+//    whose rows all lie past M (padded decode buckets) skip the math but still stage their share.
+template <int N>
+__device__ __forceinline__ void wait_vm_lgkm0() {
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(N) : "memory");
+}
+// wait until at most ahead·NPW of this wave's DMAs are outstanding (ahead ∈ [0, D))
+template <int NPW, int D>
+__device__ __forceinline__ void wait_stages(int ahead) {
+    static_assert(D <= 8 && NPW * (D - 1) <= 63, "vmcnt range");
+    switch (ahead) {
+        case 0: wait_vm_lgkm0<0>(); break;
+        case 1: wait_vm_lgkm0<NPW * (D > 1 ? 1 : 0)>(); break;
+        case 2: wait_vm_lgkm0<NPW * (D > 2 ? 2 : 0)>(); break;
+        case 3: wait_vm_lgkm0<NPW * (D > 3 ? 3 : 0)>(); break;
+        case 4: wait_vm_lgkm0<NPW * (D > 4 ? 4 : 0)>(); break;
+        case 5: wait_vm_lgkm0<NPW * (D > 5 ? 5 : 0)>(); break;
+        case 6: wait_vm_lgkm0<NPW * (D > 6 ? 6 : 0)>(); break;
+        default: wait_vm_lgkm0<NPW * (D > 7 ? 7 : 0)>(); break;
     }
-    const bool split = gridDim.z > 1;
+}
+
+template <int WM, int WN, int TI, int TJ, int NBUF>
+__global__ __launch_bounds__(256, 2) void k_gemm_q8d(const int8_t* __restrict__ X, const float* __restrict__ Xd, int M,
+                                                     const int8_t* __restrict__ W, const __half* __restrict__ Wsc,
+                                                     int N, int K, const float* __restrict__ bias, const float* res,
+                                                     float* y, int ldy, int epi, int steps_per_split,
+                                                     int8_t* __restrict__ yq, float* __restrict__ yd) {
+    static_assert(WM * WN == 4, "k_gemm_q8d: 4 waves");
+    constexpr int BM = WM * 16 * TI, BN = WN * 16 * TJ, BK = 64, NF = TI * TJ;
+    static_assert(BM % 64 == 0 && BN % 64 == 0 && BN <= 256, "k_gemm_q8d: tile sides must be multiples of 64");
+    constexpr int OB = BM * BK, OSA = OB + BN * BK, OSB = OSA + 2 * BM * 4, STAGE = OSB + BN * 4;
+    constexpr int AI = BM / 64, BI = BN / 64;           // 1-KB A / B DMA pieces per wave per stage
+    constexpr int SAW = BM / 2, ASI = (SAW + 63) / 64;  // A-scale dwords / DMA instructions per wave per stage
+    constexpr int NPW = AI + BI + ASI + 1;              // DMA instructions per wave per stage
+    constexpr int D = NBUF - 1;                         // prefetch distance (stages in flight)
+    __shared__ __attribute__((aligned(1024))) char smem[NBUF * STAGE];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wr = wave / WN, wc = wave % WN;
+    const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM;
+    const int nb = K / QK;
+    const int k_begin = blockIdx.z * steps_per_split * BK;
+    const int k_end = min(K, k_begin + steps_per_split * BK);
+    const int nsteps = max(0, (k_end - k_begin) / BK);
+
+    // ---- per-lane DMA sources (k-independent parts)
+    const int8_t* a_src[AI];
+    const int8_t* b_src[BI];
 #pragma unroll
-    for (int i = 0; i < TI; i++) {
+    for (int u = 0; u < AI; u++) {
+        const int row = 16 * (wave * AI + u) + (lane >> 2), c = (lane & 3) ^ ((row >> 2) & 3);
+        a_src[u] = X + (size_t)min(m0 + row, M - 1) * K + 16 * c;
+    }
+#pragma unroll
+    for (int u = 0; u < BI; u++) {
+        const int row = 16 * (wave * BI + u) + (lane >> 2), c = (lane & 3) ^ ((row >> 2) & 3);
+        b_src[u] = W + (size_t)min(n0 + row, N - 1) * K + 16 * c;
+    }
+    const float* sa_src[ASI];
+#pragma unroll
+    for (int u = 0; u < ASI; u++) {
+        const int p = wave * SAW + min(64 * u + lane, SAW - 1), kb = p / BM, row = p % BM;
+        sa_src[u] = Xd + (size_t)min(m0 + row, M - 1) * nb + kb;
+    }
+    const bool sb_on = lane < BN / 4;
+    const uint32_t* sb_src =
+        (const uint32_t*)Wsc + (size_t)min(n0 + wave * (BN / 4) + min(lane, BN / 4 - 1), N - 1) * (nb / 2);
+
+    // LDS byte address of this wave's pieces (wave-uniform → SGPR for M0)
+    const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
+    const uint32_t wa = __builtin_amdgcn_readfirstlane(lds0 + 1024 * (wave * AI));
+    const uint32_t wb = __builtin_amdgcn_readfirstlane(lds0 + OB + 1024 * (wave * BI));
+    const uint32_t wsa = __builtin_amdgcn_readfirstlane(lds0 + OSA + wave * SAW * 4);
+    const uint32_t wsb = __builtin_amdgcn_readfirstlane(lds0 + OSB + wave * (BN / 4) * 4);
+    auto issue = [&](int s, int buf) {
+        const int k0 = k_begin + s * BK;
+        const uint32_t so = buf * STAGE;
+#pragma unroll
+        for (int u = 0; u < AI; u++) dma_lds16(a_src[u] + k0, wa + so + 1024 * u);
+#pragma unroll
+        for (int u = 0; u < BI; u++) dma_lds16(b_src[u] + k0, wb + so + 1024 * u);
+#pragma unroll
+        for (int u = 0; u < ASI; u++)
+            if (64 * u + lane < SAW) dma_lds4(sa_src[u] + k0 / QK, wsa + so + 256 * u);
+        if (sb_on) dma_lds4(sb_src + k0 / 64, wsb + so);
+    };
+
+    const int fr = lane & 15, kh = lane >> 4, fq = 4 * kh;
+    const int arow = wr * 16 * TI, bcol = wc * 16 * TJ;
+    const bool active = m0 + arow < M;   // wave-uniform
+    const int sw = (fr >> 2) & 3;
+    const int foff0 = 16 * ((0 + (kh >> 1)) ^ sw) + 8 * (kh & 1);
+    const int foff1 = 16 * ((2 + (kh >> 1)) ^ sw) + 8 * (kh & 1);
+
+    float acc[TI][TJ][4];
+#pragma unroll
+    for (int i = 0; i < TI; i++)
+#pragma unroll
+        for (int j = 0; j < TJ; j++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) acc[i][j][r] = 0.f;
+
+#pragma unroll
+    for (int t = 0; t < D; t++)
+        if (t < nsteps) issue(t, t);
+    for (int s = 0; s < nsteps; s++) {
+        // this wave's DMAs of stage s have landed and its LDS reads of stage s-1 are done; the barrier then makes
+        // that true for every wave, so stage s is readable and buffer (s+D)%NBUF (= stage s-1's) is free
+        wait_stages<NPW, D>(min(D - 1, nsteps - 1 - s));
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (s + D < nsteps) issue(s + D, (s + D) % NBUF);
+        if (!active) continue;
+        const char* st = smem + (s % NBUF) * STAGE;
+        float sb[2][TJ], sa[2][TI][4];
+        long a[2][TI], b[2][TJ];
 #pragma unroll
         for (int j = 0; j < TJ; j++) {
-            const int col = n0 + bcol + j * 16 + fr;
+            const uint32_t v = *(const uint32_t*)(st + OSB + 4 * (bcol + 16 * j + fr));
+            sb[0][j] = __half2float(__ushort_as_half((unsigned short)(v & 0xffff)));
+            sb[1][j] = __half2float(__ushort_as_half((unsigned short)(v >> 16)));
+        }
 #pragma unroll
-            for (int r = 0; r < 4; r++) {
-                const int row = m0 + arow + i * 16 + fq + r;
-                if (row >= M || col >= N) continue;
-                if (split) {
-                    float v = acc[i][j][r];
-                    if (bias && blockIdx.z == 0) v += bias[col];
-                    atomicAdd(y + (size_t)row * ldy + col, v);
-                } else {
-                    y[(size_t)row * ldy + col] = epi_apply(epi, acc[i][j][r], row, col, bias, res, ldy);
-                }
+        for (int kb = 0; kb < 2; kb++) {
+            const int foff = kb ? foff1 : foff0;
+#pragma unroll
+            for (int i = 0; i < TI; i++) {
+                int off = (arow + 16 * i + fr) * BK + foff;
+                asm volatile("" : "+v"(off));
+                a[kb][i] = *(const long*)(st + off);
+                const float4 v = *(const float4*)(st + OSA + 4 * (kb * BM + arow + 16 * i + fq));
+                sa[kb][i][0] = v.x, sa[kb][i][1] = v.y, sa[kb][i][2] = v.z, sa[kb][i][3] = v.w;
+            }
+#pragma unroll
+            for (int j = 0; j < TJ; j++) {
+                int off = OB + (bcol + 16 * j + fr) * BK + foff;
+                asm volatile("" : "+v"(off));
+                b[kb][j] = *(const long*)(st + off);
             }
         }
+        // MFMA q (block q / NF, fragment q % NF) is issued LAG MFMAs before its rescale, so the int32 result has
+        // landed by the time the cvt/fma reach it and at most LAG+1 results are live
+        constexpr int LAG = 3, NQ = 2 * NF;
+        v4i c[LAG + 1];
+#pragma unroll
+        for (int q = 0; q < NQ + LAG; q++) {
+            if (q < NQ) {
+                const int kb = q / NF, f = q % NF;
+                c[q % (LAG + 1)] =
+                    __builtin_amdgcn_mfma_i32_16x16x32_i8(a[kb][f / TJ], b[kb][f % TJ], v4i{0, 0, 0, 0}, 0, 0, 0);
+            }
+            if (q >= LAG) {
+                const int p = q - LAG, kb = p / NF, f = p % NF, i = f / TJ, j = f % TJ;
+#pragma unroll
+                for (int r = 0; r < 4; r++)
+                    acc[i][j][r] = fmaf((float)c[p % (LAG + 1)][r], sa[kb][i][r] * sb[kb][j], acc[i][j][r]);
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < NQ; t++) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, 12, 0);
+        }
     }
+    if (!active) return;
+    gemm_epilogue<TI, TJ>(acc, M, N, m0, n0, arow, bcol, fr, fq, bias, res, y, ldy, epi, yq, yd);
 }
 
 template <int TI, int TJ>
@@ -469,32 +680,82 @@ static void launch_gemm(dim3 grid, hipStream_t s, const int8_t* xq, const float*
                         float* yd) {
     k_gemm_q8<TI, TJ><<<grid, 256, 0, s>>>(xq, xd, M, W.qs, W.sc, W.N, W.K, bias, res, y, ldy, epi, sps, yq, yd);
 }
+template <int WM, int WN, int TI, int TJ, int NBUF = 3>
+static void launch_gemm_dma(dim3 grid, hipStream_t s, const int8_t* xq, const float* xd, int M, const Q8Mat& W,
+                            const float* bias, const float* res, float* y, int ldy, int epi, int sps, int8_t* yq,
+                            float* yd) {
+    k_gemm_q8d<WM, WN, TI, TJ, NBUF><<<grid, 256, 0, s>>>(xq, xd, M, W.qs, W.sc, W.N, W.K, bias, res, y, ldy, epi, sps, yq,
+                                                    yd);
+}
 
+// GEMM configurations: 0..3 register-staged kernel (any K % 32 == 0), 4..10 LDS-DMA kernel (K % 64 == 0).
+struct GemmCfg { int bm, bn; bool dma; };
+static const GemmCfg kGemmCfgs[] = {
+    {128, 128, false}, {64, 128, false}, {64, 64, false}, {32, 64, false},        // 0..3
+    {128, 128, true}, {64, 128, true}, {64, 64, true}, {128, 64, true},           // 4..7  (2×2 waves)
+    {256, 64, true}, {128, 64, true}, {64, 64, true},                             // 8..10 (4×1 waves)
+    {64, 64, true}, {64, 128, true}, {128, 64, true}, {64, 64, true},             // 11..14 deep rings
+};
+constexpr int kNumGemmCfgs = sizeof(kGemmCfgs) / sizeof(kGemmCfgs[0]);
+
+static void launch_cfg(int cfg, dim3 grid, hipStream_t s, const int8_t* xq, const float* xd, int M, const Q8Mat& W,
+                       const float* bias, const float* res, float* y, int ldy, int epi, int sps, int8_t* yq,
+                       float* yd) {
+    switch (cfg) {
+        case 0: launch_gemm<4, 4>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
+        case 1: launch_gemm<2, 4>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
+        case 2: launch_gemm<2, 2>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
+        case 3: launch_gemm<1, 2>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
+        case 4: launch_gemm_dma<2, 2, 4, 4>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
+        case 5: launch_gemm_dma<2, 2, 2, 4>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
+        case 6: launch_gemm_dma<2, 2, 2, 2>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
+        case 7: launch_gemm_dma<2, 2, 4, 2>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
+        case 8: launch_gemm_dma<4, 1, 4, 4>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
+        case 9: launch_gemm_dma<4, 1, 2, 4>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
+        case 10: launch_gemm_dma<4, 1, 1, 4>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
+        case 11: launch_gemm_dma<2, 2, 2, 2, 6>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
+        case 12: launch_gemm_dma<2, 2, 2, 4, 4>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
+        case 13: launch_gemm_dma<4, 1, 2, 4, 4>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
+        default: launch_gemm_dma<4, 1, 1, 4, 6>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
+    }
+}
+
+// force_cfg: -1 auto, else an index into kGemmCfgs (a DMA config on K % 64 != 0 falls back to auto);
+// force_splits: split-K (0 = heuristic).
 void gemm_q8(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const float* bias, const float* res, float* y,
              int ldy, int epi, hipStream_t s, int force_cfg, int force_splits, int8_t* yq, float* yd) {
     ProfScope ps(s, "gemm_q8", 2.0 * M * W.N * W.K, q8_bytes(M, W, epi));
+    const bool dma_ok = W.K % 64 == 0;
+    int pick;
+    if (dma_ok) {
+        // decode-sized M: the whole row set in one tile (4×1 waves), so each weight panel streams once;
+        // prefill: 128×128 (64×128 when that leaves fewer than 256 tiles)
+        if (M <= 64) pick = 10;
+        else if (M <= 128) pick = 9;
+        else if (M <= 256) pick = 8;
+        else pick = (long)cdiv(W.N, 128) * cdiv(M, 128) >= 256 ? 4 : 5;
+    } else {
+        static const int order[] = {0, 1, 2, 3};
+        const int first = M <= 32 ? 3 : M <= 64 ? 1 : 0, last = M <= 32 ? 3 : 2;
+        pick = last;
+        for (int c = first; c <= last; c++)
+            if ((long)cdiv(W.N, kGemmCfgs[order[c]].bn) * cdiv(M, kGemmCfgs[order[c]].bm) >= 256) {
+                pick = c;
+                break;
+            }
+    }
+    if (force_cfg >= 0 && force_cfg < kNumGemmCfgs && (!kGemmCfgs[force_cfg].dma || dma_ok)) pick = force_cfg;
+    const GemmCfg& cf = kGemmCfgs[pick];
     if (epi == EPI_SWIGLU) {
         QASR_CHECK(W.N % 64 == 0 && yq && yd, QASR_E_INVALID, "gemm_q8: SwiGLU epilogue needs N % 64 == 0");
-        const bool big = M > 64 && (long)cdiv(W.N, 128) * cdiv(M, 128) >= 256;
-        dim3 grid(cdiv(W.N, 128), cdiv(M, big ? 128 : 64), 1);
-        if (big)
-            launch_gemm<4, 4>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, cdiv(W.K, GBK), yq, yd);
-        else
-            launch_gemm<2, 4>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, cdiv(W.K, GBK), yq, yd);
+        QASR_CHECK(pick != 2 && pick != 3 && pick != 6 && pick != 7 && pick != 11, QASR_E_INVALID,
+                   "gemm_q8: SwiGLU epilogue needs a 64-column wave tile");
+        dim3 grid(cdiv(W.N, cf.bn), cdiv(M, cf.bm), 1);
+        launch_cfg(pick, grid, s, xq, xd, M, W, bias, res, y, ldy, epi, cf.dma ? W.K / 64 : cdiv(W.K, GBK), yq, yd);
         return;
     }
-    // tile choice: the largest tile that still gives >= 256 workgroups (one per CU), else the smallest allowed
-    // for this M, then split-K up to ~512 workgroups
-    struct Cfg { int ti, tj; };
-    static const Cfg cfgs[] = {{4, 4}, {2, 4}, {2, 2}, {1, 2}};
-    const int first = M <= 32 ? 3 : M <= 64 ? 1 : 0, last = M <= 32 ? 3 : 2;
-    int pick = last;
-    for (int c = first; c <= last; c++)
-        if ((long)cdiv(W.N, 32 * cfgs[c].tj) * cdiv(M, 32 * cfgs[c].ti) >= 256) { pick = c; break; }
-    if (force_cfg >= 0 && force_cfg < 4) pick = force_cfg;
-    const int BM = 32 * cfgs[pick].ti, BN = 32 * cfgs[pick].tj;
-    const int tiles = cdiv(W.N, BN) * cdiv(M, BM);
-    const int steps = cdiv(W.K, GBK);
+    const int tiles = cdiv(W.N, cf.bn) * cdiv(M, cf.bm);
+    const int steps = cf.dma ? W.K / 64 : cdiv(W.K, GBK);
     const bool can_split = epi != EPI_GELU && ldy == W.N && (epi != EPI_RESID || res == y);
     int splits = 1;
     if (tiles < 256 && can_split) splits = std::max(1, std::min(std::min(cdiv(512, tiles), steps / 2), 8));
@@ -502,13 +763,8 @@ void gemm_q8(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const flo
     const int sps = cdiv(steps, splits);
     splits = cdiv(steps, sps);
     if (splits > 1 && epi == EPI_STORE) QASR_HIP(hipMemsetAsync(y, 0, (size_t)M * ldy * sizeof(float), s));
-    dim3 grid(cdiv(W.N, BN), cdiv(M, BM), splits);
-    switch (pick) {
-        case 0: launch_gemm<4, 4>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, nullptr, nullptr); break;
-        case 1: launch_gemm<2, 4>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, nullptr, nullptr); break;
-        case 2: launch_gemm<2, 2>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, nullptr, nullptr); break;
-        default: launch_gemm<1, 2>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, nullptr, nullptr); break;
-    }
+    dim3 grid(cdiv(W.N, cf.bn), cdiv(M, cf.bm), splits);
+    launch_cfg(pick, grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, nullptr, nullptr);
 }
 
 int64_t gate_up_interleaved_row(int64_t r, int64_t F) {

@@ -138,7 +138,12 @@ def _linear_case(torch_dev, m, n, k, path, epi, seed=0, exact=False):
     return host(y), ref.astype(np.float32)
 
 
-@pytest.mark.parametrize("path", [1, 2])
+# path: 1 GEMV, 2 auto, 16 + cfg (+ 16·splits) forces a GEMM configuration (kernels_q8.hip kGemmCfgs: 0..3 register-
+# staged, 4..10 LDS-DMA)
+GEMM_PATHS = [1, 2] + [16 + c for c in range(15)] + [16 + 4 + 16 * 2, 16 + 8 + 16 * 4, 16 + 10 + 16 * 3]
+
+
+@pytest.mark.parametrize("path", GEMM_PATHS)
 @pytest.mark.parametrize("m,n,k", [(1, 64, 1024), (3, 130, 512), (8, 64, 1024), (9, 70, 96), (64, 128, 1024),
                                    (100, 192, 512), (32, 2048, 2048), (300, 2048, 1024), (33, 96, 160)])
 def test_linear_q8_exact_integer(torch_dev, path, m, n, k):
@@ -148,7 +153,7 @@ def test_linear_q8_exact_integer(torch_dev, path, m, n, k):
     assert np.array_equal(y, ref)
 
 
-@pytest.mark.parametrize("path", [1, 2])
+@pytest.mark.parametrize("path", GEMM_PATHS)
 @pytest.mark.parametrize("epi", [0, 1, 2])
 @pytest.mark.parametrize("m,n,k", [(1, 2048, 2048), (5, 256, 6144), (37, 320, 2048), (130, 1024, 1024),
                                    (24, 2048, 6144), (257, 2048, 2048)])

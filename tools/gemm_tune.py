@@ -21,6 +21,11 @@ SHAPES = [  # (tag, M, N, K, epi)
 ]
 
 
+# 2 = auto; 16 + cfg (+ 16·splits): kernels_q8.hip kGemmCfgs — 0..3 register-staged {128², 64×128, 64², 32×64},
+# 4..7 LDS-DMA 2×2 waves {128², 64×128, 64², 128×64}, 8..10 LDS-DMA 4×1 waves {256×64, 128×64, 64×64}
+PATHS = [int(p) for p in os.environ.get("PATHS", "2,16,18,20,21,24,25,26").split(",")]
+
+
 def main():
     lib = _lib.load(os.environ.get("QASR_LIB", _lib.LIB_PATH))
     print("lib:", os.environ.get("QASR_LIB", _lib.LIB_PATH))
@@ -37,7 +42,7 @@ def main():
         res = y if epi == 1 else None
         flops = 2.0 * M * N * K
         out = []
-        for path in [2] + [16 + c for c in range(4)] + [16 + c + 8 for c in range(4)]:
+        for path in PATHS:
             def run():
                 _lib.check(lib.qasr_op_linear_q8(xq.data_ptr(), xd.data_ptr(), M, wq.data_ptr(), ws.data_ptr(), N,
                                                  K, None, res.data_ptr() if res is not None else None,
