@@ -302,8 +302,11 @@ void Session::decoder_layers(float* x, int rows, const int* d_pos, const int* d_
         const DecLayer& L = m_->dec[l];
         __half* kc = kc_ + (size_t)l * layer_kv;
         __half* vc = vc_ + (size_t)l * layer_kv;
-        rmsnorm_q8(x, rows, H, H, L.attn_norm, h.rms_eps, xq, xd, st_);
-        linear_q8(xq, xd, rows, L.qkv, nullptr, nullptr, qkv, QD + 2 * KD, EPI_STORE, st_);
+        // decode-sized steps: the norm launch also clears the QKV output, so the split-K QKV GEMM needs no memset
+        const bool zq = rows <= 256;
+        rmsnorm_q8(x, rows, H, H, L.attn_norm, h.rms_eps, xq, xd, st_, zq ? qkv : nullptr,
+                   zq ? (int64_t)rows * (QD + 2 * KD) : 0);
+        linear_q8(xq, xd, rows, L.qkv, nullptr, nullptr, qkv, QD + 2 * KD, EPI_STORE, st_, zq);
         qk_norm_rope(qkv, rows, nh, nkv, hd, d_pos, d_slot, L.q_norm, L.k_norm, rope_, h.rms_eps, qh, kc, vc, st_);
         attention(qh, QD, kc, vc, KD, d_kvs, d_kvl, rows, nh, nkv, hd, scale, nullptr, xq, xd, st_, total_keys);
         linear_q8(xq, xd, rows, L.o, nullptr, x, x, H, EPI_RESID, st_);

@@ -21,14 +21,15 @@ void synth_f16(uint64_t base, int64_t n, float scale, __half* out, hipStream_t s
 // quantise rows of x (row stride ldx floats) into q [M][K] / d [M][K/32]
 void quant_rows(const float* x, int M, int K, int ldx, int8_t* q, float* d, hipStream_t s);
 // y[M][N] (row stride ldy) = epi(X·Wᵀ); dispatches GEMV (M ≤ 8) or the MFMA GEMM
+// y_zeroed: y is already all-zero (a split-K GEMM then skips its memset)
 void linear_q8(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const float* bias, const float* res,
-               float* y, int ldy, int epi, hipStream_t s);
+               float* y, int ldy, int epi, hipStream_t s, bool y_zeroed = false);
 void gemv_q8(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const float* bias, const float* res, float* y,
              int ldy, int epi, hipStream_t s);
 // force_cfg: index into kernels_q8.hip kGemmCfgs (-1 = heuristic); force_splits: split-K (0 = heuristic)
 void gemm_q8(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const float* bias, const float* res, float* y,
              int ldy, int epi, hipStream_t s, int force_cfg = -1, int force_splits = 0, int8_t* yq = nullptr,
-             float* yd = nullptr);
+             float* yd = nullptr, bool y_zeroed = false);
 // rows of a [2F][K] gate|up matrix → interleaved by 16 (32j+t: t<16 gate 16j+t, else up 16j+t-16)
 int64_t gate_up_interleaved_row(int64_t r, int64_t F);
 void interleave_gate_up(Q8Mat& W, hipStream_t s);
@@ -36,7 +37,9 @@ void interleave_gate_up(Q8Mat& W, hipStream_t s);
 void embed_rows(const int* ids, int n, const Q8Mat& W, const float* alt, float* out, hipStream_t s);
 
 // ---- norms / elementwise (kernels_nn.hip)
-void rmsnorm_q8(const float* x, int M, int H, int ldx, const float* w, float eps, int8_t* q, float* d, hipStream_t s);
+// zero/nzero (optional): a float range cleared by the same launch (the next split-K GEMM's output)
+void rmsnorm_q8(const float* x, int M, int H, int ldx, const float* w, float eps, int8_t* q, float* d, hipStream_t s,
+                float* zero = nullptr, int64_t nzero = 0);
 void layernorm_q8(const float* x, int M, int H, const float* w, const float* b, float eps, int8_t* q, float* d,
                   float* y_opt, hipStream_t s);
 // gu rows [gate F | up F], or interleaved by 16 (interleave_gate_up layout)

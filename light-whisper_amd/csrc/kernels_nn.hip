@@ -100,13 +100,67 @@ __global__ __launch_bounds__(256) void k_rmsnorm_q8(const float* __restrict__ x,
     }
 }
 
-void rmsnorm_q8(const float* x, int M, int H, int ldx, const float* w, float eps, int8_t* q, float* d, hipStream_t s) {
+// One 256-thread workgroup per row (decode-sized launches have few rows: a wave per row leaves the chip idle and
+// serialises 8 chunks of divisions and shuffles per lane).  Thread t holds float4 chunks t, t+256, …; the sum of
+// squares is reduced by wave shuffles then across the four waves through LDS.
+template <int KC>
+__global__ __launch_bounds__(256) void k_rmsnorm_q8_wg(const float* __restrict__ x, int H, int ldx,
+                                                       const float* __restrict__ w, float eps, int8_t* __restrict__ q,
+                                                       float* __restrict__ d, float4* __restrict__ zero,
+                                                       int64_t nzero4) {
+    __shared__ float part[4];
+    const int tid = threadIdx.x, lane = tid & 63, row = blockIdx.x;
+    // optional: clear the next split-K GEMM's output (saves a memset launch per layer)
+    for (int64_t i = (int64_t)row * 256 + tid; i < nzero4; i += (int64_t)gridDim.x * 256)
+        zero[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    const int nc = H / 4;
+    const float4* xr = (const float4*)(x + (size_t)row * ldx);
+    const float4* g4 = (const float4*)w;
+    float4 v[KC], gw[KC];
+#pragma unroll
+    for (int k = 0; k < KC; k++) {
+        const int c = tid + 256 * k;
+        v[k] = c < nc ? xr[c] : make_float4(0.f, 0.f, 0.f, 0.f);
+        gw[k] = c < nc ? g4[c] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    float ss = 0.f;
+#pragma unroll
+    for (int k = 0; k < KC; k++) ss += v[k].x * v[k].x + v[k].y * v[k].y + v[k].z * v[k].z + v[k].w * v[k].w;
+    ss = wsum(ss);
+    if (lane == 0) part[tid >> 6] = ss;
+    __syncthreads();
+    ss = (part[0] + part[1]) + (part[2] + part[3]);
+    const float inv = 1.0f / sqrtf(ss / (float)H + eps);
+#pragma unroll
+    for (int k = 0; k < KC; k++) {
+        const int c = tid + 256 * k;
+        if (256 * k + (tid & ~7) < nc) {   // 8-thread blocks are all in or all out (nc % 8 == 0)
+            const float4 g = gw[k];
+            const float4 y = make_float4(v[k].x * inv * g.x, v[k].y * inv * g.y, v[k].z * inv * g.z, v[k].w * inv * g.w);
+            quant4_store(y, c, lane, q + (size_t)row * H, d + (size_t)row * (H / 32));
+        }
+    }
+}
+
+void rmsnorm_q8(const float* x, int M, int H, int ldx, const float* w, float eps, int8_t* q, float* d, hipStream_t s,
+                float* zero, int64_t nzero) {
     if (M <= 0) return;
     QASR_CHECK(H % 32 == 0 && H <= RW_MAX * 256 && ldx % 4 == 0, QASR_E_INVALID, "rmsnorm_q8: unsupported width");
-    const int kc = cdiv(H, 256);
-    if (kc <= 4)
+    QASR_CHECK(nzero % 4 == 0 && ((uintptr_t)zero & 15) == 0, QASR_E_INVALID, "rmsnorm_q8: zero range alignment");
+    const int kc = cdiv(H, 1024);   // float4 chunks per thread with a workgroup per row
+    if (M <= 2048 && kc <= 4) {
+        float4* z = zero ? (float4*)zero : nullptr;
+        const int64_t nz = zero ? nzero / 4 : 0;
+        if (kc <= 1) k_rmsnorm_q8_wg<1><<<M, 256, 0, s>>>(x, H, ldx, w, eps, q, d, z, nz);
+        else if (kc <= 2) k_rmsnorm_q8_wg<2><<<M, 256, 0, s>>>(x, H, ldx, w, eps, q, d, z, nz);
+        else k_rmsnorm_q8_wg<4><<<M, 256, 0, s>>>(x, H, ldx, w, eps, q, d, z, nz);
+        return;
+    }
+    if (zero && nzero) QASR_HIP(hipMemsetAsync(zero, 0, (size_t)nzero * sizeof(float), s));
+    const int kcw = cdiv(H, 256);
+    if (kcw <= 4)
         k_rmsnorm_q8<4><<<cdiv(M, 4), 256, 0, s>>>(x, M, H, ldx, w, eps, q, d);
-    else if (kc <= 8)
+    else if (kcw <= 8)
         k_rmsnorm_q8<8><<<cdiv(M, 4), 256, 0, s>>>(x, M, H, ldx, w, eps, q, d);
     else
         k_rmsnorm_q8<RW_MAX><<<cdiv(M, 4), 256, 0, s>>>(x, M, H, ldx, w, eps, q, d);

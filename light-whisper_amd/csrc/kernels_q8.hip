@@ -723,17 +723,15 @@ static void launch_cfg(int cfg, dim3 grid, hipStream_t s, const int8_t* xq, cons
 // force_cfg: -1 auto, else an index into kGemmCfgs (a DMA config on K % 64 != 0 falls back to auto);
 // force_splits: split-K (0 = heuristic).
 void gemm_q8(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const float* bias, const float* res, float* y,
-             int ldy, int epi, hipStream_t s, int force_cfg, int force_splits, int8_t* yq, float* yd) {
+             int ldy, int epi, hipStream_t s, int force_cfg, int force_splits, int8_t* yq, float* yd, bool y_zeroed) {
     ProfScope ps(s, "gemm_q8", 2.0 * M * W.N * W.K, q8_bytes(M, W, epi));
     const bool dma_ok = W.K % 64 == 0;
     int pick;
     if (dma_ok) {
-        // decode-sized M: the whole row set in one tile (4×1 waves), so each weight panel streams once;
-        // prefill: 128×128 (64×128 when that leaves fewer than 256 tiles)
-        if (M <= 64) pick = 10;
-        else if (M <= 128) pick = 9;
-        else if (M <= 256) pick = 8;
-        else pick = (long)cdiv(W.N, 128) * cdiv(M, 128) >= 256 ? 4 : 5;
+        // measured on the engine's shapes (tools/gemm_tune.py, profiles/): 64×128 tiles win on prefill / encoder
+        // shapes and on the vocabulary projection, 64×64 (+ split-K) on batched-decode shapes
+        if (M > 256 || W.N >= 32768) pick = M > 128 && W.N >= 32768 ? 4 : 5;
+        else pick = epi == EPI_SWIGLU ? 5 : 6;
     } else {
         static const int order[] = {0, 1, 2, 3};
         const int first = M <= 32 ? 3 : M <= 64 ? 1 : 0, last = M <= 32 ? 3 : 2;
@@ -762,7 +760,8 @@ void gemm_q8(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const flo
     if (force_splits > 0) splits = can_split ? std::min(force_splits, steps) : 1;
     const int sps = cdiv(steps, splits);
     splits = cdiv(steps, sps);
-    if (splits > 1 && epi == EPI_STORE) QASR_HIP(hipMemsetAsync(y, 0, (size_t)M * ldy * sizeof(float), s));
+    if (splits > 1 && epi == EPI_STORE && !y_zeroed)
+        QASR_HIP(hipMemsetAsync(y, 0, (size_t)M * ldy * sizeof(float), s));
     dim3 grid(cdiv(W.N, cf.bn), cdiv(M, cf.bm), splits);
     launch_cfg(pick, grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, nullptr, nullptr);
 }
@@ -794,10 +793,10 @@ void interleave_gate_up(Q8Mat& W, hipStream_t s) {
 }
 
 void linear_q8(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const float* bias, const float* res,
-               float* y, int ldy, int epi, hipStream_t s) {
+               float* y, int ldy, int epi, hipStream_t s, bool y_zeroed) {
     if (M <= 0) return;
     if (M <= 8) gemv_q8(xq, xd, M, W, bias, res, y, ldy, epi, s);
-    else gemm_q8(xq, xd, M, W, bias, res, y, ldy, epi, s);
+    else gemm_q8(xq, xd, M, W, bias, res, y, ldy, epi, s, -1, 0, nullptr, nullptr, y_zeroed);
 }
 
 // ------------------------------------------------------------------------------------------------ embeddings

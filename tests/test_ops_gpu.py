@@ -165,11 +165,12 @@ def test_linear_q8_vs_oracle(torch_dev, path, epi, m, n, k):
     assert np.abs(y - ref).max() <= 2e-5 * scale * np.sqrt(k / 256)
 
 
-def test_rmsnorm_q8(torch_dev):
+@pytest.mark.parametrize("m,h", [(9, 2048), (256, 1024), (5, 896), (3000, 2048)])
+def test_rmsnorm_q8(torch_dev, m, h):
+    """workgroup-per-row kernel (M <= 2048) and wave-per-row kernel (larger M)"""
     import torch
 
     rng = np.random.default_rng(3)
-    m, h = 9, 2048
     x = (rng.standard_normal((m, h)) * 3).astype(np.float32)
     w = (1 + 0.1 * rng.standard_normal(h)).astype(np.float32)
     xt, wt = dev(x, torch_dev), dev(w, torch_dev)
@@ -179,8 +180,10 @@ def test_rmsnorm_q8(torch_dev):
     y = x / np.sqrt((x.astype(np.float64) ** 2).mean(1, keepdims=True) + 1e-6) * w
     qr, dr = quant_ref(y.astype(np.float32))
     qh, dh = host(q), host(d)
-    assert np.allclose(dh, dr, rtol=1e-5)
-    assert (np.abs(qh.astype(int) - qr) <= 1).all() and (qh != qr).mean() < 1e-3
+    # the block scale is stored as f16: a 1-ulp f32 difference in the row norm can flip its f16 rounding (one f16
+    # ulp, 2^-10 relative) — allowed on a small fraction of blocks
+    assert np.allclose(dh, dr, rtol=1.5e-3) and np.isclose(dh, dr, rtol=1e-5).mean() > 0.99
+    assert (np.abs(qh.astype(int) - qr) <= 1).all() and (qh != qr).mean() < 1e-2
 
 
 def test_layernorm_q8(torch_dev):
