@@ -183,6 +183,12 @@ QASR_API int qasr_op_qk_norm_rope(const float* qkv, int32_t rows, int32_t nh, in
 QASR_API int qasr_op_attention(const void* q, int32_t ldq, const void* k, const void* v, int32_t ldkv,
                                const int32_t* kv_start, const int32_t* kv_len, int32_t rows, int32_t nh, int32_t nkv,
                                int32_t hd, float scale, float* o, int8_t* oq, float* od, void* stream);
+/* Same contract; dense != 0 selects the MFMA tile kernel (runs of 16 consecutive rows sharing their key range:
+   prefill prompt rows, encoder windows); P·V in f16 (see DESIGN.md §2 for the tolerance). */
+QASR_API int qasr_op_attention_dense(const void* q, int32_t ldq, const void* k, const void* v, int32_t ldkv,
+                                     const int32_t* kv_start, const int32_t* kv_len, int32_t rows, int32_t nh,
+                                     int32_t nkv, int32_t hd, float scale, float* o, int8_t* oq, float* od,
+                                     int32_t dense, void* stream);
 QASR_API int qasr_op_argmax(const float* x, int32_t M, int32_t V, int32_t* out, void* stream);
 QASR_API int qasr_op_embed_rows(const int32_t* ids, int32_t n, const int8_t* wqs, const void* wsc, int32_t K,
                                 const float* alt, float* out, void* stream);

@@ -142,6 +142,18 @@ QASR_API int qasr_op_attention(const void* q, int32_t ldq, const void* k, const 
     });
 }
 
+QASR_API int qasr_op_attention_dense(const void* q, int32_t ldq, const void* k, const void* v, int32_t ldkv,
+                                     const int32_t* kv_start, const int32_t* kv_len, int32_t rows, int32_t nh,
+                                     int32_t nkv, int32_t hd, float scale, float* o, int8_t* oq, float* od,
+                                     int32_t dense, void* stream) {
+    return guard([&] {
+        QASR_CHECK(nkv > 0 && nh % nkv == 0, QASR_E_INVALID, "attention: bad head counts");
+        attention((const __half*)q, ldq, (const __half*)k, (const __half*)v, ldkv, kv_start, kv_len, rows, nh, nkv,
+                  hd, scale, o, oq, od, S(stream), 0, dense != 0);
+        launched();
+    });
+}
+
 QASR_API int qasr_op_argmax(const float* x, int32_t M, int32_t V, int32_t* out, void* stream) {
     return guard([&] {
         argmax_rows(x, M, V, out, S(stream));

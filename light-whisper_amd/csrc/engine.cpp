@@ -266,7 +266,7 @@ void Session::encoder(FrontEnd& fe, float* enc_out_dbg) {
         linear_q8(xq, xd, N, e.qkv, e.qkv_b, nullptr, qkv, 3 * d, EPI_STORE, st_);
         to_f16(qkv, N, 3 * d, 3 * d, qkvh, 3 * d, st_);
         attention(qkvh, 3 * d, qkvh + d, qkvh + 2 * d, 3 * d, d_kvs, d_kvl, N, h.enc_heads, h.enc_heads, d / h.enc_heads,
-                  scale, nullptr, xq, xd, st_, total_keys);
+                  scale, nullptr, xq, xd, st_, total_keys, /*dense=*/true);
         linear_q8(xq, xd, N, e.o, e.o_b, hs, hs, d, EPI_RESID, st_);
         layernorm_q8(hs, N, d, e.ln2_w, e.ln2_b, h.ln_eps, xq, xd, nullptr, st_);
         linear_q8(xq, xd, N, e.up, e.up_b, nullptr, ff, F, EPI_GELU, st_);
@@ -283,7 +283,7 @@ void Session::encoder(FrontEnd& fe, float* enc_out_dbg) {
 
 // ------------------------------------------------------------------------------------------ decoder
 void Session::decoder_layers(float* x, int rows, const int* d_pos, const int* d_slot, const int* d_kvs,
-                             const int* d_kvl, int64_t total_keys) {
+                             const int* d_kvl, int64_t total_keys, bool dense) {
     const qasr_hparams& h = m_->hp;
     const int H = h.txt_h, F = h.txt_ffn, nh = h.txt_heads, nkv = h.txt_kv_heads, hd = h.head_dim;
     const int QD = nh * hd, KD = nkv * hd;
@@ -308,7 +308,7 @@ void Session::decoder_layers(float* x, int rows, const int* d_pos, const int* d_
                    zq ? (int64_t)rows * (QD + 2 * KD) : 0);
         linear_q8(xq, xd, rows, L.qkv, nullptr, nullptr, qkv, QD + 2 * KD, EPI_STORE, st_, zq);
         qk_norm_rope(qkv, rows, nh, nkv, hd, d_pos, d_slot, L.q_norm, L.k_norm, rope_, h.rms_eps, qh, kc, vc, st_);
-        attention(qh, QD, kc, vc, KD, d_kvs, d_kvl, rows, nh, nkv, hd, scale, nullptr, xq, xd, st_, total_keys);
+        attention(qh, QD, kc, vc, KD, d_kvs, d_kvl, rows, nh, nkv, hd, scale, nullptr, xq, xd, st_, total_keys, dense);
         linear_q8(xq, xd, rows, L.o, nullptr, x, x, H, EPI_RESID, st_);
         rmsnorm_q8(x, rows, H, H, L.ffn_norm, h.rms_eps, xq, xd, st_);
         if (rows > 8) {  // SwiGLU + Q8 in the gate-up GEMM epilogue (rows interleaved at load)
@@ -475,7 +475,7 @@ void Session::run_batch(const float* dpcm, const std::vector<int64_t>& off, cons
             int* dpi = upload(S_IDS, pid);
             embed_rows(dpi, P0, m_->tok_embd, nullptr, xp, st_);
             decoder_layers(xp, P0, upload(S_POS, ppos), upload(S_SLOT, pslot), upload(S_KVS, pkvs),
-                           upload(S_KVL, pkvl), (int64_t)P0 * (P0 + 1) / 2);
+                           upload(S_KVL, pkvl), (int64_t)P0 * (P0 + 1) / 2, /*dense=*/true);
             copy_kv_prefix(kc_, vc_, h.txt_layers, kv_slots_, h.txt_kv_heads * h.head_dim, pref, P0,
                            upload(S_LAST, base), count, st_);
             QASR_HIP(hipStreamSynchronize(st_));   // the small tables above are reused by the main prefill
@@ -490,7 +490,7 @@ void Session::run_batch(const float* dpcm, const std::vector<int64_t>& off, cons
         embed_rows(d_ids, T, m_->tok_embd, emb, x, st_);
         int64_t keys = 0;
         for (int v : kvl) keys += v;
-        decoder_layers(x, T, d_pos, d_slot, d_kvs, d_kvl, keys);
+        decoder_layers(x, T, d_pos, d_slot, d_kvs, d_kvl, keys, /*dense=*/true);
         int* d_last = upload(S_LAST, last);
         float* xn = (float*)sc_.get(S_XN, (size_t)count * H * sizeof(float));
         k_gather_rows<<<(unsigned)cdiv64((int64_t)count * H, 256), 256, 0, st_>>>(x, d_last, count, H, xn);
@@ -677,7 +677,7 @@ void Session::prefill_logits_host(const float* embeds, int n, std::vector<float>
     int* d_slot = upload(S_SLOT, slot);
     int* d_kvs = upload(S_KVS, kvs);
     int* d_kvl = upload(S_KVL, kvl);
-    decoder_layers(x, n, d_pos, d_slot, d_kvs, d_kvl, (int64_t)n * (n + 1) / 2);
+    decoder_layers(x, n, d_pos, d_slot, d_kvs, d_kvl, (int64_t)n * (n + 1) / 2, /*dense=*/true);
     float* lg = (float*)sc_.get(S_LOGITS, (size_t)n * h.vocab * sizeof(float));
     lm_head_rows(x, n, h.txt_h, lg);
     logits.resize((size_t)n * h.vocab);
@@ -713,7 +713,7 @@ void Session::forced_logits_host(const float* pcm, int64_t n, const int32_t* for
     float* emb = (float*)sc_.get(S_EMB, (size_t)fe.total_tokens * H * sizeof(float));
     embed_rows(d_ids, P, m_->tok_embd, emb, x, st_);
     decoder_layers(x, P, upload(S_POS, pos), upload(S_SLOT, slot), upload(S_KVS, kvs), upload(S_KVL, kvl),
-                   (int64_t)P * (P + 1) / 2);
+                   (int64_t)P * (P + 1) / 2, /*dense=*/true);
     float* lg = (float*)sc_.get(S_LOGITS, (size_t)V * sizeof(float));
     lm_head_rows(x + (size_t)(P - 1) * H, 1, H, lg);
     QASR_HIP(hipMemcpyAsync(logits.data(), lg, (size_t)V * sizeof(float), hipMemcpyDeviceToHost, st_));

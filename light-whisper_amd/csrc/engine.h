@@ -70,7 +70,8 @@ class Session {
                    float* enc_out_dbg);
     void encoder(FrontEnd& fe, float* enc_out_dbg);
     void decoder_layers(float* x, int rows, const int* d_pos, const int* d_slot, const int* d_kvs, const int* d_kvl,
-                        int64_t total_keys);
+                        int64_t total_keys,
+                        bool dense = false);
     void ensure_kv(int64_t slots);
     void decode_step(const DecState& ds, int B, bool sizing);
     void lm_head_rows(const float* x, int rows, int ldx, float* logits);

@@ -59,10 +59,11 @@ void add_posemb_gather(const float* proj, int n_chunks, int T, int d, const floa
 
 // ---- attention (kernels_attn.hip)
 // one query row r: Q[r] (f16) against keys/values slots [kv_start[r], kv_start[r]+kv_len[r]) of K/V (f16);
-// output quantised (q/d, row stride nh*hd) and/or f32 (o)
+// output quantised (q/d, row stride nh*hd) and/or f32 (o).  dense: runs of 16 consecutive rows share most of their
+// key range (prefill prompt rows, encoder windows) → the MFMA tile kernel; otherwise the per-row kernel (decode).
 void attention(const __half* Q, int ldq, const __half* K, const __half* V, int ldkv, const int* kv_start,
                const int* kv_len, int rows, int nh, int nkv, int hd, float scale, float* o, int8_t* oq, float* od,
-               hipStream_t s, int64_t total_keys = 0);
+               hipStream_t s, int64_t total_keys = 0, bool dense = false);
 
 // ---- device-resident decode state (kernels_decode.hip)
 struct DecState {

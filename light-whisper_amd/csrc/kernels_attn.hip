@@ -7,6 +7,7 @@
 // 256-byte segment).  Row r attends slots [kv_start[r], kv_start[r]+kv_len[r]) — causal prefill, single-token
 // decode and the encoder's bidirectional 104-token windows (modeling_qwen3_asr.py:276-315) are all expressed
 // by the per-row ranges.  The output is written as f32 and/or directly as Q8 blocks for the O-projection.
+#include <climits>
 #include <type_traits>
 
 #include "kernels.h"
@@ -267,6 +268,220 @@ __global__ __launch_bounds__(256) void k_attention(const __half* __restrict__ Q,
     }
 }
 
+
+// ------------------------------------------------------------------------------------------------ tiled (MFMA)
+// Prefill / encoder attention: rows come in runs that share their key range (an utterance's causal prompt rows,
+// an encoder window), so 16 consecutive rows form one tile and every K/V chunk loaded is used by all 16.
+// One wave per (16-row tile, KV head) with the G query heads of the group in the same wave:
+//   Sᵀ = K·Qᵀ on v_mfma_f32_16x16x32_f16 (keys on the MFMA rows, so each lane owns one query row's scores for
+//   its keys — row max / sum are a few in-lane ops plus two xor-shuffles), online softmax in f32, P rounded to
+//   f16 and O += P·V on the same MFMA with V read column-wise by ds_read_b64_tr_b16 from a per-wave LDS chunk.
+// Each row's own range [kv_start, kv_start+kv_len) is applied as a mask inside the union range of the tile.
+// Precision: scores and the softmax in f32, P in f16 (relative 2^-11) — the test states the tolerance.
+template <int HD, int G>
+__global__ __launch_bounds__(256) void k_attn_tile(const __half* __restrict__ Q, int ldq, const __half* __restrict__ K,
+                                                   const __half* __restrict__ V, int ldkv,
+                                                   const int* __restrict__ kv_start, const int* __restrict__ kv_len,
+                                                   int rows, int nkv, float scale, float* __restrict__ o,
+                                                   int8_t* __restrict__ oq, float* __restrict__ od) {
+    typedef _Float16 v8h __attribute__((ext_vector_type(8)));
+    typedef short v4s __attribute__((ext_vector_type(4)));
+    typedef _Float16 v4h __attribute__((ext_vector_type(4)));
+    typedef float v4f __attribute__((ext_vector_type(4)));
+    constexpr int KC = 32;          // keys per chunk
+    constexpr int DC = HD / 32;     // 32-dim slices of the QKᵀ reduction
+    constexpr int DT = HD / 16;     // 16-dim output tiles of PV
+    constexpr int CPR = HD / 8;     // 16-byte chunks per V row
+    __shared__ __attribute__((aligned(16))) _Float16 vs_all[4][KC * HD];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int ntiles = (rows + 15) >> 4;
+    const int item = blockIdx.x * 4 + w;
+    if (item >= ntiles * nkv) return;   // whole wave
+    const int tile = item / nkv, kvh = item % nkv;
+    const int fr = lane & 15, kh = lane >> 4;
+    const int r0 = tile * 16;
+    _Float16* vs = vs_all[w];
+    // V image: 16-byte chunk ch of key row kr at kr·HD·2 + 16·(ch ^ swz(kr)) (conflict-free transposed reads)
+    auto voff = [&](int kr, int ch) -> int {
+        return kr * HD * 2 + 16 * (ch ^ (((kr & 3) << 2 | ((kr >> 2) & 3)) & (CPR - 1)));
+    };
+
+    // this lane's query row (fr) and its key range
+    const int myrow = min(r0 + fr, rows - 1);
+    const bool row_ok = r0 + fr < rows;
+    const int st = kv_start[myrow], en = row_ok ? st + kv_len[myrow] : st;
+    int lo = row_ok && en > st ? st : INT_MAX, hi = row_ok ? en : INT_MIN;
+#pragma unroll
+    for (int off = 1; off < 16; off <<= 1) {
+        lo = min(lo, __shfl_xor(lo, off));
+        hi = max(hi, __shfl_xor(hi, off));
+    }
+    // Q fragments (B operand of K·Qᵀ): lane (row fr, kh) holds Q[row][32c + 8kh .. +8]
+    v8h qf[G][DC];
+#pragma unroll
+    for (int g = 0; g < G; g++)
+#pragma unroll
+        for (int c = 0; c < DC; c++)
+            qf[g][c] = *(const v8h*)(Q + (size_t)myrow * ldq + (kvh * G + g) * HD + 32 * c + 8 * kh);
+    v4f acc[G][DT];
+    float m[G], l[G];
+#pragma unroll
+    for (int g = 0; g < G; g++) {
+        m[g] = -INFINITY;
+        l[g] = 0.f;
+#pragma unroll
+        for (int t = 0; t < DT; t++) acc[g][t] = v4f{0.f, 0.f, 0.f, 0.f};
+    }
+    const __half* kbase = K + (size_t)kvh * HD;
+    const __half* vbase = V + (size_t)kvh * HD;
+    for (int k0 = lo; k0 < hi; k0 += KC) {
+        // ---- stage V[k0 .. k0+32) into this wave's LDS image; K fragments straight to registers
+        constexpr int VP = KC * CPR / 64;   // 16-byte V pieces per lane
+        int4 vp[VP];
+#pragma unroll
+        for (int u = 0; u < VP; u++) {
+            const int piece = u * 64 + lane, kr = piece / CPR, ch = piece % CPR;
+            vp[u] = *(const int4*)(vbase + (size_t)min(k0 + kr, hi - 1) * ldkv + 8 * ch);
+        }
+        v8h kf[2][DC];
+#pragma unroll
+        for (int t = 0; t < 2; t++)
+#pragma unroll
+            for (int c = 0; c < DC; c++)
+                kf[t][c] = *(const v8h*)(kbase + (size_t)min(k0 + 16 * t + fr, hi - 1) * ldkv + 32 * c + 8 * kh);
+#pragma unroll
+        for (int u = 0; u < VP; u++) {
+            const int piece = u * 64 + lane, kr = piece / CPR, ch = piece % CPR;
+            *(int4*)((char*)vs + voff(kr, ch)) = vp[u];
+        }
+        // ---- Sᵀ tiles: lane (row fr, kh) gets keys 16t + 4kh + i
+        float p[G][2][4];
+#pragma unroll
+        for (int g = 0; g < G; g++) {
+#pragma unroll
+            for (int t = 0; t < 2; t++) {
+                v4f sacc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int c = 0; c < DC; c++) sacc = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf[t][c], qf[g][c], sacc, 0, 0, 0);
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    const int key = k0 + 16 * t + 4 * kh + i;
+                    p[g][t][i] = (key >= st && key < en) ? sacc[i] * scale : -INFINITY;
+                }
+            }
+        }
+        // ---- online softmax per row (lane-local over its 8 keys, then across the 4 kh groups)
+        float alpha[G];
+        _Float16 ph[G][8];
+#pragma unroll
+        for (int g = 0; g < G; g++) {
+            float mx = -INFINITY;
+#pragma unroll
+            for (int t = 0; t < 2; t++)
+#pragma unroll
+                for (int i = 0; i < 4; i++) mx = fmaxf(mx, p[g][t][i]);
+            mx = fmaxf(mx, __shfl_xor(mx, 16));
+            mx = fmaxf(mx, __shfl_xor(mx, 32));
+            const float mn = fmaxf(m[g], mx);
+            alpha[g] = mn == -INFINITY ? 1.f : expf(m[g] - mn);
+            float ps = 0.f;
+#pragma unroll
+            for (int t = 0; t < 2; t++)
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    const float e = mn == -INFINITY ? 0.f : expf(p[g][t][i] - mn);
+                    ps += e;
+                    ph[g][4 * t + i] = (_Float16)e;
+                }
+            ps += __shfl_xor(ps, 16);
+            ps += __shfl_xor(ps, 32);
+            l[g] = l[g] * alpha[g] + ps;
+            m[g] = mn;
+        }
+        // rescale O: acc rows are 4kh+i (row on the register), alpha lives on lane (row fr)
+#pragma unroll
+        for (int g = 0; g < G; g++) {
+            float ar[4];
+#pragma unroll
+            for (int i = 0; i < 4; i++) ar[i] = __shfl(alpha[g], 4 * kh + i);
+#pragma unroll
+            for (int t = 0; t < DT; t++)
+#pragma unroll
+                for (int i = 0; i < 4; i++) acc[g][t][i] *= ar[i];
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // ---- O += P·V: P slots j ↔ keys 16(j>>2) + 4kh + (j&3); V fragment = two transposed 4×16 reads
+        const int q = fr >> 2, pp = fr & 3;
+#pragma unroll
+        for (int t = 0; t < DT; t++) {
+            v4s rr[2];
+#pragma unroll
+            for (int h2 = 0; h2 < 2; h2++) {
+                const int kr = 16 * h2 + 4 * kh + q, ch = 2 * t + (pp >> 1);
+                rr[h2] = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                    (__attribute__((address_space(3))) v4s*)((__attribute__((address_space(3))) char*)vs +
+                                                              voff(kr, ch) + 8 * (pp & 1)));
+            }
+            // whole-vector bit casts: assembling vf element by element from the shorts miscompiles (ROCm 7.2,
+            // tools/micro/tr_check.hip)
+            const v8h vf = __builtin_shufflevector(__builtin_bit_cast(v4h, rr[0]), __builtin_bit_cast(v4h, rr[1]), 0, 1,
+                                                   2, 3, 4, 5, 6, 7);
+#pragma unroll
+            for (int g = 0; g < G; g++) {
+                v8h pf;
+#pragma unroll
+                for (int j = 0; j < 8; j++) pf[j] = ph[g][j];
+                acc[g][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(pf, vf, acc[g][t], 0, 0, 0);
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    // ---- normalise and store: acc[g][t][i] = O[row 4kh+i][dim 16t + fr] of head kvh·G + g
+    const int D = nkv * G * HD;
+#pragma unroll
+    for (int g = 0; g < G; g++) {
+        const int h = kvh * G + g;
+        float inv[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const float li = __shfl(l[g], 4 * kh + i);
+            inv[i] = li > 0.f ? 1.f / li : 0.f;
+        }
+#pragma unroll
+        for (int t = 0; t < DT; t++)
+#pragma unroll
+            for (int i = 0; i < 4; i++) acc[g][t][i] *= inv[i];
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const int row = r0 + 4 * kh + i;
+            if (o && row < rows) {
+#pragma unroll
+                for (int t = 0; t < DT; t++) o[(size_t)row * D + h * HD + 16 * t + fr] = acc[g][t][i];
+            }
+            if (oq) {
+                // a Q8 block = 32 dims = tiles 2b, 2b+1 across the 16 lanes of this kh group
+#pragma unroll
+                for (int b = 0; b < DT / 2; b++) {
+                    float am = fmaxf(fabsf(acc[g][2 * b][i]), fabsf(acc[g][2 * b + 1][i]));
+#pragma unroll
+                    for (int off = 1; off < 16; off <<= 1) am = fmaxf(am, __shfl_xor(am, off));
+                    const float dd = am / 127.f;
+                    if (row < rows) {
+                        int8_t* qr = oq + (size_t)row * D + h * HD + 32 * b;
+                        qr[fr] = (int8_t)(am == 0.f ? 0 : (int)roundf(acc[g][2 * b][i] / dd));
+                        qr[16 + fr] = (int8_t)(am == 0.f ? 0 : (int)roundf(acc[g][2 * b + 1][i] / dd));
+                        if (fr == 0) od[(size_t)row * (D / 32) + (h * HD) / 32 + b] = __half2float(f2h(dd));
+                    }
+                }
+            }
+        }
+    }
+}
+
 template <int HD>
 static void launch_attention(int G, int rows, hipStream_t s, const __half* Q, int ldq, const __half* K,
                              const __half* V, int ldkv, const int* kv_start, const int* kv_len, int nh, int nkv,
@@ -282,12 +497,24 @@ static void launch_attention(int G, int rows, hipStream_t s, const __half* Q, in
 
 void attention(const __half* Q, int ldq, const __half* K, const __half* V, int ldkv, const int* kv_start,
                const int* kv_len, int rows, int nh, int nkv, int hd, float scale, float* o, int8_t* oq, float* od,
-               hipStream_t s, int64_t total_keys) {
+               hipStream_t s, int64_t total_keys, bool dense) {
     if (rows <= 0) return;
     // QKᵀ + PV: 4·hd flops per (query head, key); f16 K/V bytes read per (query head, key)
     ProfScope ps(s, "attention", 4.0 * hd * nh * (double)total_keys, 4.0 * hd * nh * (double)total_keys);
     QASR_CHECK(nkv > 0 && nh % nkv == 0, QASR_E_INVALID, "attention: bad head counts");
     const int G = nh / nkv;
+    if (dense && (G == 1 || G == 2) && (hd == 64 || hd == 128) && ldq % 8 == 0 && ldkv % 8 == 0) {
+        const unsigned grid = (unsigned)cdiv(cdiv(rows, 16) * nkv, 4);
+        if (hd == 128 && G == 2)
+            k_attn_tile<128, 2><<<grid, 256, 0, s>>>(Q, ldq, K, V, ldkv, kv_start, kv_len, rows, nkv, scale, o, oq, od);
+        else if (hd == 128)
+            k_attn_tile<128, 1><<<grid, 256, 0, s>>>(Q, ldq, K, V, ldkv, kv_start, kv_len, rows, nkv, scale, o, oq, od);
+        else if (G == 2)
+            k_attn_tile<64, 2><<<grid, 256, 0, s>>>(Q, ldq, K, V, ldkv, kv_start, kv_len, rows, nkv, scale, o, oq, od);
+        else
+            k_attn_tile<64, 1><<<grid, 256, 0, s>>>(Q, ldq, K, V, ldkv, kv_start, kv_len, rows, nkv, scale, o, oq, od);
+        return;
+    }
     if (hd == 128)
         launch_attention<128>(G, rows, s, Q, ldq, K, V, ldkv, kv_start, kv_len, nh, nkv, scale, o, oq, od);
     else if (hd == 64)
