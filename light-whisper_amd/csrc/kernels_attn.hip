@@ -8,6 +8,7 @@
 // decode and the encoder's bidirectional 104-token windows (modeling_qwen3_asr.py:276-315) are all expressed
 // by the per-row ranges.  The output is written as f32 and/or directly as Q8 blocks for the O-projection.
 #include <climits>
+#include <cstdlib>
 #include <type_traits>
 
 #include "kernels.h"
@@ -278,7 +279,7 @@ __global__ __launch_bounds__(256) void k_attention(const __half* __restrict__ Q,
 //   f16 and O += P·V on the same MFMA with V read column-wise by ds_read_b64_tr_b16 from a per-wave LDS chunk.
 // Each row's own range [kv_start, kv_start+kv_len) is applied as a mask inside the union range of the tile.
 // Precision: scores and the softmax in f32, P in f16 (relative 2^-11) — the test states the tolerance.
-template <int HD, int G>
+template <int HD, int G, bool SINGLE>
 __global__ __launch_bounds__(256) void k_attn_tile(const __half* __restrict__ Q, int ldq, const __half* __restrict__ K,
                                                    const __half* __restrict__ V, int ldkv,
                                                    const int* __restrict__ kv_start, const int* __restrict__ kv_len,
@@ -294,12 +295,14 @@ __global__ __launch_bounds__(256) void k_attn_tile(const __half* __restrict__ Q,
     constexpr int CPR = HD / 8;     // 16-byte chunks per V row
     __shared__ __attribute__((aligned(16))) _Float16 vs_all[4][KC * HD];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int ntiles = (rows + 15) >> 4;
+    // SINGLE (decode): one query row per wave, replicated on the 16 MFMA rows (the MFMA work is idle capacity
+    // beside the K/V stream; only output row 0 is stored)
+    const int ntiles = SINGLE ? rows : (rows + 15) >> 4;
     const int item = blockIdx.x * 4 + w;
     if (item >= ntiles * nkv) return;   // whole wave
     const int tile = item / nkv, kvh = item % nkv;
     const int fr = lane & 15, kh = lane >> 4;
-    const int r0 = tile * 16;
+    const int r0 = SINGLE ? tile : tile * 16;
     _Float16* vs = vs_all[w];
     // V image: 16-byte chunk ch of key row kr at kr·HD·2 + 16·(ch ^ swz(kr)) (conflict-free transposed reads)
     auto voff = [&](int kr, int ch) -> int {
@@ -307,8 +310,8 @@ __global__ __launch_bounds__(256) void k_attn_tile(const __half* __restrict__ Q,
     };
 
     // this lane's query row (fr) and its key range
-    const int myrow = min(r0 + fr, rows - 1);
-    const bool row_ok = r0 + fr < rows;
+    const int myrow = SINGLE ? r0 : min(r0 + fr, rows - 1);
+    const bool row_ok = SINGLE || r0 + fr < rows;
     const int st = kv_start[myrow], en = row_ok ? st + kv_len[myrow] : st;
     int lo = row_ok && en > st ? st : INT_MAX, hi = row_ok ? en : INT_MIN;
 #pragma unroll
@@ -334,26 +337,36 @@ __global__ __launch_bounds__(256) void k_attn_tile(const __half* __restrict__ Q,
     }
     const __half* kbase = K + (size_t)kvh * HD;
     const __half* vbase = V + (size_t)kvh * HD;
-    for (int k0 = lo; k0 < hi; k0 += KC) {
-        // ---- stage V[k0 .. k0+32) into this wave's LDS image; K fragments straight to registers
-        constexpr int VP = KC * CPR / 64;   // 16-byte V pieces per lane
-        int4 vp[VP];
+    // K/V of chunk k0 + KC are loaded while chunk k0 is computed (one chunk in flight ahead)
+    constexpr int VP = KC * CPR / 64;   // 16-byte V pieces per lane
+    int4 vp[VP];
+    v8h kn[2][DC];
+    auto load_chunk = [&](int c0) {
 #pragma unroll
         for (int u = 0; u < VP; u++) {
             const int piece = u * 64 + lane, kr = piece / CPR, ch = piece % CPR;
-            vp[u] = *(const int4*)(vbase + (size_t)min(k0 + kr, hi - 1) * ldkv + 8 * ch);
+            vp[u] = *(const int4*)(vbase + (size_t)min(c0 + kr, hi - 1) * ldkv + 8 * ch);
         }
-        v8h kf[2][DC];
 #pragma unroll
         for (int t = 0; t < 2; t++)
 #pragma unroll
             for (int c = 0; c < DC; c++)
-                kf[t][c] = *(const v8h*)(kbase + (size_t)min(k0 + 16 * t + fr, hi - 1) * ldkv + 32 * c + 8 * kh);
+                kn[t][c] = *(const v8h*)(kbase + (size_t)min(c0 + 16 * t + fr, hi - 1) * ldkv + 32 * c + 8 * kh);
+    };
+    if (lo < hi) load_chunk(lo);
+    for (int k0 = lo; k0 < hi; k0 += KC) {
+        // ---- this chunk: V into the wave's LDS image, K fragments to registers; then prefetch the next chunk
 #pragma unroll
         for (int u = 0; u < VP; u++) {
             const int piece = u * 64 + lane, kr = piece / CPR, ch = piece % CPR;
             *(int4*)((char*)vs + voff(kr, ch)) = vp[u];
         }
+        v8h kf[2][DC];
+#pragma unroll
+        for (int t = 0; t < 2; t++)
+#pragma unroll
+            for (int c = 0; c < DC; c++) kf[t][c] = kn[t][c];
+        if (k0 + KC < hi) load_chunk(k0 + KC);
         // ---- Sᵀ tiles: lane (row fr, kh) gets keys 16t + 4kh + i
         float p[G][2][4];
 #pragma unroll
@@ -457,7 +470,7 @@ __global__ __launch_bounds__(256) void k_attn_tile(const __half* __restrict__ Q,
             for (int i = 0; i < 4; i++) acc[g][t][i] *= inv[i];
 #pragma unroll
         for (int i = 0; i < 4; i++) {
-            const int row = r0 + 4 * kh + i;
+            const int row = SINGLE ? (4 * kh + i == 0 ? r0 : rows) : r0 + 4 * kh + i;   // rows = "not stored"
             if (o && row < rows) {
 #pragma unroll
                 for (int t = 0; t < DT; t++) o[(size_t)row * D + h * HD + 16 * t + fr] = acc[g][t][i];
@@ -503,16 +516,22 @@ void attention(const __half* Q, int ldq, const __half* K, const __half* V, int l
     ProfScope ps(s, "attention", 4.0 * hd * nh * (double)total_keys, 4.0 * hd * nh * (double)total_keys);
     QASR_CHECK(nkv > 0 && nh % nkv == 0, QASR_E_INVALID, "attention: bad head counts");
     const int G = nh / nkv;
-    if (dense && (G == 1 || G == 2) && (hd == 64 || hd == 128) && ldq % 8 == 0 && ldkv % 8 == 0) {
-        const unsigned grid = (unsigned)cdiv(cdiv(rows, 16) * nkv, 4);
-        if (hd == 128 && G == 2)
-            k_attn_tile<128, 2><<<grid, 256, 0, s>>>(Q, ldq, K, V, ldkv, kv_start, kv_len, rows, nkv, scale, o, oq, od);
-        else if (hd == 128)
-            k_attn_tile<128, 1><<<grid, 256, 0, s>>>(Q, ldq, K, V, ldkv, kv_start, kv_len, rows, nkv, scale, o, oq, od);
-        else if (G == 2)
-            k_attn_tile<64, 2><<<grid, 256, 0, s>>>(Q, ldq, K, V, ldkv, kv_start, kv_len, rows, nkv, scale, o, oq, od);
-        else
-            k_attn_tile<64, 1><<<grid, 256, 0, s>>>(Q, ldq, K, V, ldkv, kv_start, kv_len, rows, nkv, scale, o, oq, od);
+    // QASR_ATTN_SINGLE=1 (A/B only): decode rows as single-row MFMA tiles instead of the f32 per-row kernel, which
+    // streams the decode KV at 4-5 TB/s (tools/attn_tune.py; the single-row tiles reach 2.4-2.8)
+    static const bool single_tiles = [] {
+        const char* e = getenv("QASR_ATTN_SINGLE");
+        return e && *e == '1';
+    }();
+    if ((G == 1 || G == 2) && (hd == 64 || hd == 128) && ldq % 8 == 0 && ldkv % 8 == 0 && (dense || single_tiles)) {
+        const unsigned grid = (unsigned)cdiv((dense ? cdiv(rows, 16) : rows) * nkv, 4);
+#define QASR_TILE(HD_, G_)                                                                                         \
+    (dense ? k_attn_tile<HD_, G_, false> : k_attn_tile<HD_, G_, true>)<<<grid, 256, 0, s>>>(                       \
+        Q, ldq, K, V, ldkv, kv_start, kv_len, rows, nkv, scale, o, oq, od)
+        if (hd == 128 && G == 2) QASR_TILE(128, 2);
+        else if (hd == 128) QASR_TILE(128, 1);
+        else if (G == 2) QASR_TILE(64, 2);
+        else QASR_TILE(64, 1);
+#undef QASR_TILE
         return;
     }
     if (hd == 128)

@@ -329,14 +329,16 @@ def _attention_case(torch_dev, hd, nh, nkv, starts, lens, dense, seed):
             s = kk @ q[r, h * hd:(h + 1) * hd].astype(np.float64) * scale
             p = np.exp(s - s.max())
             ref[r, h * hd:(h + 1) * hd] = p @ vv / p.sum()
-    # per-row kernel: f32 throughout; tile kernel: P rounded to f16 before P·V (relative 2^-11 per weight)
-    assert np.abs(oh - ref).max() < (4e-3 if dense else 1e-4)
+    # MFMA tile kernel (dense rows, 1 or 2 query heads per KV head): P rounded to f16 before P·V (relative 2^-11 per
+    # weight); the f32 per-row kernel (decode rows, other group sizes): 1e-4
+    tile = dense and (nh // nkv) in (1, 2)
+    assert np.abs(oh - ref).max() < (4e-3 if tile else 1e-4)
     qr, dr = quant_ref(oh.astype(np.float32))
     assert np.array_equal(host(oq), qr) and np.array_equal(host(od), dr)
 
 
 @pytest.mark.parametrize("dense", [False, True])
-@pytest.mark.parametrize("hd,nh,nkv", [(128, 4, 2), (64, 3, 3), (128, 16, 8), (64, 2, 2)])
+@pytest.mark.parametrize("hd,nh,nkv", [(128, 4, 2), (64, 3, 3), (128, 16, 8), (64, 2, 2), (128, 8, 2)])
 def test_attention(torch_dev, hd, nh, nkv, dense):
     """ragged per-row ranges (incl. a 1-key row) on both kernels"""
     _attention_case(torch_dev, hd, nh, nkv, [0, 10, 100, 0, 300], [1, 57, 300, 513, 104], dense, hd + nh)

@@ -1,6 +1,4 @@
 set -o pipefail
-timeout -k 10 300 python -u -m pytest tests/test_ops_gpu.py -x -q --timeout 120 --timeout-method thread -k "attention" > gpurun_out/t_att.log 2>&1 || { tail -n 60 gpurun_out/t_att.log; exit 1; }
-tail -n 2 gpurun_out/t_att.log
 timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/t_all.log 2>&1 || { tail -n 60 gpurun_out/t_all.log; exit 1; }
 tail -n 2 gpurun_out/t_all.log
 timeout -k 10 400 python3 bench.py --no-cpu-baseline > gpurun_out/b.log 2>&1 || { tail -n 20 gpurun_out/b.log; exit 1; }
