@@ -30,6 +30,9 @@ void gemv_q8(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const flo
 void gemm_q8(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const float* bias, const float* res, float* y,
              int ldy, int epi, hipStream_t s, int force_cfg = -1, int force_splits = 0, int8_t* yq = nullptr,
              float* yd = nullptr, bool y_zeroed = false);
+// the Q8 GEMM on f16-carried int8 operands (x [M][K], w [N][K] f16 holding the Q8 integers; scales as gemm_q8)
+void gemm_q8h(const __half* xq, const float* xd, int M, const __half* wq, const __half* wsc, int N, int K,
+              const float* bias, const float* res, float* y, int ldy, int epi, int cfg, hipStream_t s);
 // rows of a [2F][K] gate|up matrix → interleaved by 16 (32j+t: t<16 gate 16j+t, else up 16j+t-16)
 int64_t gate_up_interleaved_row(int64_t r, int64_t F);
 void interleave_gate_up(Q8Mat& W, hipStream_t s);

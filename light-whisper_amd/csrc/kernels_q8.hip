@@ -527,19 +527,25 @@ __device__ __forceinline__ void wait_stages(int ahead) {
     }
 }
 
-template <int WM, int WN, int TI, int TJ, int NBUF>
+template <int WM, int WN, int TI, int TJ, int NBUF, int BK = 64>
 __global__ __launch_bounds__(256, 2) void k_gemm_q8d(const int8_t* __restrict__ X, const float* __restrict__ Xd, int M,
                                                      const int8_t* __restrict__ W, const __half* __restrict__ Wsc,
                                                      int N, int K, const float* __restrict__ bias, const float* res,
                                                      float* y, int ldy, int epi, int steps_per_split,
                                                      int8_t* __restrict__ yq, float* __restrict__ yd) {
     static_assert(WM * WN == 4, "k_gemm_q8d: 4 waves");
-    constexpr int BM = WM * 16 * TI, BN = WN * 16 * TJ, BK = 64, NF = TI * TJ;
-    static_assert(BM % 64 == 0 && BN % 64 == 0 && BN <= 256, "k_gemm_q8d: tile sides must be multiples of 64");
-    constexpr int OB = BM * BK, OSA = OB + BN * BK, OSB = OSA + 2 * BM * 4, STAGE = OSB + BN * 4;
-    constexpr int AI = BM / 64, BI = BN / 64;           // 1-KB A / B DMA pieces per wave per stage
-    constexpr int SAW = BM / 2, ASI = (SAW + 63) / 64;  // A-scale dwords / DMA instructions per wave per stage
-    constexpr int NPW = AI + BI + ASI + 1;              // DMA instructions per wave per stage
+    static_assert(BK == 64 || BK == 128, "k_gemm_q8d: a stage is 2 or 4 Q8 blocks");
+    constexpr int KB = BK / 32, NF = TI * TJ;
+    constexpr int BM = WM * 16 * TI, BN = WN * 16 * TJ;
+    constexpr int RP = 1024 / BK;                       // rows per 1-KB DMA piece
+    static_assert(BM % (4 * RP) == 0 && BN % (4 * RP) == 0 && BN <= 256 && BM <= 256, "k_gemm_q8d: tile sides");
+    constexpr int OB = BM * BK, OSA = OB + BN * BK, OSB = OSA + KB * BM * 4, STAGE = OSB + (KB / 2) * BN * 4;
+    constexpr int AI = BM / RP / 4, BI = BN / RP / 4;   // A / B pieces per wave per stage
+    // A scales: [KB][BM] floats gathered by 4-byte DMA (KB·BM/4 per wave); B scales: [KB/2][BN] dwords (two f16
+    // each), BN·KB/8 per wave.
+    constexpr int SAW = KB * BM / 4, ASI = (SAW + 63) / 64;
+    constexpr int SBW = BN * KB / 8, BSI = (SBW + 63) / 64;
+    constexpr int NPW = AI + BI + ASI + BSI;            // DMA instructions per wave per stage
     constexpr int D = NBUF - 1;                         // prefetch distance (stages in flight)
     __shared__ __attribute__((aligned(1024))) char smem[NBUF * STAGE];
 
@@ -550,36 +556,41 @@ __global__ __launch_bounds__(256, 2) void k_gemm_q8d(const int8_t* __restrict__ 
     const int k_begin = blockIdx.z * steps_per_split * BK;
     const int k_end = min(K, k_begin + steps_per_split * BK);
     const int nsteps = max(0, (k_end - k_begin) / BK);
+    // 16-byte chunk c of row r lives at chunk c ^ swz(r): conflict-free ds_read_b64 fragment reads on BK-byte rows
+    auto swz = [](int r) { return BK == 64 ? (r >> 2) & 3 : (r >> 1) & 7; };
 
     // ---- per-lane DMA sources (k-independent parts)
     const int8_t* a_src[AI];
     const int8_t* b_src[BI];
 #pragma unroll
     for (int u = 0; u < AI; u++) {
-        const int row = 16 * (wave * AI + u) + (lane >> 2), c = (lane & 3) ^ ((row >> 2) & 3);
+        const int row = RP * (wave * AI + u) + lane / (BK / 16), c = (lane % (BK / 16)) ^ swz(row);
         a_src[u] = X + (size_t)min(m0 + row, M - 1) * K + 16 * c;
     }
 #pragma unroll
     for (int u = 0; u < BI; u++) {
-        const int row = 16 * (wave * BI + u) + (lane >> 2), c = (lane & 3) ^ ((row >> 2) & 3);
+        const int row = RP * (wave * BI + u) + lane / (BK / 16), c = (lane % (BK / 16)) ^ swz(row);
         b_src[u] = W + (size_t)min(n0 + row, N - 1) * K + 16 * c;
     }
     const float* sa_src[ASI];
 #pragma unroll
     for (int u = 0; u < ASI; u++) {
-        const int p = wave * SAW + min(64 * u + lane, SAW - 1), kb = p / BM, row = p % BM;
-        sa_src[u] = Xd + (size_t)min(m0 + row, M - 1) * nb + kb;
+        const int p = wave * SAW + min(64 * u + lane, SAW - 1);
+        sa_src[u] = Xd + (size_t)min(m0 + p % BM, M - 1) * nb + p / BM;
     }
-    const bool sb_on = lane < BN / 4;
-    const uint32_t* sb_src =
-        (const uint32_t*)Wsc + (size_t)min(n0 + wave * (BN / 4) + min(lane, BN / 4 - 1), N - 1) * (nb / 2);
+    const uint32_t* sb_src[BSI];
+#pragma unroll
+    for (int u = 0; u < BSI; u++) {
+        const int p = wave * SBW + min(64 * u + lane, SBW - 1);
+        sb_src[u] = (const uint32_t*)Wsc + (size_t)min(n0 + p % BN, N - 1) * (nb / 2) + p / BN;
+    }
 
     // LDS byte address of this wave's pieces (wave-uniform → SGPR for M0)
     const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
     const uint32_t wa = __builtin_amdgcn_readfirstlane(lds0 + 1024 * (wave * AI));
     const uint32_t wb = __builtin_amdgcn_readfirstlane(lds0 + OB + 1024 * (wave * BI));
     const uint32_t wsa = __builtin_amdgcn_readfirstlane(lds0 + OSA + wave * SAW * 4);
-    const uint32_t wsb = __builtin_amdgcn_readfirstlane(lds0 + OSB + wave * (BN / 4) * 4);
+    const uint32_t wsb = __builtin_amdgcn_readfirstlane(lds0 + OSB + wave * SBW * 4);
     auto issue = [&](int s, int buf) {
         const int k0 = k_begin + s * BK;
         const uint32_t so = buf * STAGE;
@@ -588,17 +599,20 @@ __global__ __launch_bounds__(256, 2) void k_gemm_q8d(const int8_t* __restrict__ 
 #pragma unroll
         for (int u = 0; u < BI; u++) dma_lds16(b_src[u] + k0, wb + so + 1024 * u);
 #pragma unroll
-        for (int u = 0; u < ASI; u++)
+        for (int u = 0; u < ASI; u++) {
             if (64 * u + lane < SAW) dma_lds4(sa_src[u] + k0 / QK, wsa + so + 256 * u);
-        if (sb_on) dma_lds4(sb_src + k0 / 64, wsb + so);
+        }
+#pragma unroll
+        for (int u = 0; u < BSI; u++)
+            if (64 * u + lane < SBW) dma_lds4(sb_src[u] + k0 / 64, wsb + so + 256 * u);
     };
 
     const int fr = lane & 15, kh = lane >> 4, fq = 4 * kh;
     const int arow = wr * 16 * TI, bcol = wc * 16 * TJ;
     const bool active = m0 + arow < M;   // wave-uniform
-    const int sw = (fr >> 2) & 3;
-    const int foff0 = 16 * ((0 + (kh >> 1)) ^ sw) + 8 * (kh & 1);
-    const int foff1 = 16 * ((2 + (kh >> 1)) ^ sw) + 8 * (kh & 1);
+    int foff[KB];
+#pragma unroll
+    for (int kb = 0; kb < KB; kb++) foff[kb] = 16 * ((2 * kb + (kh >> 1)) ^ swz(fr)) + 8 * (kh & 1);
 
     float acc[TI][TJ][4];
 #pragma unroll
@@ -620,40 +634,39 @@ __global__ __launch_bounds__(256, 2) void k_gemm_q8d(const int8_t* __restrict__ 
         if (s + D < nsteps) issue(s + D, (s + D) % NBUF);
         if (!active) continue;
         const char* st = smem + (s % NBUF) * STAGE;
-        float sb[2][TJ], sa[2][TI][4];
-        long a[2][TI], b[2][TJ];
+        // fragments and scales of block kb, read just before its MFMAs (the compiler hoists what registers allow)
+        float sb[KB][TJ], sa[KB][TI][4];
+        long a[KB][TI], b[KB][TJ];
+        auto load_block = [&](int kb) {
 #pragma unroll
-        for (int j = 0; j < TJ; j++) {
-            const uint32_t v = *(const uint32_t*)(st + OSB + 4 * (bcol + 16 * j + fr));
-            sb[0][j] = __half2float(__ushort_as_half((unsigned short)(v & 0xffff)));
-            sb[1][j] = __half2float(__ushort_as_half((unsigned short)(v >> 16)));
-        }
-#pragma unroll
-        for (int kb = 0; kb < 2; kb++) {
-            const int foff = kb ? foff1 : foff0;
+            for (int j = 0; j < TJ; j++) {
+                const uint32_t v = *(const uint32_t*)(st + OSB + 4 * ((kb >> 1) * BN + bcol + 16 * j + fr));
+                sb[kb][j] = __half2float(__ushort_as_half((unsigned short)((kb & 1) ? v >> 16 : v & 0xffff)));
+            }
 #pragma unroll
             for (int i = 0; i < TI; i++) {
-                int off = (arow + 16 * i + fr) * BK + foff;
-                asm volatile("" : "+v"(off));
-                a[kb][i] = *(const long*)(st + off);
                 const float4 v = *(const float4*)(st + OSA + 4 * (kb * BM + arow + 16 * i + fq));
                 sa[kb][i][0] = v.x, sa[kb][i][1] = v.y, sa[kb][i][2] = v.z, sa[kb][i][3] = v.w;
+                int off = (arow + 16 * i + fr) * BK + foff[kb];
+                asm volatile("" : "+v"(off));
+                a[kb][i] = *(const long*)(st + off);
             }
 #pragma unroll
             for (int j = 0; j < TJ; j++) {
-                int off = OB + (bcol + 16 * j + fr) * BK + foff;
+                int off = OB + (bcol + 16 * j + fr) * BK + foff[kb];
                 asm volatile("" : "+v"(off));
                 b[kb][j] = *(const long*)(st + off);
             }
-        }
+        };
         // MFMA q (block q / NF, fragment q % NF) is issued LAG MFMAs before its rescale, so the int32 result has
         // landed by the time the cvt/fma reach it and at most LAG+1 results are live
-        constexpr int LAG = 3, NQ = 2 * NF;
+        constexpr int LAG = 3, NQ = KB * NF;
         v4i c[LAG + 1];
 #pragma unroll
         for (int q = 0; q < NQ + LAG; q++) {
             if (q < NQ) {
                 const int kb = q / NF, f = q % NF;
+                if (f == 0) load_block(kb);
                 c[q % (LAG + 1)] =
                     __builtin_amdgcn_mfma_i32_16x16x32_i8(a[kb][f / TJ], b[kb][f % TJ], v4i{0, 0, 0, 0}, 0, 0, 0);
             }
@@ -674,27 +687,175 @@ __global__ __launch_bounds__(256, 2) void k_gemm_q8d(const int8_t* __restrict__ 
     gemm_epilogue<TI, TJ>(acc, M, N, m0, n0, arow, bcol, fr, fq, bias, res, y, ldy, epi, yq, yd);
 }
 
+// ------------------------------------------------------------------------------------------------ GEMM (f16 operands)
+// Same contract as k_gemm_q8d, with the int8 operands carried as f16 (every Q8 value is exact in f16):
+// v_mfma_f32_16x16x32_f16 returns each block's exact integer sum already in f32, so the per-block rescale is
+// d_x·d_w and one fma (no int→float conversion).  A stage is one Q8 block (K = 32 → 64-B rows of f16), chunk c of
+// row r at c ^ (3·((r >> 3) & 1)) so the ds_read_b128 fragment reads are conflict-free; NBUF stages in flight.
+template <int WM, int WN, int TI, int TJ, int NBUF>
+__global__ __launch_bounds__(256, 2) void k_gemm_q8h(const __half* __restrict__ X, const float* __restrict__ Xd, int M,
+                                                     const __half* __restrict__ W, const __half* __restrict__ Wsc,
+                                                     int N, int K, const float* __restrict__ bias, const float* res,
+                                                     float* y, int ldy, int epi, int steps_per_split,
+                                                     int8_t* __restrict__ yq, float* __restrict__ yd) {
+    typedef _Float16 v8h __attribute__((ext_vector_type(8)));
+    typedef float v4f __attribute__((ext_vector_type(4)));
+    static_assert(WM * WN == 4, "4 waves");
+    constexpr int BM = WM * 16 * TI, BN = WN * 16 * TJ, BK = 32, NF = TI * TJ;
+    static_assert(BM % 64 == 0 && BN % 64 == 0 && BM <= 256 && BN <= 256, "tile sides: multiples of 64, <= 256");
+    constexpr int OB = BM * 64, OSA = OB + BN * 64, OSB = OSA + BM * 4, STAGE = OSB + BN * 4;
+    constexpr int AI = BM / 64, BI = BN / 64;
+    constexpr int NPW = AI + BI + 2;
+    constexpr int D = NBUF - 1;
+    __shared__ __attribute__((aligned(1024))) char smem[NBUF * STAGE];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wr = wave / WN, wc = wave % WN;
+    const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM;
+    const int nb = K / QK;
+    const int k_begin = blockIdx.z * steps_per_split * BK;
+    const int k_end = min(K, k_begin + steps_per_split * BK);
+    const int nsteps = max(0, (k_end - k_begin) / BK);
+
+    auto sw = [](int r) { return ((r >> 3) & 1) * 3; };
+    const __half* a_src[AI];
+    const __half* b_src[BI];
+#pragma unroll
+    for (int u = 0; u < AI; u++) {
+        const int row = 16 * (wave * AI + u) + (lane >> 2), c = (lane & 3) ^ sw(row);
+        a_src[u] = X + (size_t)min(m0 + row, M - 1) * K + 8 * c;
+    }
+#pragma unroll
+    for (int u = 0; u < BI; u++) {
+        const int row = 16 * (wave * BI + u) + (lane >> 2), c = (lane & 3) ^ sw(row);
+        b_src[u] = W + (size_t)min(n0 + row, N - 1) * K + 8 * c;
+    }
+    const bool sa_on = lane < BM / 4, sb_on = lane < BN / 4;
+    const float* sa_src = Xd + (size_t)min(m0 + wave * (BM / 4) + min(lane, BM / 4 - 1), M - 1) * nb;
+    const uint32_t* sb_src =
+        (const uint32_t*)Wsc + (size_t)min(n0 + wave * (BN / 4) + min(lane, BN / 4 - 1), N - 1) * (nb / 2);
+
+    const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
+    const uint32_t wa = __builtin_amdgcn_readfirstlane(lds0 + 1024 * (wave * AI));
+    const uint32_t wb = __builtin_amdgcn_readfirstlane(lds0 + OB + 1024 * (wave * BI));
+    const uint32_t wsa = __builtin_amdgcn_readfirstlane(lds0 + OSA + wave * (BM / 4) * 4);
+    const uint32_t wsb = __builtin_amdgcn_readfirstlane(lds0 + OSB + wave * (BN / 4) * 4);
+    auto issue = [&](int s, int buf) {
+        const int k0 = k_begin + s * BK;
+        const uint32_t so = buf * STAGE;
+#pragma unroll
+        for (int u = 0; u < AI; u++) dma_lds16(a_src[u] + k0, wa + so + 1024 * u);
+#pragma unroll
+        for (int u = 0; u < BI; u++) dma_lds16(b_src[u] + k0, wb + so + 1024 * u);
+        if (sa_on) dma_lds4(sa_src + k0 / QK, wsa + so);
+        if (sb_on) dma_lds4(sb_src + k0 / 64, wsb + so);
+    };
+
+    const int fr = lane & 15, kh = lane >> 4, fq = 4 * kh;
+    const int arow = wr * 16 * TI, bcol = wc * 16 * TJ;
+    const bool active = m0 + arow < M;
+    const int foff = 16 * (kh ^ (((fr >> 3) & 1) * 3));
+
+    float acc[TI][TJ][4];
+#pragma unroll
+    for (int i = 0; i < TI; i++)
+#pragma unroll
+        for (int j = 0; j < TJ; j++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) acc[i][j][r] = 0.f;
+
+#pragma unroll
+    for (int t = 0; t < D; t++)
+        if (t < nsteps) issue(t, t);
+    for (int s = 0; s < nsteps; s++) {
+        wait_stages<NPW, D>(min(D - 1, nsteps - 1 - s));
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (s + D < nsteps) issue(s + D, (s + D) % NBUF);
+        if (!active) continue;
+        const char* st = smem + (s % NBUF) * STAGE;
+        const int hsel = ((k_begin + s * BK) / QK) & 1;
+        float sb[TJ], sa[TI][4];
+        v8h a[TI], b[TJ];
+#pragma unroll
+        for (int j = 0; j < TJ; j++) {
+            const uint32_t v = *(const uint32_t*)(st + OSB + 4 * (bcol + 16 * j + fr));
+            sb[j] = __half2float(__ushort_as_half((unsigned short)(hsel ? v >> 16 : v & 0xffff)));
+        }
+#pragma unroll
+        for (int i = 0; i < TI; i++) {
+            int off = (arow + 16 * i + fr) * 64 + foff;
+            asm volatile("" : "+v"(off));
+            a[i] = *(const v8h*)(st + off);
+            const float4 v = *(const float4*)(st + OSA + 4 * (arow + 16 * i + fq));
+            sa[i][0] = v.x, sa[i][1] = v.y, sa[i][2] = v.z, sa[i][3] = v.w;
+        }
+#pragma unroll
+        for (int j = 0; j < TJ; j++) {
+            int off = OB + (bcol + 16 * j + fr) * 64 + foff;
+            asm volatile("" : "+v"(off));
+            b[j] = *(const v8h*)(st + off);
+        }
+        constexpr int LAG = 3;
+        v4f c[LAG + 1];
+#pragma unroll
+        for (int q = 0; q < NF + LAG; q++) {
+            if (q < NF)
+                c[q % (LAG + 1)] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[q / TJ], b[q % TJ], v4f{0.f, 0.f, 0.f, 0.f},
+                                                                          0, 0, 0);
+            if (q >= LAG) {
+                const int p = q - LAG, i = p / TJ, j = p % TJ;
+#pragma unroll
+                for (int r = 0; r < 4; r++) acc[i][j][r] = fmaf(c[p % (LAG + 1)][r], sa[i][r] * sb[j], acc[i][j][r]);
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < NF; t++) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, 8, 0);
+        }
+    }
+    if (!active) return;
+    gemm_epilogue<TI, TJ>(acc, M, N, m0, n0, arow, bcol, fr, fq, bias, res, y, ldy, epi, yq, yd);
+}
+
+void gemm_q8h(const __half* xq, const float* xd, int M, const __half* wq, const __half* wsc, int N, int K,
+              const float* bias, const float* res, float* y, int ldy, int epi, int cfg, hipStream_t s) {
+    QASR_CHECK(K % 64 == 0, QASR_E_INVALID, "gemm_q8h: K % 64");
+    ProfScope ps(s, "gemm_q8", 2.0 * M * N * K, 0.0);
+    static const int bm[] = {128, 64, 64, 128}, bn[] = {128, 128, 64, 64};
+    cfg = cfg < 0 || cfg > 3 ? 1 : cfg;
+    dim3 grid(cdiv(N, bn[cfg]), cdiv(M, bm[cfg]), 1);
+    const int sps = K / 32;
+    switch (cfg) {
+        case 0: k_gemm_q8h<2, 2, 4, 4, 4><<<grid, 256, 0, s>>>(xq, xd, M, wq, wsc, N, K, bias, res, y, ldy, epi, sps, nullptr, nullptr); break;
+        case 1: k_gemm_q8h<2, 2, 2, 4, 4><<<grid, 256, 0, s>>>(xq, xd, M, wq, wsc, N, K, bias, res, y, ldy, epi, sps, nullptr, nullptr); break;
+        case 2: k_gemm_q8h<2, 2, 2, 2, 4><<<grid, 256, 0, s>>>(xq, xd, M, wq, wsc, N, K, bias, res, y, ldy, epi, sps, nullptr, nullptr); break;
+        default: k_gemm_q8h<2, 2, 4, 2, 4><<<grid, 256, 0, s>>>(xq, xd, M, wq, wsc, N, K, bias, res, y, ldy, epi, sps, nullptr, nullptr); break;
+    }
+}
+
 template <int TI, int TJ>
 static void launch_gemm(dim3 grid, hipStream_t s, const int8_t* xq, const float* xd, int M, const Q8Mat& W,
                         const float* bias, const float* res, float* y, int ldy, int epi, int sps, int8_t* yq,
                         float* yd) {
     k_gemm_q8<TI, TJ><<<grid, 256, 0, s>>>(xq, xd, M, W.qs, W.sc, W.N, W.K, bias, res, y, ldy, epi, sps, yq, yd);
 }
-template <int WM, int WN, int TI, int TJ, int NBUF = 3>
+template <int WM, int WN, int TI, int TJ, int NBUF = 3, int BK = 64>
 static void launch_gemm_dma(dim3 grid, hipStream_t s, const int8_t* xq, const float* xd, int M, const Q8Mat& W,
                             const float* bias, const float* res, float* y, int ldy, int epi, int sps, int8_t* yq,
                             float* yd) {
-    k_gemm_q8d<WM, WN, TI, TJ, NBUF><<<grid, 256, 0, s>>>(xq, xd, M, W.qs, W.sc, W.N, W.K, bias, res, y, ldy, epi, sps, yq,
+    k_gemm_q8d<WM, WN, TI, TJ, NBUF, BK><<<grid, 256, 0, s>>>(xq, xd, M, W.qs, W.sc, W.N, W.K, bias, res, y, ldy, epi, sps, yq,
                                                     yd);
 }
 
-// GEMM configurations: 0..3 register-staged kernel (any K % 32 == 0), 4..10 LDS-DMA kernel (K % 64 == 0).
-struct GemmCfg { int bm, bn; bool dma; };
+// GEMM configurations: 0..3 register-staged kernel (any K % 32 == 0), 4..11 LDS-DMA kernel, 2×2 waves, stages of
+// 64 (4..7) or 128 (8..11) K (K % bk == 0).
+struct GemmCfg { int bm, bn, bk; bool dma; };
 static const GemmCfg kGemmCfgs[] = {
-    {128, 128, false}, {64, 128, false}, {64, 64, false}, {32, 64, false},        // 0..3
-    {128, 128, true}, {64, 128, true}, {64, 64, true}, {128, 64, true},           // 4..7  (2×2 waves)
-    {256, 64, true}, {128, 64, true}, {64, 64, true},                             // 8..10 (4×1 waves)
-    {64, 64, true}, {64, 128, true}, {128, 64, true}, {64, 64, true},             // 11..14 deep rings
+    {128, 128, 128, false}, {64, 128, 128, false}, {64, 64, 128, false}, {32, 64, 128, false},   // 0..3
+    {128, 128, 64, true}, {64, 128, 64, true}, {64, 64, 64, true}, {128, 64, 64, true},          // 4..7
+    {128, 128, 128, true}, {64, 128, 128, true}, {64, 64, 128, true}, {128, 64, 128, true},      // 8..11
 };
 constexpr int kNumGemmCfgs = sizeof(kGemmCfgs) / sizeof(kGemmCfgs[0]);
 
@@ -706,17 +867,14 @@ static void launch_cfg(int cfg, dim3 grid, hipStream_t s, const int8_t* xq, cons
         case 1: launch_gemm<2, 4>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
         case 2: launch_gemm<2, 2>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
         case 3: launch_gemm<1, 2>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
-        case 4: launch_gemm_dma<2, 2, 4, 4>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
-        case 5: launch_gemm_dma<2, 2, 2, 4>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
-        case 6: launch_gemm_dma<2, 2, 2, 2>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
-        case 7: launch_gemm_dma<2, 2, 4, 2>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
-        case 8: launch_gemm_dma<4, 1, 4, 4>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
-        case 9: launch_gemm_dma<4, 1, 2, 4>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
-        case 10: launch_gemm_dma<4, 1, 1, 4>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
-        case 11: launch_gemm_dma<2, 2, 2, 2, 6>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
-        case 12: launch_gemm_dma<2, 2, 2, 4, 4>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
-        case 13: launch_gemm_dma<4, 1, 2, 4, 4>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
-        default: launch_gemm_dma<4, 1, 1, 4, 6>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
+        case 4: launch_gemm_dma<2, 2, 4, 4, 3, 64>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
+        case 5: launch_gemm_dma<2, 2, 2, 4, 3, 64>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
+        case 6: launch_gemm_dma<2, 2, 2, 2, 3, 64>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
+        case 7: launch_gemm_dma<2, 2, 4, 2, 3, 64>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
+        case 8: launch_gemm_dma<2, 2, 4, 4, 2, 128>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
+        case 9: launch_gemm_dma<2, 2, 2, 4, 3, 128>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
+        case 10: launch_gemm_dma<2, 2, 2, 2, 3, 128>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
+        default: launch_gemm_dma<2, 2, 4, 2, 3, 128>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
     }
 }
 
@@ -725,35 +883,37 @@ static void launch_cfg(int cfg, dim3 grid, hipStream_t s, const int8_t* xq, cons
 void gemm_q8(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const float* bias, const float* res, float* y,
              int ldy, int epi, hipStream_t s, int force_cfg, int force_splits, int8_t* yq, float* yd, bool y_zeroed) {
     ProfScope ps(s, "gemm_q8", 2.0 * M * W.N * W.K, q8_bytes(M, W, epi));
-    const bool dma_ok = W.K % 64 == 0;
+    auto usable = [&](int c) { return !kGemmCfgs[c].dma || W.K % kGemmCfgs[c].bk == 0; };
     int pick;
-    if (dma_ok) {
-        // measured on the engine's shapes (tools/gemm_tune.py, profiles/): 64×128 tiles win on prefill / encoder
-        // shapes and on the vocabulary projection, 64×64 (+ split-K) on batched-decode shapes
-        if (M > 256 || W.N >= 32768) pick = M > 128 && W.N >= 32768 ? 4 : 5;
-        else pick = epi == EPI_SWIGLU ? 5 : 6;
+    if (W.K % 64 == 0) {
+        // measured on the engine's shapes (tools/gemm_tune.py, profiles/): 128×128 tiles with K-64 stages on prefill
+        // / encoder shapes; 64×64 tiles with K-128 stages (+ split-K) on batched decode; the vocabulary projection
+        // by row count; the SwiGLU epilogue needs 128-column tiles
+        const bool k128 = W.K % 128 == 0;
+        if (W.N >= 32768) pick = !k128 ? 5 : M > 128 ? 8 : M > 32 ? 9 : 10;
+        else if (M > 256) pick = 4;
+        else if (epi == EPI_SWIGLU) pick = k128 ? 9 : 5;
+        else pick = k128 ? 10 : 6;
     } else {
-        static const int order[] = {0, 1, 2, 3};
         const int first = M <= 32 ? 3 : M <= 64 ? 1 : 0, last = M <= 32 ? 3 : 2;
         pick = last;
         for (int c = first; c <= last; c++)
-            if ((long)cdiv(W.N, kGemmCfgs[order[c]].bn) * cdiv(M, kGemmCfgs[order[c]].bm) >= 256) {
+            if ((long)cdiv(W.N, kGemmCfgs[c].bn) * cdiv(M, kGemmCfgs[c].bm) >= 256) {
                 pick = c;
                 break;
             }
     }
-    if (force_cfg >= 0 && force_cfg < kNumGemmCfgs && (!kGemmCfgs[force_cfg].dma || dma_ok)) pick = force_cfg;
+    if (force_cfg >= 0 && force_cfg < kNumGemmCfgs && usable(force_cfg)) pick = force_cfg;
     const GemmCfg& cf = kGemmCfgs[pick];
+    const int steps = cf.dma ? W.K / cf.bk : cdiv(W.K, GBK);
     if (epi == EPI_SWIGLU) {
         QASR_CHECK(W.N % 64 == 0 && yq && yd, QASR_E_INVALID, "gemm_q8: SwiGLU epilogue needs N % 64 == 0");
-        QASR_CHECK(pick != 2 && pick != 3 && pick != 6 && pick != 7 && pick != 11, QASR_E_INVALID,
-                   "gemm_q8: SwiGLU epilogue needs a 64-column wave tile");
+        QASR_CHECK(cf.bn == 128, QASR_E_INVALID, "gemm_q8: SwiGLU epilogue needs a 64-column wave tile");
         dim3 grid(cdiv(W.N, cf.bn), cdiv(M, cf.bm), 1);
-        launch_cfg(pick, grid, s, xq, xd, M, W, bias, res, y, ldy, epi, cf.dma ? W.K / 64 : cdiv(W.K, GBK), yq, yd);
+        launch_cfg(pick, grid, s, xq, xd, M, W, bias, res, y, ldy, epi, steps, yq, yd);
         return;
     }
     const int tiles = cdiv(W.N, cf.bn) * cdiv(M, cf.bm);
-    const int steps = cf.dma ? W.K / 64 : cdiv(W.K, GBK);
     const bool can_split = epi != EPI_GELU && ldy == W.N && (epi != EPI_RESID || res == y);
     int splits = 1;
     if (tiles < 256 && can_split) splits = std::max(1, std::min(std::min(cdiv(512, tiles), steps / 2), 8));

@@ -140,7 +140,7 @@ def _linear_case(torch_dev, m, n, k, path, epi, seed=0, exact=False):
 
 # path: 1 GEMV, 2 auto, 16 + cfg (+ 16·splits) forces a GEMM configuration (kernels_q8.hip kGemmCfgs: 0..3 register-
 # staged, 4..10 LDS-DMA)
-GEMM_PATHS = [1, 2] + [16 + c for c in range(15)] + [16 + 4 + 16 * 2, 16 + 8 + 16 * 4, 16 + 10 + 16 * 3]
+GEMM_PATHS = [1, 2] + [16 + c for c in range(12)] + [16 + 4 + 16 * 2, 16 + 9 + 16 * 4, 16 + 10 + 16 * 3]
 
 
 @pytest.mark.parametrize("path", GEMM_PATHS)

@@ -22,8 +22,8 @@ SHAPES = [  # (tag, M, N, K, epi)
 
 
 # 2 = auto; 16 + cfg (+ 16·splits): kernels_q8.hip kGemmCfgs — 0..3 register-staged {128², 64×128, 64², 32×64},
-# 4..7 LDS-DMA 2×2 waves {128², 64×128, 64², 128×64}, 8..10 LDS-DMA 4×1 waves {256×64, 128×64, 64×64}
-PATHS = [int(p) for p in os.environ.get("PATHS", "2,16,18,20,21,24,25,26").split(",")]
+# 4..7 LDS-DMA K-64 stages {128², 64×128, 64², 128×64}, 8..11 LDS-DMA K-128 stages (same tiles)
+PATHS = [int(p) for p in os.environ.get("PATHS", "2,20,21,22,24,25,26,27").split(",")]
 
 
 def main():
