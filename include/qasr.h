@@ -176,6 +176,10 @@ QASR_API int qasr_op_interleave_gate_up(int8_t* qs, void* sc, int32_t N, int32_t
 /* h = silu(x·Wgᵀ)·(x·Wuᵀ) quantised to Q8 rows (hq [M][N/2], hd [M][N/64]) in the GEMM epilogue; W interleaved */
 QASR_API int qasr_op_gemm_swiglu_q8(const int8_t* xq, const float* xd, int32_t M, const int8_t* wqs, const void* wsc,
                                     int32_t N, int32_t K, int8_t* hq, float* hd, void* stream);
+/* Same, with the GEMM configuration forced (kernels_q8.hip kGemmCfgs index; -1 = heuristic) — tuning and tests. */
+QASR_API int qasr_op_gemm_swiglu_q8_cfg(const int8_t* xq, const float* xd, int32_t M, const int8_t* wqs,
+                                        const void* wsc, int32_t N, int32_t K, int8_t* hq, float* hd, int32_t cfg,
+                                        void* stream);
 /* Q8 GEMM on f16-carried operands (each f16 holds a Q8 integer exactly): y = epi(X·Wᵀ), scales as qasr_op_linear_q8;
    K % 64 == 0; cfg 0..3 = tiles 128x128, 64x128, 64x64, 128x64. */
 QASR_API int qasr_op_linear_q8h(const void* xq16, const float* xd, int32_t M, const void* wq16, const void* wsc,

@@ -124,6 +124,21 @@ QASR_API int qasr_op_gemm_swiglu_q8(const int8_t* xq, const float* xd, int32_t M
     });
 }
 
+QASR_API int qasr_op_gemm_swiglu_q8_cfg(const int8_t* xq, const float* xd, int32_t M, const int8_t* wqs,
+                                        const void* wsc, int32_t N, int32_t K, int8_t* hq, float* hd, int32_t cfg,
+                                        void* stream) {
+    return guard([&] {
+        QASR_CHECK(N % 64 == 0 && K % QK == 0 && M >= 0, QASR_E_INVALID, "gemm_swiglu_q8: bad shape");
+        Q8Mat W;
+        W.qs = (int8_t*)wqs;
+        W.sc = (__half*)wsc;
+        W.N = N;
+        W.K = K;
+        gemm_q8(xq, xd, M, W, nullptr, nullptr, nullptr, N, EPI_SWIGLU, S(stream), cfg, 0, hq, hd);
+        launched();
+    });
+}
+
 QASR_API int qasr_op_swiglu_q8_interleaved(const float* gu, int32_t M, int32_t F, int8_t* q, float* d, void* stream) {
     return guard([&] {
         QASR_CHECK(F % QK == 0, QASR_E_INVALID, "swiglu_q8: F must be a multiple of 32");

@@ -850,12 +850,13 @@ static void launch_gemm_dma(dim3 grid, hipStream_t s, const int8_t* xq, const fl
 }
 
 // GEMM configurations: 0..3 register-staged kernel (any K % 32 == 0), 4..11 LDS-DMA kernel, 2×2 waves, stages of
-// 64 (4..7) or 128 (8..11) K (K % bk == 0).
+// 64 (4..7) or 128 (8..11) K (K % bk == 0); 12..13 LDS-DMA, 4×1 waves (64-column wave tiles), K-128 stages.
 struct GemmCfg { int bm, bn, bk; bool dma; };
 static const GemmCfg kGemmCfgs[] = {
     {128, 128, 128, false}, {64, 128, 128, false}, {64, 64, 128, false}, {32, 64, 128, false},   // 0..3
     {128, 128, 64, true}, {64, 128, 64, true}, {64, 64, 64, true}, {128, 64, 64, true},          // 4..7
     {128, 128, 128, true}, {64, 128, 128, true}, {64, 64, 128, true}, {128, 64, 128, true},      // 8..11
+    {64, 64, 128, true}, {128, 64, 128, true},                                                   // 12..13 4×1 waves
 };
 constexpr int kNumGemmCfgs = sizeof(kGemmCfgs) / sizeof(kGemmCfgs[0]);
 
@@ -874,7 +875,10 @@ static void launch_cfg(int cfg, dim3 grid, hipStream_t s, const int8_t* xq, cons
         case 8: launch_gemm_dma<2, 2, 4, 4, 2, 128>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
         case 9: launch_gemm_dma<2, 2, 2, 4, 3, 128>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
         case 10: launch_gemm_dma<2, 2, 2, 2, 3, 128>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
-        default: launch_gemm_dma<2, 2, 4, 2, 3, 128>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
+        case 11: launch_gemm_dma<2, 2, 4, 2, 3, 128>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
+        // 4×1 waves of 64 columns: the SwiGLU epilogue on 64-column workgroup tiles
+        case 12: launch_gemm_dma<4, 1, 1, 4, 3, 128>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
+        default: launch_gemm_dma<4, 1, 2, 4, 3, 128>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
     }
 }
 
@@ -888,11 +892,11 @@ void gemm_q8(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const flo
     if (W.K % 64 == 0) {
         // measured on the engine's shapes (tools/gemm_tune.py, profiles/): 128×128 tiles with K-64 stages on prefill
         // / encoder shapes; 64×64 tiles with K-128 stages (+ split-K) on batched decode; the vocabulary projection
-        // by row count; the SwiGLU epilogue needs 128-column tiles
+        // by row count; decode SwiGLU epilogue on 4×1 waves of 64 columns
         const bool k128 = W.K % 128 == 0;
         if (W.N >= 32768) pick = !k128 ? 5 : M > 128 ? 8 : M > 32 ? 9 : 10;
         else if (M > 256) pick = 4;
-        else if (epi == EPI_SWIGLU) pick = k128 ? 9 : 5;
+        else if (epi == EPI_SWIGLU) pick = k128 ? 12 : 5;
         else pick = k128 ? 10 : 6;
     } else {
         const int first = M <= 32 ? 3 : M <= 64 ? 1 : 0, last = M <= 32 ? 3 : 2;
@@ -908,7 +912,7 @@ void gemm_q8(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const flo
     const int steps = cf.dma ? W.K / cf.bk : cdiv(W.K, GBK);
     if (epi == EPI_SWIGLU) {
         QASR_CHECK(W.N % 64 == 0 && yq && yd, QASR_E_INVALID, "gemm_q8: SwiGLU epilogue needs N % 64 == 0");
-        QASR_CHECK(cf.bn == 128, QASR_E_INVALID, "gemm_q8: SwiGLU epilogue needs a 64-column wave tile");
+        QASR_CHECK(cf.bn == 128 || pick >= 12, QASR_E_INVALID, "gemm_q8: SwiGLU epilogue needs a 64-column wave tile");
         dim3 grid(cdiv(W.N, cf.bn), cdiv(M, cf.bm), 1);
         launch_cfg(pick, grid, s, xq, xd, M, W, bias, res, y, ldy, epi, steps, yq, yd);
         return;

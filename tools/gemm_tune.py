@@ -18,6 +18,8 @@ SHAPES = [  # (tag, M, N, K, epi)
     ("dec64 qkv", 64, 4096, 2048, 0), ("dec64 o", 64, 2048, 2048, 1), ("dec64 gu", 64, 12288, 2048, 0),
     ("dec64 down", 64, 2048, 6144, 1), ("dec64 lm", 64, 151936, 2048, 0),
     ("dec16 gu", 16, 12288, 2048, 0), ("dec16 down", 16, 2048, 6144, 1), ("dec16 lm", 16, 151936, 2048, 0),
+    ("dec256 swiglu", 256, 12288, 2048, 3), ("dec128 swiglu", 128, 12288, 2048, 3), ("dec64 swiglu", 64, 12288, 2048, 3),
+    ("dec16 swiglu", 16, 12288, 2048, 3), ("prefill swiglu", 27200, 12288, 2048, 3),
 ]
 
 
@@ -40,14 +42,25 @@ def main():
         ws = (torch.rand(N, K // 32, device=dev) * 0.01).half()
         y = torch.zeros(M, N, device=dev)
         res = y if epi == 1 else None
+        hq = torch.empty(M, N // 2, dtype=torch.int8, device=dev)
+        hd = torch.empty(M, N // 64, device=dev)
         flops = 2.0 * M * N * K
         out = []
         for path in PATHS:
             def run():
+                if epi == 3:   # fused SwiGLU + Q8 epilogue; path → forced config
+                    _lib.check(lib.qasr_op_gemm_swiglu_q8_cfg(xq.data_ptr(), xd.data_ptr(), M, wq.data_ptr(),
+                                                              ws.data_ptr(), N, K, hq.data_ptr(), hd.data_ptr(),
+                                                              -1 if path == 2 else (path - 16) % 16, None))
+                    return
                 _lib.check(lib.qasr_op_linear_q8(xq.data_ptr(), xd.data_ptr(), M, wq.data_ptr(), ws.data_ptr(), N,
                                                  K, None, res.data_ptr() if res is not None else None,
                                                  y.data_ptr(), N, epi, path, None))
-            run()
+            try:
+                run()
+            except _lib.QasrError:
+                out.append(f"{path}:      n/a")
+                continue
             torch.cuda.synchronize()
             iters = max(3, min(50, int(2e12 / flops * 20)))
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
