@@ -527,30 +527,36 @@ __device__ __forceinline__ void wait_stages(int ahead) {
     }
 }
 
-template <int WM, int WN, int TI, int TJ, int NBUF, int BK = 64>
-__global__ __launch_bounds__(256, 2) void k_gemm_q8d(const int8_t* __restrict__ X, const float* __restrict__ Xd, int M,
+template <int WM, int WN, int TI, int TJ, int NBUF, int BK = 64, int KG = 1>
+__global__ __launch_bounds__(256 * KG, 2 / KG) void k_gemm_q8d(const int8_t* __restrict__ X, const float* __restrict__ Xd, int M,
                                                      const int8_t* __restrict__ W, const __half* __restrict__ Wsc,
                                                      int N, int K, const float* __restrict__ bias, const float* res,
                                                      float* y, int ldy, int epi, int steps_per_split,
                                                      int8_t* __restrict__ yq, float* __restrict__ yd) {
-    static_assert(WM * WN == 4, "k_gemm_q8d: 4 waves");
+    static_assert(WM * WN == 4, "k_gemm_q8d: 4 waves per K group");
     static_assert(BK == 64 || BK == 128, "k_gemm_q8d: a stage is 2 or 4 Q8 blocks");
+    // KG K groups of 4 waves share the tile: group g takes blocks [g·KB/KG, (g+1)·KB/KG) of every stage and the
+    // groups' accumulators are summed through LDS at the end (more waves per tile without split-K atomics)
+    static_assert(KG == 1 || (KG == 2 && BK == 128), "k_gemm_q8d: K groups");
+    constexpr int NW = 4 * KG;
     constexpr int KB = BK / 32, NF = TI * TJ;
     constexpr int BM = WM * 16 * TI, BN = WN * 16 * TJ;
     constexpr int RP = 1024 / BK;                       // rows per 1-KB DMA piece
     static_assert(BM % (4 * RP) == 0 && BN % (4 * RP) == 0 && BN <= 256 && BM <= 256, "k_gemm_q8d: tile sides");
     constexpr int OB = BM * BK, OSA = OB + BN * BK, OSB = OSA + KB * BM * 4, STAGE = OSB + (KB / 2) * BN * 4;
-    constexpr int AI = BM / RP / 4, BI = BN / RP / 4;   // A / B pieces per wave per stage
-    // A scales: [KB][BM] floats gathered by 4-byte DMA (KB·BM/4 per wave); B scales: [KB/2][BN] dwords (two f16
-    // each), BN·KB/8 per wave.
-    constexpr int SAW = KB * BM / 4, ASI = (SAW + 63) / 64;
-    constexpr int SBW = BN * KB / 8, BSI = (SBW + 63) / 64;
+    constexpr int AI = BM / RP / NW, BI = BN / RP / NW;   // A / B pieces per wave per stage
+    static_assert(AI * RP * NW == BM && BI * RP * NW == BN, "k_gemm_q8d: pieces per wave");
+    // A scales: [KB][BM] floats gathered by 4-byte DMA (KB·BM/NW per wave); B scales: [KB/2][BN] dwords (two f16
+    // each), BN·KB/(2·NW) per wave.
+    constexpr int SAW = KB * BM / NW, ASI = (SAW + 63) / 64;
+    constexpr int SBW = BN * KB / (2 * NW), BSI = (SBW + 63) / 64;
     constexpr int NPW = AI + BI + ASI + BSI;            // DMA instructions per wave per stage
     constexpr int D = NBUF - 1;                         // prefetch distance (stages in flight)
     __shared__ __attribute__((aligned(1024))) char smem[NBUF * STAGE];
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int wr = wave / WN, wc = wave % WN;
+    const int kg = wave >> 2, lw = wave & 3;
+    const int wr = lw / WN, wc = lw % WN;
     const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM;
     const int nb = K / QK;
     const int k_begin = blockIdx.z * steps_per_split * BK;
@@ -635,38 +641,40 @@ __global__ __launch_bounds__(256, 2) void k_gemm_q8d(const int8_t* __restrict__ 
         if (!active) continue;
         const char* st = smem + (s % NBUF) * STAGE;
         // fragments and scales of block kb, read just before its MFMAs (the compiler hoists what registers allow)
-        float sb[KB][TJ], sa[KB][TI][4];
-        long a[KB][TI], b[KB][TJ];
-        auto load_block = [&](int kb) {
+        constexpr int KBG = KB / KG;   // blocks of this K group per stage
+        float sb[KBG][TJ], sa[KBG][TI][4];
+        long a[KBG][TI], b[KBG][TJ];
+        auto load_block = [&](int sl, int kb) {
 #pragma unroll
             for (int j = 0; j < TJ; j++) {
                 const uint32_t v = *(const uint32_t*)(st + OSB + 4 * ((kb >> 1) * BN + bcol + 16 * j + fr));
-                sb[kb][j] = __half2float(__ushort_as_half((unsigned short)((kb & 1) ? v >> 16 : v & 0xffff)));
+                sb[sl][j] = __half2float(__ushort_as_half((unsigned short)((kb & 1) ? v >> 16 : v & 0xffff)));
             }
 #pragma unroll
             for (int i = 0; i < TI; i++) {
                 const float4 v = *(const float4*)(st + OSA + 4 * (kb * BM + arow + 16 * i + fq));
-                sa[kb][i][0] = v.x, sa[kb][i][1] = v.y, sa[kb][i][2] = v.z, sa[kb][i][3] = v.w;
+                sa[sl][i][0] = v.x, sa[sl][i][1] = v.y, sa[sl][i][2] = v.z, sa[sl][i][3] = v.w;
                 int off = (arow + 16 * i + fr) * BK + foff[kb];
                 asm volatile("" : "+v"(off));
-                a[kb][i] = *(const long*)(st + off);
+                a[sl][i] = *(const long*)(st + off);
             }
 #pragma unroll
             for (int j = 0; j < TJ; j++) {
                 int off = OB + (bcol + 16 * j + fr) * BK + foff[kb];
                 asm volatile("" : "+v"(off));
-                b[kb][j] = *(const long*)(st + off);
+                b[sl][j] = *(const long*)(st + off);
             }
         };
         // MFMA q (block q / NF, fragment q % NF) is issued LAG MFMAs before its rescale, so the int32 result has
         // landed by the time the cvt/fma reach it and at most LAG+1 results are live
-        constexpr int LAG = 3, NQ = KB * NF;
+        constexpr int LAG = 3, NQ = (KB / KG) * NF;
+        const int kb0 = kg * (KB / KG);
         v4i c[LAG + 1];
 #pragma unroll
         for (int q = 0; q < NQ + LAG; q++) {
             if (q < NQ) {
                 const int kb = q / NF, f = q % NF;
-                if (f == 0) load_block(kb);
+                if (f == 0) load_block(kb, kb0 + kb);
                 c[q % (LAG + 1)] =
                     __builtin_amdgcn_mfma_i32_16x16x32_i8(a[kb][f / TJ], b[kb][f % TJ], v4i{0, 0, 0, 0}, 0, 0, 0);
             }
@@ -681,6 +689,30 @@ __global__ __launch_bounds__(256, 2) void k_gemm_q8d(const int8_t* __restrict__ 
         for (int t = 0; t < NQ; t++) {
             __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
             __builtin_amdgcn_sched_group_barrier(0x002, 12, 0);
+        }
+    }
+    if constexpr (KG == 2) {
+        // group 1 hands its partial sums to group 0 through the (now idle) staging LDS
+        static_assert(4 * 64 * TI * TJ * 4 * 4 <= NBUF * STAGE, "k_gemm_q8d: reduction buffer");
+        __syncthreads();
+        float4* red = (float4*)smem + (size_t)lw * 64 * TI * TJ + lane;
+        if (kg == 1 && active) {
+#pragma unroll
+            for (int i = 0; i < TI; i++)
+#pragma unroll
+                for (int j = 0; j < TJ; j++)
+                    red[(i * TJ + j) * 64] = make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+        }
+        __syncthreads();
+        if (kg == 1) return;
+        if (active) {
+#pragma unroll
+            for (int i = 0; i < TI; i++)
+#pragma unroll
+                for (int j = 0; j < TJ; j++) {
+                    const float4 v = red[(i * TJ + j) * 64];
+                    acc[i][j][0] += v.x, acc[i][j][1] += v.y, acc[i][j][2] += v.z, acc[i][j][3] += v.w;
+                }
         }
     }
     if (!active) return;
@@ -841,11 +873,11 @@ static void launch_gemm(dim3 grid, hipStream_t s, const int8_t* xq, const float*
                         float* yd) {
     k_gemm_q8<TI, TJ><<<grid, 256, 0, s>>>(xq, xd, M, W.qs, W.sc, W.N, W.K, bias, res, y, ldy, epi, sps, yq, yd);
 }
-template <int WM, int WN, int TI, int TJ, int NBUF = 3, int BK = 64>
+template <int WM, int WN, int TI, int TJ, int NBUF = 3, int BK = 64, int KG = 1>
 static void launch_gemm_dma(dim3 grid, hipStream_t s, const int8_t* xq, const float* xd, int M, const Q8Mat& W,
                             const float* bias, const float* res, float* y, int ldy, int epi, int sps, int8_t* yq,
                             float* yd) {
-    k_gemm_q8d<WM, WN, TI, TJ, NBUF, BK><<<grid, 256, 0, s>>>(xq, xd, M, W.qs, W.sc, W.N, W.K, bias, res, y, ldy, epi, sps, yq,
+    k_gemm_q8d<WM, WN, TI, TJ, NBUF, BK, KG><<<grid, 256 * KG, 0, s>>>(xq, xd, M, W.qs, W.sc, W.N, W.K, bias, res, y, ldy, epi, sps, yq,
                                                     yd);
 }
 
@@ -857,6 +889,7 @@ static const GemmCfg kGemmCfgs[] = {
     {128, 128, 64, true}, {64, 128, 64, true}, {64, 64, 64, true}, {128, 64, 64, true},          // 4..7
     {128, 128, 128, true}, {64, 128, 128, true}, {64, 64, 128, true}, {128, 64, 128, true},      // 8..11
     {64, 64, 128, true}, {128, 64, 128, true},                                                   // 12..13 4×1 waves
+    {64, 64, 128, true}, {64, 64, 128, true},                        // 14..15 = 10 / 12 with two K groups (8 waves)
 };
 constexpr int kNumGemmCfgs = sizeof(kGemmCfgs) / sizeof(kGemmCfgs[0]);
 
@@ -878,7 +911,9 @@ static void launch_cfg(int cfg, dim3 grid, hipStream_t s, const int8_t* xq, cons
         case 11: launch_gemm_dma<2, 2, 4, 2, 3, 128>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
         // 4×1 waves of 64 columns: the SwiGLU epilogue on 64-column workgroup tiles
         case 12: launch_gemm_dma<4, 1, 1, 4, 3, 128>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
-        default: launch_gemm_dma<4, 1, 2, 4, 3, 128>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
+        case 13: launch_gemm_dma<4, 1, 2, 4, 3, 128>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
+        case 14: launch_gemm_dma<2, 2, 2, 2, 3, 128, 2>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
+        default: launch_gemm_dma<4, 1, 1, 4, 3, 128, 2>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
     }
 }
 
@@ -892,12 +927,13 @@ void gemm_q8(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const flo
     if (W.K % 64 == 0) {
         // measured on the engine's shapes (tools/gemm_tune.py, profiles/): 128×128 tiles with K-64 stages on prefill
         // / encoder shapes; 64×64 tiles with K-128 stages (+ split-K) on batched decode; the vocabulary projection
-        // by row count; decode SwiGLU epilogue on 4×1 waves of 64 columns
+        // by row count; decode SwiGLU epilogue on 4×1 waves of 64 columns; two K groups (8 waves per tile) where
+        // the tile count is low
         const bool k128 = W.K % 128 == 0;
         if (W.N >= 32768) pick = !k128 ? 5 : M > 128 ? 8 : M > 32 ? 9 : 10;
         else if (M > 256) pick = 4;
-        else if (epi == EPI_SWIGLU) pick = k128 ? 12 : 5;
-        else pick = k128 ? 10 : 6;
+        else if (epi == EPI_SWIGLU) pick = !k128 ? 5 : M > 128 ? 12 : 15;
+        else pick = !k128 ? 6 : W.N <= 4096 ? 14 : 10;
     } else {
         const int first = M <= 32 ? 3 : M <= 64 ? 1 : 0, last = M <= 32 ? 3 : 2;
         pick = last;
@@ -912,7 +948,8 @@ void gemm_q8(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const flo
     const int steps = cf.dma ? W.K / cf.bk : cdiv(W.K, GBK);
     if (epi == EPI_SWIGLU) {
         QASR_CHECK(W.N % 64 == 0 && yq && yd, QASR_E_INVALID, "gemm_q8: SwiGLU epilogue needs N % 64 == 0");
-        QASR_CHECK(cf.bn == 128 || pick >= 12, QASR_E_INVALID, "gemm_q8: SwiGLU epilogue needs a 64-column wave tile");
+        QASR_CHECK(cf.bn == 128 || pick == 12 || pick == 13 || pick == 15, QASR_E_INVALID,
+                   "gemm_q8: SwiGLU epilogue needs a 64-column wave tile");
         dim3 grid(cdiv(W.N, cf.bn), cdiv(M, cf.bm), 1);
         launch_cfg(pick, grid, s, xq, xd, M, W, bias, res, y, ldy, epi, steps, yq, yd);
         return;

@@ -140,7 +140,7 @@ def _linear_case(torch_dev, m, n, k, path, epi, seed=0, exact=False):
 
 # path: 1 GEMV, 2 auto, 16 + cfg (+ 16·splits) forces a GEMM configuration (kernels_q8.hip kGemmCfgs: 0..3 register-
 # staged, 4..10 LDS-DMA)
-GEMM_PATHS = [1, 2] + [16 + c for c in range(14)] + [16 + 4 + 16 * 2, 16 + 9 + 16 * 4, 16 + 10 + 16 * 3]
+GEMM_PATHS = [1, 2] + [16 + c for c in range(16)] + [16 + 4 + 16 * 2, 16 + 9 + 16 * 4, 16 + 10 + 16 * 3]
 
 
 @pytest.mark.parametrize("path", GEMM_PATHS)
@@ -210,7 +210,7 @@ def _il16(f):
     return np.where(r < f, 32 * (r // 16) + r % 16, 32 * ((r - f) // 16) + 16 + (r - f) % 16)
 
 
-@pytest.mark.parametrize("cfg", [-1, 1, 4, 5, 8, 9, 12, 13])
+@pytest.mark.parametrize("cfg", [-1, 1, 4, 5, 8, 9, 12, 13, 15])
 @pytest.mark.parametrize("m,f,k", [(3, 256, 512), (40, 512, 1024), (300, 1024, 512)])
 def test_gemm_swiglu_q8(torch_dev, m, f, k, cfg):
     """fused gate-up GEMM + SwiGLU + Q8 epilogue vs the oracle's linear_q8 of gate and up"""
