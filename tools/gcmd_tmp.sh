@@ -1,5 +1,4 @@
 set -o pipefail
-timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/t_all.log 2>&1 || { tail -n 60 gpurun_out/t_all.log; exit 1; }
-tail -n 1 gpurun_out/t_all.log
-timeout -k 10 400 python3 bench.py --no-cpu-baseline > gpurun_out/b.log 2>&1 || { tail -n 20 gpurun_out/b.log; exit 1; }
-tail -n 1 gpurun_out/b.log | cut -c1-1500
+PATHS=20,21 timeout -k 10 300 python -u tools/gemm_tune.py prefill enc dec256 > gpurun_out/tune.log 2>&1 || { tail -n 20 gpurun_out/tune.log; exit 1; }
+QASR_LIB=light-whisper_amd/libqasr_slp.so PATHS=20,21 timeout -k 10 300 python -u tools/gemm_tune.py prefill enc dec256 > gpurun_out/tune2.log 2>&1 || { tail -n 20 gpurun_out/tune2.log; exit 1; }
+grep -v amdgpu gpurun_out/tune.log; grep -v amdgpu gpurun_out/tune2.log
