@@ -347,11 +347,61 @@ __global__ __launch_bounds__(256) void k_qk_norm_rope(const float* __restrict__ 
     }
 }
 
+// Row-per-workgroup form (hd = 128): the row's position, slot and RoPE factors are loaded once per wave and
+// reused for every head the wave takes (heads w, w+4, …); all head loads are issued before the first use, 8-byte
+// loads and 4-byte f16 stores per lane.
+template <int NHW>
+__global__ __launch_bounds__(256) void k_qk_norm_rope_row(const float* __restrict__ qkv, int nh, int nkv,
+                                                          const int* __restrict__ pos, const int* __restrict__ slot,
+                                                          const float* __restrict__ qnw, const float* __restrict__ knw,
+                                                          const float* __restrict__ rope_cs, float eps,
+                                                          __half* __restrict__ qout, __half* __restrict__ kc,
+                                                          __half* __restrict__ vc) {
+    constexpr int HD = 128, half = 64;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = blockIdx.x;
+    const int nslot = nh + 2 * nkv, ld = nslot * HD, kvd = nkv * HD;
+    const float* src = qkv + (size_t)r * ld;
+    float2 v[NHW];
+#pragma unroll
+    for (int t = 0; t < NHW; t++) {
+        const int h = w + 4 * t;
+        v[t] = h < nslot ? *(const float2*)(src + h * HD + 2 * lane) : make_float2(0.f, 0.f);
+    }
+    const float2 qw = *(const float2*)(qnw + 2 * lane), kw = *(const float2*)(knw + 2 * lane);
+    const int p = pos[r], sl = slot[r];
+    // dims 2·lane, 2·lane+1: RoPE pair index e = dim mod 64, partner lane = lane ^ 32
+    const int e0 = (2 * lane) & (half - 1);
+    const float4 cs = *(const float4*)(rope_cs + ((size_t)p * half + e0) * 2);   // (cos, sin) of e0, e0+1
+    const bool lo = 2 * lane < half;
+#pragma unroll
+    for (int t = 0; t < NHW; t++) {
+        const int h = w + 4 * t;
+        if (h >= nslot) break;
+        if (h >= nh + nkv) {   // v head: copy into its cache slot
+            *(__half2*)(vc + (size_t)sl * kvd + (h - nh - nkv) * HD + 2 * lane) = __floats2half2_rn(v[t].x, v[t].y);
+            continue;
+        }
+        const float2 g = h < nh ? qw : kw;
+        const float inv = 1.0f / sqrtf(wsum(v[t].x * v[t].x + v[t].y * v[t].y) / (float)HD + eps);
+        const float a = v[t].x * inv * g.x, b = v[t].y * inv * g.y;
+        const float pa = __shfl_xor(a, 32), pb = __shfl_xor(b, 32);
+        const float oa = lo ? a * cs.x - pa * cs.y : a * cs.x + pa * cs.y;
+        const float ob = lo ? b * cs.z - pb * cs.w : b * cs.z + pb * cs.w;
+        __half* dst = h < nh ? qout + (size_t)r * nh * HD + h * HD : kc + (size_t)sl * kvd + (h - nh) * HD;
+        *(__half2*)(dst + 2 * lane) = __floats2half2_rn(oa, ob);
+    }
+}
+
 void qk_norm_rope(const float* qkv, int rows, int nh, int nkv, int hd, const int* pos, const int* slot,
                   const float* qnw, const float* knw, const float* rope_cs, float eps, __half* qout, __half* kc,
                   __half* vc, hipStream_t s) {
     if (rows <= 0) return;
-    const int waves = rows * (nh + 2 * nkv);
+    const int nslot = nh + 2 * nkv;
+    if (hd == 128 && nslot <= 32) {
+        k_qk_norm_rope_row<8><<<rows, 256, 0, s>>>(qkv, nh, nkv, pos, slot, qnw, knw, rope_cs, eps, qout, kc, vc);
+        return;
+    }
+    const int waves = rows * nslot;
     if (hd == 128)
         k_qk_norm_rope<128><<<cdiv(waves, 4), 256, 0, s>>>(qkv, rows, nh, nkv, pos, slot, qnw, knw, rope_cs, eps, qout, kc, vc);
     else if (hd == 64)

@@ -264,11 +264,13 @@ def test_swiglu_q8(torch_dev):
     assert (np.abs(host(q).astype(int) - qr) <= 1).all()
 
 
-def test_qk_norm_rope(torch_dev):
+@pytest.mark.parametrize("nh,nkv,hd", [(4, 2, 128), (16, 8, 128), (4, 4, 64)])
+def test_qk_norm_rope(torch_dev, nh, nkv, hd):
+    """row-per-workgroup kernel (hd 128) and head-per-wave kernel (hd 64)"""
     import torch
 
     rng = np.random.default_rng(6)
-    rows, nh, nkv, hd = 3, 4, 2, 128
+    rows = 3
     qkv = rng.standard_normal((rows, (nh + 2 * nkv) * hd)).astype(np.float32)
     pos = np.array([0, 5, 77], np.int32)
     slot = np.array([2, 0, 1], np.int32)
