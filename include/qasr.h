@@ -180,6 +180,12 @@ QASR_API int qasr_op_gemm_swiglu_q8(const int8_t* xq, const float* xd, int32_t M
 QASR_API int qasr_op_gemm_swiglu_q8_cfg(const int8_t* xq, const float* xd, int32_t M, const int8_t* wqs,
                                         const void* wsc, int32_t N, int32_t K, int8_t* hq, float* hd, int32_t cfg,
                                         void* stream);
+/* Q8 GEMM with a fused output epilogue (M > 8, the MFMA path): epi 4 = erf-GELU(acc + bias) quantised to Q8 rows
+   (yq [M][N] int8, yd [M][N/32] f32 block scales; y unused), epi 5 = f16(acc + bias) into y (__half, row stride
+   ldy).  cfg: GEMM configuration (-1 = heuristic). */
+QASR_API int qasr_op_linear_q8_ex(const int8_t* xq, const float* xd, int32_t M, const int8_t* wqs, const void* wsc,
+                                  int32_t N, int32_t K, const float* bias, void* y, int32_t ldy, int32_t epi,
+                                  int8_t* yq, float* yd, int32_t cfg, void* stream);
 /* Q8 GEMM on f16-carried operands (each f16 holds a Q8 integer exactly): y = epi(X·Wᵀ), scales as qasr_op_linear_q8;
    K % 64 == 0; cfg 0..3 = tiles 128x128, 64x128, 64x64, 128x64. */
 QASR_API int qasr_op_linear_q8h(const void* xq16, const float* xd, int32_t M, const void* wq16, const void* wsc,

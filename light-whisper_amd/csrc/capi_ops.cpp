@@ -59,6 +59,22 @@ QASR_API int qasr_op_linear_q8(const int8_t* xq, const float* xd, int32_t M, con
     });
 }
 
+QASR_API int qasr_op_linear_q8_ex(const int8_t* xq, const float* xd, int32_t M, const int8_t* wqs, const void* wsc,
+                                  int32_t N, int32_t K, const float* bias, void* y, int32_t ldy, int32_t epi,
+                                  int8_t* yq, float* yd, int32_t cfg, void* stream) {
+    return guard([&] {
+        QASR_CHECK(K % QK == 0 && N > 0 && M > 8 && ldy >= N && (epi == 4 || epi == 5), QASR_E_INVALID,
+                   "linear_q8_ex: bad shape / epilogue");
+        Q8Mat W;
+        W.qs = (int8_t*)wqs;
+        W.sc = (__half*)wsc;
+        W.N = N;
+        W.K = K;
+        gemm_q8(xq, xd, M, W, bias, nullptr, (float*)y, ldy, epi, S(stream), cfg, 0, yq, yd);
+        launched();
+    });
+}
+
 QASR_API int qasr_op_linear_q8h(const void* xq16, const float* xd, int32_t M, const void* wq16, const void* wsc,
                                 int32_t N, int32_t K, const float* bias, const float* res, float* y, int32_t ldy,
                                 int32_t epi, int32_t cfg, void* stream) {

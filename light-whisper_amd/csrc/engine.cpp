@@ -260,22 +260,42 @@ void Session::encoder(FrontEnd& fe, float* enc_out_dbg) {
     __half* qkvh = (__half*)sc_.get(S_QKVH, (size_t)N * 3 * d * sizeof(__half));
     float* ff = (float*)sc_.get(S_FF, (size_t)N * std::max(F, d) * sizeof(float));
     const float scale = 1.0f / sqrtf((float)(d / h.enc_heads));
+    // MFMA-GEMM row counts (> 8) take the fused epilogues: QKV written as f16 for the attention, up-projection
+    // GELU quantised to the down-projection's Q8 rows in place; GEMV row counts keep the separate passes
+    const bool fused = N > 8;
+    int8_t* hq = fused ? (int8_t*)sc_.get(S_HQ, (size_t)N * std::max(F, d)) : nullptr;
+    float* hdq = fused ? (float*)sc_.get(S_HD, (size_t)N * (std::max(F, d) / QK) * sizeof(float)) : nullptr;
     for (int l = 0; l < h.enc_layers; l++) {
         const EncLayer& e = m_->enc[l];
         layernorm_q8(hs, N, d, e.ln1_w, e.ln1_b, h.ln_eps, xq, xd, nullptr, st_);
-        linear_q8(xq, xd, N, e.qkv, e.qkv_b, nullptr, qkv, 3 * d, EPI_STORE, st_);
-        to_f16(qkv, N, 3 * d, 3 * d, qkvh, 3 * d, st_);
+        if (fused) {
+            gemm_q8(xq, xd, N, e.qkv, e.qkv_b, nullptr, (float*)qkvh, 3 * d, EPI_STORE_F16, st_);
+        } else {
+            linear_q8(xq, xd, N, e.qkv, e.qkv_b, nullptr, qkv, 3 * d, EPI_STORE, st_);
+            to_f16(qkv, N, 3 * d, 3 * d, qkvh, 3 * d, st_);
+        }
         attention(qkvh, 3 * d, qkvh + d, qkvh + 2 * d, 3 * d, d_kvs, d_kvl, N, h.enc_heads, h.enc_heads, d / h.enc_heads,
                   scale, nullptr, xq, xd, st_, total_keys, /*dense=*/true);
         linear_q8(xq, xd, N, e.o, e.o_b, hs, hs, d, EPI_RESID, st_);
         layernorm_q8(hs, N, d, e.ln2_w, e.ln2_b, h.ln_eps, xq, xd, nullptr, st_);
-        linear_q8(xq, xd, N, e.up, e.up_b, nullptr, ff, F, EPI_GELU, st_);
-        quant_rows(ff, N, F, F, xq, xd, st_);
-        linear_q8(xq, xd, N, e.down, e.down_b, hs, hs, d, EPI_RESID, st_);
+        if (fused) {
+            gemm_q8(xq, xd, N, e.up, e.up_b, nullptr, nullptr, F, EPI_GELU_Q8, st_, -1, 0, hq, hdq);
+            linear_q8(hq, hdq, N, e.down, e.down_b, hs, hs, d, EPI_RESID, st_);
+        } else {
+            linear_q8(xq, xd, N, e.up, e.up_b, nullptr, ff, F, EPI_GELU, st_);
+            quant_rows(ff, N, F, F, xq, xd, st_);
+            linear_q8(xq, xd, N, e.down, e.down_b, hs, hs, d, EPI_RESID, st_);
+        }
     }
     layernorm_q8(hs, N, d, m_->ln_post_w, m_->ln_post_b, h.ln_eps, xq, xd, enc_out_dbg, st_);
-    linear_q8(xq, xd, N, m_->proj1, m_->proj1_b, nullptr, ff, d, EPI_GELU, st_);
-    quant_rows(ff, N, d, d, xq, xd, st_);
+    if (fused) {
+        gemm_q8(xq, xd, N, m_->proj1, m_->proj1_b, nullptr, nullptr, d, EPI_GELU_Q8, st_, -1, 0, hq, hdq);
+        std::swap(xq, hq);
+        std::swap(xd, hdq);
+    } else {
+        linear_q8(xq, xd, N, m_->proj1, m_->proj1_b, nullptr, ff, d, EPI_GELU, st_);
+        quant_rows(ff, N, d, d, xq, xd, st_);
+    }
     float* emb = (float*)sc_.get(S_EMB, (size_t)N * H * sizeof(float));
     linear_q8(xq, xd, N, m_->proj2, m_->proj2_b, nullptr, emb, H, EPI_STORE, st_);
     QASR_HIP(hipGetLastError());

@@ -11,6 +11,8 @@ enum Epi : int {
     EPI_RESID = 1,  // y = res + acc (+ bias)      (y may alias res)
     EPI_GELU = 2,   // y = gelu_erf(acc + bias)
     EPI_SWIGLU = 3, // W rows gate/up interleaved by 16 (interleave_gate_up): h = silu(g)·u → Q8 rows (yq, yd)
+    EPI_GELU_Q8 = 4,   // h = gelu_erf(acc + bias) → Q8 rows (yq [M][N], yd [M][N/32]); y unused
+    EPI_STORE_F16 = 5, // y (as __half, row stride ldy) = f16(acc + bias)
 };
 
 // ---- Q8_0 weights / activations (kernels_q8.hip)

@@ -288,6 +288,53 @@ __device__ __forceinline__ void gemm_epilogue(const float (&acc)[TI][TJ][4], int
             return;
         }
     }
+    if constexpr (TJ % 2 == 0) {
+        if (epi == EPI_GELU_Q8) {
+            // erf-GELU(acc + bias) quantised to Q8 rows: fragments 2b, 2b+1 = one 32-column block of the output
+#pragma unroll
+            for (int i = 0; i < TI; i++) {
+#pragma unroll
+                for (int b = 0; b < TJ / 2; b++) {
+                    const int c0 = n0 + bcol + 32 * b;
+                    const float b0 = bias && c0 + fr < N ? bias[c0 + fr] : 0.f;
+                    const float b1 = bias && c0 + 16 + fr < N ? bias[c0 + 16 + fr] : 0.f;
+#pragma unroll
+                    for (int r = 0; r < 4; r++) {
+                        const int row = m0 + arow + i * 16 + fq + r;
+                        const float h0 = gelu_erf(acc[i][2 * b][r] + b0), h1 = gelu_erf(acc[i][2 * b + 1][r] + b1);
+                        float am = fmaxf(fabsf(h0), fabsf(h1));
+                        am = fmaxf(am, __shfl_xor(am, 1));
+                        am = fmaxf(am, __shfl_xor(am, 2));
+                        am = fmaxf(am, __shfl_xor(am, 4));
+                        am = fmaxf(am, __shfl_xor(am, 8));
+                        const float dd = am / 127.f;
+                        if (row < M && c0 < N) {
+                            int8_t* qr = yq + (size_t)row * N + c0;
+                            qr[fr] = (int8_t)(am == 0.f ? 0 : (int)roundf(h0 / dd));
+                            qr[16 + fr] = (int8_t)(am == 0.f ? 0 : (int)roundf(h1 / dd));
+                            if (fr == 0) yd[(size_t)row * (N / QK) + c0 / QK] = __half2float(f2h(dd));
+                        }
+                    }
+                }
+            }
+            return;
+        }
+    }
+    if (epi == EPI_STORE_F16) {
+#pragma unroll
+        for (int i = 0; i < TI; i++)
+#pragma unroll
+            for (int j = 0; j < TJ; j++) {
+                const int col = n0 + bcol + j * 16 + fr;
+                const float bv = bias && col < N ? bias[col] : 0.f;
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    const int row = m0 + arow + i * 16 + fq + r;
+                    if (row < M && col < N) ((__half*)y)[(size_t)row * ldy + col] = f2h(acc[i][j][r] + bv);
+                }
+            }
+        return;
+    }
     const bool split = gridDim.z > 1;
 #pragma unroll
     for (int i = 0; i < TI; i++) {
@@ -955,7 +1002,9 @@ void gemm_q8(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const flo
         return;
     }
     const int tiles = cdiv(W.N, cf.bn) * cdiv(M, cf.bm);
-    const bool can_split = epi != EPI_GELU && ldy == W.N && (epi != EPI_RESID || res == y);
+    const bool can_split = (epi == EPI_STORE || epi == EPI_RESID) && ldy == W.N && (epi != EPI_RESID || res == y);
+    if (epi == EPI_GELU_Q8)
+        QASR_CHECK(W.N % 32 == 0 && yq && yd && cf.bn >= 64, QASR_E_INVALID, "gemm_q8: GELU+Q8 epilogue shape");
     int splits = 1;
     if (tiles < 256 && can_split) splits = std::max(1, std::min(std::min(cdiv(512, tiles), steps / 2), 8));
     if (force_splits > 0) splits = can_split ? std::min(force_splits, steps) : 1;
@@ -964,7 +1013,7 @@ void gemm_q8(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const flo
     if (splits > 1 && epi == EPI_STORE && !y_zeroed)
         QASR_HIP(hipMemsetAsync(y, 0, (size_t)M * ldy * sizeof(float), s));
     dim3 grid(cdiv(W.N, cf.bn), cdiv(M, cf.bm), splits);
-    launch_cfg(pick, grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, nullptr, nullptr);
+    launch_cfg(pick, grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd);
 }
 
 int64_t gate_up_interleaved_row(int64_t r, int64_t F) {

@@ -165,6 +165,39 @@ def test_linear_q8_vs_oracle(torch_dev, path, epi, m, n, k):
     assert np.abs(y - ref).max() <= 2e-5 * scale * np.sqrt(k / 256)
 
 
+@pytest.mark.parametrize("cfg", [-1, 0, 2, 4, 5, 10, 14])
+@pytest.mark.parametrize("m,n,k", [(37, 320, 2048), (300, 1024, 1024), (9, 64, 96)])
+def test_linear_fused_epilogues(torch_dev, m, n, k, cfg):
+    """GELU + Q8 quantisation (encoder up-projection, projector) and f16 store (encoder QKV) in the GEMM epilogue"""
+    import torch
+    from scipy.special import erf
+
+    rng = np.random.default_rng(m + n + k)
+    x = rng.standard_normal((m, k)).astype(np.float32)
+    blocks = oracle.synth_q8(k, "w", n, k, 0.05)
+    bias = rng.standard_normal(n).astype(np.float32)
+    oracle.set_mode(engine=True)
+    ref = oracle.linear_q8(x, blocks, n, bias).astype(np.float64)
+    g = (0.5 * ref * (1 + erf(ref / np.sqrt(2)))).astype(np.float32)
+    qr, dr = quant_ref(g)
+    qs, sc = q8_split(blocks, n, k)
+    xq = empty((m, k), torch.int8, torch_dev)
+    xdd = empty((m, k // 32), torch.float32, torch_dev)
+    keep = [dev(a, torch_dev) for a in (x, qs, sc, bias)]
+    _lib.check(L().qasr_op_quant_rows(ptr(keep[0]), m, k, k, ptr(xq), ptr(xdd), None))
+    hq = empty((m, n), torch.int8, torch_dev)
+    hd = empty((m, n // 32), torch.float32, torch_dev)
+    _lib.check(L().qasr_op_linear_q8_ex(ptr(xq), ptr(xdd), m, ptr(keep[1]), ptr(keep[2]), n, k, ptr(keep[3]), None, n,
+                                        4, ptr(hq), ptr(hd), cfg, None))
+    assert np.allclose(host(hd), dr, rtol=2e-3)
+    assert (np.abs(host(hq).astype(int) - qr) <= 1).all() and (host(hq) != qr).mean() < 1e-2
+    yh = empty((m, n + 8), torch.float16, torch_dev)
+    _lib.check(L().qasr_op_linear_q8_ex(ptr(xq), ptr(xdd), m, ptr(keep[1]), ptr(keep[2]), n, k, ptr(keep[3]), ptr(yh),
+                                        n + 8, 5, None, None, cfg, None))
+    y = host(yh)[:, :n].astype(np.float32)
+    assert np.abs(y - ref).max() <= 1e-3 * np.abs(ref).max() + 2e-5 * np.abs(ref).max() * np.sqrt(k / 256)
+
+
 @pytest.mark.parametrize("m,h", [(9, 2048), (256, 1024), (5, 896), (3000, 2048)])
 def test_rmsnorm_q8(torch_dev, m, h):
     """workgroup-per-row kernel (M <= 2048) and wave-per-row kernel (larger M)"""
