@@ -151,6 +151,7 @@ void quant_rows(const float* x, int M, int K, int ldx, int8_t* q, float* d, hipS
 }
 
 typedef int v4i __attribute__((ext_vector_type(4)));
+typedef float v16f __attribute__((ext_vector_type(16)));
 
 // ------------------------------------------------------------------------------------------------ GEMV
 // Weight streaming for M ≤ 8 rows.  One wave per 4 output columns (weight rows): per 2 KB K-segment each lane
@@ -689,18 +690,32 @@ __global__ __launch_bounds__(256 * KG, 2 / KG) void k_gemm_q8d(const int8_t* __r
         const char* st = smem + (s % NBUF) * STAGE;
         // fragments and scales of block kb, read just before its MFMAs (the compiler hoists what registers allow)
         constexpr int KBG = KB / KG;   // blocks of this K group per stage
-        float sb[KBG][TJ], sa[KBG][TI][4];
+        // OP (outer-product scales): the 16×16·TJ products d_x(row)·d_w(col) of one i-fragment come from one
+        // v_mfma_f32_16x16x1_4b_f32 (lane l supplies d_x of row l&15 and d_w of column l; register 4j+r of lane
+        // (fr, kh) = d_x[4kh+r]·d_w[16j+fr]) instead of 4·TJ VALU multiplies — the rescale becomes cvt + fma
+        constexpr bool OP = TJ <= 4 && KG == 1 && (BK == 64 || TI == 1);
+        float sb[KBG][TJ], sa[KBG][TI][4], sal[KBG][TI], sbl[KBG];
         long a[KBG][TI], b[KBG][TJ];
         auto load_block = [&](int sl, int kb) {
+            if constexpr (OP) {
+                const int cl = min(lane, 16 * TJ - 1);
+                const uint32_t v = *(const uint32_t*)(st + OSB + 4 * ((kb >> 1) * BN + bcol + cl));
+                sbl[sl] = __half2float(__ushort_as_half((unsigned short)((kb & 1) ? v >> 16 : v & 0xffff)));
+            } else {
 #pragma unroll
-            for (int j = 0; j < TJ; j++) {
-                const uint32_t v = *(const uint32_t*)(st + OSB + 4 * ((kb >> 1) * BN + bcol + 16 * j + fr));
-                sb[sl][j] = __half2float(__ushort_as_half((unsigned short)((kb & 1) ? v >> 16 : v & 0xffff)));
+                for (int j = 0; j < TJ; j++) {
+                    const uint32_t v = *(const uint32_t*)(st + OSB + 4 * ((kb >> 1) * BN + bcol + 16 * j + fr));
+                    sb[sl][j] = __half2float(__ushort_as_half((unsigned short)((kb & 1) ? v >> 16 : v & 0xffff)));
+                }
             }
 #pragma unroll
             for (int i = 0; i < TI; i++) {
-                const float4 v = *(const float4*)(st + OSA + 4 * (kb * BM + arow + 16 * i + fq));
-                sa[sl][i][0] = v.x, sa[sl][i][1] = v.y, sa[sl][i][2] = v.z, sa[sl][i][3] = v.w;
+                if constexpr (OP) {
+                    sal[sl][i] = *(const float*)(st + OSA + 4 * (kb * BM + arow + 16 * i + fr));
+                } else {
+                    const float4 v = *(const float4*)(st + OSA + 4 * (kb * BM + arow + 16 * i + fq));
+                    sa[sl][i][0] = v.x, sa[sl][i][1] = v.y, sa[sl][i][2] = v.z, sa[sl][i][3] = v.w;
+                }
                 int off = (arow + 16 * i + fr) * BK + foff[kb];
                 asm volatile("" : "+v"(off));
                 a[sl][i] = *(const long*)(st + off);
@@ -715,27 +730,39 @@ __global__ __launch_bounds__(256 * KG, 2 / KG) void k_gemm_q8d(const int8_t* __r
         // MFMA q (block q / NF, fragment q % NF) is issued LAG MFMAs before its rescale, so the int32 result has
         // landed by the time the cvt/fma reach it and at most LAG+1 results are live
         constexpr int LAG = 3, NQ = (KB / KG) * NF;
+        constexpr int NPR = LAG / TJ + 2;   // outer-product results live at once (ring)
         const int kb0 = kg * (KB / KG);
         v4i c[LAG + 1];
+        v16f prod[NPR];
 #pragma unroll
         for (int q = 0; q < NQ + LAG; q++) {
             if (q < NQ) {
                 const int kb = q / NF, f = q % NF;
                 if (f == 0) load_block(kb, kb0 + kb);
+                if constexpr (OP) {
+                    if (f % TJ == 0) {
+                        const v16f z = {};
+                        prod[(q / TJ) % NPR] = __builtin_amdgcn_mfma_f32_16x16x1f32(sal[kb][f / TJ], sbl[kb], z, 0, 0, 0);
+                    }
+                }
                 c[q % (LAG + 1)] =
                     __builtin_amdgcn_mfma_i32_16x16x32_i8(a[kb][f / TJ], b[kb][f % TJ], v4i{0, 0, 0, 0}, 0, 0, 0);
             }
             if (q >= LAG) {
                 const int p = q - LAG, kb = p / NF, f = p % NF, i = f / TJ, j = f % TJ;
 #pragma unroll
-                for (int r = 0; r < 4; r++)
-                    acc[i][j][r] = fmaf((float)c[p % (LAG + 1)][r], sa[kb][i][r] * sb[kb][j], acc[i][j][r]);
+                for (int r = 0; r < 4; r++) {
+                    if constexpr (OP)
+                        acc[i][j][r] = fmaf((float)c[p % (LAG + 1)][r], prod[(p / TJ) % NPR][4 * j + r], acc[i][j][r]);
+                    else
+                        acc[i][j][r] = fmaf((float)c[p % (LAG + 1)][r], sa[kb][i][r] * sb[kb][j], acc[i][j][r]);
+                }
             }
         }
 #pragma unroll
         for (int t = 0; t < NQ; t++) {
             __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-            __builtin_amdgcn_sched_group_barrier(0x002, 12, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, OP ? 8 : 12, 0);
         }
     }
     if constexpr (KG == 2) {
