@@ -133,9 +133,18 @@ def main():
     import torch
     import torch.distributed as dist
 
+    # QASR_DIST_BACKEND=gloo: rehearsal of the N>1 flow on a box with fewer GPUs than ranks (ranks share cards,
+    # collectives staged through host memory); the driver's multi-GPU runs use the default, RCCL
+    backend = os.environ.get("QASR_DIST_BACKEND", "nccl")
+    if backend == "gloo":
+        local = local % torch.cuda.device_count()
     torch.cuda.set_device(local)
+    coll_dev = torch.device("cpu") if backend == "gloo" else torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "gloo":
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     from qasr import _lib
     from qasr.transcribe_cpp import Model
@@ -149,11 +158,21 @@ def main():
     torch.cuda.synchronize()
     audio_s = sum(lens) / 16000.0
 
-    model = Model.synthetic(args.arch, seed=0)
+    collectives = {}
+    if world > 1:
+        # rank 0 builds the weights, every other rank opens a shell of the same device layout and
+        # ONE RCCL broadcast over the whole blob fills it (qasr/dist.py); untimed, like a server's load
+        from qasr import dist as qdist
+
+        model = Model.synthetic(args.arch, seed=0) if rank == 0 else Model.shell(args.arch)
+        collectives["weight_broadcast"] = qdist.broadcast_weights(model, rank, torch.device("cuda", local))
+        collectives["backend"] = backend
+    else:
+        model = Model.synthetic(args.arch, seed=0)
     sess = model.session(kv_type="f16", n_ctx=32768)
 
-    def step():
-        sess.run_batch_device(dev.data_ptr(), offs, lens, force_tokens_per_s=FORCE_TPS, want_results=False)
+    def step(want=False):
+        return sess.run_batch_device(dev.data_ptr(), offs, lens, force_tokens_per_s=FORCE_TPS, want_results=want)
 
     for _ in range(args.warmup):
         step()
@@ -176,7 +195,7 @@ def main():
         # stream (eager launches; the timed steps replay step graphs, which events per launch would perturb)
         _lib.check(lib.qasr_prof_reset())
         _lib.check(lib.qasr_prof_enable(1))
-        step()
+        results = step(True)
         torch.cuda.synchronize()
         _lib.check(lib.qasr_prof_enable(0))
         need = C.c_size_t()
@@ -184,8 +203,20 @@ def main():
         buf = C.create_string_buffer(need.value)
         _lib.check(lib.qasr_prof_report(buf, need.value, C.byref(need)))
         prof = json.loads(buf.value.decode())
-    t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
-    tot = torch.tensor([audio_s * args.steps], dtype=torch.float64, device=f"cuda:{local}")
+    else:
+        results = step(True)
+    streams = [r.tokens for r in results]
+    if world > 1:
+        # token streams of every rank to rank 0 (untimed): all-gather of counts, then of the ragged payload
+        t_g = time.perf_counter()
+        every = qdist.gather_token_streams(streams, coll_dev)
+        collectives["token_gather"] = {"segments": sum(len(e) for e in every),
+                                       "tokens": sum(len(x) for e in every for x in e),
+                                       "ms": round((time.perf_counter() - t_g) * 1e3, 3)}
+    else:
+        collectives["token_gather"] = {"segments": len(streams), "tokens": sum(len(x) for x in streams), "ms": 0.0}
+    t = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
+    tot = torch.tensor([audio_s * args.steps], dtype=torch.float64, device=coll_dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dist.all_reduce(tot, op=dist.ReduceOp.SUM)
@@ -238,6 +269,7 @@ def main():
                        "audio_s_per_rank": round(audio_s, 1), "parallelism": f"dp{world}"},
             "roofline": roof,
             "cpu_baseline": cpu,
+            "collectives": collectives,
         }
         print(json.dumps(line, ensure_ascii=False), flush=True)
     sess.close()

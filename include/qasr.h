@@ -91,10 +91,24 @@ QASR_API int qasr_model_open(const char* gguf_path, const char* backend, qasr_mo
    custom qasr_hparams when arch == NULL; generated on the device from `seed` by the generator shared with
    the oracle.  Used when the GGUF weights are not provisioned. */
 QASR_API int qasr_model_open_synthetic(const char* arch, const qasr_hparams* hp, uint64_t seed, qasr_model** out);
+/* One-time weight broadcast (north_star "RCCL ... only to broadcast Q8 weights"): a model keeps every
+   weight and table in ONE device blob whose offsets depend only on the hyper-parameters, so rank 0 loads (or
+   generates) the model, every other rank opens a shell — the same layout allocated, nothing read or generated —
+   and one collective over the blob (torch.distributed / RCCL, bench.py) makes the shells identical to rank 0's
+   model.  gguf_path != NULL: hyper-parameters and tokenizer from the file's metadata (no tensor data read);
+   otherwise arch / hp as qasr_model_open_synthetic.  Sessions refuse a shell until
+   qasr_model_weights_received. */
+QASR_API int qasr_model_open_shell(const char* gguf_path, const char* arch, const qasr_hparams* hp, qasr_model** out);
+QASR_API int qasr_model_weight_blob(qasr_model* m, void** dev, size_t* bytes);
+QASR_API int qasr_model_weights_received(qasr_model* m);
 QASR_API int qasr_model_hparams(const qasr_model* m, qasr_hparams* out);
 QASR_API int64_t qasr_model_weight_bytes(const qasr_model* m);
 /* copy one tensor back to host in its GGUF storage form (Q8_0 blocks / f32 / f16) — for parity tests */
 QASR_API int qasr_model_export_tensor(const qasr_model* m, const char* name, void* dst, size_t cap, size_t* written);
+/* JSON {name: [ggml type, rows, cols, conv_cin]} of every GGUF tensor the model holds (rows × cols in GGUF terms:
+   Q8_0 matrices N × K; f32 vectors n × 1; f16 conv kernels Cout·Cin·9 × 1 with conv_cin = Cin).  buf == NULL:
+   only *needed is set. */
+QASR_API int qasr_model_tensor_table(const qasr_model* m, char* buf, size_t cap, size_t* needed);
 QASR_API void qasr_model_close(qasr_model* m);
 
 /* -------------------------------------------------------------------------------------------- session */

@@ -1,5 +1,6 @@
 // extern "C": model / session / batch / VAD / audio-io entry points (include/qasr.h).
 #include <math.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -103,6 +104,42 @@ QASR_API int qasr_model_open_synthetic(const char* arch, const qasr_hparams* hp,
     });
 }
 
+QASR_API int qasr_model_open_shell(const char* gguf_path, const char* arch, const qasr_hparams* hp, qasr_model** out) {
+    return guard([&] {
+        QASR_CHECK(out, QASR_E_INVALID, "null argument");
+        check_backend("hip");
+        auto m = std::make_unique<qasr_model>();
+        if (gguf_path) {
+            m->m = load_gguf_model(gguf_path, true);
+        } else {
+            qasr_hparams h;
+            if (arch) default_hparams(arch, &h);
+            else {
+                QASR_CHECK(hp, QASR_E_INVALID, "either a GGUF path, arch or hparams");
+                h = *hp;
+            }
+            m->m = make_synthetic_shell(h, arch ? arch : "custom");
+        }
+        *out = m.release();
+    });
+}
+
+QASR_API int qasr_model_weight_blob(qasr_model* m, void** dev, size_t* bytes) {
+    return guard([&] {
+        QASR_CHECK(m && dev && bytes, QASR_E_INVALID, "null argument");
+        *dev = m->m->mem.base;
+        *bytes = m->m->mem.bytes;
+    });
+}
+
+QASR_API int qasr_model_weights_received(qasr_model* m) {
+    return guard([&] {
+        QASR_CHECK(m, QASR_E_INVALID, "null argument");
+        QASR_HIP(hipDeviceSynchronize());
+        m->m->weights_pending = false;
+    });
+}
+
 QASR_API int qasr_model_hparams(const qasr_model* m, qasr_hparams* out) {
     return guard([&] {
         QASR_CHECK(m && out, QASR_E_INVALID, "null argument");
@@ -119,6 +156,24 @@ QASR_API int qasr_model_export_tensor(const qasr_model* m, const char* name, voi
     });
 }
 
+QASR_API int qasr_model_tensor_table(const qasr_model* m, char* buf, size_t cap, size_t* needed) {
+    return guard([&] {
+        QASR_CHECK(m && needed, QASR_E_INVALID, "null argument");
+        std::string j = "{";
+        for (const auto& kv : m->m->slots) {
+            const TensorSlot& t = kv.second;
+            char b[256];
+            snprintf(b, sizeof b, "%s\"%s\": [%u, %lld, %lld, %d]", j.size() > 1 ? ", " : "", kv.first.c_str(), t.type,
+                     (long long)t.rows, (long long)t.cols, t.conv_cin);
+            j += b;
+        }
+        j += "}";
+        *needed = j.size() + 1;
+        if (buf && cap >= j.size() + 1) memcpy(buf, j.c_str(), j.size() + 1);
+        else if (buf) QASR_CHECK(false, QASR_E_CAPACITY, "buffer too small");
+    });
+}
+
 QASR_API void qasr_model_close(qasr_model* m) { delete m; }
 
 // ------------------------------------------------------------------------------------------------ session
@@ -126,6 +181,8 @@ QASR_API int qasr_session_open(qasr_model* m, const char* kv_type, int32_t n_ctx
     return guard([&] {
         QASR_CHECK(m && out, QASR_E_INVALID, "null argument");
         QASR_CHECK(!kv_type || std::string(kv_type) == "f16", QASR_E_INVALID, "kv_type must be \"f16\"");
+        QASR_CHECK(!m->m->weights_pending, QASR_E_INVALID,
+                   "model is a shell whose weights have not arrived (qasr_model_weights_received)");
         auto s = std::make_unique<qasr_session>();
         s->s = std::make_unique<Session>(m->m.get(), n_ctx > 0 ? n_ctx : 32768);
         *out = s.release();

@@ -11,16 +11,22 @@
 
 namespace qasr {
 
+void DevAlloc::reserve(size_t n) {
+    QASR_CHECK(!base && !counting, QASR_E_INVALID, "weight arena reserved twice");
+    QASR_HIP(hipMalloc((void**)&base, n));
+    QASR_HIP(hipMemset(base, 0, n));   // padding bytes too: equal layouts hold equal images (broadcast checksum)
+    cap = n;
+}
 void* DevAlloc::alloc(size_t n) {
-    void* p = nullptr;
     n = (n + 255) / 256 * 256;
-    QASR_HIP(hipMalloc(&p, n));
-    ptrs.push_back(p);
+    const size_t off = bytes;
     bytes += n;
-    return p;
+    if (counting) return (void*)(uintptr_t)(off + 256);   // distinct non-null placeholders, never dereferenced
+    QASR_CHECK(base && bytes <= cap, QASR_E_INVALID, "weight arena overflow");
+    return base + off;
 }
 DevAlloc::~DevAlloc() {
-    for (void* p : ptrs) (void)hipFree(p);
+    if (base) (void)hipFree(base);
 }
 
 static void set_special_defaults(qasr_hparams* hp) {
@@ -206,6 +212,31 @@ void build_layout(Model& m) {
     }
 }
 
+constexpr size_t DFT_BASIS_FLOATS = (size_t)400 * 402;
+
+// the whole device layout: weights, the untied vocabulary projection when the checkpoint has one, and the
+// fixed tables — the probe pass (mem.counting) sizes the arena, the second pass carves it
+void layout_all(Model& m, bool untied) {
+    build_layout(m);
+    if (untied) {
+        m.lm_head = alloc_q8(m, m.hp.vocab, m.hp.txt_h);
+        reg_q8(m, "output.weight", m.lm_head, 0, m.hp.vocab);
+    }
+    m.pos_emb = (float*)m.mem.alloc((size_t)13 * m.hp.enc_d * sizeof(float));
+    m.mel_filters = (float*)m.mem.alloc((size_t)201 * m.hp.n_mels * sizeof(float));
+    m.dft_basis = (float*)m.mem.alloc(DFT_BASIS_FLOATS * sizeof(float));
+}
+
+void make_layout(Model& m, bool untied) {
+    Model probe;
+    probe.hp = m.hp;
+    probe.mem.counting = true;
+    layout_all(probe, untied);
+    m.mem.reserve(probe.mem.bytes);
+    layout_all(m, untied);
+    QASR_CHECK(m.mem.bytes == probe.mem.bytes, QASR_E_INVALID, "layout probe mismatch");
+}
+
 // fixed tables: sinusoid position embedding (SinusoidsPositionEmbedding, modeling_qwen3_asr.py:245-263),
 // Slaney mel filters (feature_extraction_qwen3_asr.py:94-102) and the windowed DFT basis of the STFT
 void build_tables(Model& m, hipStream_t s) {
@@ -218,14 +249,12 @@ void build_tables(Model& m, hipStream_t s) {
             pe[(size_t)t * d + i] = sinf(st);
             pe[(size_t)t * d + d / 2 + i] = cosf(st);
         }
-    m.pos_emb = (float*)m.mem.alloc(pe.size() * sizeof(float));
     QASR_HIP(hipMemcpyAsync(m.pos_emb, pe.data(), pe.size() * sizeof(float), hipMemcpyHostToDevice, s));
     std::vector<float> filt((size_t)201 * nmel), basis;
     mel_filter_table(nmel, filt.data());
-    m.mel_filters = (float*)m.mem.alloc(filt.size() * sizeof(float));
     QASR_HIP(hipMemcpyAsync(m.mel_filters, filt.data(), filt.size() * sizeof(float), hipMemcpyHostToDevice, s));
     dft_basis_table(basis);
-    m.dft_basis = (float*)m.mem.alloc(basis.size() * sizeof(float));
+    QASR_CHECK(basis.size() == DFT_BASIS_FLOATS, QASR_E_INVALID, "DFT basis size");
     QASR_HIP(hipMemcpyAsync(m.dft_basis, basis.data(), basis.size() * sizeof(float), hipMemcpyHostToDevice, s));
     QASR_HIP(hipStreamSynchronize(s));
 }
@@ -245,9 +274,10 @@ void make_tokenizer_synthetic(Model& m) {
 // The per-tensor (sigma | center, scale) table mirrors orc_model_synth in oracle/qasr_oracle.c.
 // device layouts the kernels want, applied once after load: decoder gate|up rows interleaved by 16 so the
 // gate-up GEMM epilogue computes SwiGLU and its Q8 blocks in registers (kernels_q8.hip EPI_SWIGLU)
-void finalize_layout(Model& m, hipStream_t s) {
+// (a shell receives the blob already interleaved: it only records the slot layout)
+void finalize_layout(Model& m, hipStream_t s, bool data = true) {
     for (int l = 0; l < m.hp.txt_layers; l++) {
-        interleave_gate_up(m.dec[l].gu, s);
+        if (data) interleave_gate_up(m.dec[l].gu, s);
         for (const char* n : {"blk.%d.ffn_gate.weight", "blk.%d.ffn_up.weight"}) m.slots.at(nm(n, l)).il16_F = m.hp.txt_ffn;
     }
 }
@@ -258,7 +288,7 @@ std::unique_ptr<Model> make_synthetic_model(const qasr_hparams& hp, uint64_t see
     Model& m = *mp;
     m.hp = hp;
     m.arch = arch;
-    build_layout(m);
+    make_layout(m, false);
     hipStream_t s = nullptr;
     const int C = hp.conv_ch, d = hp.enc_d, H = hp.txt_h, F3 = m.audio_F3();
     const int QD = hp.txt_heads * hp.head_dim;
@@ -329,11 +359,25 @@ std::unique_ptr<Model> make_synthetic_model(const qasr_hparams& hp, uint64_t see
     return mp;
 }
 
+std::unique_ptr<Model> make_synthetic_shell(const qasr_hparams& hp, const std::string& arch) {
+    validate(hp);
+    auto mp = std::make_unique<Model>();
+    Model& m = *mp;
+    m.hp = hp;
+    m.arch = arch;
+    make_layout(m, false);
+    finalize_layout(m, nullptr, false);
+    build_tables(m, nullptr);
+    make_tokenizer_synthetic(m);
+    m.weights_pending = true;
+    return mp;
+}
+
 // ----------------------------------------------------------------------------------------------- GGUF
 // Metadata keys and tensor names of this engine's GGUF convention (DESIGN.md §tensor names).  The text
 // decoder uses llama.cpp's qwen3 names; audio tensors use the "a." prefix.  Every tensor is validated
 // against the shape implied by the metadata before upload.
-std::unique_ptr<Model> load_gguf_model(const std::string& path) {
+std::unique_ptr<Model> load_gguf_model(const std::string& path, bool shell) {
     GgufFile f(path);
     qasr_hparams hp;
     default_hparams("qwen3-asr-1.7b", &hp);
@@ -380,11 +424,16 @@ std::unique_ptr<Model> load_gguf_model(const std::string& path) {
     Model& m = *mp;
     m.hp = hp;
     m.arch = f.get_str("general.name", "qwen3-asr");
-    build_layout(m);
+    const GgufTensor* out = f.tensor("output.weight");   // untied checkpoints carry their own vocabulary projection
+    if (out)
+        QASR_CHECK(out->type == GGML_Q8_0 && out->dims.size() == 2 && out->dims[0] == hp.txt_h && out->dims[1] == hp.vocab,
+                   QASR_E_FORMAT, "output.weight: shape mismatch");
+    make_layout(m, out != nullptr);
     hipStream_t s = nullptr;
     uint8_t* staging = nullptr;
     size_t staging_cap = 0;
     for (auto& kv : m.slots) {
+        if (shell) break;
         const std::string& name = kv.first;
         const TensorSlot& t = kv.second;
         const GgufTensor* g = f.tensor(name);
@@ -415,20 +464,9 @@ std::unique_ptr<Model> load_gguf_model(const std::string& path) {
         }
     }
     if (staging) QASR_HIP(hipFree(staging));
-    if (const GgufTensor* out = f.tensor("output.weight")) {  // untied checkpoints
-        QASR_CHECK(out->type == GGML_Q8_0 && out->dims[0] == hp.txt_h && out->dims[1] == hp.vocab, QASR_E_FORMAT,
-                   "output.weight: shape mismatch");
-        m.lm_head = alloc_q8(m, hp.vocab, hp.txt_h);
-        reg_q8(m, "output.weight", m.lm_head, 0, hp.vocab);
-        uint8_t* tmp = nullptr;
-        QASR_HIP(hipMalloc(&tmp, out->nbytes));
-        QASR_HIP(hipMemcpy(tmp, out->data, out->nbytes, hipMemcpyHostToDevice));
-        repack_q8(tmp, (int64_t)hp.vocab * (hp.txt_h / QK), m.lm_head.qs, m.lm_head.sc, s);
-        QASR_HIP(hipStreamSynchronize(s));
-        QASR_HIP(hipFree(tmp));
-    }
-    finalize_layout(m, s);
+    finalize_layout(m, s, !shell);
     build_tables(m, s);
+    m.weights_pending = shell;
     if (toks && toks->arr_type == 8 && (int)toks->arr_s.size() >= hp.vocab) {
         m.tok.pieces = toks->arr_s;
         m.tok.is_special.assign(m.tok.pieces.size(), 0);

@@ -15,10 +15,18 @@
 
 namespace qasr {
 
+// Every weight and table of a model lives in ONE device allocation whose offsets depend only on the
+// hyper-parameters (and on whether the checkpoint has an untied output.weight): the blob a rank-0 load fills
+// and one RCCL broadcast copies into every other rank's identically laid-out shell.
 struct DevAlloc {
-    std::vector<void*> ptrs;
-    size_t bytes = 0;
+    char* base = nullptr;
+    size_t cap = 0, bytes = 0;
+    bool counting = false;   // layout probe: hands out offsets only, touches no memory
+    void reserve(size_t n);
     void* alloc(size_t n);
+    DevAlloc() = default;
+    DevAlloc(const DevAlloc&) = delete;
+    DevAlloc& operator=(const DevAlloc&) = delete;
     ~DevAlloc();
 };
 
@@ -67,13 +75,18 @@ struct Model {
     Tokenizer tok;
     std::map<std::string, TensorSlot> slots;
 
+    bool weights_pending = false;   // a shell: layout allocated, weights still to arrive (broadcast)
+
     int audio_F3() const { return (((hp.n_mels + 1) / 2 + 1) / 2 + 1) / 2; }
     int64_t weight_bytes() const { return (int64_t)mem.bytes; }
 };
 
 void default_hparams(const char* arch, qasr_hparams* hp);
-std::unique_ptr<Model> load_gguf_model(const std::string& path);
+// shell = true: hyper-parameters and tokenizer from the GGUF metadata, the device layout allocated, no tensor
+// data read (the receiving side of the weight broadcast)
+std::unique_ptr<Model> load_gguf_model(const std::string& path, bool shell = false);
 std::unique_ptr<Model> make_synthetic_model(const qasr_hparams& hp, uint64_t seed, const std::string& arch);
+std::unique_ptr<Model> make_synthetic_shell(const qasr_hparams& hp, const std::string& arch);
 void export_tensor(const Model& m, const std::string& name, void* dst, size_t cap, size_t* written);
 
 }  // namespace qasr

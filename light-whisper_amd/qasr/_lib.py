@@ -69,6 +69,10 @@ SIGNATURES = {
     "qasr_model_open_synthetic": (C.c_int, [C.c_char_p, C.POINTER(HParams), C.c_uint64, C.POINTER(P)]),
     "qasr_model_hparams": (C.c_int, [P, C.POINTER(HParams)]),
     "qasr_model_weight_bytes": (C.c_int64, [P]),
+    "qasr_model_open_shell": (C.c_int, [C.c_char_p, C.c_char_p, C.POINTER(HParams), C.POINTER(P)]),
+    "qasr_model_weight_blob": (C.c_int, [P, C.POINTER(P), C.POINTER(C.c_size_t)]),
+    "qasr_model_weights_received": (C.c_int, [P]),
+    "qasr_model_tensor_table": (C.c_int, [P, C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)]),
     "qasr_model_export_tensor": (C.c_int, [P, C.c_char_p, P, SZ, C.POINTER(SZ)]),
     "qasr_model_close": (None, [P]),
     "qasr_session_open": (C.c_int, [P, C.c_char_p, I32, C.POINTER(P)]),

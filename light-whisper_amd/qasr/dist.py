@@ -1,0 +1,113 @@
+"""The two collectives of the multi-GPU path (north_star: "RCCL over xGMI used only to broadcast Q8
+weights and gather token streams").  One process per GPU, torch.distributed with the "nccl" backend (= RCCL on
+ROCm) on the GPU box, "gloo" in the CPU tests; nothing here runs inside a timed step.
+
+* `broadcast_weights`: rank 0 holds the loaded (or generated) model, every other rank a shell with the identical
+  device layout (`Model.shell`, include/qasr.h qasr_model_open_shell); ONE broadcast over the whole weight blob
+  (2.2 GB for 1.7B — a single large message, the shape a per-link-bound ring over xGMI wants) makes them equal,
+  and a wrapping int64 checksum gathered from every rank proves it.
+* `gather_token_streams`: after a batch, every rank's per-segment token ids reach rank 0 as two all-gathers —
+  the (segments, tokens) counts, then the ragged payload padded to the largest rank.
+
+The reference has no multi-GPU path (SURVEY §8(e) "Reference equivalent: none").
+"""
+from __future__ import annotations
+
+import time
+
+import numpy as np
+
+
+def device_bytes(ptr: int, nbytes: int, device):
+    """A uint8 torch tensor over `nbytes` of device memory owned elsewhere (the model's weight blob), through
+    __cuda_array_interface__ — no copy; the owner must outlive the view."""
+    import torch
+
+    class _Iface:
+        __cuda_array_interface__ = {"shape": (int(nbytes),), "typestr": "|u1", "data": (int(ptr), False),
+                                    "version": 3, "strides": None}
+
+    t = torch.as_tensor(_Iface(), device=device)
+    assert t.data_ptr() == int(ptr) and t.numel() == int(nbytes), "device view does not alias the blob"
+    return t
+
+
+def blob_checksum(t) -> int:
+    """Wrapping int64 sum of a byte blob (length a multiple of 8; the weight arena is 256-B granular):
+    order-independent, so every rank's reduction gives the same value for the same bytes."""
+    import torch
+
+    assert t.numel() % 8 == 0
+    return int(t.view(torch.int64).sum(dtype=torch.int64).item())
+
+
+def broadcast_blob(t, src: int = 0) -> dict:
+    """Broadcast the byte tensor `t` from `src` and verify it arrived: returns bytes, wall ms of the collective
+    and whether every rank's checksum equals the source's."""
+    import torch
+    import torch.distributed as dist
+
+    sync = torch.cuda.synchronize if t.is_cuda else (lambda: None)
+    staged = t.is_cuda and dist.get_backend() == "gloo"   # rehearsal runs: gloo moves host tensors only
+    sync()
+    dist.barrier()
+    t0 = time.perf_counter()
+    if staged:
+        h = t.cpu()
+        dist.broadcast(h, src=src)
+        t.copy_(h)
+    else:
+        dist.broadcast(t, src=src)
+    sync()
+    ms = (time.perf_counter() - t0) * 1e3
+    cdev = torch.device("cpu") if staged else t.device
+    mine = torch.tensor([blob_checksum(t)], dtype=torch.int64, device=cdev)
+    every = [torch.zeros_like(mine) for _ in range(dist.get_world_size())]
+    dist.all_gather(every, mine)
+    sums = [int(x.item()) for x in every]
+    return {"bytes": int(t.numel()), "ms": round(ms, 3), "staged_via_host": staged,
+            "GB_per_s": round(t.numel() / ms / 1e6, 1) if ms > 0 else None,
+            "checksums_agree": all(s == sums[src] for s in sums)}
+
+
+def broadcast_weights(model, rank: int, device, src: int = 0) -> dict:
+    """Rank `src` passes its loaded model, the others a `Model.shell` of the same layout; afterwards every rank's
+    model holds rank `src`'s weights and the shells accept sessions."""
+    ptr, nbytes = model.weight_blob()
+    info = broadcast_blob(device_bytes(ptr, nbytes, device), src=src)
+    if not info["checksums_agree"]:
+        raise RuntimeError("weight broadcast: checksums differ across ranks")
+    if rank != src:
+        model.weights_received()
+    return info
+
+
+def gather_token_streams(streams: list[list[int]], device) -> list[list[list[int]]]:
+    """All-gather every rank's per-segment token ids; returns, on every rank, [rank][segment] -> ids."""
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size()
+    lens = np.array([len(s) for s in streams], dtype=np.int32)
+    flat = np.concatenate([np.asarray(s, np.int32) for s in streams]) if lens.sum() else np.zeros(0, np.int32)
+    counts = torch.tensor([lens.size, flat.size], dtype=torch.int64, device=device)
+    all_counts = [torch.zeros_like(counts) for _ in range(world)]
+    dist.all_gather(all_counts, counts)
+    all_counts = [tuple(int(v) for v in c.tolist()) for c in all_counts]
+    max_seg = max(1, max(c[0] for c in all_counts))
+    max_tok = max(1, max(c[1] for c in all_counts))
+    lens_t = torch.zeros(max_seg, dtype=torch.int32, device=device)
+    lens_t[: lens.size] = torch.from_numpy(lens).to(device)
+    tok_t = torch.zeros(max_tok, dtype=torch.int32, device=device)
+    tok_t[: flat.size] = torch.from_numpy(flat).to(device)
+    all_lens = [torch.zeros_like(lens_t) for _ in range(world)]
+    all_toks = [torch.zeros_like(tok_t) for _ in range(world)]
+    dist.all_gather(all_lens, lens_t)
+    dist.all_gather(all_toks, tok_t)
+    out = []
+    for (nseg, ntok), lt, tt in zip(all_counts, all_lens, all_toks):
+        ln = lt[:nseg].cpu().numpy()
+        tk = tt[:ntok].cpu().numpy()
+        offs = np.concatenate([[0], np.cumsum(ln)])
+        out.append([tk[offs[i]:offs[i + 1]].tolist() for i in range(nseg)])
+    return out

@@ -68,6 +68,41 @@ class Model:
                                             int(seed), C.byref(h)))
         return cls(f"synthetic:{arch or 'custom'}:{seed}", _handle=h)
 
+    @classmethod
+    def shell(cls, arch: str | None = "qwen3-asr-1.7b", gguf_path: str | None = None, hparams: dict | None = None):
+        """Receiving side of the one-time weight broadcast: the device layout of `arch` (or of the GGUF's metadata)
+        allocated but not filled.  Fill `weight_blob()` (one collective from rank 0), then `weights_received()`."""
+        lib = _lib.load()
+        h = C.c_void_p()
+        hp = None
+        if hparams is not None:
+            hp = HParams()
+            for k, v in hparams.items():
+                setattr(hp, k, v)
+        check(lib.qasr_model_open_shell(gguf_path.encode() if gguf_path else None, arch.encode() if arch else None,
+                                        C.byref(hp) if hp is not None else None, C.byref(h)))
+        return cls(gguf_path or f"shell:{arch or 'custom'}", _handle=h)
+
+    def weight_blob(self):
+        """(device pointer, bytes) of the single allocation holding every weight and table."""
+        p, n = C.c_void_p(), C.c_size_t()
+        check(_lib.load().qasr_model_weight_blob(self._h, C.byref(p), C.byref(n)))
+        return int(p.value or 0), int(n.value)
+
+    def tensor_table(self) -> dict:
+        """{name: (ggml type, rows, cols, conv_cin)} of every GGUF tensor of the model."""
+        import json
+
+        lib = _lib.load()
+        need = C.c_size_t()
+        check(lib.qasr_model_tensor_table(self._h, None, 0, C.byref(need)))
+        buf = C.create_string_buffer(need.value)
+        check(lib.qasr_model_tensor_table(self._h, buf, need.value, C.byref(need)))
+        return {k: tuple(v) for k, v in json.loads(buf.value.decode()).items()}
+
+    def weights_received(self):
+        check(_lib.load().qasr_model_weights_received(self._h))
+
     @property
     def hparams(self) -> dict:
         hp = HParams()

@@ -175,3 +175,86 @@ def test_graph_decode_equals_eager(gpu, golden):
     assert graph == eager
     singles = [s.run(a, max_new_tokens=24).tokens for a in audios[:5]]
     assert graph[:5] == singles
+
+
+def _blob(m, dev):
+    from qasr import dist as qdist
+
+    p, n = m.weight_blob()
+    return qdist.device_bytes(p, n, dev)
+
+
+def _tokens(sess, golden, n=10):
+    audios = [golden["a__audio"], golden["b__audio"], golden["c__audio"]]
+    return [r.tokens for r in sess.run_batch(audios, max_new_tokens=n)]
+
+
+def test_shell_receives_broadcast_image(gpu, golden, torch_dev):
+    """The receiving side of the weight broadcast (qasr/dist.py): a shell has rank 0's exact layout, refuses
+    sessions until its blob is filled, and then decodes exactly like the model the blob came from."""
+    import torch
+
+    from qasr.transcribe_cpp import Model
+
+    m, s = gpu
+    sh = Model.shell(arch=None, hparams=tiny_hparams())
+    try:
+        with pytest.raises(RuntimeError):
+            sh.session(kv_type="f16", n_ctx=2048)
+        a, b = _blob(m, torch_dev), _blob(sh, torch_dev)
+        assert a.numel() == b.numel() and a.data_ptr() != b.data_ptr()
+        assert sh.tensor_table() == m.tensor_table()
+        b.copy_(a)                       # what dist.broadcast does over RCCL
+        torch.cuda.synchronize()
+        sh.weights_received()
+        s2 = sh.session(kv_type="f16", n_ctx=2048)
+        assert _tokens(s2, golden) == _tokens(s, golden)
+        s2.close()
+    finally:
+        sh.close()
+
+
+@pytest.mark.parametrize("untied", [False, True])
+def test_gguf_round_trip(gpu, golden, torch_dev, tmp_path, untied):
+    """GGUF loader parity: the tiny synthetic model written out as GGUF (tools/gguf_export.py)
+    and loaded by qasr_model_open gives a bit-identical device image (tied) and identical tokens; the untied form
+    (its own output.weight) and a GGUF-metadata shell filled by the broadcast image decode the same."""
+    import torch
+
+    from gguf_export import export_gguf
+    from qasr.transcribe_cpp import Model
+
+    m, s = gpu
+    hp = m.hparams
+    special = {v: k for k, v in SPECIAL.items()}
+    pieces = [f"<|{special[i]}|>" if i in special else "abcdefghij"[i % 10] * (1 + i % 3) for i in range(hp["vocab"])]
+    types = [3 if i in special else 1 for i in range(hp["vocab"])]
+    path = str(tmp_path / "tiny.gguf")
+    export_gguf(m, path, tokens=pieces, token_types=types, untied=untied)
+    g = Model(path, backend="hip")
+    try:
+        assert g.hparams == hp
+        if not untied:
+            assert torch.equal(_blob(g, torch_dev), _blob(m, torch_dev))
+        else:
+            assert "output.weight" in g.tensor_table()
+        gs = g.session(kv_type="f16", n_ctx=2048)
+        want = _tokens(s, golden)
+        assert _tokens(gs, golden) == want
+        r = gs.run(golden["a__audio"], max_new_tokens=6)
+        assert r.raw == "".join(pieces[t] for t in r.tokens)
+        gs.close()
+        sh = Model.shell(gguf_path=path)
+        try:
+            a, b = _blob(g, torch_dev), _blob(sh, torch_dev)
+            assert a.numel() == b.numel()
+            b.copy_(a)
+            torch.cuda.synchronize()
+            sh.weights_received()
+            s3 = sh.session(kv_type="f16", n_ctx=2048)
+            assert _tokens(s3, golden) == want
+            s3.close()
+        finally:
+            sh.close()
+    finally:
+        g.close()

@@ -75,3 +75,45 @@ def test_workload_deterministic():
     b = bench.make_workload(2, 1)
     assert len(a) == len(b) and all(np.array_equal(x, y) for x, y in zip(a, b))
     assert all(x.dtype == np.float32 and np.abs(x).max() <= 1.0 for x in a)
+
+
+def _collectives_rank(rank, world, port, q):
+    """bench.py's two collectives (qasr/dist.py) on gloo: the weight-blob broadcast into a shell and the ragged
+    token-stream gather (rank 1 has an empty segment; the last rank has no segments at all)."""
+    import torch
+    import torch.distributed as dist
+
+    sys.path.insert(0, os.path.join(ROOT, "light-whisper_amd"))
+    from qasr import dist as qdist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    blob = torch.from_numpy(np.random.default_rng(7).integers(0, 256, 4096, dtype=np.uint8)) if rank == 0 \
+        else torch.zeros(4096, dtype=torch.uint8)
+    info = qdist.broadcast_blob(blob, src=0)
+    streams = [] if rank == world - 1 else [list(range(rank * 100, rank * 100 + n)) for n in (3, 0, 5 + rank)]
+    got = qdist.gather_token_streams(streams, torch.device("cpu"))
+    q.put((rank, info, blob.numpy().tobytes(), got))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_weight_broadcast_and_token_gather_gloo(world):
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_collectives_rank, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = sorted((q.get(timeout=120) for _ in range(world)), key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    src = np.random.default_rng(7).integers(0, 256, 4096, dtype=np.uint8).tobytes()
+    want = [[] if r == world - 1 else [list(range(r * 100, r * 100 + n)) for n in (3, 0, 5 + r)] for r in range(world)]
+    for rank, info, blob, got in out:
+        assert info["bytes"] == 4096 and info["checksums_agree"]
+        assert blob == src
+        assert got == want
