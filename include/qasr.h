@@ -173,9 +173,9 @@ QASR_API int qasr_resample_linear(const float* x, size_t n, int32_t source_rate,
 /* -------------------------------------------------------------------------------------------- kernel ops */
 QASR_API int qasr_op_quant_rows(const float* x, int32_t M, int32_t K, int32_t ldx, int8_t* q, float* d, void* stream);
 QASR_API int qasr_op_repack_q8(const uint8_t* blocks, int64_t nblk, int8_t* qs, void* sc, void* stream);
-/* path: 0 auto, 1 GEMV, 2 MFMA GEMM; 16 + cfg + 8*splits: MFMA GEMM with a forced tile config (0 128x128,
- * 1 64x128, 2 64x64, 3 32x64, 7 heuristic) and split-K count (0 heuristic) — tuning only.
- * epi: 0 store, 1 residual, 2 gelu */
+/* path: 0 auto, 1 GEMV (M <= 8), 2 MFMA GEMM, 3 / 4 / 5 GEMV with 1 / 2 / 4 columns per wave;
+ * 16 + cfg + 32*splits: MFMA GEMM with a forced configuration (kernels_q8.hip kGemmCfgs, 0..15; 31 = heuristic)
+ * and split-K count (0 heuristic) — tuning only.  epi: 0 store, 1 residual, 2 gelu */
 QASR_API int qasr_op_linear_q8(const int8_t* xq, const float* xd, int32_t M, const int8_t* wqs, const void* wsc,
                                int32_t N, int32_t K, const float* bias, const float* res, float* y, int32_t ldy,
                                int32_t epi, int32_t path, void* stream);
@@ -209,6 +209,14 @@ QASR_API int qasr_op_swiglu_q8_interleaved(const float* gu, int32_t M, int32_t F
 QASR_API int qasr_op_qk_norm_rope(const float* qkv, int32_t rows, int32_t nh, int32_t nkv, int32_t hd,
                                   const int32_t* pos, const int32_t* slot, const float* qnw, const float* knw,
                                   const float* rope_cs, float eps, void* qout, void* kc, void* vc, void* stream);
+/* decode attention with the q/k norm + RoPE and the KV-cache write fused in (hd 128): qkv f32 rows as for
+   qasr_op_qk_norm_rope, K/V caches as for qasr_op_attention (ld = nkv·hd); output Q8 rows (oq, od).  Same
+   results as qasr_op_qk_norm_rope followed by qasr_op_attention. */
+QASR_API int qasr_op_attention_decode_fused(const float* qkv, int32_t rows, int32_t nh, int32_t nkv, int32_t hd,
+                                            const int32_t* pos, const int32_t* slot, const float* qnw,
+                                            const float* knw, const float* rope_cs, float eps, void* kc, void* vc,
+                                            const int32_t* kv_start, const int32_t* kv_len, float scale, int8_t* oq,
+                                            float* od, void* stream);
 QASR_API int qasr_op_attention(const void* q, int32_t ldq, const void* k, const void* v, int32_t ldkv,
                                const int32_t* kv_start, const int32_t* kv_len, int32_t rows, int32_t nh, int32_t nkv,
                                int32_t hd, float scale, float* o, int8_t* oq, float* od, void* stream);

@@ -44,14 +44,14 @@ QASR_API int qasr_op_linear_q8(const int8_t* xq, const float* xd, int32_t M, con
         W.sc = (__half*)wsc;
         W.N = N;
         W.K = K;
-        if (path == 1) {
+        if (path == 1 || (path >= 3 && path <= 5)) {   // GEMV: auto, or 1 / 2 / 4 columns per wave
             QASR_CHECK(M <= 8, QASR_E_INVALID, "linear_q8: GEMV path supports M <= 8");
-            gemv_q8(xq, xd, M, W, bias, res, y, ldy, epi, S(stream));
+            gemv_q8(xq, xd, M, W, bias, res, y, ldy, epi, S(stream), path == 1 ? 0 : 1 << (path - 3));
         } else if (path == 2) {
             gemm_q8(xq, xd, M, W, bias, res, y, ldy, epi, S(stream));
         } else if (path >= 16) {
-            const int cfg = (path - 16) % 16, splits = (path - 16) / 16;
-            gemm_q8(xq, xd, M, W, bias, res, y, ldy, epi, S(stream), cfg == 15 ? -1 : cfg, splits);
+            const int cfg = (path - 16) % 32, splits = (path - 16) / 32;
+            gemm_q8(xq, xd, M, W, bias, res, y, ldy, epi, S(stream), cfg == 31 ? -1 : cfg, splits);
         } else {
             linear_q8(xq, xd, M, W, bias, res, y, ldy, epi, S(stream));
         }
@@ -170,6 +170,20 @@ QASR_API int qasr_op_qk_norm_rope(const float* qkv, int32_t rows, int32_t nh, in
         QASR_CHECK(nkv > 0 && nh % nkv == 0, QASR_E_INVALID, "qk_norm_rope: bad head counts");
         qk_norm_rope(qkv, rows, nh, nkv, hd, pos, slot, qnw, knw, rope_cs, eps, (__half*)qout, (__half*)kc,
                      (__half*)vc, S(stream));
+        launched();
+    });
+}
+
+QASR_API int qasr_op_attention_decode_fused(const float* qkv, int32_t rows, int32_t nh, int32_t nkv, int32_t hd,
+                                            const int32_t* pos, const int32_t* slot, const float* qnw,
+                                            const float* knw, const float* rope_cs, float eps, void* kc, void* vc,
+                                            const int32_t* kv_start, const int32_t* kv_len, float scale, int8_t* oq,
+                                            float* od, void* stream) {
+    return guard([&] {
+        QASR_CHECK(hd == 128 && nkv > 0 && nh % nkv == 0 && oq && od, QASR_E_INVALID,
+                   "attention_decode_fused: hd 128, Q8 output");
+        const QkFuse fz{qkv, pos, slot, qnw, knw, rope_cs, eps, (__half*)kc, (__half*)vc};
+        attention_decode_fused(fz, nkv * hd, kv_start, kv_len, rows, nh, nkv, hd, scale, oq, od, S(stream));
         launched();
     });
 }

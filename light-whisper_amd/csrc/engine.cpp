@@ -260,9 +260,9 @@ void Session::encoder(FrontEnd& fe, float* enc_out_dbg) {
     __half* qkvh = (__half*)sc_.get(S_QKVH, (size_t)N * 3 * d * sizeof(__half));
     float* ff = (float*)sc_.get(S_FF, (size_t)N * std::max(F, d) * sizeof(float));
     const float scale = 1.0f / sqrtf((float)(d / h.enc_heads));
-    // MFMA-GEMM row counts (> 8) take the fused epilogues: QKV written as f16 for the attention, up-projection
-    // GELU quantised to the down-projection's Q8 rows in place; GEMV row counts keep the separate passes
-    const bool fused = N > 8;
+    // MFMA-GEMM row counts (> kGemvRows) take the fused epilogues: QKV written as f16 for the attention,
+    // up-projection GELU quantised to the down-projection's Q8 rows in place; GEMV row counts keep separate passes
+    const bool fused = N > kGemvRows;
     int8_t* hq = fused ? (int8_t*)sc_.get(S_HQ, (size_t)N * std::max(F, d)) : nullptr;
     float* hdq = fused ? (float*)sc_.get(S_HD, (size_t)N * (std::max(F, d) / QK) * sizeof(float)) : nullptr;
     for (int l = 0; l < h.enc_layers; l++) {
@@ -312,12 +312,14 @@ void Session::decoder_layers(float* x, int rows, const int* d_pos, const int* d_
     float* xd = (float*)sc_.get(S_XD, (size_t)rows * (kmax / QK) * sizeof(float));
     float* qkv = (float*)sc_.get(S_QKV, (size_t)rows * (QD + 2 * KD) * sizeof(float));
     __half* qh = (__half*)sc_.get(S_QH, (size_t)rows * QD * sizeof(__half));
-    float* gu = rows > 8 ? nullptr : (float*)sc_.get(S_GU, (size_t)rows * 2 * F * sizeof(float));
+    const bool fused = rows > kGemvRows;
+    float* gu = fused ? nullptr : (float*)sc_.get(S_GU, (size_t)rows * 2 * F * sizeof(float));
     // the fused gate-up epilogue writes the SwiGLU rows into a second Q8 buffer (its input xq is still being read)
-    int8_t* hq = rows > 8 ? (int8_t*)sc_.get(S_HQ, (size_t)rows * F) : nullptr;
-    float* hd_ = rows > 8 ? (float*)sc_.get(S_HD, (size_t)rows * (F / QK) * sizeof(float)) : nullptr;
+    int8_t* hq = fused ? (int8_t*)sc_.get(S_HQ, (size_t)rows * F) : nullptr;
+    float* hd_ = fused ? (float*)sc_.get(S_HD, (size_t)rows * (F / QK) * sizeof(float)) : nullptr;
     const float scale = 1.0f / sqrtf((float)hd);
     const size_t layer_kv = (size_t)kv_slots_ * KD;
+    const bool fuse_qk = !dense && hd == 128 && (nh / nkv == 2 || nh / nkv == 4) && !getenv("QASR_NO_QK_FUSE");
     for (int l = 0; l < h.txt_layers; l++) {
         const DecLayer& L = m_->dec[l];
         __half* kc = kc_ + (size_t)l * layer_kv;
@@ -327,11 +329,17 @@ void Session::decoder_layers(float* x, int rows, const int* d_pos, const int* d_
         rmsnorm_q8(x, rows, H, H, L.attn_norm, h.rms_eps, xq, xd, st_, zq ? qkv : nullptr,
                    zq ? (int64_t)rows * (QD + 2 * KD) : 0);
         linear_q8(xq, xd, rows, L.qkv, nullptr, nullptr, qkv, QD + 2 * KD, EPI_STORE, st_, zq);
-        qk_norm_rope(qkv, rows, nh, nkv, hd, d_pos, d_slot, L.q_norm, L.k_norm, rope_, h.rms_eps, qh, kc, vc, st_);
-        attention(qh, QD, kc, vc, KD, d_kvs, d_kvl, rows, nh, nkv, hd, scale, nullptr, xq, xd, st_, total_keys, dense);
+        if (fuse_qk) {   // decode rows: q/k norm + RoPE + KV write inside the attention kernel
+            const QkFuse fz{qkv, d_pos, d_slot, L.q_norm, L.k_norm, rope_, h.rms_eps, kc, vc};
+            attention_decode_fused(fz, KD, d_kvs, d_kvl, rows, nh, nkv, hd, scale, xq, xd, st_, total_keys);
+        } else {
+            qk_norm_rope(qkv, rows, nh, nkv, hd, d_pos, d_slot, L.q_norm, L.k_norm, rope_, h.rms_eps, qh, kc, vc, st_);
+            attention(qh, QD, kc, vc, KD, d_kvs, d_kvl, rows, nh, nkv, hd, scale, nullptr, xq, xd, st_, total_keys,
+                      dense);
+        }
         linear_q8(xq, xd, rows, L.o, nullptr, x, x, H, EPI_RESID, st_);
         rmsnorm_q8(x, rows, H, H, L.ffn_norm, h.rms_eps, xq, xd, st_);
-        if (rows > 8) {  // SwiGLU + Q8 in the gate-up GEMM epilogue (rows interleaved at load)
+        if (fused) {  // SwiGLU + Q8 in the gate-up GEMM epilogue (rows interleaved at load)
             gemm_q8(xq, xd, rows, L.gu, nullptr, nullptr, nullptr, 2 * F, EPI_SWIGLU, st_, -1, 0, hq, hd_);
             std::swap(xq, hq);
             std::swap(xd, hd_);
@@ -340,7 +348,7 @@ void Session::decoder_layers(float* x, int rows, const int* d_pos, const int* d_
             swiglu_q8(gu, rows, F, xq, xd, st_, true);
         }
         linear_q8(xq, xd, rows, L.down, nullptr, x, x, H, EPI_RESID, st_);
-        if (rows > 8) {
+        if (fused) {
             std::swap(xq, hq);
             std::swap(xd, hd_);
         }
@@ -356,7 +364,7 @@ void Session::lm_head_rows(const float* x, int rows, int ldx, float* logits) {
     linear_q8(xq, xd, rows, m_->lm_head, nullptr, nullptr, logits, h.vocab, EPI_STORE, st_);
 }
 
-// row bucket of a decode step: 1/2/4/8 rows on the GEMV path, then steps of 16 / 32 / 64 / 128 rows
+// row bucket of a decode step: 1/2/4 rows (GEMV path), 8, then steps of 16 / 32 / 64 / 128 rows
 int row_bucket(int m) {
     if (m <= 1) return 1;
     if (m <= 2) return 2;
@@ -538,7 +546,7 @@ void Session::run_batch(const float* dpcm, const std::vector<int64_t>& off, cons
         sc_.get(S_LOGITS, (size_t)bmax * V * sizeof(float));
         sc_.get(S_TOK, (size_t)bmax * sizeof(int));
         sc_.get(S_ARGP, argmax_scratch_bytes(bmax));
-        sc_.get(S_GU, (size_t)8 * 2 * h.txt_ffn * sizeof(float));  // the unfused (GEMV) SwiGLU of buckets <= 8
+        sc_.get(S_GU, (size_t)kGemvRows * 2 * h.txt_ffn * sizeof(float));  // the unfused (GEMV-row) SwiGLU
         decode_step(ds, bmax, true);  // also sizes the layer scratch
         QASR_HIP(hipEventRecord(step_ev_[0], st_));
     }

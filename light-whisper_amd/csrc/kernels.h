@@ -26,8 +26,11 @@ void quant_rows(const float* x, int M, int K, int ldx, int8_t* q, float* d, hipS
 // y_zeroed: y is already all-zero (a split-K GEMM then skips its memset)
 void linear_q8(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const float* bias, const float* res,
                float* y, int ldy, int epi, hipStream_t s, bool y_zeroed = false);
+// rows up to which linear_q8 streams weights with the GEMV kernel; more rows take the MFMA GEMM and its fused
+// epilogues (tools/gemv_tune.py: at 8 rows the GEMM is faster on every decoder shape, at 4 the GEMV mostly is)
+constexpr int kGemvRows = 4;
 void gemv_q8(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const float* bias, const float* res, float* y,
-             int ldy, int epi, hipStream_t s);
+             int ldy, int epi, hipStream_t s, int cols = 0);
 // force_cfg: index into kernels_q8.hip kGemmCfgs (-1 = heuristic); force_splits: split-K (0 = heuristic)
 void gemm_q8(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const float* bias, const float* res, float* y,
              int ldy, int epi, hipStream_t s, int force_cfg = -1, int force_splits = 0, int8_t* yq = nullptr,
@@ -66,6 +69,21 @@ void add_posemb_gather(const float* proj, int n_chunks, int T, int d, const floa
 // one query row r: Q[r] (f16) against keys/values slots [kv_start[r], kv_start[r]+kv_len[r]) of K/V (f16);
 // output quantised (q/d, row stride nh*hd) and/or f32 (o).  dense: runs of 16 consecutive rows share most of their
 // key range (prefill prompt rows, encoder windows) → the MFMA tile kernel; otherwise the per-row kernel (decode).
+// decode attention with the q/k RMS-norm + RoPE and the KV-cache write of the new row fused in (hd 128, G 2 / 4):
+// reads the f32 QKV rows directly; same results as qk_norm_rope followed by attention
+struct QkFuse {
+    const float* qkv;
+    const int* pos;
+    const int* slot;
+    const float* qnw;
+    const float* knw;
+    const float* rope_cs;
+    float eps;
+    __half* kc;
+    __half* vc;
+};
+void attention_decode_fused(const QkFuse& fz, int ldkv, const int* kv_start, const int* kv_len, int rows, int nh,
+                            int nkv, int hd, float scale, int8_t* oq, float* od, hipStream_t s, int64_t total_keys = 0);
 void attention(const __half* Q, int ldq, const __half* K, const __half* V, int ldkv, const int* kv_start,
                const int* kv_len, int rows, int nh, int nkv, int hd, float scale, float* o, int8_t* oq, float* od,
                hipStream_t s, int64_t total_keys = 0, bool dense = false);

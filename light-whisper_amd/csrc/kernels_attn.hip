@@ -12,6 +12,7 @@
 #include <type_traits>
 
 #include "kernels.h"
+#include "qk_rope.h"
 
 namespace qasr {
 
@@ -56,12 +57,12 @@ __device__ __forceinline__ float qk_dot(const float* qv, const __half* kr) {
     return part;
 }
 
-template <int HD, int G, int NW>
-__global__ __launch_bounds__(256) void k_attention(const __half* __restrict__ Q, int ldq, const __half* __restrict__ K,
-                                                   const __half* __restrict__ V, int ldkv,
+template <int HD, int G, int NW, bool FUSED = false>
+__global__ __launch_bounds__(256) void k_attention(const __half* __restrict__ Q, int ldq, const __half* K,
+                                                   const __half* V, int ldkv,
                                                    const int* __restrict__ kv_start, const int* __restrict__ kv_len,
                                                    int rows, int nh, int nkv, float scale, float* __restrict__ o,
-                                                   int8_t* __restrict__ oq, float* __restrict__ od) {
+                                                   int8_t* __restrict__ oq, float* __restrict__ od, QkFuse fz = {}) {
     constexpr int CH = 256;
     constexpr int QD = HD / 8;    // dims per lane in QKᵀ
     constexpr int PD = HD / 64;   // dims per lane in PV / output
@@ -83,11 +84,48 @@ __global__ __launch_bounds__(256) void k_attention(const __half* __restrict__ Q,
     const int sub = lane & 7, kk = lane >> 3;
 
     float qv[G][QD];
+    if constexpr (FUSED) {
+        // decode rows (NW = 4, hd = 128): the q/k RMS-norm + RoPE of this row's G query heads and its KV head, and
+        // the new K/V cache row, computed here instead of by k_qk_norm_rope_row (same arithmetic, same f16
+        // rounding: bit-identical).  q stays in LDS; K/V go to the cache and the barrier makes the new row
+        // visible to the waves that read it below (workgroup-scope ordering of global memory).
+        static_assert(HD == 128 && NW == 4, "fused q/k prologue: hd 128 decode kernel");
+        __shared__ float qs[G][HD];
+        const int nslot = nh + 2 * nkv, kvd = nkv * HD;
+        const float* src = fz.qkv + (size_t)r * nslot * HD;
+        const int p = fz.pos[r], sl = fz.slot[r];
+        const int e0 = (2 * lane) & (HD / 2 - 1);
+        const float4 cs = *(const float4*)(fz.rope_cs + ((size_t)p * (HD / 2) + e0) * 2);
+        const bool lo = 2 * lane < HD / 2;
+        for (int t = w; t < G + 2; t += 4) {
+            const int h = t < G ? kvh * G + t : t == G ? nh + kvh : nh + nkv + kvh;
+            const float2 v = *(const float2*)(src + h * HD + 2 * lane);
+            if (t == G + 1) {
+                *(__half2*)(fz.vc + (size_t)sl * kvd + kvh * HD + 2 * lane) = __floats2half2_rn(v.x, v.y);
+                continue;
+            }
+            const float2 g = *(const float2*)((t < G ? fz.qnw : fz.knw) + 2 * lane);
+            const __half2 hv = norm_rope_hd128(v, g, cs, lo, fz.eps);
+            if (t < G) {
+                const float2 back = __half22float2(hv);
+                qs[t][2 * lane] = back.x;
+                qs[t][2 * lane + 1] = back.y;
+            } else {
+                *(__half2*)(fz.kc + (size_t)sl * kvd + kvh * HD + 2 * lane) = hv;
+            }
+        }
+        __syncthreads();
 #pragma unroll
-    for (int g = 0; g < G; g++) {
-        const __half* qp = Q + (size_t)r * ldq + (kvh * G + g) * HD + sub * QD;
+        for (int g = 0; g < G; g++)
 #pragma unroll
-        for (int j = 0; j < QD; j++) qv[g][j] = __half2float(qp[j]);
+            for (int j = 0; j < QD; j++) qv[g][j] = qs[g][sub * QD + j];
+    } else {
+#pragma unroll
+        for (int g = 0; g < G; g++) {
+            const __half* qp = Q + (size_t)r * ldq + (kvh * G + g) * HD + sub * QD;
+#pragma unroll
+            for (int j = 0; j < QD; j++) qv[g][j] = __half2float(qp[j]);
+        }
     }
     float acc[G][PD];
     float m[G], lsum[G];
@@ -506,6 +544,23 @@ static void launch_attention(int G, int rows, hipStream_t s, const __half* Q, in
         case 4: k_attention<HD, 4, 4><<<b4, 256, 0, s>>>(Q, ldq, K, V, ldkv, kv_start, kv_len, rows, nh, nkv, scale, o, oq, od); break;
         default: throw Error(QASR_E_INVALID, "attention: query heads per KV head must be 1, 2 or 4");
     }
+}
+
+void attention_decode_fused(const QkFuse& fz, int ldkv, const int* kv_start, const int* kv_len, int rows, int nh,
+                            int nkv, int hd, float scale, int8_t* oq, float* od, hipStream_t s, int64_t total_keys) {
+    if (rows <= 0) return;
+    ProfScope ps(s, "attention", 4.0 * hd * nh * (double)total_keys, 4.0 * hd * nh * (double)total_keys);
+    QASR_CHECK(hd == 128 && nkv > 0 && nh % nkv == 0, QASR_E_INVALID, "attention_decode_fused: hd 128 only");
+    const int G = nh / nkv;
+    const unsigned b4 = (unsigned)(rows * nkv);
+    if (G == 2)
+        k_attention<128, 2, 4, true><<<b4, 256, 0, s>>>(nullptr, 0, fz.kc, fz.vc, ldkv, kv_start, kv_len, rows, nh, nkv,
+                                                        scale, nullptr, oq, od, fz);
+    else if (G == 4)
+        k_attention<128, 4, 4, true><<<b4, 256, 0, s>>>(nullptr, 0, fz.kc, fz.vc, ldkv, kv_start, kv_len, rows, nh, nkv,
+                                                        scale, nullptr, oq, od, fz);
+    else
+        throw Error(QASR_E_INVALID, "attention_decode_fused: query heads per KV head must be 2 or 4");
 }
 
 void attention(const __half* Q, int ldq, const __half* K, const __half* V, int ldkv, const int* kv_start,

@@ -3,6 +3,7 @@
 #include <algorithm>
 
 #include "kernels.h"
+#include "qk_rope.h"
 
 namespace qasr {
 
@@ -254,10 +255,39 @@ __global__ void k_swiglu_q8(const float* __restrict__ gu, int M, int F, int8_t* 
     quant32(g, q + (size_t)m * F + b * 32, d + (size_t)m * nb + b);
 }
 
+// one lane per element (a Q8 block = 32 lanes, amax by xor-shuffles): the decode's few-row case, where one
+// thread per block leaves the chip idle behind a 32-deep serial chain.  Same arithmetic as k_swiglu_q8 / quant32.
+__global__ __launch_bounds__(256) void k_swiglu_q8_lane(const float* __restrict__ gu, int M, int F,
+                                                        int8_t* __restrict__ q, float* __restrict__ d, int interleaved) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)M * F) return;     // F % 32 == 0: a 32-lane group never straddles the bound
+    const int m = (int)(i / F), f = (int)(i % F), b = f >> 5, j = f & 31;
+    const float* row = gu + (size_t)m * 2 * F;
+    float g, u;
+    if (interleaved) {   // h columns 32b..32b+31 = [g 16 | u 16 | g 16 | u 16] at 64b
+        const int c = 64 * b + (j < 16 ? j : j + 16);
+        g = row[c];
+        u = row[c + 16];
+    } else {
+        g = row[f];
+        u = row[F + f];
+    }
+    const float v = g / (1.f + expf(-g)) * u;
+    float amax = fabsf(v);
+#pragma unroll
+    for (int o = 16; o >= 1; o >>= 1) amax = fmaxf(amax, __shfl_xor(amax, o));
+    const float dd = amax / 127.f;
+    q[(size_t)m * F + f] = (int8_t)(amax == 0.f ? 0 : (int)roundf(v / dd));
+    if (j == 0) d[(size_t)m * (F / 32) + b] = __half2float(f2h(dd));
+}
+
 void swiglu_q8(const float* gu, int M, int F, int8_t* q, float* d, hipStream_t s, bool interleaved) {
     int64_t n = (int64_t)M * (F / 32);
     if (n <= 0) return;
-    k_swiglu_q8<<<(unsigned)cdiv64(n, 256), 256, 0, s>>>(gu, M, F, q, d, interleaved ? 1 : 0);
+    if (M <= 16)
+        k_swiglu_q8_lane<<<(unsigned)cdiv64(n * 32, 256), 256, 0, s>>>(gu, M, F, q, d, interleaved ? 1 : 0);
+    else
+        k_swiglu_q8<<<(unsigned)cdiv64(n, 256), 256, 0, s>>>(gu, M, F, q, d, interleaved ? 1 : 0);
 }
 
 __global__ void k_gelu_q8(const float* __restrict__ x, int M, int K, int8_t* __restrict__ q, float* __restrict__ d) {
@@ -381,14 +411,8 @@ __global__ __launch_bounds__(256) void k_qk_norm_rope_row(const float* __restric
             *(__half2*)(vc + (size_t)sl * kvd + (h - nh - nkv) * HD + 2 * lane) = __floats2half2_rn(v[t].x, v[t].y);
             continue;
         }
-        const float2 g = h < nh ? qw : kw;
-        const float inv = 1.0f / sqrtf(wsum(v[t].x * v[t].x + v[t].y * v[t].y) / (float)HD + eps);
-        const float a = v[t].x * inv * g.x, b = v[t].y * inv * g.y;
-        const float pa = __shfl_xor(a, 32), pb = __shfl_xor(b, 32);
-        const float oa = lo ? a * cs.x - pa * cs.y : a * cs.x + pa * cs.y;
-        const float ob = lo ? b * cs.z - pb * cs.w : b * cs.z + pb * cs.w;
         __half* dst = h < nh ? qout + (size_t)r * nh * HD + h * HD : kc + (size_t)sl * kvd + (h - nh) * HD;
-        *(__half2*)(dst + 2 * lane) = __floats2half2_rn(oa, ob);
+        *(__half2*)(dst + 2 * lane) = norm_rope_hd128(v[t], h < nh ? qw : kw, cs, lo, eps);
     }
 }
 

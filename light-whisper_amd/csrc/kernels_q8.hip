@@ -230,15 +230,26 @@ static double q8_bytes(int M, const Q8Mat& W, int epi) {
            (double)M * W.N * 4.0 * (epi == EPI_RESID ? 2 : 1);
 }
 
+template <int MR>
+static void gemv_launch(int cols, const int8_t* xq, const float* xd, int M, const Q8Mat& W, const float* bias,
+                        const float* res, float* y, int ldy, int epi, hipStream_t s) {
+    const dim3 g(cdiv(W.N, 4 * cols));
+    if (cols == 1) k_gemv_q8<MR, 1><<<g, 256, 0, s>>>(W.qs, W.sc, W.N, W.K, xq, xd, M, bias, res, y, ldy, epi);
+    else if (cols == 2) k_gemv_q8<MR, 2><<<g, 256, 0, s>>>(W.qs, W.sc, W.N, W.K, xq, xd, M, bias, res, y, ldy, epi);
+    else k_gemv_q8<MR, 4><<<g, 256, 0, s>>>(W.qs, W.sc, W.N, W.K, xq, xd, M, bias, res, y, ldy, epi);
+}
+
 void gemv_q8(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const float* bias, const float* res, float* y,
-             int ldy, int epi, hipStream_t s) {
+             int ldy, int epi, hipStream_t s, int cols) {
     ProfScope ps(s, "gemv_q8", 2.0 * M * W.N * W.K, q8_bytes(M, W, epi));
     QASR_CHECK(W.K % 32 == 0 && W.K >= 32, QASR_E_INVALID, "gemv_q8: K must be a multiple of 32");
-    const dim3 g4(cdiv(W.N, 16)), g2(cdiv(W.N, 8));
-    if (M <= 1) k_gemv_q8<1, 4><<<g4, 256, 0, s>>>(W.qs, W.sc, W.N, W.K, xq, xd, M, bias, res, y, ldy, epi);
-    else if (M <= 2) k_gemv_q8<2, 4><<<g4, 256, 0, s>>>(W.qs, W.sc, W.N, W.K, xq, xd, M, bias, res, y, ldy, epi);
-    else if (M <= 4) k_gemv_q8<4, 4><<<g4, 256, 0, s>>>(W.qs, W.sc, W.N, W.K, xq, xd, M, bias, res, y, ldy, epi);
-    else k_gemv_q8<8, 2><<<g2, 256, 0, s>>>(W.qs, W.sc, W.N, W.K, xq, xd, M, bias, res, y, ldy, epi);
+    // measured with cold weights (tools/gemv_tune.py): one column per wave except the vocabulary projection and
+    // the single-row QKV, where two per wave keep more loads in flight per lane
+    if (cols <= 0) cols = (W.N >= 32768 || (M == 1 && W.K <= 2048 && W.N <= 4096)) ? 2 : 1;
+    if (M <= 1) gemv_launch<1>(cols, xq, xd, M, W, bias, res, y, ldy, epi, s);
+    else if (M <= 2) gemv_launch<2>(cols, xq, xd, M, W, bias, res, y, ldy, epi, s);
+    else if (M <= 4) gemv_launch<4>(cols, xq, xd, M, W, bias, res, y, ldy, epi, s);
+    else gemv_launch<8>(std::min(cols, 2), xq, xd, M, W, bias, res, y, ldy, epi, s);
 }
 
 // ------------------------------------------------------------------------------------------------ GEMM (MFMA)
@@ -1072,7 +1083,7 @@ void interleave_gate_up(Q8Mat& W, hipStream_t s) {
 void linear_q8(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const float* bias, const float* res,
                float* y, int ldy, int epi, hipStream_t s, bool y_zeroed) {
     if (M <= 0) return;
-    if (M <= 8) gemv_q8(xq, xd, M, W, bias, res, y, ldy, epi, s);
+    if (M <= kGemvRows) gemv_q8(xq, xd, M, W, bias, res, y, ldy, epi, s);
     else gemm_q8(xq, xd, M, W, bias, res, y, ldy, epi, s, -1, 0, nullptr, nullptr, y_zeroed);
 }
 

@@ -50,6 +50,13 @@ Vad::Vad(const std::string& path) {
         pos += 52;
     }
     pos = (pos + 15) / 16 * 16;
+    std::vector<float> win(400), banks(80 * 256);
+    {   // one device allocation for every array + the two fbank tables (256-B granules, as DevAlloc hands out)
+        size_t total = 0;
+        for (const auto& mi : meta) total += (mi.second * 4 + 255) / 256 * 256;
+        total += (win.size() * 4 + 255) / 256 * 256 + (banks.size() * 4 + 255) / 256 * 256;
+        mem_.reserve(total);
+    }
     for (uint32_t i = 0; i < n; i++) {
         QASR_CHECK(meta[i].first == kOrder[i], QASR_E_FORMAT, "unexpected .qvad array " + meta[i].first);
         const size_t bytes = meta[i].second * 4;
@@ -60,7 +67,6 @@ Vad::Vad(const std::string& path) {
         arr_[meta[i].first] = d;
         pos += (bytes + 15) / 16 * 16;
     }
-    std::vector<float> win(400), banks(80 * 256);
     povey_window(win.data());
     kaldi_mel_banks(banks.data());
     win_ = (float*)mem_.alloc(win.size() * 4);

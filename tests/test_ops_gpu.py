@@ -140,14 +140,14 @@ def _linear_case(torch_dev, m, n, k, path, epi, seed=0, exact=False):
 
 # path: 1 GEMV, 2 auto, 16 + cfg (+ 16·splits) forces a GEMM configuration (kernels_q8.hip kGemmCfgs: 0..3 register-
 # staged, 4..10 LDS-DMA)
-GEMM_PATHS = [1, 2] + [16 + c for c in range(16)] + [16 + 4 + 16 * 2, 16 + 9 + 16 * 4, 16 + 10 + 16 * 3]
+GEMM_PATHS = [1, 2, 3, 4, 5] + [16 + c for c in range(16)] + [16 + 4 + 32 * 2, 16 + 9 + 32 * 4, 16 + 10 + 32 * 3]
 
 
 @pytest.mark.parametrize("path", GEMM_PATHS)
 @pytest.mark.parametrize("m,n,k", [(1, 64, 1024), (3, 130, 512), (8, 64, 1024), (9, 70, 96), (64, 128, 1024),
                                    (100, 192, 512), (32, 2048, 2048), (300, 2048, 1024), (33, 96, 160)])
 def test_linear_q8_exact_integer(torch_dev, path, m, n, k):
-    if path == 1 and m > 8:
+    if path in (1, 3, 4, 5) and m > 8:
         pytest.skip("GEMV path is M<=8")
     y, ref = _linear_case(torch_dev, m, n, k, path, 0, seed=m + n, exact=True)
     assert np.array_equal(y, ref)
@@ -158,7 +158,7 @@ def test_linear_q8_exact_integer(torch_dev, path, m, n, k):
 @pytest.mark.parametrize("m,n,k", [(1, 2048, 2048), (5, 256, 6144), (37, 320, 2048), (130, 1024, 1024),
                                    (24, 2048, 6144), (257, 2048, 2048)])
 def test_linear_q8_vs_oracle(torch_dev, path, epi, m, n, k):
-    if path == 1 and m > 8:
+    if path in (1, 3, 4, 5) and m > 8:
         pytest.skip("GEMV path is M<=8")
     y, ref = _linear_case(torch_dev, m, n, k, path, epi, seed=k + epi)
     scale = np.abs(ref).max() + 1e-6
@@ -280,11 +280,13 @@ def test_gemm_swiglu_q8(torch_dev, m, f, k, cfg):
     assert (np.abs(host(q2).astype(int) - qr) <= 1).all()
 
 
-def test_swiglu_q8(torch_dev):
+@pytest.mark.parametrize("m", [1, 4, 40])
+def test_swiglu_q8(torch_dev, m):
+    """lane-per-element kernel (M <= 16) and thread-per-block kernel (larger M)"""
     import torch
 
     rng = np.random.default_rng(5)
-    m, f = 4, 512
+    f = 512
     gu = rng.standard_normal((m, 2 * f)).astype(np.float32) * 3
     gt = dev(gu, torch_dev)
     q = empty((m, f), torch.int8, torch_dev)
@@ -336,6 +338,53 @@ def test_qk_norm_rope(torch_dev, nh, nkv, hd):
             assert np.abs(kh[slot[r], h * hd:(h + 1) * hd] - ref).max() < 2e-3 * np.abs(ref).max()
             vref = qkv[r, (nh + nkv + h) * hd:(nh + nkv + h + 1) * hd]
             assert np.abs(vh[slot[r], h * hd:(h + 1) * hd] - vref).max() < 2e-3 * np.abs(vref).max()
+
+
+@pytest.mark.parametrize("nh,nkv", [(16, 8), (16, 4)])
+def test_attention_decode_fused(torch_dev, nh, nkv):
+    """decode attention with the q/k norm + RoPE + KV write fused in == qk_norm_rope then attention, bit for bit
+    (Q8 output rows and both caches), over short and long key ranges"""
+    import torch
+
+    hd, rows = 128, 5
+    rng = np.random.default_rng(11)
+    lens = np.array([1, 7, 40, 130, 300], np.int32)
+    starts = np.concatenate([[3], 3 + np.cumsum(lens[:-1] + 2)]).astype(np.int32)
+    slots = int(starts[-1] + lens[-1] + 4)
+    qkv = rng.standard_normal((rows, (nh + 2 * nkv) * hd)).astype(np.float32)
+    pos = (lens - 1).astype(np.int32)
+    slot = (starts + lens - 1).astype(np.int32)
+    qnw = (1 + 0.1 * rng.standard_normal(hd)).astype(np.float32)
+    knw = (1 + 0.1 * rng.standard_normal(hd)).astype(np.float32)
+    tab = np.empty((512, hd // 2, 2), np.float32)
+    _lib.check(L().qasr_op_rope_table(512, hd, 1e6, tab.ctypes.data_as(C.c_void_p)))
+    kc0 = rng.standard_normal((slots, nkv * hd)).astype(np.float16)
+    vc0 = rng.standard_normal((slots, nkv * hd)).astype(np.float16)
+    keep = [dev(a, torch_dev) for a in (qkv, pos, slot, qnw, knw, tab, starts, lens)]
+    scale = 1.0 / np.sqrt(hd)
+    outs = []
+    for fused in (False, True):
+        kc, vc = dev(kc0, torch_dev), dev(vc0, torch_dev)
+        oq = torch.zeros((rows, nh * hd), dtype=torch.int8, device=torch_dev)
+        od = torch.zeros((rows, nh * hd // 32), dtype=torch.float32, device=torch_dev)
+        if fused:
+            _lib.check(L().qasr_op_attention_decode_fused(ptr(keep[0]), rows, nh, nkv, hd, ptr(keep[1]), ptr(keep[2]),
+                                                          ptr(keep[3]), ptr(keep[4]), ptr(keep[5]), 1e-6, ptr(kc),
+                                                          ptr(vc), ptr(keep[6]), ptr(keep[7]), scale, ptr(oq),
+                                                          ptr(od), None))
+        else:
+            qo = torch.zeros((rows, nh * hd), dtype=torch.float16, device=torch_dev)
+            _lib.check(L().qasr_op_qk_norm_rope(ptr(keep[0]), rows, nh, nkv, hd, ptr(keep[1]), ptr(keep[2]),
+                                                ptr(keep[3]), ptr(keep[4]), ptr(keep[5]), 1e-6, ptr(qo), ptr(kc),
+                                                ptr(vc), None))
+            _lib.check(L().qasr_op_attention(ptr(qo), nh * hd, ptr(kc), ptr(vc), nkv * hd, ptr(keep[6]),
+                                             ptr(keep[7]), rows, nh, nkv, hd, scale, None, ptr(oq), ptr(od), None))
+        torch.cuda.synchronize()
+        outs.append([host(t) for t in (oq, od, kc, vc)])
+    for name, a, b in zip(("oq", "od", "kc", "vc"), *outs):
+        bad = np.argwhere(a != b)
+        assert bad.size == 0, f"{name}: {len(bad)} differ, first {bad[:4].tolist()}"
+    assert not np.array_equal(outs[1][2], kc0)   # the new K rows were written
 
 
 def _attention_case(torch_dev, hd, nh, nkv, starts, lens, dense, seed):

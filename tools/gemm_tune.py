@@ -23,7 +23,7 @@ SHAPES = [  # (tag, M, N, K, epi)
 ]
 
 
-# 2 = auto; 16 + cfg (+ 16·splits): kernels_q8.hip kGemmCfgs — 0..3 register-staged {128², 64×128, 64², 32×64},
+# 2 = auto; 16 + cfg (+ 32·splits): kernels_q8.hip kGemmCfgs — 0..3 register-staged {128², 64×128, 64², 32×64},
 # 4..7 LDS-DMA K-64 stages {128², 64×128, 64², 128×64}, 8..11 LDS-DMA K-128 stages (same tiles)
 PATHS = [int(p) for p in os.environ.get("PATHS", "2,20,21,22,24,25,26,27").split(",")]
 
@@ -51,7 +51,7 @@ def main():
                 if epi == 3:   # fused SwiGLU + Q8 epilogue; path → forced config
                     _lib.check(lib.qasr_op_gemm_swiglu_q8_cfg(xq.data_ptr(), xd.data_ptr(), M, wq.data_ptr(),
                                                               ws.data_ptr(), N, K, hq.data_ptr(), hd.data_ptr(),
-                                                              -1 if path == 2 else (path - 16) % 16, None))
+                                                              -1 if path == 2 else (path - 16) % 32, None))
                     return
                 _lib.check(lib.qasr_op_linear_q8(xq.data_ptr(), xd.data_ptr(), M, wq.data_ptr(), ws.data_ptr(), N,
                                                  K, None, res.data_ptr() if res is not None else None,

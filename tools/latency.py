@@ -17,10 +17,12 @@ from qasr.transcribe_cpp import Model  # noqa: E402
 
 
 def main():
-    for arch in ("qwen3-asr-0.6b", "qwen3-asr-1.7b"):
+    archs = sys.argv[1].split(",") if len(sys.argv) > 1 else ["qwen3-asr-0.6b", "qwen3-asr-1.7b"]
+    lengths = [float(x) for x in sys.argv[2].split(",")] if len(sys.argv) > 2 else [1.0, 5.0, 12.0]
+    for arch in archs:
         m = Model.synthetic(arch, seed=0)
         s = m.session(kv_type="f16", n_ctx=32768)
-        for secs in (1.0, 5.0, 12.0):
+        for secs in lengths:
             audio = speech_like(np.random.default_rng(0), int(secs * 16000))
             for _ in range(2):
                 s.run(audio, force_tokens_per_s=8)
