@@ -166,6 +166,9 @@ QASR_API void qasr_vad_close(qasr_vad* v);
 
 /* -------------------------------------------------------------------------------------------- audio io */
 /* returns the f32 sample count; base64 of pcm_s16le → f32 = s/32768 (server_common.py:145-170) */
+/* Detokenised bytes → valid UTF-8 exactly as Python's bytes.decode("utf-8", errors="replace") (the Qwen2
+   tokenizer's decode): every transcript string the library returns has been through it.  out may be NULL to size. */
+QASR_API int qasr_utf8_replace_invalid(const char* in, size_t n, char* out, size_t cap, size_t* written);
 QASR_API int qasr_decode_pcm_s16le(const char* b64, size_t len, float* out, size_t cap, size_t* n_out);
 QASR_API int qasr_resample_linear(const float* x, size_t n, int32_t source_rate, float* out, size_t cap,
                                   size_t* n_out);

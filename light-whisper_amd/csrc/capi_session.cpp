@@ -378,19 +378,37 @@ QASR_API void qasr_vad_close(qasr_vad* v) { delete v; }
 
 // ------------------------------------------------------------------------------------------------ audio io
 // base64 with Python's b64decode(validate=True) acceptance rules and error texts (server_common.py:155-158)
+QASR_API int qasr_utf8_replace_invalid(const char* in, size_t n, char* out, size_t cap, size_t* written) {
+    return guard([&] {
+        QASR_CHECK((in || n == 0) && written, QASR_E_INVALID, "null argument");
+        const std::string r = utf8_replace_invalid(std::string(in ? in : "", n));
+        *written = r.size();
+        QASR_CHECK(out && cap >= r.size(), QASR_E_CAPACITY, "output buffer too small");
+        memcpy(out, r.data(), r.size());
+    });
+}
+
+namespace {
+struct B64Table {
+    int8_t v[256];
+    constexpr B64Table() : v() {
+        for (int i = 0; i < 256; i++) v[i] = -1;
+        for (int i = 0; i < 26; i++) v['A' + i] = (int8_t)i, v['a' + i] = (int8_t)(26 + i);
+        for (int i = 0; i < 10; i++) v['0' + i] = (int8_t)(52 + i);
+        v['+'] = 62;
+        v['/'] = 63;
+    }
+};
+constexpr B64Table kB64{};
+}  // namespace
+
 QASR_API int qasr_decode_pcm_s16le(const char* b64, size_t len, float* out, size_t cap, size_t* n_out) {
     return guard([&] {
         QASR_CHECK(b64 || len == 0, QASR_E_INVALID, "null argument");
-        auto val = [](char c) -> int {
-            if (c >= 'A' && c <= 'Z') return c - 'A';
-            if (c >= 'a' && c <= 'z') return c - 'a' + 26;
-            if (c >= '0' && c <= '9') return c - '0' + 52;
-            if (c == '+') return 62;
-            if (c == '/') return 63;
-            return -1;
-        };
+        const unsigned char* u = (const unsigned char*)b64;
+        // table-driven (branch-free on the data: a 12 s window is 512 KB of random-looking characters)
         size_t q = 0;
-        while (q < len && val(b64[q]) >= 0) q++;
+        while (q < len && kB64.v[u[q]] >= 0) q++;
         size_t p = 0;
         while (q + p < len && b64[q + p] == '=') p++;
         QASR_CHECK(q + p == len && p <= 2, QASR_E_FORMAT, "Non-base64 digit found");
@@ -398,28 +416,29 @@ QASR_API int qasr_decode_pcm_s16le(const char* b64, size_t len, float* out, size
                    "Invalid base64-encoded string: number of data characters (" + std::to_string(q) +
                        ") cannot be 1 more than a multiple of 4");
         QASR_CHECK(q % 4 == 0 || (q % 4) + p >= 4, QASR_E_FORMAT, "Incorrect padding");
-        std::vector<uint8_t> bytes;
-        bytes.reserve(q * 3 / 4 + 3);
-        uint32_t acc = 0;
-        int bits = 0;
-        for (size_t i = 0; i < q; i++) {
-            acc = (acc << 6) | (uint32_t)val(b64[i]);
-            bits += 6;
-            if (bits >= 8) {
-                bits -= 8;
-                bytes.push_back((uint8_t)((acc >> bits) & 0xff));
-            }
-        }
+        const size_t nbytes = q / 4 * 3 + (q % 4 ? q % 4 - 1 : 0);
         // odd byte count: distinct code (QASR_E_INVALID) so callers can order it after the sample-rate check
-        QASR_CHECK(bytes.size() % 2 == 0, QASR_E_INVALID, "PCM s16le 数据字节数必须为偶数");
-        const size_t ns = bytes.size() / 2;
+        QASR_CHECK(nbytes % 2 == 0, QASR_E_INVALID, "PCM s16le 数据字节数必须为偶数");
+        const size_t ns = nbytes / 2;
         if (n_out) *n_out = ns;
         QASR_CHECK(!out || cap >= ns, QASR_E_CAPACITY, "sample buffer too small");
-        if (out)
-            for (size_t i = 0; i < ns; i++) {
-                int16_t s = (int16_t)(bytes[2 * i] | (bytes[2 * i + 1] << 8));
-                out[i] = (float)s / 32768.0f;
-            }
+        if (!out) return;
+        std::vector<uint8_t> bytes(nbytes + 3);
+        size_t o = 0, i = 0;
+        for (; i + 4 <= q; i += 4, o += 3) {
+            const uint32_t v = (uint32_t)kB64.v[u[i]] << 18 | (uint32_t)kB64.v[u[i + 1]] << 12 |
+                               (uint32_t)kB64.v[u[i + 2]] << 6 | (uint32_t)kB64.v[u[i + 3]];
+            bytes[o] = (uint8_t)(v >> 16);
+            bytes[o + 1] = (uint8_t)(v >> 8);
+            bytes[o + 2] = (uint8_t)v;
+        }
+        if (i < q) {   // 2 or 3 trailing characters → 1 or 2 bytes
+            uint32_t v = 0;
+            for (size_t k = 0; k < 4; k++) v = v << 6 | (uint32_t)(i + k < q ? kB64.v[u[i + k]] : 0);
+            bytes[o] = (uint8_t)(v >> 16);
+            bytes[o + 1] = (uint8_t)(v >> 8);
+        }
+        for (size_t k = 0; k < ns; k++) out[k] = (float)(int16_t)(bytes[2 * k] | (bytes[2 * k + 1] << 8)) / 32768.0f;
     });
 }
 

@@ -8,7 +8,9 @@
 //
 // Model resolution follows hf_cache_utils.find_hf_snapshot_file (hf_cache_utils.py:73-117).  Test hooks
 // (never used by the app): QASR_SYNTHETIC=1 loads seeded synthetic weights when no GGUF is provisioned;
-// QASR_PROTOCOL_TEST_FAKE=1 replaces model + VAD by the reference tests' fakes (test_qwen3_asr_server.py:15-57).
+// QASR_PROTOCOL_TEST_FAKE=1 replaces model + VAD by the reference tests' fakes (test_qwen3_asr_server.py:15-57);
+// QASR_FORCE_TOKENS_PER_S=k fixes the decode length at round(k·seconds)+1 tokens (benchmarks: deterministic work
+// on synthetic weights, SURVEY §8(d) "decode length control").
 #include <dirent.h>
 #include <signal.h>
 #include <stdarg.h>
@@ -503,7 +505,9 @@ struct Server {
                 language = "Chinese";
             } else {
                 qasr_result res;
-                if (qasr_session_run(session, speech_audio.data(), speech_audio.size(), 0, &res) != QASR_OK)
+                static const int force_tps = getenv("QASR_FORCE_TOKENS_PER_S") ? atoi(getenv("QASR_FORCE_TOKENS_PER_S")) : 0;
+                const qasr_run_opts o{0, force_tps, 0};
+                if (qasr_session_run_opts(session, speech_audio.data(), speech_audio.size(), &o, &res) != QASR_OK)
                     throw std::runtime_error(qasr_last_error());
                 text = res.text ? res.text : "";
                 language = res.language ? res.language : "";
@@ -590,16 +594,12 @@ struct Server {
         logf("%s 服务器启动", engine.c_str());
         reply(initialize());
         std::string line;
+        char* lbuf = nullptr;   // POSIX getline: one buffered read per line (a 12 s window is a ~0.5 MB line)
+        size_t lcap = 0;
         while (g_running) {
-            line.clear();
-            int c;
-            bool got = false;
-            while ((c = fgetc(stdin)) != EOF) {
-                got = true;
-                if (c == '\n') break;
-                line += (char)c;
-            }
-            if (!got) break;
+            const ssize_t got = getline(&lbuf, &lcap, stdin);
+            if (got < 0) break;
+            line.assign(lbuf, (size_t)(got > 0 && lbuf[got - 1] == '\n' ? got - 1 : got));
             // str.strip()
             size_t b = 0, e = line.size();
             while (b < e && isspace((unsigned char)line[b])) b++;
@@ -660,6 +660,7 @@ struct Server {
             if (has_rid) result.set("request_id", rid);
             reply(result);
         }
+        free(lbuf);
         logf("%s 服务器退出", engine.c_str());
         close_runtime();
         return 0;

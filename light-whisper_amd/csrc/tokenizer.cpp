@@ -40,6 +40,49 @@ void append_utf8(std::string& s, int cp) {
 }
 }  // namespace
 
+// bytes → valid UTF-8 the way Python's bytes.decode("utf-8", errors="replace") does it (the Qwen2 byte-level BPE
+// tokenizer's decode, errors="replace"): each maximal ill-formed subpart becomes one U+FFFD
+std::string utf8_replace_invalid(const std::string& in) {
+    const unsigned char* s = (const unsigned char*)in.data();
+    const size_t n = in.size();
+    std::string out;
+    out.reserve(n);
+    size_t i = 0;
+    while (i < n) {
+        const unsigned c = s[i];
+        if (c < 0x80) {
+            out += (char)c;
+            i++;
+            continue;
+        }
+        int len = 0;
+        unsigned lo = 0x80, hi = 0xBF;   // allowed range of the second byte
+        if (c >= 0xC2 && c <= 0xDF) len = 2;
+        else if (c == 0xE0) len = 3, lo = 0xA0;
+        else if ((c >= 0xE1 && c <= 0xEC) || c == 0xEE || c == 0xEF) len = 3;
+        else if (c == 0xED) len = 3, hi = 0x9F;
+        else if (c == 0xF0) len = 4, lo = 0x90;
+        else if (c >= 0xF1 && c <= 0xF3) len = 4;
+        else if (c == 0xF4) len = 4, hi = 0x8F;
+        int ok = 1;   // bytes of the sequence accepted so far
+        if (len > 0) {
+            for (; ok < len && i + ok < n; ok++) {
+                const unsigned b = s[i + ok];
+                const bool good = ok == 1 ? (b >= lo && b <= hi) : (b >= 0x80 && b <= 0xBF);
+                if (!good) break;
+            }
+        }
+        if (len > 0 && ok == len) {
+            out.append((const char*)s + i, (size_t)len);
+            i += (size_t)len;
+        } else {
+            out += "\xEF\xBF\xBD";
+            i += (size_t)ok;
+        }
+    }
+    return out;
+}
+
 std::string Tokenizer::decode(const int32_t* ids, int n) const {
     const ByteMap& bm = bmap();
     std::string out;
@@ -67,7 +110,7 @@ std::string Tokenizer::decode(const int32_t* ids, int n) const {
             k += (size_t)len;
         }
     }
-    return out;
+    return utf8_replace_invalid(out);
 }
 
 void Tokenizer::parse(const std::string& raw, std::string& language, std::string& text) {

@@ -19,4 +19,6 @@ struct Tokenizer {
     void make_synthetic(int vocab, const int32_t* special_ids, const char* const* special_text, int n_special);
 };
 
+std::string utf8_replace_invalid(const std::string& in);
+
 }  // namespace qasr

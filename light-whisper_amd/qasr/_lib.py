@@ -96,6 +96,7 @@ SIGNATURES = {
     "qasr_vad_timestamps_from_probabilities": (C.c_int, [P, SZ, I64, C.POINTER(VadOptions), C.POINTER(Segment),
                                                          SZ, C.POINTER(SZ)]),
     "qasr_vad_close": (None, [P]),
+    "qasr_utf8_replace_invalid": (C.c_int, [C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)]),
     "qasr_decode_pcm_s16le": (C.c_int, [C.c_char_p, SZ, P, SZ, C.POINTER(SZ)]),
     "qasr_resample_linear": (C.c_int, [P, SZ, I32, P, SZ, C.POINTER(SZ)]),
     "qasr_op_quant_rows": (C.c_int, [P, I32, I32, I32, P, P, P]),

@@ -96,3 +96,18 @@ def test_base64_edge_cases():
     assert lib.qasr_decode_pcm_s16le(b"AAE", 3, None, 0, C.byref(n)) == 3           # Incorrect padding
     assert lib.qasr_decode_pcm_s16le(b"AAAA", 4, None, 0, C.byref(n)) == 1          # odd byte count (3 bytes)
     assert lib.qasr_decode_pcm_s16le(b"!!!!", 4, None, 0, C.byref(n)) == 3          # Non-base64 digit found
+
+
+def test_utf8_replace_matches_python():
+    """transcript bytes → UTF-8 exactly as bytes.decode("utf-8", "replace") (the Qwen2 tokenizer's decode)"""
+    lib = _lib.load()
+    rng = np.random.default_rng(3)
+    pool = [bytes([b]) for b in range(256)] + [c.encode() for c in "aé中😀ß€"] + [b"\xe4\xb8", b"\xf0\x9f\x98",
+                                                                               b"\xed\xa0\x80", b"\xc0\xaf"]
+    cases = [b"", b"plain ascii", "中文 text".encode(), b"\xff\xfe", b"\xe4\xb8\x41", b"\xf4\x90\x80\x80"]
+    cases += [b"".join(pool[i] for i in rng.integers(0, len(pool), int(rng.integers(1, 40)))) for _ in range(3000)]
+    buf = C.create_string_buffer(512)
+    n = C.c_size_t()
+    for b in cases:
+        _lib.check(lib.qasr_utf8_replace_invalid(b, len(b), buf, 512, C.byref(n)))
+        assert buf.raw[: n.value] == b.decode("utf-8", "replace").encode(), b
