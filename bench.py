@@ -123,6 +123,8 @@ def main():
     ap.add_argument("--segments", type=int, default=SEG_PER_RANK)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-prof", action="store_true")
+    ap.add_argument("--precision", default="q8", choices=["q8", "mxfp8"],
+                    help="mxfp8: SURVEY §8(d) C5 precision (block-scaled fp8 GEMMs; tolerance parity only)")
     args = ap.parse_args()
 
     SEG_PER_RANK = args.segments
@@ -169,6 +171,8 @@ def main():
         collectives["backend"] = backend
     else:
         model = Model.synthetic(args.arch, seed=0)
+    if args.precision != "q8":
+        model.set_precision(args.precision)
     sess = model.session(kv_type="f16", n_ctx=32768)
 
     def step(want=False):
@@ -228,8 +232,9 @@ def main():
         if prof:
             name, p = max(prof.items(), key=lambda kv: kv[1]["ms"])
             avg_s = p["ms"] / p["count"] / 1e3
-            if name in ("gemm_q8", "conv3x3_f16", "mel_frames"):
-                peak = 5000.0 if name == "gemm_q8" else 2500.0   # dense i8 / f16 MFMA (MI355X_MICROARCH.md)
+            if name in ("gemm_q8", "gemm_mx", "conv3x3_f16", "mel_frames"):
+                # dense i8 / MX-fp8 / f16 MFMA peaks (MI355X_MICROARCH.md)
+                peak = 5000.0 if name in ("gemm_q8", "gemm_mx") else 2500.0
                 ach = p["flops"] / p["count"] / avg_s / 1e12
                 roof = {"bound": "mfma", "kernel": name, "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
                         "frac": round(ach / peak, 4), "traffic": traffic_per_launch(name),
@@ -251,7 +256,8 @@ def main():
                 cpu = {"value": None, "error": str(e)}
         value = total_audio / elapsed
         line = {
-            "metric": "audio-sec/wall-sec (RTF⁻¹) Qwen3-ASR-1.7B Q8",
+            "metric": "audio-sec/wall-sec (RTF⁻¹) Qwen3-ASR-1.7B " + ("Q8" if args.precision == "q8" else
+                                                                     "MXFP8 (C5 precision)"),
             "value": round(value, 2),
             "unit": "audio-s/s",
             "n_gpus": world,
@@ -261,7 +267,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "i8",
+            "dtype": "i8" if args.precision == "q8" else "fp8e4m3+e8m0",
             "data": "synthetic (seeded speech-like 16 kHz audio; seeded synthetic Q8_0 weights with 1.7B shapes)",
             "config": {"workload": f"C4: {SEG_PER_RANK} VAD-split segments/rank, U[2,12] s, LPT-sharded, "
                                    f"{FORCE_TPS} forced tokens/audio-s",

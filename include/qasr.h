@@ -101,6 +101,10 @@ QASR_API int qasr_model_open_synthetic(const char* arch, const qasr_hparams* hp,
 QASR_API int qasr_model_open_shell(const char* gguf_path, const char* arch, const qasr_hparams* hp, qasr_model** out);
 QASR_API int qasr_model_weight_blob(qasr_model* m, void** dev, size_t* bytes);
 QASR_API int qasr_model_weights_received(qasr_model* m);
+/* Precision of the model's GEMMs: "q8" (default — the reference's Q8_0 W8A8 arithmetic) or "mxfp8" (SURVEY §8(d)
+   C5: the weights' OCP MXFP8 image — e4m3 + e8m0 per 32 — multiplied on the block-scaled fp8 matrix cores, the
+   activations converted per GEMM; tolerance parity only).  Set it before opening sessions. */
+QASR_API int qasr_model_set_precision(qasr_model* m, const char* mode);
 QASR_API int qasr_model_hparams(const qasr_model* m, qasr_hparams* out);
 QASR_API int64_t qasr_model_weight_bytes(const qasr_model* m);
 /* copy one tensor back to host in its GGUF storage form (Q8_0 blocks / f32 / f16) — for parity tests */
@@ -200,6 +204,15 @@ QASR_API int qasr_op_gemm_swiglu_q8_cfg(const int8_t* xq, const float* xd, int32
 /* Q8 GEMM with a fused output epilogue (M > 8, the MFMA path): epi 4 = erf-GELU(acc + bias) quantised to Q8 rows
    (yq [M][N] int8, yd [M][N/32] f32 block scales; y unused), epi 5 = f16(acc + bias) into y (__half, row stride
    ldy).  cfg: GEMM configuration (-1 = heuristic). */
+/* MXFP8 precision mode: Q8 blocks (q int8, d f32 or f16) → OCP MXFP8 (e4m3 elements q·d·2^-E
+   rounded to nearest even, e8m0 byte E+127 with E the smallest exponent putting the block maximum ≤ 448). */
+QASR_API int qasr_op_q8_to_mx(const int8_t* q, const void* d, int32_t d_is_f16, int64_t nblk, uint8_t* q8,
+                             uint8_t* s8, void* stream);
+/* y = epi(X·Wᵀ) on MXFP8 operands (v_mfma_scale_f32_16x16x128_f8f6f4); epi as qasr_op_linear_q8 (0-2), 3 SwiGLU
+   (yq/yd), 4 GELU+Q8 (yq/yd); cfg -1 auto, 0 128×128, 1 64×64, 2 64×128.  K % 128 == 0. */
+QASR_API int qasr_op_gemm_mx(const uint8_t* x8, const uint8_t* xs, int32_t M, const uint8_t* w8, const uint8_t* ws,
+                             int32_t N, int32_t K, const float* bias, const float* res, float* y, int32_t ldy,
+                             int32_t epi, int8_t* yq, float* yd, int32_t cfg, void* stream);
 QASR_API int qasr_op_linear_q8_ex(const int8_t* xq, const float* xd, int32_t M, const int8_t* wqs, const void* wsc,
                                   int32_t N, int32_t K, const float* bias, void* y, int32_t ldy, int32_t epi,
                                   int8_t* yq, float* yd, int32_t cfg, void* stream);

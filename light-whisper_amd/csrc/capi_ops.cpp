@@ -59,6 +59,32 @@ QASR_API int qasr_op_linear_q8(const int8_t* xq, const float* xd, int32_t M, con
     });
 }
 
+QASR_API int qasr_op_q8_to_mx(const int8_t* q, const void* d, int32_t d_is_f16, int64_t nblk, uint8_t* q8,
+                             uint8_t* s8, void* stream) {
+    return guard([&] {
+        QASR_CHECK(nblk >= 0, QASR_E_INVALID, "q8_to_mx: bad size");
+        if (d_is_f16) q8w_to_mx(q, (const __half*)d, nblk, q8, s8, S(stream));
+        else q8_to_mx(q, (const float*)d, nblk, q8, s8, S(stream));
+        launched();
+    });
+}
+
+QASR_API int qasr_op_gemm_mx(const uint8_t* x8, const uint8_t* xs, int32_t M, const uint8_t* w8, const uint8_t* ws,
+                             int32_t N, int32_t K, const float* bias, const float* res, float* y, int32_t ldy,
+                             int32_t epi, int8_t* yq, float* yd, int32_t cfg, void* stream) {
+    return guard([&] {
+        QASR_CHECK(K % 128 == 0 && N > 0 && M > 0 && ldy >= (epi == EPI_SWIGLU ? 0 : N) && epi >= 0 && epi <= 4,
+                   QASR_E_INVALID, "gemm_mx: bad shape / epilogue");
+        Q8Mat W;
+        W.N = N;
+        W.K = K;
+        W.mx = (uint8_t*)w8;
+        W.mxs = (uint8_t*)ws;
+        gemm_mx(x8, xs, M, W, bias, res, y, ldy, epi, S(stream), yq, yd, false, cfg);
+        launched();
+    });
+}
+
 QASR_API int qasr_op_linear_q8_ex(const int8_t* xq, const float* xd, int32_t M, const int8_t* wqs, const void* wsc,
                                   int32_t N, int32_t K, const float* bias, void* y, int32_t ldy, int32_t epi,
                                   int8_t* yq, float* yd, int32_t cfg, void* stream) {

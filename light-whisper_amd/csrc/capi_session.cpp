@@ -140,6 +140,13 @@ QASR_API int qasr_model_weights_received(qasr_model* m) {
     });
 }
 
+QASR_API int qasr_model_set_precision(qasr_model* m, const char* mode) {
+    return guard([&] {
+        QASR_CHECK(m && mode, QASR_E_INVALID, "null argument");
+        set_precision(*m->m, mode);
+    });
+}
+
 QASR_API int qasr_model_hparams(const qasr_model* m, qasr_hparams* out) {
     return guard([&] {
         QASR_CHECK(m && out, QASR_E_INVALID, "null argument");

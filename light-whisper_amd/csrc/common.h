@@ -42,6 +42,9 @@ struct Q8Mat {
     int8_t* qs = nullptr;
     __half* sc = nullptr;
     int N = 0, K = 0;
+    // MXFP8 image of the same rows (precision mode "mxfp8"): e4m3 [N][K] + e8m0 [N][K/32]
+    uint8_t* mx = nullptr;
+    uint8_t* mxs = nullptr;
 };
 
 // Quantised activations X[M][K]: int8 values + per-32-block f16-rounded scale stored as f32.

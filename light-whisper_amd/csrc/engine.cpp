@@ -18,7 +18,7 @@ namespace {
 enum SlotId {
     S_UTTS, S_WORK, S_CHUNK_UTT, S_UMAX, S_LM, S_MELX, S_A1, S_A2, S_A3, S_XQ, S_XD, S_PROJ, S_VALID, S_HS,
     S_QKV, S_QKVH, S_FF, S_KVS, S_KVL, S_EMB, S_IDS, S_POS, S_SLOT, S_X, S_QH, S_GU, S_LAST, S_XN, S_LOGITS,
-    S_TOK, S_PCM, S_ENC, S_DSTATE, S_DOUT, S_DTAB, S_ARGP, S_HQ, S_HD, S_COUNT
+    S_TOK, S_PCM, S_ENC, S_DSTATE, S_DOUT, S_DTAB, S_ARGP, S_HQ, S_HD, S_MX, S_COUNT
 };
 
 inline int post_cnn_len(int l) {
@@ -224,6 +224,7 @@ void Session::front_end(const float* dpcm, const std::vector<int64_t>& off, cons
     float* xd = (float*)sc_.get(S_XD, (size_t)rows * (K / QK) * sizeof(float));
     quant_rows(a3, rows, K, K, xq, xd, st_);
     float* proj = (float*)sc_.get(S_PROJ, (size_t)rows * d * sizeof(float));
+    mx_ws(rows, K);
     linear_q8(xq, xd, rows, m_->conv_out, nullptr, nullptr, proj, d, EPI_STORE, st_);
     int* d_valid = upload(S_VALID, valid_idx);
     float* hs = (float*)sc_.get(S_HS, (size_t)fe.total_tokens * d * sizeof(float));
@@ -263,6 +264,7 @@ void Session::encoder(FrontEnd& fe, float* enc_out_dbg) {
     // MFMA-GEMM row counts (> kGemvRows) take the fused epilogues: QKV written as f16 for the attention,
     // up-projection GELU quantised to the down-projection's Q8 rows in place; GEMV row counts keep separate passes
     const bool fused = N > kGemvRows;
+    mx_ws(N, std::max(F, d));
     int8_t* hq = fused ? (int8_t*)sc_.get(S_HQ, (size_t)N * std::max(F, d)) : nullptr;
     float* hdq = fused ? (float*)sc_.get(S_HD, (size_t)N * (std::max(F, d) / QK) * sizeof(float)) : nullptr;
     for (int l = 0; l < h.enc_layers; l++) {
@@ -313,6 +315,7 @@ void Session::decoder_layers(float* x, int rows, const int* d_pos, const int* d_
     float* qkv = (float*)sc_.get(S_QKV, (size_t)rows * (QD + 2 * KD) * sizeof(float));
     __half* qh = (__half*)sc_.get(S_QH, (size_t)rows * QD * sizeof(__half));
     const bool fused = rows > kGemvRows;
+    mx_ws(rows, kmax);
     float* gu = fused ? nullptr : (float*)sc_.get(S_GU, (size_t)rows * 2 * F * sizeof(float));
     // the fused gate-up epilogue writes the SwiGLU rows into a second Q8 buffer (its input xq is still being read)
     int8_t* hq = fused ? (int8_t*)sc_.get(S_HQ, (size_t)rows * F) : nullptr;
@@ -356,11 +359,19 @@ void Session::decoder_layers(float* x, int rows, const int* d_pos, const int* d_
     QASR_HIP(hipGetLastError());
 }
 
+// MXFP8 precision mode: the activations' fp8 image for GEMMs of up to rows × kmax (thread-local registration)
+void Session::mx_ws(int64_t rows, int64_t kmax) {
+    if (!m_->mx()) return;
+    const size_t bytes = mx_workspace_bytes(rows, kmax);
+    set_mx_workspace(sc_.get(S_MX, bytes), bytes);
+}
+
 void Session::lm_head_rows(const float* x, int rows, int ldx, float* logits) {
     const qasr_hparams& h = m_->hp;
     int8_t* xq = (int8_t*)sc_.get(S_XQ, (size_t)std::max(rows, 1) * std::max(h.txt_h, std::max(h.txt_ffn, h.txt_heads * h.head_dim)));
     float* xd = (float*)sc_.get(S_XD, (size_t)std::max(rows, 1) * (std::max(h.txt_h, std::max(h.txt_ffn, h.txt_heads * h.head_dim)) / QK) * sizeof(float));
     rmsnorm_q8(x, rows, h.txt_h, ldx, m_->out_norm, h.rms_eps, xq, xd, st_);
+    mx_ws(rows, h.txt_h);
     linear_q8(xq, xd, rows, m_->lm_head, nullptr, nullptr, logits, h.vocab, EPI_STORE, st_);
 }
 
@@ -673,6 +684,7 @@ void Session::encode_host(const float* mel, int t_pad, int t_valid, std::vector<
     float* xd = (float*)sc_.get(S_XD, (size_t)rows * (K / QK) * sizeof(float));
     quant_rows(a3, rows, K, K, xq, xd, st_);
     float* proj = (float*)sc_.get(S_PROJ, (size_t)rows * d * sizeof(float));
+    mx_ws(rows, K);
     linear_q8(xq, xd, rows, m_->conv_out, nullptr, nullptr, proj, d, EPI_STORE, st_);
     int* d_valid = upload(S_VALID, valid_idx);
     float* hs = (float*)sc_.get(S_HS, (size_t)fe.total_tokens * d * sizeof(float));

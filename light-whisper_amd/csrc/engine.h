@@ -75,6 +75,7 @@ class Session {
     void ensure_kv(int64_t slots);
     void decode_step(const DecState& ds, int B, bool sizing);
     void lm_head_rows(const float* x, int rows, int ldx, float* logits);
+    void mx_ws(int64_t rows, int64_t kmax);
     template <class T>
     T* upload(int slot, const std::vector<T>& v);
 

@@ -38,6 +38,16 @@ void gemm_q8(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const flo
 // the Q8 GEMM on f16-carried int8 operands (x [M][K], w [N][K] f16 holding the Q8 integers; scales as gemm_q8)
 void gemm_q8h(const __half* xq, const float* xd, int M, const __half* wq, const __half* wsc, int N, int K,
               const float* bias, const float* res, float* y, int ldy, int epi, int cfg, hipStream_t s);
+// MXFP8 precision mode (C5): Q8 blocks → e4m3 elements + e8m0 block exponents (activations f32 d, weights f16 d);
+// the block-scaled fp8 GEMM (same epilogues as gemm_q8, K % 128 == 0); gemm_q8 routes to it when W.mx is set,
+// converting the Q8 activations into the workspace registered by set_mx_workspace
+void q8_to_mx(const int8_t* q, const float* d, int64_t nblk, uint8_t* q8, uint8_t* s8, hipStream_t s);
+void q8w_to_mx(const int8_t* q, const __half* d, int64_t nblk, uint8_t* q8, uint8_t* s8, hipStream_t s);
+void gemm_mx(const uint8_t* x8, const uint8_t* xs, int M, const Q8Mat& W, const float* bias, const float* res,
+             float* y, int ldy, int epi, hipStream_t s, int8_t* yq = nullptr, float* yd = nullptr,
+             bool y_zeroed = false, int force_cfg = -1);
+void set_mx_workspace(void* p, size_t bytes);
+size_t mx_workspace_bytes(int64_t M, int64_t K);
 // rows of a [2F][K] gate|up matrix → interleaved by 16 (32j+t: t<16 gate 16j+t, else up 16j+t-16)
 int64_t gate_up_interleaved_row(int64_t r, int64_t F);
 void interleave_gate_up(Q8Mat& W, hipStream_t s);

@@ -1002,10 +1002,249 @@ static void launch_cfg(int cfg, dim3 grid, hipStream_t s, const int8_t* xq, cons
     }
 }
 
+// ------------------------------------------------------------------------------------------------ MXFP8 (C5)
+// The fp8 precision mode (tolerance parity only): operands as OCP MXFP8 — e4m3 elements with one
+// e8m0 (power-of-two) scale per 32-element block — multiplied by v_mfma_scale_f32_16x16x128_f8f6f4, which applies
+// the block scales inside the matrix core: no per-block VALU rescale, K = 128 per instruction at twice the bf16
+// rate.  Operand layout of that instruction (pinned by tools/micro/mx_check.hip / mx_probe.hip): lane l holds
+// row (or column) l&15, bytes 0-15 = k 16(l>>4)+j, bytes 16-31 = k 64+16(l>>4)+j; its scale byte is that of
+// K-block l>>4 (k 32b..32b+31), not of its own bytes.
+
+// e8m0 exponent E of a block: the smallest E with amax·2^-E ≤ 448 (the e4m3 maximum), clamped to [-127, 127]
+__device__ __forceinline__ int mx_block_exp(float amax) {
+    if (!(amax > 0.f)) return -127;
+    int e;
+    const float m = frexpf(amax, &e);   // amax = m·2^e, m ∈ [0.5, 1); 448 = 0.875·2^9
+    return max(-127, min(127, m <= 0.875f ? e - 9 : e - 8));
+}
+
+// e4m3 (OCP, no inf, 0x7f = NaN never produced) of |v| ≤ 448, round to nearest even; subnormals below 2^-6
+__device__ __forceinline__ uint32_t e4m3_rne(float v) {
+    const uint32_t sg = v < 0.f ? 0x80u : 0u;
+    const float a = fabsf(v);
+    if (a < 0.015625f) return sg | (uint32_t)__builtin_rintf(a * 512.f);   // 0..8 (8 = 2^-6, the same bits)
+    int x;
+    frexpf(a, &x);
+    int e = x - 1;                                                      // a ∈ [2^e, 2^(e+1))
+    int m = (int)__builtin_rintf(ldexpf(a, 3 - e));                     // 8..16
+    if (m == 16) e++, m = 8;
+    return sg | (uint32_t)((e + 7) << 3) | (uint32_t)(m - 8);
+}
+
+// Q8 blocks (int8 q + scale d) → MXFP8 (e4m3 q·d·2^-E, e8m0 E+127): one thread per 32-block
+template <typename SC>
+__global__ __launch_bounds__(256) void k_q8_to_mx(const int8_t* __restrict__ q, const SC* __restrict__ d, int64_t nblk,
+                                                  uint8_t* __restrict__ q8, uint8_t* __restrict__ s8) {
+    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= nblk) return;
+    const int4 w0 = *(const int4*)(q + b * 32), w1 = *(const int4*)(q + b * 32 + 16);
+    const int8_t* v = (const int8_t*)&w0;
+    const int8_t* u = (const int8_t*)&w1;
+    const float dd = (float)d[b];
+    int mq = 0;
+#pragma unroll
+    for (int j = 0; j < 16; j++) mq = max(mq, max(abs((int)v[j]), abs((int)u[j])));
+    const int E = mx_block_exp(fabsf(dd) * (float)mq);
+    const float sc = mq == 0 ? 0.f : ldexpf(dd, -E);   // exact power-of-two rescale of d (empty block: 0)
+    uint32_t o[8];
+#pragma unroll
+    for (int w = 0; w < 8; w++) {
+        uint32_t r = 0;
+#pragma unroll
+        for (int t = 0; t < 4; t++) {
+            const int j = 4 * w + t;
+            const float x = (float)(j < 16 ? v[j] : u[j - 16]) * sc;   // q·d·2^-E: 18 significant bits, exact
+            r |= e4m3_rne(x) << (8 * t);
+        }
+        o[w] = r;
+    }
+    *(int4*)(q8 + b * 32) = make_int4((int)o[0], (int)o[1], (int)o[2], (int)o[3]);
+    *(int4*)(q8 + b * 32 + 16) = make_int4((int)o[4], (int)o[5], (int)o[6], (int)o[7]);
+    s8[b] = (uint8_t)(E + 127);
+}
+
+void q8_to_mx(const int8_t* q, const float* d, int64_t nblk, uint8_t* q8, uint8_t* s8, hipStream_t s) {
+    if (nblk > 0) k_q8_to_mx<float><<<(unsigned)cdiv64(nblk, 256), 256, 0, s>>>(q, d, nblk, q8, s8);
+}
+void q8w_to_mx(const int8_t* q, const __half* d, int64_t nblk, uint8_t* q8, uint8_t* s8, hipStream_t s) {
+    if (nblk > 0) k_q8_to_mx<__half><<<(unsigned)cdiv64(nblk, 256), 256, 0, s>>>(q, d, nblk, q8, s8);
+}
+
+typedef int v8i __attribute__((ext_vector_type(8)));
+typedef float v4f __attribute__((ext_vector_type(4)));
+
+// MXFP8 GEMM y = epi(X·Wᵀ): 2×2 waves of (16·TI)×(16·TJ), K stages of 128 (one MFMA deep) staged global → LDS by
+// DMA in an NBUF ring (the k_gemm_q8d pipeline: counted vmcnt, one barrier per stage, 128-B rows with chunk
+// c ^ ((r >> 1) & 7)); the stage's block scales are one dword per row (4 e8m0 bytes), lane l picks byte l>>4.
+template <int TI, int TJ, int NBUF>
+__global__ __launch_bounds__(256, NBUF <= 2 ? 2 : 1) void k_gemm_mx(const uint8_t* __restrict__ X,
+                                                             const uint8_t* __restrict__ Xs, int M,
+                                                             const uint8_t* __restrict__ W,
+                                                             const uint8_t* __restrict__ Ws, int N, int K,
+                                                             const float* __restrict__ bias, const float* res,
+                                                             float* y, int ldy, int epi, int steps_per_split,
+                                                             int8_t* __restrict__ yq, float* __restrict__ yd) {
+    constexpr int BK = 128, NW = 4, RP = 8;
+    constexpr int BM = 32 * TI, BN = 32 * TJ;
+    constexpr int OB = BM * BK, OSA = OB + BN * BK, OSB = OSA + BM * 4, STAGE = OSB + BN * 4;
+    constexpr int AI = BM / RP / NW, BI = BN / RP / NW;
+    static_assert(AI * RP * NW == BM && BI * RP * NW == BN, "k_gemm_mx: pieces per wave");
+    constexpr int SAW = BM / NW, SBW = BN / NW;   // scale dwords per wave per stage (≤ 64)
+    constexpr int NPW = AI + BI + 2;
+    constexpr int D = NBUF - 1;
+    __shared__ __attribute__((aligned(1024))) char smem[NBUF * STAGE];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wr = wave >> 1, wc = wave & 1;
+    const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM;
+    const int kq = K / BK;   // scale dwords per row
+    const int k_begin = blockIdx.z * steps_per_split * BK;
+    const int k_end = min(K, k_begin + steps_per_split * BK);
+    const int nsteps = max(0, (k_end - k_begin) / BK);
+    auto swz = [](int r) { return (r >> 1) & 7; };
+
+    const uint8_t* a_src[AI];
+    const uint8_t* b_src[BI];
+#pragma unroll
+    for (int u = 0; u < AI; u++) {
+        const int row = RP * (wave * AI + u) + lane / 8, c = (lane % 8) ^ swz(row);
+        a_src[u] = X + (size_t)min(m0 + row, M - 1) * K + 16 * c;
+    }
+#pragma unroll
+    for (int u = 0; u < BI; u++) {
+        const int row = RP * (wave * BI + u) + lane / 8, c = (lane % 8) ^ swz(row);
+        b_src[u] = W + (size_t)min(n0 + row, N - 1) * K + 16 * c;
+    }
+    const uint32_t* sa_src = (const uint32_t*)Xs + (size_t)min(m0 + wave * SAW + min(lane, SAW - 1), M - 1) * kq;
+    const uint32_t* sb_src = (const uint32_t*)Ws + (size_t)min(n0 + wave * SBW + min(lane, SBW - 1), N - 1) * kq;
+    const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
+    const uint32_t wa = __builtin_amdgcn_readfirstlane(lds0 + 1024 * (wave * AI));
+    const uint32_t wb = __builtin_amdgcn_readfirstlane(lds0 + OB + 1024 * (wave * BI));
+    const uint32_t wsa = __builtin_amdgcn_readfirstlane(lds0 + OSA + wave * SAW * 4);
+    const uint32_t wsb = __builtin_amdgcn_readfirstlane(lds0 + OSB + wave * SBW * 4);
+    auto issue = [&](int s, int buf) {
+        const int k0 = k_begin + s * BK;
+        const uint32_t so = buf * STAGE;
+#pragma unroll
+        for (int u = 0; u < AI; u++) dma_lds16(a_src[u] + k0, wa + so + 1024 * u);
+#pragma unroll
+        for (int u = 0; u < BI; u++) dma_lds16(b_src[u] + k0, wb + so + 1024 * u);
+        if (lane < SAW) dma_lds4(sa_src + k0 / BK, wsa + so);
+        if (lane < SBW) dma_lds4(sb_src + k0 / BK, wsb + so);
+    };
+
+    const int fr = lane & 15, kh = lane >> 4, fq = 4 * kh;
+    const int arow = wr * 16 * TI, bcol = wc * 16 * TJ;
+    const bool active = m0 + arow < M;
+    const int flo = 16 * (kh ^ swz(fr)), fhi = 16 * ((4 + kh) ^ swz(fr));
+    v4f acc[TI][TJ];
+#pragma unroll
+    for (int i = 0; i < TI; i++)
+#pragma unroll
+        for (int j = 0; j < TJ; j++) acc[i][j] = (v4f){0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+    for (int t = 0; t < D; t++)
+        if (t < nsteps) issue(t, t);
+    for (int s = 0; s < nsteps; s++) {
+        wait_stages<NPW, D>(min(D - 1, nsteps - 1 - s));
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (s + D < nsteps) issue(s + D, (s + D) % NBUF);
+        if (!active) continue;
+        const char* st = smem + (s % NBUF) * STAGE;
+        v8i a[TI], b[TJ];
+        int sa[TI], sb[TJ];
+#pragma unroll
+        for (int i = 0; i < TI; i++) {
+            const char* r = st + (arow + 16 * i + fr) * BK;
+            const int4 lo = *(const int4*)(r + flo), hi = *(const int4*)(r + fhi);
+            a[i] = (v8i){lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+            sa[i] = (int)((*(const uint32_t*)(st + OSA + 4 * (arow + 16 * i + fr)) >> (8 * kh)) & 0xffu);
+        }
+#pragma unroll
+        for (int j = 0; j < TJ; j++) {
+            const char* r = st + OB + (bcol + 16 * j + fr) * BK;
+            const int4 lo = *(const int4*)(r + flo), hi = *(const int4*)(r + fhi);
+            b[j] = (v8i){lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+            sb[j] = (int)((*(const uint32_t*)(st + OSB + 4 * (bcol + 16 * j + fr)) >> (8 * kh)) & 0xffu);
+        }
+#pragma unroll
+        for (int i = 0; i < TI; i++)
+#pragma unroll
+            for (int j = 0; j < TJ; j++)
+                acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a[i], b[j], acc[i][j], 0, 0, 0, sa[i], 0,
+                                                                           sb[j]);
+    }
+    if (!active) return;
+    float out[TI][TJ][4];
+#pragma unroll
+    for (int i = 0; i < TI; i++)
+#pragma unroll
+        for (int j = 0; j < TJ; j++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) out[i][j][r] = acc[i][j][r];
+    gemm_epilogue<TI, TJ>(out, M, N, m0, n0, arow, bcol, fr, fq, bias, res, y, ldy, epi, yq, yd);
+}
+
+// workspace for the activations' MXFP8 image (set by the session before its GEMMs; sized for its largest M·K)
+static thread_local uint8_t* g_mx_ws = nullptr;
+static thread_local size_t g_mx_ws_bytes = 0;
+void set_mx_workspace(void* p, size_t bytes) {
+    g_mx_ws = (uint8_t*)p;
+    g_mx_ws_bytes = bytes;
+}
+size_t mx_workspace_bytes(int64_t M, int64_t K) { return (size_t)(M * K + M * (K / QK) + 256); }
+
+void gemm_mx(const uint8_t* x8, const uint8_t* xs, int M, const Q8Mat& W, const float* bias, const float* res,
+             float* y, int ldy, int epi, hipStream_t s, int8_t* yq, float* yd, bool y_zeroed, int force_cfg) {
+    ProfScope ps(s, "gemm_mx", 2.0 * M * W.N * W.K, (double)W.N * W.K * (1 + 1.0 / 32) + (double)M * W.K * (1 + 1.0 / 32));
+    QASR_CHECK(W.mx && W.K % 128 == 0, QASR_E_INVALID, "gemm_mx: needs the MXFP8 weights and K % 128 == 0");
+    // measured (tools/gemm_mx_tune.py): 128×128 tiles for prefill-sized M and the batched vocabulary projection,
+    // 64×128 for the vocabulary projection of fewer rows, 64×64 (+ split-K) for the other decode GEMMs;
+    // SwiGLU needs 64-column wave tiles
+    int cfg = force_cfg;
+    if (cfg < 0) cfg = M > 256 ? 0 : W.N >= 32768 ? (M > 128 ? 0 : 2) : 1;
+    if (epi == EPI_SWIGLU && cfg == 1) cfg = 2;
+    const int bm = cfg == 0 ? 128 : cfg == 1 ? 64 : 64, bn = cfg == 0 ? 128 : cfg == 1 ? 64 : 128;
+    const int steps = W.K / 128, tiles = cdiv(W.N, bn) * cdiv(M, bm);
+    const bool can_split = (epi == EPI_STORE || epi == EPI_RESID) && ldy == W.N && (epi != EPI_RESID || res == y);
+    int splits = 1;
+    if (tiles < 256 && can_split) splits = std::max(1, std::min(std::min(cdiv(512, tiles), steps / 2), 8));
+    const int sps = cdiv(steps, splits);
+    splits = cdiv(steps, sps);
+    if (splits > 1 && epi == EPI_STORE && !y_zeroed) QASR_HIP(hipMemsetAsync(y, 0, (size_t)M * ldy * sizeof(float), s));
+    if (epi == EPI_SWIGLU) QASR_CHECK(W.N % 64 == 0 && yq && yd, QASR_E_INVALID, "gemm_mx: SwiGLU epilogue shape");
+    if (epi == EPI_GELU_Q8) QASR_CHECK(W.N % 32 == 0 && yq && yd, QASR_E_INVALID, "gemm_mx: GELU+Q8 epilogue shape");
+    const dim3 grid(cdiv(W.N, bn), cdiv(M, bm), splits);
+    if (cfg == 0)
+        k_gemm_mx<4, 4, 2><<<grid, 256, 0, s>>>(x8, xs, M, W.mx, W.mxs, W.N, W.K, bias, res, y, ldy, epi, sps, yq, yd);
+    else if (cfg == 1)
+        k_gemm_mx<2, 2, 3><<<grid, 256, 0, s>>>(x8, xs, M, W.mx, W.mxs, W.N, W.K, bias, res, y, ldy, epi, sps, yq, yd);
+    else
+        k_gemm_mx<2, 4, 3><<<grid, 256, 0, s>>>(x8, xs, M, W.mx, W.mxs, W.N, W.K, bias, res, y, ldy, epi, sps, yq, yd);
+}
+
+// Q8 activations in, MXFP8 GEMM: the activations' MXFP8 image goes to the session workspace first
+static void gemm_mx_q8in(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const float* bias,
+                         const float* res, float* y, int ldy, int epi, hipStream_t s, int8_t* yq, float* yd,
+                         bool y_zeroed) {
+    const size_t need = mx_workspace_bytes(M, W.K);
+    QASR_CHECK(g_mx_ws && g_mx_ws_bytes >= need, QASR_E_INVALID, "gemm_mx: MXFP8 activation workspace too small");
+    uint8_t* x8 = g_mx_ws;
+    uint8_t* xs = g_mx_ws + (size_t)M * W.K;
+    q8_to_mx(xq, xd, (int64_t)M * (W.K / QK), x8, xs, s);
+    gemm_mx(x8, xs, M, W, bias, res, y, ldy, epi, s, yq, yd, y_zeroed, -1);
+}
+
 // force_cfg: -1 auto, else an index into kGemmCfgs (a DMA config on K % 64 != 0 falls back to auto);
 // force_splits: split-K (0 = heuristic).
 void gemm_q8(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const float* bias, const float* res, float* y,
              int ldy, int epi, hipStream_t s, int force_cfg, int force_splits, int8_t* yq, float* yd, bool y_zeroed) {
+    if (W.mx && force_cfg < 0 && W.K % 128 == 0) {   // the model runs in MXFP8 precision mode
+        gemm_mx_q8in(xq, xd, M, W, bias, res, y, ldy, epi, s, yq, yd, y_zeroed);
+        return;
+    }
     ProfScope ps(s, "gemm_q8", 2.0 * M * W.N * W.K, q8_bytes(M, W, epi));
     auto usable = [&](int c) { return !kGemmCfgs[c].dma || W.K % kGemmCfgs[c].bk == 0; };
     int pick;

@@ -479,6 +479,46 @@ std::unique_ptr<Model> load_gguf_model(const std::string& path, bool shell) {
     return mp;
 }
 
+// ----------------------------------------------------------------------------------------------- precision
+namespace {
+template <typename F>
+void for_each_gemm_weight(Model& m, F f) {
+    f(m.conv_out);
+    for (auto& e : m.enc) f(e.qkv), f(e.o), f(e.up), f(e.down);
+    f(m.proj1);
+    f(m.proj2);
+    for (auto& L : m.dec) f(L.qkv), f(L.o), f(L.gu), f(L.down);
+    f(m.lm_head);   // tied: a copy of tok_embd's pointers; the embedding lookup keeps reading the Q8 rows
+}
+}  // namespace
+
+void set_precision(Model& m, const std::string& mode) {
+    QASR_CHECK(mode == "q8" || mode == "mxfp8", QASR_E_INVALID, "precision must be \"q8\" or \"mxfp8\"");
+    QASR_CHECK(!m.weights_pending, QASR_E_INVALID, "set_precision: the model's weights have not arrived");
+    if (mode == "q8") {
+        for_each_gemm_weight(m, [](Q8Mat& w) { w.mx = nullptr, w.mxs = nullptr; });
+        m.mx_mem.reset();
+        return;
+    }
+    if (m.mx()) return;
+    auto mem = std::make_unique<DevAlloc>();
+    DevAlloc probe;
+    probe.counting = true;
+    for_each_gemm_weight(m, [&](Q8Mat& w) {
+        if (w.K % 128 == 0) probe.alloc((size_t)w.N * w.K), probe.alloc((size_t)w.N * (w.K / QK));
+    });
+    mem->reserve(probe.bytes);
+    hipStream_t s = nullptr;
+    for_each_gemm_weight(m, [&](Q8Mat& w) {
+        if (w.K % 128 != 0) return;   // stays on the Q8 GEMM
+        w.mx = (uint8_t*)mem->alloc((size_t)w.N * w.K);
+        w.mxs = (uint8_t*)mem->alloc((size_t)w.N * (w.K / QK));
+        q8w_to_mx(w.qs, w.sc, (int64_t)w.N * (w.K / QK), w.mx, w.mxs, s);
+    });
+    QASR_HIP(hipStreamSynchronize(s));
+    m.mx_mem = std::move(mem);
+}
+
 // ----------------------------------------------------------------------------------------------- export
 void export_tensor(const Model& m, const std::string& name, void* dst, size_t cap, size_t* written) {
     auto it = m.slots.find(name);

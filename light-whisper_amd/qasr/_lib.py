@@ -72,6 +72,7 @@ SIGNATURES = {
     "qasr_model_open_shell": (C.c_int, [C.c_char_p, C.c_char_p, C.POINTER(HParams), C.POINTER(P)]),
     "qasr_model_weight_blob": (C.c_int, [P, C.POINTER(P), C.POINTER(C.c_size_t)]),
     "qasr_model_weights_received": (C.c_int, [P]),
+    "qasr_model_set_precision": (C.c_int, [P, C.c_char_p]),
     "qasr_model_tensor_table": (C.c_int, [P, C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)]),
     "qasr_model_export_tensor": (C.c_int, [P, C.c_char_p, P, SZ, C.POINTER(SZ)]),
     "qasr_model_close": (None, [P]),
@@ -110,6 +111,8 @@ SIGNATURES = {
     "qasr_op_gemm_swiglu_q8_cfg": (C.c_int, [P, P, I32, P, P, I32, I32, P, P, I32, P]),
     "qasr_op_swiglu_q8_interleaved": (C.c_int, [P, I32, I32, P, P, P]),
     "qasr_op_qk_norm_rope": (C.c_int, [P, I32, I32, I32, I32, P, P, P, P, P, F32, P, P, P, P]),
+    "qasr_op_q8_to_mx": (C.c_int, [P, P, I32, C.c_int64, P, P, P]),
+    "qasr_op_gemm_mx": (C.c_int, [P, P, I32, P, P, I32, I32, P, P, P, I32, I32, P, P, I32, P]),
     "qasr_op_linear_q8_ex": (C.c_int, [P, P, I32, P, P, I32, I32, P, P, I32, I32, P, P, I32, P]),
     "qasr_op_linear_q8h": (C.c_int, [P, P, I32, P, P, I32, I32, P, P, P, I32, I32, I32, P]),
     "qasr_op_attention_decode_fused": (C.c_int, [P, I32, I32, I32, I32, P, P, P, P, P, F32, P, P, P, P, F32, P, P,

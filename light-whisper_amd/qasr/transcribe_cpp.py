@@ -100,6 +100,10 @@ class Model:
         check(lib.qasr_model_tensor_table(self._h, buf, need.value, C.byref(need)))
         return {k: tuple(v) for k, v in json.loads(buf.value.decode()).items()}
 
+    def set_precision(self, mode: str):
+        """"q8" (the reference's arithmetic) or "mxfp8" (block-scaled fp8 GEMMs)"""
+        check(_lib.load().qasr_model_set_precision(self._h, mode.encode()))
+
     def weights_received(self):
         check(_lib.load().qasr_model_weights_received(self._h))
 

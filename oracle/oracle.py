@@ -356,3 +356,57 @@ class KV:
                                eos.size, int(max_new), int(force_len), _p(out), None if lg is None else _p(lg))
         assert n >= 0
         return (out[:n].copy(), lg[:n].copy()) if want_logits else out[:n].copy()
+
+
+# ---------------------------------------------------------------------------------------------------- MXFP8 (C5)
+# The fp8 precision mode has no counterpart in the reference ("tolerance parity only"); these
+# restate the OCP Microscaling v1.0 formats it uses — e4m3 elements (bias 7, no infinities, max 448) and e8m0
+# block exponents — with the engine's choices: E = the smallest exponent putting the block maximum ≤ 448,
+# round-to-nearest-even elements.
+
+def mx_block_exp(amax: np.ndarray) -> np.ndarray:
+    amax = np.asarray(amax, np.float32)
+    m, e = np.frexp(amax)
+    E = np.where(m <= 0.875, e - 9, e - 8)
+    return np.clip(np.where(amax > 0, E, -127), -127, 127).astype(np.int32)
+
+
+def e4m3_rne(x: np.ndarray) -> np.ndarray:
+    """float32 values with |x| ≤ 448 → e4m3 codes (uint8), round to nearest even"""
+    x = np.asarray(x, np.float32)
+    a = np.abs(x).astype(np.float64)
+    sg = np.where(x < 0, 0x80, 0).astype(np.int64)
+    sub = np.rint(a * 512.0).astype(np.int64)
+    _, ex = np.frexp(a)
+    e = ex.astype(np.int64) - 1
+    m = np.rint(np.ldexp(a, (3 - e).astype(np.int32))).astype(np.int64)
+    carry = m == 16
+    e = e + carry
+    m = np.where(carry, 8, m)
+    normal = ((e + 7) << 3) | (m - 8)
+    return (sg | np.where(a < 2.0 ** -6, sub, normal)).astype(np.uint8)
+
+
+def e4m3_value(code: np.ndarray) -> np.ndarray:
+    c = np.asarray(code, np.int64)
+    s = np.where(c & 0x80, -1.0, 1.0)
+    e = (c >> 3) & 15
+    m = c & 7
+    return s * np.where(e == 0, m * 2.0 ** -9, (1 + m / 8.0) * np.ldexp(1.0, (e - 7).astype(np.int32)))
+
+
+def q8_to_mx(q: np.ndarray, d: np.ndarray):
+    """Q8 blocks q [nblk, 32] int8, d [nblk] (f32 or f16 values) → (codes [nblk, 32] uint8, E [nblk] int32)"""
+    q = np.asarray(q, np.int8).reshape(-1, 32)
+    d = np.asarray(d, np.float32).reshape(-1)
+    mq = np.abs(q.astype(np.int32)).max(axis=1).astype(np.float32)
+    E = mx_block_exp(np.abs(d) * mq)
+    with np.errstate(over="ignore"):
+        sc = np.where(mq == 0, 0.0, np.ldexp(d, -E)).astype(np.float32)
+    return e4m3_rne(q.astype(np.float32) * sc[:, None]), E
+
+
+def mx_matrix(codes: np.ndarray, E: np.ndarray, rows: int, k: int) -> np.ndarray:
+    """the real values an MXFP8 matrix stands for, float64 [rows][k]"""
+    v = e4m3_value(codes).reshape(rows, k // 32, 32) * np.ldexp(1.0, E.reshape(rows, k // 32, 1))
+    return v.reshape(rows, k)

@@ -258,3 +258,35 @@ def test_gguf_round_trip(gpu, golden, torch_dev, tmp_path, untied):
             sh.close()
     finally:
         g.close()
+
+
+def test_mxfp8_precision_mode(golden, torch_dev):
+    """C5 precision mode (tolerance parity only): the same seeded model with its GEMMs on MXFP8 block-scaled fp8
+    matrix cores stays close to the Q8 path — prefill logits within 10 % of their range, the top token kept on
+    clear margins — and switching back to "q8" restores the Q8 logits bit for bit."""
+    from qasr.transcribe_cpp import Model
+
+    m = Model.synthetic(arch=None, seed=TINY_SEED, hparams=tiny_hparams())
+    try:
+        audio = golden["a__audio"]
+        forced = np.array([11, 12, 13, 14], np.int32)
+        s = m.session(kv_type="f16", n_ctx=2048)
+        ref = s.forced_logits(audio, forced)
+        s.close()
+        m.set_precision("mxfp8")
+        s = m.session(kv_type="f16", n_ctx=2048)
+        got = s.forced_logits(audio, forced)
+        toks = s.run(audio, max_new_tokens=8).tokens
+        s.close()
+        assert len(toks) > 0
+        span = np.abs(ref).max()
+        assert np.abs(got - ref).max() < 0.1 * span
+        top2 = np.sort(ref, 1)[:, -2:]
+        clear = (top2[:, 1] - top2[:, 0]) > 0.1 * span
+        assert (got.argmax(1) == ref.argmax(1))[clear].all()
+        m.set_precision("q8")
+        s = m.session(kv_type="f16", n_ctx=2048)
+        assert np.array_equal(s.forced_logits(audio, forced), ref)
+        s.close()
+    finally:
+        m.close()
