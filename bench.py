@@ -49,6 +49,19 @@ def speech_like(rng, n, sr=16000):
     return (out / (np.abs(out).max() + 1e-9) * 10 ** (-12 / 20)).astype(np.float32)
 
 
+def recording(seconds, seed):
+    """A long recording: utterances U[1,8] s of the speech-like signal separated by
+    U[0.4,1.2] s of −60 dBFS noise."""
+    rng = np.random.default_rng(seed)
+    parts, n = [], 0
+    while n < seconds * 16000:
+        u = speech_like(rng, int(rng.uniform(1.0, 8.0) * 16000))
+        s = (rng.standard_normal(int(rng.uniform(0.4, 1.2) * 16000)) * 1e-3).astype(np.float32)
+        parts += [u, s]
+        n += u.size + s.size
+    return np.concatenate(parts)[: int(seconds * 16000)]
+
+
 def lpt_shard(lengths, world):
     """Longest-processing-time greedy assignment of segment indices to ranks."""
     order = np.argsort(-np.asarray(lengths), kind="stable")
@@ -123,9 +136,17 @@ def main():
     ap.add_argument("--segments", type=int, default=SEG_PER_RANK)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-prof", action="store_true")
-    ap.add_argument("--precision", default="q8", choices=["q8", "mxfp8"],
-                    help="mxfp8: SURVEY §8(d) C5 precision (block-scaled fp8 GEMMs; tolerance parity only)")
+    ap.add_argument("--precision", default=None, choices=["q8", "mxfp8"],
+                    help="mxfp8: SURVEY §8(d) C5 precision (block-scaled fp8 GEMMs; tolerance parity only); "
+                         "default q8 (c4), mxfp8 (c5)")
+    ap.add_argument("--workload", default="c4", choices=["c4", "c5"],
+                    help="c4: 256 VAD-split segments per rank (BASELINE metric); c5: one 3,600 s recording "
+                         "(seed 2) VAD-segmented across the ranks (halo-sharded FireRedVAD, probability "
+                         "all-gather), segments LPT-sharded for ASR — strong scaling")
+    ap.add_argument("--c5-seconds", type=float, default=3600.0)
     args = ap.parse_args()
+    if args.precision is None:
+        args.precision = "mxfp8" if args.workload == "c5" else "q8"
 
     SEG_PER_RANK = args.segments
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -153,12 +174,19 @@ def main():
 
     lib = _lib.load()
     _lib.check(lib.qasr_set_device(local))
-    audio = make_workload(world, rank)
-    lens = [a.size for a in audio]
-    offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int64)
-    dev = torch.from_numpy(np.concatenate(audio)).to(f"cuda:{local}")   # inputs resident in HBM
+    if args.workload == "c4":
+        audio = make_workload(world, rank)
+        lens = [a.size for a in audio]
+        offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int64)
+        dev = torch.from_numpy(np.concatenate(audio)).to(f"cuda:{local}")   # inputs resident in HBM
+        audio_s = sum(lens) / 16000.0
+    else:
+        # C5: every rank holds the whole recording (host, and in HBM for the ASR segments); work is divided by
+        # the VAD frame shards and the segment shards inside each step
+        longrec = recording(args.c5_seconds, seed=2)
+        dev = torch.from_numpy(longrec).to(f"cuda:{local}")
+        audio_s = longrec.size / 16000.0 / world   # this rank's share of the job's audio (summed over ranks below)
     torch.cuda.synchronize()
-    audio_s = sum(lens) / 16000.0
 
     collectives = {}
     if world > 1:
@@ -175,8 +203,31 @@ def main():
         model.set_precision(args.precision)
     sess = model.session(kv_type="f16", n_ctx=32768)
 
-    def step(want=False):
-        return sess.run_batch_device(dev.data_ptr(), offs, lens, force_tokens_per_s=FORCE_TPS, want_results=want)
+    c5_info = {}
+    if args.workload == "c4":
+        def step(want=False):
+            return sess.run_batch_device(dev.data_ptr(), offs, lens, force_tokens_per_s=FORCE_TPS,
+                                         want_results=want)
+    else:
+        from qasr import longform
+        from qasr.firered_vad import FireRedVad
+
+        vad = FireRedVad()
+
+        def step(want=False):
+            # halo-sharded VAD → all-gather of the probabilities → host segmenter (same on every rank) → this
+            # rank's LPT share of the speech segments through the ASR batch
+            local_p = longform.shard_probabilities(vad, longrec, rank, world)
+            probs = longform.gather_probabilities(local_p, coll_dev) if world > 1 else local_p
+            segs = longform.segments(probs, longrec.size)
+            mine = sorted(lpt_shard([e - s for s, e in segs], world)[rank]) if segs else []
+            c5_info.update(segments=len(segs), speech_s=round(sum(e - s for s, e in segs) / 16000.0, 1),
+                           rank0_segments=len(mine))
+            if not mine:
+                return []
+            return sess.run_batch_device(dev.data_ptr(), [segs[i][0] for i in mine], [segs[i][1] - segs[i][0]
+                                                                                      for i in mine],
+                                         force_tokens_per_s=FORCE_TPS, want_results=want)
 
     for _ in range(args.warmup):
         step()
@@ -257,7 +308,8 @@ def main():
         value = total_audio / elapsed
         line = {
             "metric": "audio-sec/wall-sec (RTF⁻¹) Qwen3-ASR-1.7B " + ("Q8" if args.precision == "q8" else
-                                                                     "MXFP8 (C5 precision)"),
+                                                                     "MXFP8 (C5 precision)")
+                      + ("" if args.workload == "c4" else ", C5 long-form (VAD-segmented)"),
             "value": round(value, 2),
             "unit": "audio-s/s",
             "n_gpus": world,
@@ -265,12 +317,16 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 2),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "weak" if args.workload == "c4" else "strong",
             "vs_baseline": None,
             "dtype": "i8" if args.precision == "q8" else "fp8e4m3+e8m0",
             "data": "synthetic (seeded speech-like 16 kHz audio; seeded synthetic Q8_0 weights with 1.7B shapes)",
-            "config": {"workload": f"C4: {SEG_PER_RANK} VAD-split segments/rank, U[2,12] s, LPT-sharded, "
-                                   f"{FORCE_TPS} forced tokens/audio-s",
+            "config": {"workload": (f"C4: {SEG_PER_RANK} VAD-split segments/rank, U[2,12] s, LPT-sharded, "
+                                    f"{FORCE_TPS} forced tokens/audio-s") if args.workload == "c4" else
+                                   (f"C5: {args.c5_seconds:g} s recording (seed 2), FireRedVAD halo-sharded over "
+                                    f"{world} rank(s) + probability all-gather, {c5_info.get('segments')} speech "
+                                    f"segments ({c5_info.get('speech_s')} s) LPT-sharded, {FORCE_TPS} forced "
+                                    f"tokens/audio-s"),
                        "model": args.arch, "segments_per_rank": SEG_PER_RANK,
                        "audio_s_per_rank": round(audio_s, 1), "parallelism": f"dp{world}"},
             "roofline": roof,

@@ -117,3 +117,40 @@ def test_weight_broadcast_and_token_gather_gloo(world):
         assert info["bytes"] == 4096 and info["checksums_agree"]
         assert blob == src
         assert got == want
+
+
+def _prob_gather_rank(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+
+    sys.path.insert(0, os.path.join(ROOT, "light-whisper_amd"))
+    from qasr import longform
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    T = 1001
+    f0, f1, h0, h1 = longform.frame_shard(T, rank, world)
+    local = np.arange(f0, f1, dtype=np.float32) / T
+    q.put((rank, longform.gather_probabilities(local, torch.device("cpu")), (f0, f1, h0, h1)))
+    dist.destroy_process_group()
+
+
+def test_long_form_probability_gather_gloo():
+    """the ranks' core frame ranges tile the recording and the all-gather reassembles it in time order"""
+    import torch.multiprocessing as mp
+
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_prob_gather_rank, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = sorted((q.get(timeout=120) for _ in range(world)), key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want = np.arange(1001, dtype=np.float32) / 1001
+    for rank, got, (f0, f1, h0, h1) in out:
+        assert np.array_equal(got, want)
+        assert h0 == max(0, f0 - 160) and h1 == min(1001, f1 + 160)

@@ -64,3 +64,21 @@ def test_speech_timestamps_match_oracle_pipeline(vad):
     pr = oracle.vad_probabilities(oracle.fbank(pcm), w)
     assert np.abs(p - pr).max() < 1e-3
     assert vad.speech_timestamps(audio) == oracle.vad_segments(p, audio.size)
+
+
+def test_sharded_long_form_probabilities_bit_identical(vad):
+    """SURVEY §8(e) long-form VAD: each rank's halo-extended frame range gives exactly the single-pass
+    probabilities of its core frames, for any number of ranks (here 1, 2, 3 and 7 simulated in one process)"""
+    import sys
+
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), ".."))
+    from bench import recording
+    from qasr import longform
+
+    audio = recording(45.0, seed=2)
+    full = vad.probabilities(audio)
+    assert full.size == longform.n_frames(audio.size)
+    for world in (1, 2, 3, 7):
+        parts = [longform.shard_probabilities(vad, audio, r, world) for r in range(world)]
+        assert np.array_equal(np.concatenate(parts), full), world
+    assert longform.segments(full, audio.size) == [(s["start"], s["end"]) for s in vad.speech_timestamps(audio)]

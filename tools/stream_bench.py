@@ -29,23 +29,11 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-from bench import speech_like  # noqa: E402
+from bench import recording  # noqa: E402
 
 SR = 16000
 MIN_INTERIM_S, MIN_GROWTH, WINDOW_S = 0.2, 1024, 12.0
 I_MIN, I_BASE, I_MAX, I_DOWN, I_UP, HEAVY, LIGHT = 140, 220, 460, 24, 42, 420, 180
-
-
-def recording(seconds, seed=3):
-    """Utterances U[1,8] s of the bench's speech-like signal separated by U[0.4,1.2] s of −60 dBFS noise."""
-    rng = np.random.default_rng(seed)
-    parts, n = [], 0
-    while n < seconds * SR:
-        u = speech_like(rng, int(rng.uniform(1.0, 8.0) * SR))
-        s = (rng.standard_normal(int(rng.uniform(0.4, 1.2) * SR)) * 1e-3).astype(np.float32)
-        parts += [u, s]
-        n += u.size + s.size
-    return np.concatenate(parts)[: int(seconds * SR)]
 
 
 def adjust_interval(cur, elapsed_ms):   # interim.rs adjust_interval, executed = true
@@ -102,7 +90,7 @@ def main():
     ap.add_argument("--seconds", type=float, default=60.0)
     ap.add_argument("--engine", default="qwen3-asr-1.7b")
     a = ap.parse_args()
-    audio = recording(a.seconds)
+    audio = recording(a.seconds, seed=3)
     hot = [f"热词{i:03d}" for i in range(100)]
     with tempfile.TemporaryDirectory() as tmp:
         eng = Engine(a.engine, {"QASR_SYNTHETIC": "1", "QASR_FORCE_TOKENS_PER_S": "8", "HF_HUB_CACHE": tmp,
