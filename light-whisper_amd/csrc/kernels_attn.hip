@@ -32,27 +32,21 @@ __device__ __forceinline__ void wave_sync_lds() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+typedef _Float16 h2v __attribute__((ext_vector_type(2)));
+
+// one lane's QD dims of q·k: v_dot2_f32_f16 on the f16 q and K (products exact in f32, f32 accumulation)
 template <int QD>
-__device__ __forceinline__ float qk_dot(const float* qv, const __half* kr) {
+__device__ __forceinline__ float qk_dot(const h2v* qh, const __half* kr) {
     float part = 0.f;
+    const int4 a = *(const int4*)kr;
+    const h2v* ha = (const h2v*)&a;
+#pragma unroll
+    for (int t = 0; t < 4; t++) part = __builtin_amdgcn_fdot2(qh[t], ha[t], part, false);
     if constexpr (QD == 16) {
-        const int4 a = *(const int4*)kr, b = *(const int4*)(kr + 8);
-        const __half2* ha = (const __half2*)&a;
-        const __half2* hb = (const __half2*)&b;
+        const int4 b = *(const int4*)(kr + 8);
+        const h2v* hb = (const h2v*)&b;
 #pragma unroll
-        for (int t = 0; t < 4; t++) {
-            const float2 fa = __half22float2(ha[t]), fb = __half22float2(hb[t]);
-            part += qv[2 * t] * fa.x + qv[2 * t + 1] * fa.y;
-            part += qv[8 + 2 * t] * fb.x + qv[8 + 2 * t + 1] * fb.y;
-        }
-    } else {
-        const int4 a = *(const int4*)kr;
-        const __half2* ha = (const __half2*)&a;
-#pragma unroll
-        for (int t = 0; t < 4; t++) {
-            const float2 fa = __half22float2(ha[t]);
-            part += qv[2 * t] * fa.x + qv[2 * t + 1] * fa.y;
-        }
+        for (int t = 0; t < 4; t++) part = __builtin_amdgcn_fdot2(qh[4 + t], hb[t], part, false);
     }
     return part;
 }
@@ -83,7 +77,7 @@ __global__ __launch_bounds__(256) void k_attention(const __half* __restrict__ Q,
     const int s0 = kv_start[r] + part * qn, L = max(0, min(qn, Lr - part * qn));
     const int sub = lane & 7, kk = lane >> 3;
 
-    float qv[G][QD];
+    h2v qv[G][QD / 2];   // the f16 q dims of this lane (q is f16-rounded on every path)
     if constexpr (FUSED) {
         // decode rows (NW = 4, hd = 128): the q/k RMS-norm + RoPE of this row's G query heads and its KV head, and
         // the new K/V cache row, computed here instead of by k_qk_norm_rope_row (same arithmetic, same f16
@@ -118,13 +112,14 @@ __global__ __launch_bounds__(256) void k_attention(const __half* __restrict__ Q,
 #pragma unroll
         for (int g = 0; g < G; g++)
 #pragma unroll
-            for (int j = 0; j < QD; j++) qv[g][j] = qs[g][sub * QD + j];
+            for (int j = 0; j < QD / 2; j++)
+                qv[g][j] = (h2v){(_Float16)qs[g][sub * QD + 2 * j], (_Float16)qs[g][sub * QD + 2 * j + 1]};
     } else {
 #pragma unroll
         for (int g = 0; g < G; g++) {
             const __half* qp = Q + (size_t)r * ldq + (kvh * G + g) * HD + sub * QD;
 #pragma unroll
-            for (int j = 0; j < QD; j++) qv[g][j] = __half2float(qp[j]);
+            for (int j = 0; j < QD / 2; j++) qv[g][j] = *(const h2v*)(qp + 2 * j);
         }
     }
     float acc[G][PD];
