@@ -209,7 +209,7 @@ QASR_API int qasr_op_gemm_swiglu_q8_cfg(const int8_t* xq, const float* xd, int32
 QASR_API int qasr_op_q8_to_mx(const int8_t* q, const void* d, int32_t d_is_f16, int64_t nblk, uint8_t* q8,
                              uint8_t* s8, void* stream);
 /* y = epi(X·Wᵀ) on MXFP8 operands (v_mfma_scale_f32_16x16x128_f8f6f4); epi as qasr_op_linear_q8 (0-2), 3 SwiGLU
-   (yq/yd), 4 GELU+Q8 (yq/yd); cfg -1 auto, 0 128×128, 1 64×64, 2 64×128.  K % 128 == 0. */
+   (yq/yd), 4 GELU+Q8 (yq/yd); cfg -1 auto, 0 128×128, 1 64×64, 2 64×128, 3 128×128 3-stage ring, 4 128×64.  K % 128 == 0. */
 QASR_API int qasr_op_gemm_mx(const uint8_t* x8, const uint8_t* xs, int32_t M, const uint8_t* w8, const uint8_t* ws,
                              int32_t N, int32_t K, const float* bias, const float* res, float* y, int32_t ldy,
                              int32_t epi, int8_t* yq, float* yd, int32_t cfg, void* stream);

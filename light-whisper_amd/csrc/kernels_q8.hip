@@ -1200,13 +1200,15 @@ void gemm_mx(const uint8_t* x8, const uint8_t* xs, int M, const Q8Mat& W, const 
              float* y, int ldy, int epi, hipStream_t s, int8_t* yq, float* yd, bool y_zeroed, int force_cfg) {
     ProfScope ps(s, "gemm_mx", 2.0 * M * W.N * W.K, (double)W.N * W.K * (1 + 1.0 / 32) + (double)M * W.K * (1 + 1.0 / 32));
     QASR_CHECK(W.mx && W.K % 128 == 0, QASR_E_INVALID, "gemm_mx: needs the MXFP8 weights and K % 128 == 0");
-    // measured (tools/gemm_mx_tune.py): 128×128 tiles for prefill-sized M and the batched vocabulary projection,
-    // 64×128 for the vocabulary projection of fewer rows, 64×64 (+ split-K) for the other decode GEMMs;
+    // measured (tools/gemm_mx_tune.py): 128×128 tiles for prefill-sized M and the batched vocabulary projection
+    // (128×64 where K ≤ 1024 or N, K ≤ 2048: more tiles, shorter K loops), 64×128 for the vocabulary projection of
+    // fewer rows, 64×64 (+ split-K) for the other decode GEMMs;
     // SwiGLU needs 64-column wave tiles
     int cfg = force_cfg;
-    if (cfg < 0) cfg = M > 256 ? 0 : W.N >= 32768 ? (M > 128 ? 0 : 2) : 1;
+    if (cfg < 0)
+        cfg = M > 256 ? ((W.K <= 1024 || (W.N <= 2048 && W.K <= 2048)) ? 4 : 0) : W.N >= 32768 ? (M > 128 ? 0 : 2) : 1;
     if (epi == EPI_SWIGLU && cfg == 1) cfg = 2;
-    const int bm = cfg == 0 ? 128 : cfg == 1 ? 64 : 64, bn = cfg == 0 ? 128 : cfg == 1 ? 64 : 128;
+    const int bm = cfg == 0 || cfg == 3 || cfg == 4 ? 128 : 64, bn = cfg == 0 || cfg == 2 || cfg == 3 ? 128 : 64;
     const int steps = W.K / 128, tiles = cdiv(W.N, bn) * cdiv(M, bm);
     const bool can_split = (epi == EPI_STORE || epi == EPI_RESID) && ldy == W.N && (epi != EPI_RESID || res == y);
     int splits = 1;
@@ -1221,8 +1223,12 @@ void gemm_mx(const uint8_t* x8, const uint8_t* xs, int M, const Q8Mat& W, const 
         k_gemm_mx<4, 4, 2><<<grid, 256, 0, s>>>(x8, xs, M, W.mx, W.mxs, W.N, W.K, bias, res, y, ldy, epi, sps, yq, yd);
     else if (cfg == 1)
         k_gemm_mx<2, 2, 3><<<grid, 256, 0, s>>>(x8, xs, M, W.mx, W.mxs, W.N, W.K, bias, res, y, ldy, epi, sps, yq, yd);
-    else
+    else if (cfg == 2)
         k_gemm_mx<2, 4, 3><<<grid, 256, 0, s>>>(x8, xs, M, W.mx, W.mxs, W.N, W.K, bias, res, y, ldy, epi, sps, yq, yd);
+    else if (cfg == 3)
+        k_gemm_mx<4, 4, 3><<<grid, 256, 0, s>>>(x8, xs, M, W.mx, W.mxs, W.N, W.K, bias, res, y, ldy, epi, sps, yq, yd);
+    else
+        k_gemm_mx<4, 2, 2><<<grid, 256, 0, s>>>(x8, xs, M, W.mx, W.mxs, W.N, W.K, bias, res, y, ldy, epi, sps, yq, yd);
 }
 
 // Q8 activations in, MXFP8 GEMM: the activations' MXFP8 image goes to the session workspace first

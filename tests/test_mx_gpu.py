@@ -59,7 +59,7 @@ def _mx_operands(rng, rows, k, torch_dev, f16):
     return dev(q8.reshape(rows, k), torch_dev), dev(s8, torch_dev), oracle.mx_matrix(q8, s8.astype(np.int32) - 127, rows, k)
 
 
-@pytest.mark.parametrize("cfg", [-1, 0, 1, 2])
+@pytest.mark.parametrize("cfg", [-1, 0, 1, 2, 3, 4])
 @pytest.mark.parametrize("m,n,k,epi", [(5, 128, 256, 0), (130, 192, 512, 0), (300, 256, 1024, 1), (64, 128, 2048, 2),
                                        (257, 384, 384, 1), (40, 64, 128, 0)])
 def test_gemm_mx_vs_float64(torch_dev, cfg, m, n, k, epi):
