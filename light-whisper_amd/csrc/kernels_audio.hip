@@ -330,9 +330,9 @@ __global__ __launch_bounds__(256) void k_conv3x3_gelu_c32(const __half* __restri
 // (three 32-deep MFMA slices), one LDS buffer (row stride 104 halves: conflict-free b128 fragments; 47 KB so
 // two workgroups share a CU) refilled from a register prefetch of the next step between two barriers, and
 // unconditional clamped staging loads (padding taps and tails zeroed by masks at the LDS write).
-constexpr int CV_BM = 128, CV_BN = 96, CV_BK = 96, CV_LD = CV_BK + 8;
+constexpr int CV_BM = 128, CV_BN = 160, CV_BK = 96, CV_LD = CV_BK + 8, CV_TJ = CV_BN / 32;
 constexpr int CV_ACH = CV_BM * (CV_BK / 8) / 256;                    // 6 A chunks of 16 B per thread
-constexpr int CV_BCH = (CV_BN * (CV_BK / 8) + 255) / 256;            // 5 B chunks (last partial)
+constexpr int CV_BCH = (CV_BN * (CV_BK / 8) + 255) / 256;            // B chunks per thread (last partial)
 
 __global__ __launch_bounds__(256) void k_conv3x3_gelu(const __half* __restrict__ in, int n_chunks, int Hi, int Wi,
                                                       const __half* __restrict__ w, const float* __restrict__ bias,
@@ -359,11 +359,11 @@ __global__ __launch_bounds__(256) void k_conv3x3_gelu(const __half* __restrict__
         a_base[c] = chn * Hi;
     }
     const int kper = C / CV_BK, steps = 9 * kper;
-    v4f acc[4][3];
+    v4f acc[4][CV_TJ];
 #pragma unroll
     for (int i = 0; i < 4; i++)
 #pragma unroll
-        for (int j = 0; j < 3; j++) acc[i][j] = (v4f){0.f, 0.f, 0.f, 0.f};
+        for (int j = 0; j < CV_TJ; j++) acc[i][j] = (v4f){0.f, 0.f, 0.f, 0.f};
 
     int4 ra[CV_ACH], rb[CV_BCH];
     unsigned oka = 0, okb = 0;
@@ -416,15 +416,15 @@ __global__ __launch_bounds__(256) void k_conv3x3_gelu(const __half* __restrict__
         const _Float16* bs = Bs[0];
 #pragma unroll
         for (int ks = 0; ks < CV_BK / 32; ks++) {
-            v8h a[4], b[3];
+            v8h a[4], b[CV_TJ];
 #pragma unroll
             for (int i = 0; i < 4; i++) a[i] = *(const v8h*)(as + (wr * 64 + i * 16 + fr) * CV_LD + ks * 32 + fk);
 #pragma unroll
-            for (int j = 0; j < 3; j++) b[j] = *(const v8h*)(bs + (wc * 48 + j * 16 + fr) * CV_LD + ks * 32 + fk);
+            for (int j = 0; j < CV_TJ; j++) b[j] = *(const v8h*)(bs + (wc * 16 * CV_TJ + j * 16 + fr) * CV_LD + ks * 32 + fk);
 #pragma unroll
             for (int i = 0; i < 4; i++)
 #pragma unroll
-                for (int j = 0; j < 3; j++)
+                for (int j = 0; j < CV_TJ; j++)
                     acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[i], b[j], acc[i][j], 0, 0, 0);
         }
         __syncthreads();
@@ -436,8 +436,8 @@ __global__ __launch_bounds__(256) void k_conv3x3_gelu(const __half* __restrict__
 #pragma unroll
     for (int i = 0; i < 4; i++) {
 #pragma unroll
-        for (int j = 0; j < 3; j++) {
-            const int col = n0 + wc * 48 + j * 16 + fr;
+        for (int j = 0; j < CV_TJ; j++) {
+            const int col = n0 + wc * 16 * CV_TJ + j * 16 + fr;
             if (col >= C) continue;
             const float bv = bias[col];
 #pragma unroll
