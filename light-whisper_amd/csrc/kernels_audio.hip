@@ -326,15 +326,17 @@ __global__ __launch_bounds__(256) void k_conv3x3_gelu_c32(const __half* __restri
 
 // conv 3×3 stride 2 pad 1 as an implicit GEMM on v_mfma_f32_16x16x32_f16: rows = output positions (chunk, oy, ox),
 // columns = output channels, K = (tap, input channel) with channel-last f16 activations so each (position, tap)
-// contributes one contiguous 2·BK-byte run.  Tile 128 positions × 96 channels, 4 waves of 64×48, K step 96
-// (three 32-deep MFMA slices), one LDS buffer (row stride 104 halves: conflict-free b128 fragments; 47 KB so
-// two workgroups share a CU) refilled from a register prefetch of the next step between two barriers, and
-// unconditional clamped staging loads (padding taps and tails zeroed by masks at the LDS write).
-constexpr int CV_BM = 128, CV_BN = 160, CV_BK = 96, CV_LD = CV_BK + 8, CV_TJ = CV_BN / 32;
-constexpr int CV_ACH = CV_BM * (CV_BK / 8) / 256;                    // 6 A chunks of 16 B per thread
-constexpr int CV_BCH = (CV_BN * (CV_BK / 8) + 255) / 256;            // B chunks per thread (last partial)
+// contributes one contiguous 2·BK-byte run.  Tile 256 positions × 160 channels (C = 480: three column tiles, so
+// each gathered activation panel is re-read 3×, not 5× as with 96-channel tiles — the kernel is bound by these
+// L2/Infinity-Cache re-reads, ≈120 GB per C4 step at 96×128), 8 waves of 64×80, K step 96 (three 32-deep MFMA
+// slices), one LDS buffer (row stride 104 halves: conflict-free b128 fragments; 86 KB) refilled from a register
+// prefetch of the next step between two barriers, and unconditional clamped staging loads (padding taps and tails
+// zeroed by masks at the LDS write).  128×96 → 128×160 → 256×160: 20.6 → 16.1 → 15.0 ms per C4 step.
+constexpr int CV_BM = 256, CV_BN = 160, CV_BK = 96, CV_LD = CV_BK + 8, CV_TJ = CV_BN / 32, CV_NT = 512;
+constexpr int CV_ACH = CV_BM * (CV_BK / 8) / CV_NT;                  // 6 A chunks of 16 B per thread
+constexpr int CV_BCH = (CV_BN * (CV_BK / 8) + CV_NT - 1) / CV_NT;            // B chunks per thread (last partial)
 
-__global__ __launch_bounds__(256) void k_conv3x3_gelu(const __half* __restrict__ in, int n_chunks, int Hi, int Wi,
+__global__ __launch_bounds__(CV_NT) void k_conv3x3_gelu(const __half* __restrict__ in, int n_chunks, int Hi, int Wi,
                                                       const __half* __restrict__ w, const float* __restrict__ bias,
                                                       int C, void* __restrict__ out, int out_mode) {
     __shared__ __attribute__((aligned(16))) _Float16 As[1][CV_BM * CV_LD];
@@ -350,7 +352,7 @@ __global__ __launch_bounds__(256) void k_conv3x3_gelu(const __half* __restrict__
     bool a_in[CV_ACH];
 #pragma unroll
     for (int c = 0; c < CV_ACH; c++) {
-        const int ch = tid + 256 * c, row = m0 + ch / SEG;
+        const int ch = tid + CV_NT * c, row = m0 + ch / SEG;
         a_in[c] = row < M;
         const int rr = min(row, M - 1);
         const int chn = rr / (Ho * Wo), rem = rr % (Ho * Wo);
@@ -373,7 +375,7 @@ __global__ __launch_bounds__(256) void k_conv3x3_gelu(const __half* __restrict__
         oka = 0;
 #pragma unroll
         for (int c = 0; c < CV_ACH; c++) {
-            const int ch = tid + 256 * c, seg = ch % SEG;
+            const int ch = tid + CV_NT * c, seg = ch % SEG;
             const int iy = 2 * a_oy[c] - 1 + ky, ix = 2 * a_ox[c] - 1 + kx;
             const bool ok = a_in[c] && iy >= 0 && iy < Hi && ix >= 0 && ix < Wi;
             oka |= (unsigned)ok << c;
@@ -383,7 +385,7 @@ __global__ __launch_bounds__(256) void k_conv3x3_gelu(const __half* __restrict__
         okb = 0;
 #pragma unroll
         for (int c = 0; c < CV_BCH; c++) {
-            const int ch = tid + 256 * c, row = ch / SEG, seg = ch % SEG;
+            const int ch = tid + CV_NT * c, row = ch / SEG, seg = ch % SEG;
             const bool ok = ch < CV_BN * SEG && n0 + row < C;
             okb |= (unsigned)ok << c;
             const int co = min(n0 + row, C - 1);
@@ -397,12 +399,12 @@ __global__ __launch_bounds__(256) void k_conv3x3_gelu(const __half* __restrict__
     auto lstore = [&](int buf) {
 #pragma unroll
         for (int c = 0; c < CV_ACH; c++) {
-            const int ch = tid + 256 * c;
+            const int ch = tid + CV_NT * c;
             *(int4*)(&As[buf][(ch / SEG) * CV_LD + (ch % SEG) * 8]) = masked(ra[c], oka >> c);
         }
 #pragma unroll
         for (int c = 0; c < CV_BCH; c++) {
-            const int ch = tid + 256 * c;
+            const int ch = tid + CV_NT * c;
             if (ch < CV_BN * SEG) *(int4*)(&Bs[buf][(ch / SEG) * CV_LD + (ch % SEG) * 8]) = masked(rb[c], okb >> c);
         }
     };
@@ -464,7 +466,7 @@ void conv3x3_gelu(const __half* in, int n_chunks, int Hi, int Wi, const __half* 
     ProfScope ps(s, "conv3x3_f16", 2.0 * M * C * 9.0 * C, (double)M * 9 * C * 2 / 4 + (double)M * C * 2);
     if (C % CV_BK == 0) {
         dim3 grid(cdiv(C, CV_BN), cdiv(M, CV_BM));
-        k_conv3x3_gelu<<<grid, 256, 0, s>>>(in, n_chunks, Hi, Wi, w, b, C, out, out_mode);
+        k_conv3x3_gelu<<<grid, CV_NT, 0, s>>>(in, n_chunks, Hi, Wi, w, b, C, out, out_mode);
     } else {
         dim3 grid(cdiv(C, CT), cdiv(M, CT));
         k_conv3x3_gelu_c32<<<grid, 256, 0, s>>>(in, n_chunks, Hi, Wi, w, b, C, out, out_mode);
