@@ -118,6 +118,16 @@ QASR_API void qasr_model_close(qasr_model* m);
 /* -------------------------------------------------------------------------------------------- session */
 QASR_API int qasr_session_open(qasr_model* m, const char* kv_type, int32_t n_ctx, qasr_session** out);
 QASR_API int qasr_session_run(qasr_session* s, const float* pcm16k, size_t n, int32_t timestamps, qasr_result* out);
+/* Hot-word context (opt-in — the reference ignores hot_words): token ids placed in the system turn
+   of the chat prompt (HF Qwen3-ASR `prompt=`, processing_qwen3_asr.py:513-538) for the session's following runs;
+   n = 0 restores the reference's prompt.  qasr_model_tokenize: UTF-8 → ids by greedy longest match over the
+   byte-level vocabulary (decodes back to the same text; not the canonical BPE segmentation). */
+QASR_API int qasr_session_set_context(qasr_session* s, const int32_t* ids, int32_t n);
+QASR_API int qasr_model_tokenize(const qasr_model* m, const char* text, size_t len, int32_t* ids, size_t cap,
+                                size_t* n_out);
+/* ids → UTF-8 text (the transcript decoder: byte-level pieces, invalid sequences replaced as Python does) */
+QASR_API int qasr_model_detokenize(const qasr_model* m, const int32_t* ids, int32_t n, char* out, size_t cap,
+                                  size_t* written);
 QASR_API int qasr_session_run_opts(qasr_session* s, const float* pcm16k, size_t n, const qasr_run_opts* opts,
                                    qasr_result* out);
 /* Batched: `count` utterances (16 kHz f32 host buffers) encoded/prefilled/decoded together on this device. */

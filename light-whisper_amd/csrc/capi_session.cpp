@@ -196,6 +196,35 @@ QASR_API int qasr_session_open(qasr_model* m, const char* kv_type, int32_t n_ctx
     });
 }
 
+QASR_API int qasr_model_tokenize(const qasr_model* m, const char* text, size_t len, int32_t* ids, size_t cap,
+                                size_t* n_out) {
+    return guard([&] {
+        QASR_CHECK(m && (text || len == 0) && n_out, QASR_E_INVALID, "null argument");
+        const std::vector<int32_t> v = m->m->tok.encode(std::string(text ? text : "", len));
+        *n_out = v.size();
+        QASR_CHECK(!ids || cap >= v.size(), QASR_E_CAPACITY, "id buffer too small");
+        if (ids && !v.empty()) memcpy(ids, v.data(), v.size() * sizeof(int32_t));
+    });
+}
+
+QASR_API int qasr_model_detokenize(const qasr_model* m, const int32_t* ids, int32_t n, char* out, size_t cap,
+                                  size_t* written) {
+    return guard([&] {
+        QASR_CHECK(m && (ids || n == 0) && n >= 0 && written, QASR_E_INVALID, "null argument");
+        const std::string t = m->m->tok.decode(ids, n);
+        *written = t.size();
+        QASR_CHECK(!out || cap >= t.size(), QASR_E_CAPACITY, "text buffer too small");
+        if (out && !t.empty()) memcpy(out, t.data(), t.size());
+    });
+}
+
+QASR_API int qasr_session_set_context(qasr_session* s, const int32_t* ids, int32_t n) {
+    return guard([&] {
+        QASR_CHECK(s && n >= 0 && (ids || n == 0), QASR_E_INVALID, "bad arguments");
+        s->s->set_context(std::vector<int32_t>(ids, ids + n));
+    });
+}
+
 QASR_API int qasr_session_run_opts(qasr_session* s, const float* pcm16k, size_t n, const qasr_run_opts* opts,
                                    qasr_result* out) {
     return guard([&] {

@@ -65,11 +65,16 @@ void mel_dims(int64_t n, int& t_valid, int& t_pad) {
     t_pad = (t_valid + 99) / 100 * 100;
 }
 
-const int kPromptPrefix = 9;
+const int kPromptPrefix = 9;   // prefix tokens before the audio without a system context
 
-std::vector<int32_t> build_prompt(const qasr_hparams& h, int n_audio, int audio_row0) {
-    std::vector<int32_t> p = {h.tok_im_start, h.tok_system, h.tok_newline, h.tok_im_end, h.tok_newline,
-                              h.tok_im_start, h.tok_user, h.tok_newline, h.tok_audio_start};
+// chat prompt (processing_qwen3_asr.py:534-553): the optional system context (hot words, SURVEY §8(f) 4: opt-in,
+// the reference sends none) sits between "system\n" and its <|im_end|>, like HF's `prompt=` system message
+std::vector<int32_t> build_prompt(const qasr_hparams& h, int n_audio, int audio_row0,
+                                  const std::vector<int32_t>& context = {}) {
+    std::vector<int32_t> p = {h.tok_im_start, h.tok_system, h.tok_newline};
+    p.insert(p.end(), context.begin(), context.end());
+    const int32_t pre[] = {h.tok_im_end, h.tok_newline, h.tok_im_start, h.tok_user, h.tok_newline, h.tok_audio_start};
+    p.insert(p.end(), pre, pre + 6);
     for (int i = 0; i < n_audio; i++) p.push_back(-(audio_row0 + i + 1));
     const int32_t tail[] = {h.tok_audio_end, h.tok_im_end, h.tok_newline, h.tok_im_start, h.tok_assistant,
                             h.tok_newline};
@@ -429,11 +434,11 @@ void Session::run_batch(const float* dpcm, const std::vector<int64_t>& off, cons
     // the prompt prefix before the audio (im_start system \n im_end \n im_start user \n audio_start) is the same
     // tokens at the same positions for every utterance, so its K/V is computed once and copied into each
     // utterance's slots; the packed prefill then starts at position P0
-    const int P0 = kPromptPrefix;
+    const int P0 = kPromptPrefix + (int)context_.size();
     const int skip = count >= 4 ? P0 : 0;
     int64_t slots = 0;
     for (int u = 0; u < count; u++) {
-        std::vector<int32_t> p = build_prompt(h, fe.n_tok[u], fe.tok_base[u]);
+        std::vector<int32_t> p = build_prompt(h, fe.n_tok[u], fe.tok_base[u], context_);
         n_prompt[u] = (int)p.size();
         row0[u] = (int)ids.size();
         ids.insert(ids.end(), p.begin() + skip, p.end());
@@ -502,7 +507,7 @@ void Session::run_batch(const float* dpcm, const std::vector<int64_t>& off, cons
         Timer t(st_, times ? &times->prefill : nullptr);
         sc_.get(S_X, (size_t)std::max(T, P0) * H * sizeof(float));
         if (skip) {
-            const std::vector<int32_t> full = build_prompt(h, 0, 0);
+            const std::vector<int32_t> full = build_prompt(h, 0, 0, context_);
             std::vector<int32_t> pid(full.begin(), full.begin() + P0);
             std::vector<int> ppos(P0), pslot(P0), pkvs(P0, (int)pref), pkvl(P0);
             for (int i = 0; i < P0; i++) {
@@ -737,7 +742,7 @@ void Session::forced_logits_host(const float* pcm, int64_t n, const int32_t* for
     std::vector<int64_t> off = {0}, len = {n};
     front_end(d, off, len, fe, nullptr);
     encoder(fe, nullptr);
-    std::vector<int32_t> ids = build_prompt(h, fe.n_tok[0], 0);
+    std::vector<int32_t> ids = build_prompt(h, fe.n_tok[0], 0, context_);
     const int P = (int)ids.size();
     QASR_CHECK(P + n_forced <= n_ctx_, QASR_E_CAPACITY, "forced sequence exceeds n_ctx");
     ensure_kv(P + n_forced + 1);

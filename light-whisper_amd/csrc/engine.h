@@ -59,6 +59,8 @@ class Session {
 
     Model& model() { return *m_; }
     int n_ctx() const { return n_ctx_; }
+    // system-prompt context tokens for the following runs (hot-word biasing; empty = the reference's prompt)
+    void set_context(const std::vector<int32_t>& ids) { context_ = ids; }
     hipStream_t stream() const { return st_; }
 
    private:
@@ -81,6 +83,7 @@ class Session {
 
     Model* m_;
     int n_ctx_;
+    std::vector<int32_t> context_;
     hipStream_t st_ = nullptr;
     Scratch sc_;
     __half* kc_ = nullptr;

@@ -398,6 +398,26 @@ struct Server {
         return out;
     }
 
+    // QASR_HOTWORD_CONTEXT=1 (opt-in): the request's hot_words, joined by ", ", become the system
+    // context of the prompt (HF Qwen3-ASR `prompt=`).  Default: ignored, exactly like the reference server.
+    void set_hotword_context(const Value* hw) {
+        static const bool on = getenv("QASR_HOTWORD_CONTEXT") && std::string(getenv("QASR_HOTWORD_CONTEXT")) == "1";
+        std::vector<int32_t> ids;
+        if (on && hw && hw->type == Value::Arr) {
+            std::string text;
+            for (const Value& w : hw->a)
+                if (w.type == Value::Str && !w.s.empty()) text += (text.empty() ? "" : ", ") + w.s;
+            if (!text.empty()) {
+                size_t n = 0;
+                if (qasr_model_tokenize(model, text.data(), text.size(), nullptr, 0, &n) == QASR_OK && n > 0) {
+                    ids.resize(n);
+                    if (qasr_model_tokenize(model, text.data(), text.size(), ids.data(), n, &n) != QASR_OK) ids.clear();
+                }
+            }
+        }
+        qasr_session_set_context(session, ids.empty() ? nullptr : ids.data(), (int32_t)ids.size());
+    }
+
     Value transcribe(const Value& cmd) {
         if (!initialized) {
             Value ir = initialize();
@@ -505,6 +525,7 @@ struct Server {
                 language = "Chinese";
             } else {
                 qasr_result res;
+                set_hotword_context(cmd.get("hot_words"));
                 static const int force_tps = getenv("QASR_FORCE_TOKENS_PER_S") ? atoi(getenv("QASR_FORCE_TOKENS_PER_S")) : 0;
                 const qasr_run_opts o{0, force_tps, 0};
                 if (qasr_session_run_opts(session, speech_audio.data(), speech_audio.size(), &o, &res) != QASR_OK)

@@ -2,6 +2,9 @@
 
 #include <string.h>
 
+#include <algorithm>
+#include <unordered_map>
+
 #include "common.h"
 
 namespace qasr {
@@ -130,6 +133,39 @@ void Tokenizer::parse(const std::string& raw, std::string& language, std::string
     while (!language.empty() && (language.back() == ' ' || language.back() == '\n')) language.pop_back();
     while (!language.empty() && (language[0] == ' ' || language[0] == '\n')) language.erase(0, 1);
     if (language == "None") language.clear();
+}
+
+std::vector<int32_t> Tokenizer::encode(const std::string& text) const {
+    const ByteMap& bm = bmap();
+    std::unordered_map<std::string, int32_t> index;
+    size_t maxlen = 1;
+    for (int32_t id = 0; id < (int32_t)pieces.size(); id++) {
+        if (!is_special.empty() && is_special[id]) continue;
+        if (pieces[id].empty()) continue;
+        index.emplace(pieces[id], id);   // first id wins for duplicate pieces
+        maxlen = std::max(maxlen, pieces[id].size());
+    }
+    std::string u;   // the text in the byte-level alphabet (each byte one codepoint, 1-2 UTF-8 bytes)
+    for (unsigned char c : text) append_utf8(u, bm.byte2cp[c]);
+    std::vector<int32_t> out;
+    size_t i = 0;
+    while (i < u.size()) {
+        size_t best = 0;
+        int32_t best_id = -1;
+        for (size_t L = std::min(maxlen, u.size() - i); L >= 1; L--) {
+            if (i + L < u.size() && ((unsigned char)u[i + L] & 0xC0) == 0x80) continue;   // codepoint boundary
+            auto it = index.find(u.substr(i, L));
+            if (it != index.end()) {
+                best = L;
+                best_id = it->second;
+                break;
+            }
+        }
+        QASR_CHECK(best_id >= 0, QASR_E_FORMAT, "tokenizer: byte without a piece");
+        out.push_back(best_id);
+        i += best;
+    }
+    return out;
 }
 
 void Tokenizer::make_synthetic(int vocab, const int32_t* special_ids, const char* const* special_text, int n_special) {

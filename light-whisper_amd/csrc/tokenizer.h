@@ -13,6 +13,10 @@ struct Tokenizer {
     std::vector<uint8_t> is_special;   // control / added tokens render literally
     // decode ids to UTF-8 bytes
     std::string decode(const int32_t* ids, int n) const;
+    // UTF-8 text → ids by greedy longest match over the byte-level pieces (special tokens excluded).  Not the
+    // canonical BPE merge order (the GGUF merges are not read), but every byte has a piece, so
+    // decode(encode(t)) == t; used only for the opt-in hot-word context.
+    std::vector<int32_t> encode(const std::string& text) const;
     // split "language X<asr_text>text" → (language, text); raw kept by the caller
     static void parse(const std::string& raw, std::string& language, std::string& text);
     // synthetic vocabulary for synthetic weights: byte tokens, letter pieces, and the special tokens

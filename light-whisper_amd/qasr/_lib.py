@@ -73,6 +73,9 @@ SIGNATURES = {
     "qasr_model_weight_blob": (C.c_int, [P, C.POINTER(P), C.POINTER(C.c_size_t)]),
     "qasr_model_weights_received": (C.c_int, [P]),
     "qasr_model_set_precision": (C.c_int, [P, C.c_char_p]),
+    "qasr_model_tokenize": (C.c_int, [P, C.c_char_p, C.c_size_t, P, C.c_size_t, C.POINTER(C.c_size_t)]),
+    "qasr_session_set_context": (C.c_int, [P, P, I32]),
+    "qasr_model_detokenize": (C.c_int, [P, P, I32, C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)]),
     "qasr_model_tensor_table": (C.c_int, [P, C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)]),
     "qasr_model_export_tensor": (C.c_int, [P, C.c_char_p, P, SZ, C.POINTER(SZ)]),
     "qasr_model_close": (None, [P]),

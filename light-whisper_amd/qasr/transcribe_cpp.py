@@ -104,6 +104,26 @@ class Model:
         """"q8" (the reference's arithmetic) or "mxfp8" (block-scaled fp8 GEMMs)"""
         check(_lib.load().qasr_model_set_precision(self._h, mode.encode()))
 
+    def tokenize(self, text: str) -> list[int]:
+        """UTF-8 text → token ids (greedy longest match; for the opt-in hot-word context)"""
+        b = text.encode("utf-8")
+        n = C.c_size_t()
+        lib = _lib.load()
+        check(lib.qasr_model_tokenize(self._h, b, len(b), None, 0, C.byref(n)))
+        ids = np.empty(max(1, n.value), np.int32)
+        check(lib.qasr_model_tokenize(self._h, b, len(b), ids.ctypes.data_as(C.c_void_p), ids.size, C.byref(n)))
+        return ids[: n.value].tolist()
+
+    def detokenize(self, ids) -> str:
+        a = np.ascontiguousarray(np.asarray(ids, dtype=np.int32).reshape(-1))
+        n = C.c_size_t()
+        lib = _lib.load()
+        p = a.ctypes.data_as(C.c_void_p) if a.size else None
+        check(lib.qasr_model_detokenize(self._h, p, int(a.size), None, 0, C.byref(n)))
+        buf = C.create_string_buffer(max(1, n.value))
+        check(lib.qasr_model_detokenize(self._h, p, int(a.size), buf, n.value, C.byref(n)))
+        return buf.raw[: n.value].decode("utf-8")
+
     def weights_received(self):
         check(_lib.load().qasr_model_weights_received(self._h))
 
@@ -174,6 +194,12 @@ class Session:
         opts = RunOpts(int(max_new_tokens), int(force_tokens_per_s), 0)
         check(_lib.load().qasr_run_batch_device(self._h, C.c_void_p(dev_ptr), off, ln, n, C.byref(opts), res))
         return [_take_result(res[i]) for i in range(n)] if want_results else None
+
+    def set_context(self, ids):
+        """system-prompt context token ids for the following runs (hot words; [] = the reference's prompt)"""
+        a = np.ascontiguousarray(np.asarray(ids, dtype=np.int32).reshape(-1))
+        check(_lib.load().qasr_session_set_context(self._h, a.ctypes.data_as(C.c_void_p) if a.size else None,
+                                                   int(a.size)))
 
     def forced_logits(self, audio, forced) -> np.ndarray:
         a = _f32(audio)

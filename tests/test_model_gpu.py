@@ -290,3 +290,35 @@ def test_mxfp8_precision_mode(golden, torch_dev):
         s.close()
     finally:
         m.close()
+
+
+def test_hotword_context_prompt_matches_oracle(gpu, orc, golden):
+    """SURVEY §8(f) 4 (opt-in; the reference ignores hot_words): context tokens in the system turn of the prompt
+    (HF `prompt=`).  Tokenizer round trip through the model's vocabulary; forced-decode logits with the context
+    against the oracle run on the same prompt; an empty context restores the reference prompt."""
+    m, s = gpu
+    text = "Kubernetes, 张三, ROCm"
+    ctx = m.tokenize(text)
+    assert len(ctx) > 0 and m.detokenize(ctx) == text
+    audio = golden["b__audio"]
+    mel, tv = oracle.mel(audio)
+    emb = orc.encode(mel, tv)
+    base = prompt_ids(emb.shape[0])
+    p = base[:3] + ctx + base[3:]
+    kv = oracle.KV(orc, 1024)
+    toks, ref = kv.generate(p, SPECIAL["tok_audio_pad"], emb, eos=(), max_new=8, force_len=8, want_logits=True)
+    before = s.run(audio, max_new_tokens=6).tokens
+    s.set_context(ctx)
+    try:
+        got = s.forced_logits(audio, toks[:-1])
+        r = s.run(audio, max_new_tokens=4)
+        assert r.n_prompt == len(p)
+        batch = s.run_batch([audio] * 5, max_new_tokens=4)    # shared-prefix path (≥ 4 utterances)
+        assert all(b.n_prompt == len(p) and b.tokens == batch[0].tokens for b in batch)
+    finally:
+        s.set_context([])
+    assert rel_err(got, ref) < 3e-2
+    top2 = np.sort(ref, 1)[:, -2:]
+    clear = (top2[:, 1] - top2[:, 0]) > 0.02 * np.abs(ref).max()
+    assert (got.argmax(1) == ref.argmax(1))[clear].all()
+    assert s.run(audio, max_new_tokens=6).tokens == before
