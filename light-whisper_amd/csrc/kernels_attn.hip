@@ -51,6 +51,31 @@ __device__ __forceinline__ float qk_dot(const h2v* qh, const __half* kr) {
     return part;
 }
 
+// acc + p·(low / high f16 half of h), one v_fma_mix_f32 (the f16 operand is widened inside the FMA: no converts,
+// so the V registers stay packed)
+__device__ __forceinline__ float fma_mix_lo(float p, uint32_t h, float acc) {
+    float d;
+    asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel_hi:[0,1,0]" : "=v"(d) : "v"(p), "v"(h), "v"(acc));
+    return d;
+}
+__device__ __forceinline__ float fma_mix_hi(float p, uint32_t h, float acc) {
+    float d;
+    asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel:[0,1,0] op_sel_hi:[0,1,0]" : "=v"(d) : "v"(p), "v"(h), "v"(acc));
+    return d;
+}
+
+// q·k of one lane's 16 dims held in two registers (the decode path's chunk-wide loads)
+__device__ __forceinline__ float qk_dot16(const h2v* qh, int4 a, int4 b) {
+    float part = 0.f;
+    const h2v* ha = (const h2v*)&a;
+    const h2v* hb = (const h2v*)&b;
+#pragma unroll
+    for (int t = 0; t < 4; t++) part = __builtin_amdgcn_fdot2(qh[t], ha[t], part, false);
+#pragma unroll
+    for (int t = 0; t < 4; t++) part = __builtin_amdgcn_fdot2(qh[4 + t], hb[t], part, false);
+    return part;
+}
+
 template <int HD, int G, int NW, bool FUSED = false>
 __global__ __launch_bounds__(256) void k_attention(const __half* __restrict__ Q, int ldq, const __half* K,
                                                    const __half* V, int ldkv,
@@ -133,8 +158,86 @@ __global__ __launch_bounds__(256) void k_attention(const __half* __restrict__ Q,
     }
     const __half* kbase = K + (size_t)kvh * HD + sub * QD;
     const __half* vbase = V + (size_t)kvh * HD + lane * PD;
+    // decoder rows (hd 128, 4 waves): 64-key chunks whose K and V loads are all issued together (one memory round
+    // trip per chunk instead of one per 8 keys); PV with 16 lanes per key (16-B V loads, dims 8·(lane&15)..+8,
+    // key group lane>>4), the 4 key groups summed once at the end
+    constexpr bool DEC = HD == 128 && NW == 4;
+    const int vg = lane >> 4, vd = 8 * (lane & 15);
+    float av[G][8];
+#pragma unroll
+    for (int g = 0; g < G; g++)
+#pragma unroll
+        for (int j = 0; j < 8; j++) av[g][j] = 0.f;
+    if constexpr (DEC) {
+        const __half* vbase16 = V + (size_t)kvh * HD + vd;
+        for (int c0 = 0; c0 < L; c0 += 64) {
+            const int n = min(64, L - c0);
+            const __half* kc = kbase + (size_t)(s0 + c0) * ldkv;
+            const __half* vc = vbase16 + (size_t)(s0 + c0) * ldkv;
+            int4 ka[8], kb[8], vr[16];
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                const int j = min(8 * u + kk, n - 1);   // rows past n re-read row n-1 (their scores are dropped)
+                ka[u] = *(const int4*)(kc + (size_t)j * ldkv);
+                kb[u] = *(const int4*)(kc + (size_t)j * ldkv + 8);
+            }
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                const int j = 8 * u + kk;
+#pragma unroll
+                for (int g = 0; g < G; g++) {
+                    float p = qk_dot16(qv[g], ka[u], kb[u]);
+                    p += __shfl_xor(p, 1);
+                    p += __shfl_xor(p, 2);
+                    p += __shfl_xor(p, 4);
+                    if (sub == 0 && j < n) sp[w][g][j] = p * scale;
+                }
+            }
+            wave_sync_lds();
+            // the V loads fly while the softmax runs (issued after the scores so K and V are never live together)
+#pragma unroll
+            for (int u = 0; u < 16; u++) {
+                const int j = min(4 * u + vg, n - 1);   // rows past n: weight p = 0
+                vr[u] = *(const int4*)(vc + (size_t)j * ldkv);
+            }
+#pragma unroll
+            for (int g = 0; g < G; g++) {
+                const float x = lane < n ? sp[w][g][lane] : -INFINITY;
+                const float mnew = fmaxf(m[g], wmax(x));
+                const float alpha = expf(m[g] - mnew);
+                const float p = lane < n ? expf(x - mnew) : 0.f;
+                lsum[g] = lsum[g] * alpha + wsum_a(p);
+                m[g] = mnew;
+                sp[w][g][lane] = p;
+#pragma unroll
+                for (int j = 0; j < 8; j++) av[g][j] *= alpha;
+            }
+            wave_sync_lds();
+#pragma unroll
+            for (int u = 0; u < 16; u++) {
+                const uint32_t* hv = (const uint32_t*)&vr[u];
+#pragma unroll
+                for (int g = 0; g < G; g++) {
+                    const float p = sp[w][g][4 * u + vg];
+#pragma unroll
+                    for (int t = 0; t < 4; t++) {
+                        av[g][2 * t] = fma_mix_lo(p, hv[t], av[g][2 * t]);
+                        av[g][2 * t + 1] = fma_mix_hi(p, hv[t], av[g][2 * t + 1]);
+                    }
+                }
+            }
+            wave_sync_lds();
+        }
+#pragma unroll
+        for (int g = 0; g < G; g++)
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                av[g][j] += __shfl_xor(av[g][j], 16);
+                av[g][j] += __shfl_xor(av[g][j], 32);
+            }
+    }
 
-    for (int c0 = 0; c0 < L; c0 += CH) {
+    for (int c0 = 0; c0 < (DEC ? 0 : L); c0 += CH) {
         const int n = min(CH, L - c0);
         const __half* kc = kbase + (size_t)(s0 + c0) * ldkv;
         const __half* vb = vbase + (size_t)(s0 + c0) * ldkv;
@@ -250,8 +353,15 @@ __global__ __launch_bounds__(256) void k_attention(const __half* __restrict__ Q,
                 cm_s[w][g] = m[g];
                 cl_s[w][g] = lsum[g];
             }
+            if constexpr (DEC) {
+                if (vg == 0) {
 #pragma unroll
-            for (int j = 0; j < PD; j++) ca_s[w][g][lane * PD + j] = acc[g][j];
+                    for (int j = 0; j < 8; j++) ca_s[w][g][vd + j] = av[g][j];
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < PD; j++) ca_s[w][g][lane * PD + j] = acc[g][j];
+            }
         }
         __syncthreads();
         if (w != 0) return;
