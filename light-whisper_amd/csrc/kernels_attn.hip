@@ -64,6 +64,40 @@ __device__ __forceinline__ float fma_mix_hi(float p, uint32_t h, float acc) {
     return d;
 }
 
+// cross-lane steps of the decode path on DPP (VALU, no LDS round trip like ds_bpermute): xor 1 / xor 2 =
+// quad_perm, the 8- and 16-lane halves = row_half_mirror / row_mirror (a mirror pairs lane i with a lane of the
+// other half, which is all a reduction needs; semantics pinned by tools/micro/xlane_check.hip); the four 16-lane
+// row totals are combined through v_readlane (a wave-uniform result)
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float sum8(float v) {   // over aligned groups of 8 lanes, in every lane
+    v += dpp<0xB1>(v);
+    v += dpp<0x4E>(v);
+    return v + dpp<0x141>(v);
+}
+__device__ __forceinline__ float wave_sum(float v) {
+    v = sum8(v);
+    v += dpp<0x140>(v);
+    const float a = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 0));
+    const float b = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 16));
+    const float c = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 32));
+    const float d = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 48));
+    return (a + b) + (c + d);
+}
+__device__ __forceinline__ float wave_max(float v) {
+    v = fmaxf(v, dpp<0xB1>(v));
+    v = fmaxf(v, dpp<0x4E>(v));
+    v = fmaxf(v, dpp<0x141>(v));
+    v = fmaxf(v, dpp<0x140>(v));
+    const float a = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 0));
+    const float b = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 16));
+    const float c = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 32));
+    const float d = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 48));
+    return fmaxf(fmaxf(a, b), fmaxf(c, d));
+}
+
 // q·k of one lane's 16 dims held in two registers (the decode path's chunk-wide loads)
 __device__ __forceinline__ float qk_dot16(const h2v* qh, int4 a, int4 b) {
     float part = 0.f;
@@ -186,10 +220,7 @@ __global__ __launch_bounds__(256) void k_attention(const __half* __restrict__ Q,
                 const int j = 8 * u + kk;
 #pragma unroll
                 for (int g = 0; g < G; g++) {
-                    float p = qk_dot16(qv[g], ka[u], kb[u]);
-                    p += __shfl_xor(p, 1);
-                    p += __shfl_xor(p, 2);
-                    p += __shfl_xor(p, 4);
+                    const float p = sum8(qk_dot16(qv[g], ka[u], kb[u]));
                     if (sub == 0 && j < n) sp[w][g][j] = p * scale;
                 }
             }
@@ -203,10 +234,10 @@ __global__ __launch_bounds__(256) void k_attention(const __half* __restrict__ Q,
 #pragma unroll
             for (int g = 0; g < G; g++) {
                 const float x = lane < n ? sp[w][g][lane] : -INFINITY;
-                const float mnew = fmaxf(m[g], wmax(x));
+                const float mnew = fmaxf(m[g], wave_max(x));
                 const float alpha = expf(m[g] - mnew);
                 const float p = lane < n ? expf(x - mnew) : 0.f;
-                lsum[g] = lsum[g] * alpha + wsum_a(p);
+                lsum[g] = lsum[g] * alpha + wave_sum(p);
                 m[g] = mnew;
                 sp[w][g][lane] = p;
 #pragma unroll
@@ -232,7 +263,7 @@ __global__ __launch_bounds__(256) void k_attention(const __half* __restrict__ Q,
         for (int g = 0; g < G; g++)
 #pragma unroll
             for (int j = 0; j < 8; j++) {
-                av[g][j] += __shfl_xor(av[g][j], 16);
+                av[g][j] += __shfl_xor(av[g][j], 16);   // once per workgroup: ds_bpermute is fine here
                 av[g][j] += __shfl_xor(av[g][j], 32);
             }
     }
