@@ -13,19 +13,10 @@
 
 #include "kernels.h"
 #include "qk_rope.h"
+#include "xlane.h"
 
 namespace qasr {
 
-__device__ __forceinline__ float wmax(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
-    return v;
-}
-__device__ __forceinline__ float wsum_a(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    return v;
-}
 __device__ __forceinline__ void wave_sync_lds() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -62,40 +53,6 @@ __device__ __forceinline__ float fma_mix_hi(float p, uint32_t h, float acc) {
     float d;
     asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel:[0,1,0] op_sel_hi:[0,1,0]" : "=v"(d) : "v"(p), "v"(h), "v"(acc));
     return d;
-}
-
-// cross-lane steps of the decode path on DPP (VALU, no LDS round trip like ds_bpermute): xor 1 / xor 2 =
-// quad_perm, the 8- and 16-lane halves = row_half_mirror / row_mirror (a mirror pairs lane i with a lane of the
-// other half, which is all a reduction needs; semantics pinned by tools/micro/xlane_check.hip); the four 16-lane
-// row totals are combined through v_readlane (a wave-uniform result)
-template <int CTRL>
-__device__ __forceinline__ float dpp(float v) {
-    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xf, 0xf, false));
-}
-__device__ __forceinline__ float sum8(float v) {   // over aligned groups of 8 lanes, in every lane
-    v += dpp<0xB1>(v);
-    v += dpp<0x4E>(v);
-    return v + dpp<0x141>(v);
-}
-__device__ __forceinline__ float wave_sum(float v) {
-    v = sum8(v);
-    v += dpp<0x140>(v);
-    const float a = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 0));
-    const float b = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 16));
-    const float c = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 32));
-    const float d = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 48));
-    return (a + b) + (c + d);
-}
-__device__ __forceinline__ float wave_max(float v) {
-    v = fmaxf(v, dpp<0xB1>(v));
-    v = fmaxf(v, dpp<0x4E>(v));
-    v = fmaxf(v, dpp<0x141>(v));
-    v = fmaxf(v, dpp<0x140>(v));
-    const float a = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 0));
-    const float b = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 16));
-    const float c = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 32));
-    const float d = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 48));
-    return fmaxf(fmaxf(a, b), fmaxf(c, d));
 }
 
 // q·k of one lane's 16 dims held in two registers (the decode path's chunk-wide loads)
@@ -292,9 +249,7 @@ __global__ __launch_bounds__(256) void k_attention(const __half* __restrict__ Q,
 #pragma unroll
                 for (int g = 0; g < G; g++) {
                     float p = part[u][g];
-                    p += __shfl_xor(p, 1);
-                    p += __shfl_xor(p, 2);
-                    p += __shfl_xor(p, 4);
+                    p = sum8(p);
                     if (sub == 0 && j < n) sp[w][g][j] = p * scale;
                 }
             }
@@ -305,7 +260,7 @@ __global__ __launch_bounds__(256) void k_attention(const __half* __restrict__ Q,
             float* spw = sp[w][g];
             float cm = -INFINITY;
             for (int i = lane; i < n; i += 64) cm = fmaxf(cm, spw[i]);
-            cm = wmax(cm);
+            cm = wave_max(cm);
             const float mnew = fmaxf(m[g], cm);
             const float alpha = expf(m[g] - mnew);
 #pragma unroll
@@ -316,7 +271,7 @@ __global__ __launch_bounds__(256) void k_attention(const __half* __restrict__ Q,
                 spw[i] = p;
                 ps += p;
             }
-            lsum[g] = lsum[g] * alpha + wsum_a(ps);
+            lsum[g] = lsum[g] * alpha + wave_sum(ps);
             m[g] = mnew;
         }
         wave_sync_lds();
@@ -429,8 +384,12 @@ __global__ __launch_bounds__(256) void k_attention(const __half* __restrict__ Q,
             float amax = 0.f;
 #pragma unroll
             for (int j = 0; j < PD; j++) amax = fmaxf(amax, fabsf(out[j]));
+            if constexpr (PD == 2) {
+                amax = max16(amax);
+            } else {
 #pragma unroll
-            for (int off = 1; off < 32 / PD; off <<= 1) amax = fmaxf(amax, __shfl_xor(amax, off));
+                for (int off = 1; off < 32 / PD; off <<= 1) amax = fmaxf(amax, __shfl_xor(amax, off));
+            }
             const float d = amax / 127.f;
 #pragma unroll
             for (int j = 0; j < PD; j++) {

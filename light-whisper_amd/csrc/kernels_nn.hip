@@ -4,14 +4,11 @@
 
 #include "kernels.h"
 #include "qk_rope.h"
+#include "xlane.h"
 
 namespace qasr {
 
-__device__ __forceinline__ float wsum(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    return v;
-}
+__device__ __forceinline__ float wsum(float v) { return wave_sum(v); }
 
 __device__ __forceinline__ void quant32(const float* v, int8_t* q, float* dout) {
     float amax = 0.f;
@@ -45,15 +42,11 @@ __device__ __forceinline__ void load32(const float* p, float* v) {
 }
 
 // Row kernels: one wave per row, the row held in registers as float4 chunks (lane + 64·k), one HBM pass.  A Q8
-// block is 8 consecutive lanes' chunks: its amax is three xor-shuffles, each lane packs its 4 int8 into one
+// block is 8 consecutive lanes' chunks: its amax is three DPP steps, each lane packs its 4 int8 into one
 // dword (coalesced stores), the block's first lane writes the scale.  Rows up to RW_MAX·256 elements.
 constexpr int RW_MAX = 16;
 
-__device__ __forceinline__ float amax8(float v) {
-    v = fmaxf(v, __shfl_xor(v, 1));
-    v = fmaxf(v, __shfl_xor(v, 2));
-    return fmaxf(v, __shfl_xor(v, 4));
-}
+__device__ __forceinline__ float amax8(float v) { return max8(v); }
 
 __device__ __forceinline__ void quant4_store(float4 v, int c, int lane, int8_t* qrow, float* drow) {
     const float am = amax8(fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));

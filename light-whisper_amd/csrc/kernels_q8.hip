@@ -9,15 +9,11 @@
 
 #include "kernels.h"
 #include "lds_dma.h"
+#include "xlane.h"
 
 namespace qasr {
 
 // ------------------------------------------------------------------------------------------------ helpers
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    return v;
-}
 
 __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
 
@@ -208,7 +204,7 @@ __global__ __launch_bounds__(256) void k_gemv_q8(const int8_t* __restrict__ W, c
                     p = __builtin_amdgcn_sdot4(w[c][t].y, x[m][t].y, p, false);
                     p = __builtin_amdgcn_sdot4(w[c][t].z, x[m][t].z, p, false);
                     p = __builtin_amdgcn_sdot4(w[c][t].w, x[m][t].w, p, false);
-                    p += __shfl_xor(p, 1);
+                    p += __builtin_amdgcn_update_dpp(0, p, 0xB1, 0xf, 0xf, false);   // + lane ^ 1
                     acc[c][m] += (even && in[t]) ? (float)p * (dw[c][t] * dx[m][t]) : 0.f;
                 }
             }
@@ -285,10 +281,7 @@ __device__ __forceinline__ void gemm_epilogue(const float (&acc)[TI][TJ][4], int
                     const float h0 = g0 / (1.f + expf(-g0)) * acc[i][1][r];
                     const float h1 = g1 / (1.f + expf(-g1)) * acc[i][3][r];
                     float am = fmaxf(fabsf(h0), fabsf(h1));
-                    am = fmaxf(am, __shfl_xor(am, 1));
-                    am = fmaxf(am, __shfl_xor(am, 2));
-                    am = fmaxf(am, __shfl_xor(am, 4));
-                    am = fmaxf(am, __shfl_xor(am, 8));
+                    am = max16(am);
                     const float dd = am / 127.f;
                     if (row < M && hb < F) {
                         int8_t* qr = yq + (size_t)row * F + hb;
@@ -316,10 +309,7 @@ __device__ __forceinline__ void gemm_epilogue(const float (&acc)[TI][TJ][4], int
                         const int row = m0 + arow + i * 16 + fq + r;
                         const float h0 = gelu_erf(acc[i][2 * b][r] + b0), h1 = gelu_erf(acc[i][2 * b + 1][r] + b1);
                         float am = fmaxf(fabsf(h0), fabsf(h1));
-                        am = fmaxf(am, __shfl_xor(am, 1));
-                        am = fmaxf(am, __shfl_xor(am, 2));
-                        am = fmaxf(am, __shfl_xor(am, 4));
-                        am = fmaxf(am, __shfl_xor(am, 8));
+                        am = max16(am);
                         const float dd = am / 127.f;
                         if (row < M && c0 < N) {
                             int8_t* qr = yq + (size_t)row * N + c0;
