@@ -71,10 +71,12 @@ typedef struct {
     int32_t n_audio_tokens;
     int32_t n_prompt;
     double ms_mel, ms_encoder, ms_prefill, ms_decode;
+    int32_t truncated;  /* 1: decoding stopped at the token budget, not at EOS (natural mode only) */
 } qasr_result;
 
 typedef struct {
-    int32_t max_new_tokens;      /* 0 → default cap (DESIGN.md §decode length) */
+    int32_t max_new_tokens;      /* 0 → until EOS or n_ctx for one utterance (the reference's session.run);
+                                    a batch of several: 64 + 32·seconds each */
     int32_t force_tokens_per_s;  /* >0: throughput mode, exactly round(k·seconds)+1 tokens, EOS ignored */
     int32_t return_logits;       /* reserved */
 } qasr_run_opts;
@@ -184,8 +186,19 @@ QASR_API void qasr_vad_close(qasr_vad* v);
    tokenizer's decode): every transcript string the library returns has been through it.  out may be NULL to size. */
 QASR_API int qasr_utf8_replace_invalid(const char* in, size_t n, char* out, size_t cap, size_t* written);
 QASR_API int qasr_decode_pcm_s16le(const char* b64, size_t len, float* out, size_t cap, size_t* n_out);
-QASR_API int qasr_resample_linear(const float* x, size_t n, int32_t source_rate, float* out, size_t cap,
+/* source_rate is the request's rate as given (a float rate is not truncated: `sample_rate or 16_000` feeds
+   np.interp directly, qwen3_asr_server.py:252-253) */
+QASR_API int qasr_resample_linear(const float* x, size_t n, double source_rate, float* out, size_t cap,
                                   size_t* n_out);
+
+/* Path-mode input: Qwen3ASRServer._load_audio's file branch (qwen3_asr_server.py:256-267: sf.read float32 →
+   channel mean → _resample) for WAV files (PCM 8/16/24/32, float32) → 16 kHz mono f32.  out == NULL: size only. */
+QASR_API int qasr_audio_load_path(const char* path, float* out, size_t cap, size_t* n_out);
+/* The model output's (language, transcription) split that session.run's result.language / result.text carry
+   (qwen3_asr_server.py:326-327): restates the Qwen3-ASR reference parser (transformers processing_qwen3_asr.py:
+   159-196, incl. its repetition fix); language "" = none.  Buffers may be NULL to size. */
+QASR_API int qasr_parse_transcript(const char* raw, size_t n, char* language, size_t lang_cap, size_t* lang_len,
+                                   char* text, size_t text_cap, size_t* text_len);
 
 /* -------------------------------------------------------------------------------------------- kernel ops */
 QASR_API int qasr_op_quant_rows(const float* x, int32_t M, int32_t K, int32_t ldx, int8_t* q, float* d, void* stream);

@@ -1,4 +1,5 @@
 // extern "C": errors, version, device info.
+#include <stdio.h>
 #include <string.h>
 
 #include "../../include/qasr.h"
@@ -30,7 +31,10 @@ QASR_API int qasr_device_info(char* name, size_t name_cap, double* mem_total_gb,
         hipDeviceProp_t p;
         QASR_HIP(hipGetDeviceProperties(&p, dev));
         if (name && name_cap) {
-            strncpy(name, p.name, name_cap - 1);
+            // the marketing name comes from libdrm's amdgpu.ids; without that file it is empty → the ISA name
+            char arch[64];
+            snprintf(arch, sizeof arch, "AMD Instinct %s", p.gcnArchName);
+            strncpy(name, p.name[0] ? p.name : arch, name_cap - 1);
             name[name_cap - 1] = 0;
         }
         if (mem_total_gb) *mem_total_gb = (double)p.totalGlobalMem / (1024.0 * 1024.0 * 1024.0);

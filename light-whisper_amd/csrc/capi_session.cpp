@@ -4,6 +4,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <cmath>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -59,6 +60,7 @@ void fill_result(const UttResult& u, const StageTimes& t, qasr_result* r) {
     r->ms_encoder = t.encoder;
     r->ms_prefill = t.prefill;
     r->ms_decode = t.decode;
+    r->truncated = u.truncated ? 1 : 0;
 }
 
 }  // namespace
@@ -424,6 +426,21 @@ QASR_API int qasr_utf8_replace_invalid(const char* in, size_t n, char* out, size
     });
 }
 
+QASR_API int qasr_parse_transcript(const char* raw, size_t n, char* language, size_t lang_cap, size_t* lang_len,
+                                   char* text, size_t text_cap, size_t* text_len) {
+    return guard([&] {
+        QASR_CHECK((raw || n == 0) && lang_len && text_len, QASR_E_INVALID, "null argument");
+        std::string lang, txt;
+        Tokenizer::parse(utf8_replace_invalid(std::string(raw ? raw : "", n)), lang, txt);
+        *lang_len = lang.size();
+        *text_len = txt.size();
+        QASR_CHECK((!language || lang_cap >= lang.size()) && (!text || text_cap >= txt.size()), QASR_E_CAPACITY,
+                   "output buffer too small");
+        if (language && !lang.empty()) memcpy(language, lang.data(), lang.size());
+        if (text && !txt.empty()) memcpy(text, txt.data(), txt.size());
+    });
+}
+
 namespace {
 struct B64Table {
     int8_t v[256];
@@ -479,17 +496,17 @@ QASR_API int qasr_decode_pcm_s16le(const char* b64, size_t len, float* out, size
 }
 
 // np.interp(np.linspace(0, N-1, round(N·16000/sr)), arange(N), x) in float64, cast to f32
-QASR_API int qasr_resample_linear(const float* x, size_t n, int32_t source_rate, float* out, size_t cap,
+QASR_API int qasr_resample_linear(const float* x, size_t n, double source_rate, float* out, size_t cap,
                                   size_t* n_out) {
     return guard([&] {
-        QASR_CHECK(source_rate > 0, QASR_E_INVALID, "bad sample rate");
-        if (source_rate == 16000) {
+        QASR_CHECK(source_rate > 0 && std::isfinite(source_rate), QASR_E_INVALID, "bad sample rate");
+        if (source_rate == 16000.0) {
             if (n_out) *n_out = n;
             QASR_CHECK(!out || cap >= n, QASR_E_CAPACITY, "buffer too small");
             if (out && n) memcpy(out, x, n * sizeof(float));
             return;
         }
-        const double tl = nearbyint((double)n * 16000.0 / (double)source_rate);
+        const double tl = nearbyint((double)n * 16000.0 / source_rate);
         const int64_t target = (int64_t)tl;
         if (n_out) *n_out = target > 0 ? (size_t)target : 0;
         if (target <= 0) return;

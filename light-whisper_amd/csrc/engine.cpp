@@ -115,7 +115,8 @@ Session::Session(Model* m, int n_ctx) : m_(m), n_ctx_(n_ctx) {
     rope_table(n_ctx, m->hp.head_dim, m->hp.rope_theta, tab.data());
     QASR_HIP(hipMalloc(&rope_, tab.size() * sizeof(float)));
     QASR_HIP(hipMemcpy(rope_, tab.data(), tab.size() * sizeof(float), hipMemcpyHostToDevice));
-    ensure_kv(n_ctx);  // the reference session reserves the full f16 KV for n_ctx (qwen3_asr_server.py:123)
+    // the reference session reserves the full f16 KV for n_ctx (qwen3_asr_server.py:123); + the dummy slot
+    ensure_kv(n_ctx + 1);
 }
 
 Session::~Session() {
@@ -443,8 +444,10 @@ void Session::run_batch(const float* dpcm, const std::vector<int64_t>& off, cons
         row0[u] = (int)ids.size();
         ids.insert(ids.end(), p.begin() + skip, p.end());
         const double secs = (double)len[u] / 16000.0;
+        // one utterance decodes until EOS or n_ctx, like the reference's session.run; a batch caps each utterance
+        // (its KV slot range is reserved up front)
         if (force_tps > 0) budget[u] = std::max(1, (int)lround(force_tps * secs) + 1);
-        else budget[u] = max_new > 0 ? max_new : 64 + (int)ceil(32.0 * secs);
+        else budget[u] = max_new > 0 ? max_new : count == 1 ? n_ctx_ : 64 + (int)ceil(32.0 * secs);
         budget[u] = std::min(budget[u], n_ctx_ - n_prompt[u]);
         QASR_CHECK(budget[u] > 0, QASR_E_CAPACITY, "utterance exceeds n_ctx");
         base[u] = (int)slots;
@@ -566,10 +569,12 @@ void Session::run_batch(const float* dpcm, const std::vector<int64_t>& off, cons
         decode_step(ds, bmax, true);  // also sizes the layer scratch
         QASR_HIP(hipEventRecord(step_ev_[0], st_));
     }
-    if (graph_epoch_ != sc_.epoch + kv_epoch_ * 1000003ull) {
+    // captured step graphs hold scratch, KV and weight pointers: any reallocation or precision change retires them
+    const uint64_t key[3] = {sc_.epoch, kv_epoch_, m_->precision_gen};
+    if (memcmp(key, graph_key_, sizeof key) != 0) {
         for (auto& g : graphs_) (void)hipGraphExecDestroy(g.second);
         graphs_.clear();
-        graph_epoch_ = sc_.epoch + kv_epoch_ * 1000003ull;
+        memcpy(graph_key_, key, sizeof key);
     }
     int step = 1;
     while (bound > 0) {
@@ -614,6 +619,7 @@ void Session::run_batch(const float* dpcm, const std::vector<int64_t>& off, cons
         for (int u = 0; u < count; u++) {
             const int g = hb[ucap_ + u];
             out[u].tokens.assign(ho.begin() + (size_t)u * ld, ho.begin() + (size_t)u * ld + g);
+            out[u].truncated = force_tps <= 0 && g >= budget[u];
         }
     }
     for (int u = 0; u < count; u++) {

@@ -29,6 +29,7 @@ struct UttResult {
     std::vector<int32_t> tokens;
     std::string raw, text, language;
     int n_audio = 0, n_prompt = 0;
+    bool truncated = false;   // stopped at the token budget, not at EOS (natural mode)
 };
 
 struct StageTimes {
@@ -99,7 +100,7 @@ class Session {
     void* pin_cnt_ = nullptr;
     hipEvent_t step_ev_[2] = {nullptr, nullptr};
     std::map<int, hipGraphExec_t> graphs_;
-    uint64_t graph_epoch_ = ~0ull;
+    uint64_t graph_key_[3] = {~0ull, ~0ull, ~0ull};   // scratch epoch, KV epoch, model precision generation
     uint64_t kv_epoch_ = 0;
     int ucap_ = 0;
 };

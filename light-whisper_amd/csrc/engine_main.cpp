@@ -10,7 +10,8 @@
 // (never used by the app): QASR_SYNTHETIC=1 loads seeded synthetic weights when no GGUF is provisioned;
 // QASR_PROTOCOL_TEST_FAKE=1 replaces model + VAD by the reference tests' fakes (test_qwen3_asr_server.py:15-57);
 // QASR_FORCE_TOKENS_PER_S=k fixes the decode length at round(k·seconds)+1 tokens (benchmarks: deterministic work
-// on synthetic weights, SURVEY §8(d) "decode length control").
+// on synthetic weights, SURVEY §8(d) "decode length control"); QASR_MAX_NEW_TOKENS=n caps the natural-EOS decode
+// (synthetic weights rarely emit EOS: without a cap each request would decode to n_ctx).
 #include <dirent.h>
 #include <signal.h>
 #include <stdarg.h>
@@ -206,60 +207,6 @@ std::string py_str(const Value* v) {  // str() of a JSON value, as the reference
     }
 }
 
-// ------------------------------------------------------------------------------------------ WAV (path mode)
-bool read_wav(const std::string& path, std::vector<float>& mono, int& rate, std::string& err) {
-    std::string d = read_file(path);
-    if (d.size() < 12 || d.compare(0, 4, "RIFF") != 0 || d.compare(8, 4, "WAVE") != 0) {
-        err = "Format not recognised.";
-        return false;
-    }
-    size_t pos = 12;
-    int fmt = 0, ch = 0, bits = 0;
-    rate = 0;
-    while (pos + 8 <= d.size()) {
-        std::string id = d.substr(pos, 4);
-        uint32_t sz;
-        memcpy(&sz, &d[pos + 4], 4);
-        const size_t body = pos + 8;
-        if (id == "fmt " && body + 16 <= d.size()) {
-            uint16_t f16, c16, b16;
-            memcpy(&f16, &d[body], 2);
-            memcpy(&c16, &d[body + 2], 2);
-            memcpy(&rate, &d[body + 4], 4);
-            memcpy(&b16, &d[body + 14], 2);
-            fmt = f16;
-            ch = c16;
-            bits = b16;
-            if (fmt == 0xFFFE && sz >= 26 && body + 26 <= d.size()) memcpy(&f16, &d[body + 24], 2), fmt = f16;
-        } else if (id == "data") {
-            if (ch <= 0 || rate <= 0) break;
-            const size_t n = std::min<size_t>(sz, d.size() - body);
-            const int bps = bits / 8;
-            const size_t frames = n / (size_t)(bps * ch);
-            mono.assign(frames, 0.f);
-            for (size_t i = 0; i < frames; i++) {
-                float acc = 0.f;
-                for (int c = 0; c < ch; c++) {
-                    const unsigned char* p = (const unsigned char*)&d[body + (i * ch + c) * bps];
-                    float v = 0.f;
-                    if (fmt == 1 && bits == 16) v = (float)(int16_t)(p[0] | (p[1] << 8)) / 32768.f;
-                    else if (fmt == 1 && bits == 24) v = (float)((int32_t)((p[0] << 8) | (p[1] << 16) | (p[2] << 24)) >> 8) / 8388608.f;
-                    else if (fmt == 1 && bits == 32) v = (float)((int32_t)(p[0] | (p[1] << 8) | (p[2] << 16) | ((uint32_t)p[3] << 24))) / 2147483648.f;
-                    else if (fmt == 1 && bits == 8) v = ((float)p[0] - 128.f) / 128.f;
-                    else if (fmt == 3 && bits == 32) memcpy(&v, p, 4);
-                    else { err = "Unsupported WAV sample format"; return false; }
-                    acc += v;
-                }
-                mono[i] = acc / (float)ch;  // audio.mean(axis=1) (qwen3_asr_server.py:265)
-            }
-            return true;
-        }
-        pos = body + sz + (sz & 1);
-    }
-    err = "Format not recognised.";
-    return false;
-}
-
 // ------------------------------------------------------------------------------------------ server
 struct Server {
     std::string engine;
@@ -450,11 +397,11 @@ struct Server {
                     audio.resize(ns);
                     const double rate = sr_v->type == Value::Int ? (double)sr_v->i : sr_v->f;
                     duration = (double)ns / rate;
-                    if ((int)rate != 16000) {
+                    if (rate != 16000.0) {   // the float rate as given (no truncation: np.interp gets it as is)
                         size_t nout = 0;
-                        qasr_resample_linear(audio.data(), audio.size(), (int)rate, nullptr, 0, &nout);
+                        qasr_resample_linear(audio.data(), audio.size(), rate, nullptr, 0, &nout);
                         std::vector<float> rs(nout);
-                        if (nout && qasr_resample_linear(audio.data(), audio.size(), (int)rate, rs.data(), nout, &nout) != QASR_OK)
+                        if (nout && qasr_resample_linear(audio.data(), audio.size(), rate, rs.data(), nout, &nout) != QASR_OK)
                             throw std::runtime_error(qasr_last_error());
                         audio.swap(rs);
                     }
@@ -467,16 +414,13 @@ struct Server {
                 const std::string p = path && path->type == Value::Str ? path->s : py_str(path);
                 struct stat st;
                 if (!path || !path->truthy() || stat(p.c_str(), &st) != 0) throw std::runtime_error("音频文件不存在: " + p);
-                int rate = 0;
-                std::string err;
-                if (!read_wav(p, audio, rate, err)) throw std::runtime_error("Error opening '" + p + "': " + err);
-                if (rate != 16000) {
-                    size_t nout = 0;
-                    qasr_resample_linear(audio.data(), audio.size(), rate, nullptr, 0, &nout);
-                    std::vector<float> rs(nout);
-                    if (nout) qasr_resample_linear(audio.data(), audio.size(), rate, rs.data(), nout, &nout);
-                    audio.swap(rs);
-                }
+                // soundfile read → mono mean → _resample (qwen3_asr_server.py:256-267), in libqasr
+                size_t ns = 0;
+                if (qasr_audio_load_path(p.c_str(), nullptr, 0, &ns) != QASR_OK) throw std::runtime_error(qasr_last_error());
+                audio.resize(ns);
+                if (ns && qasr_audio_load_path(p.c_str(), audio.data(), ns, &ns) != QASR_OK)
+                    throw std::runtime_error(qasr_last_error());
+                audio.resize(ns);
                 duration = (double)audio.size() / 16000.0;
             }
             total_audio_duration += duration;
@@ -527,7 +471,8 @@ struct Server {
                 qasr_result res;
                 set_hotword_context(cmd.get("hot_words"));
                 static const int force_tps = getenv("QASR_FORCE_TOKENS_PER_S") ? atoi(getenv("QASR_FORCE_TOKENS_PER_S")) : 0;
-                const qasr_run_opts o{0, force_tps, 0};
+                static const int max_new = getenv("QASR_MAX_NEW_TOKENS") ? atoi(getenv("QASR_MAX_NEW_TOKENS")) : 0;
+                const qasr_run_opts o{max_new, force_tps, 0};
                 if (qasr_session_run_opts(session, speech_audio.data(), speech_audio.size(), &o, &res) != QASR_OK)
                     throw std::runtime_error(qasr_last_error());
                 text = res.text ? res.text : "";

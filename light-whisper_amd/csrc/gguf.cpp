@@ -58,7 +58,10 @@ void read_scalar(Reader& r, uint32_t t, int64_t& i, double& f, std::string& s) {
 
 uint64_t ggml_nbytes(uint32_t type, const std::vector<int64_t>& dims) {
     uint64_t n = 1;
-    for (auto d : dims) n *= (uint64_t)d;
+    for (auto d : dims) {
+        QASR_CHECK(d >= 0 && !__builtin_mul_overflow(n, (uint64_t)d, &n), QASR_E_FORMAT, "gguf: tensor size overflows");
+    }
+    QASR_CHECK(n <= (UINT64_MAX >> 3), QASR_E_FORMAT, "gguf: tensor size overflows");
     switch (type) {
         case GGML_F32: return n * 4;
         case GGML_F16: return n * 2;
@@ -116,11 +119,16 @@ GgufFile::GgufFile(const std::string& path) {
             ti.nbytes = ggml_nbytes(ti.type, ti.dims);
             tensors_[ti.name] = ti;
         }
-        uint64_t align = (uint64_t)get_int("general.alignment", 32);
-        uint64_t data0 = (r.pos + align - 1) / align * align;
+        const int64_t align_i = get_int("general.alignment", 32);
+        QASR_CHECK(align_i > 0 && align_i <= (1 << 20), QASR_E_FORMAT, "gguf: bad general.alignment");
+        const uint64_t align = (uint64_t)align_i;
+        const uint64_t data0 = (r.pos + align - 1) / align * align;
         for (auto& kvp : tensors_) {
             auto& ti = kvp.second;
-            QASR_CHECK(data0 + ti.offset + ti.nbytes <= size_, QASR_E_FORMAT, "gguf: tensor data out of range: " + ti.name);
+            uint64_t end = 0;
+            QASR_CHECK(!__builtin_add_overflow(data0, ti.offset, &end) && !__builtin_add_overflow(end, ti.nbytes, &end) &&
+                           end <= size_,
+                       QASR_E_FORMAT, "gguf: tensor data out of range: " + ti.name);
             ti.data = (const uint8_t*)map_ + data0 + ti.offset;
         }
     } catch (...) {

@@ -496,8 +496,11 @@ void set_precision(Model& m, const std::string& mode) {
     QASR_CHECK(mode == "q8" || mode == "mxfp8", QASR_E_INVALID, "precision must be \"q8\" or \"mxfp8\"");
     QASR_CHECK(!m.weights_pending, QASR_E_INVALID, "set_precision: the model's weights have not arrived");
     if (mode == "q8") {
+        if (!m.mx()) return;
+        QASR_HIP(hipDeviceSynchronize());   // queued GEMMs may still read the fp8 images
         for_each_gemm_weight(m, [](Q8Mat& w) { w.mx = nullptr, w.mxs = nullptr; });
         m.mx_mem.reset();
+        m.precision_gen++;
         return;
     }
     if (m.mx()) return;
@@ -517,6 +520,7 @@ void set_precision(Model& m, const std::string& mode) {
     });
     QASR_HIP(hipStreamSynchronize(s));
     m.mx_mem = std::move(mem);
+    m.precision_gen++;
 }
 
 // ----------------------------------------------------------------------------------------------- export

@@ -79,6 +79,9 @@ struct Model {
     // precision mode "mxfp8" (SURVEY §8(d) C5): MXFP8 images of the GEMM weights in their own allocation
     std::unique_ptr<DevAlloc> mx_mem;
     bool mx() const { return mx_mem != nullptr; }
+    // bumped by every precision change: sessions' captured decode graphs hold the GEMM weight pointers of the
+    // precision they were captured in, so a change invalidates them (engine.cpp run_batch)
+    uint64_t precision_gen = 0;
 
     int audio_F3() const { return (((hp.n_mels + 1) / 2 + 1) / 2 + 1) / 2; }
     int64_t weight_bytes() const { return (int64_t)mem.bytes; }
@@ -92,7 +95,7 @@ std::unique_ptr<Model> make_synthetic_model(const qasr_hparams& hp, uint64_t see
 std::unique_ptr<Model> make_synthetic_shell(const qasr_hparams& hp, const std::string& arch);
 void export_tensor(const Model& m, const std::string& name, void* dst, size_t cap, size_t* written);
 // "q8" (default: the reference's W8A8 arithmetic) or "mxfp8" (block-scaled fp8 GEMMs; tolerance parity only).
-// Open sessions keep graphs on the old weights: set the precision before opening them.
+// Open sessions re-capture their decode graphs on their next run (precision_gen).
 void set_precision(Model& m, const std::string& mode);
 
 }  // namespace qasr

@@ -116,23 +116,134 @@ std::string Tokenizer::decode(const int32_t* ids, int n) const {
     return utf8_replace_invalid(out);
 }
 
+namespace {
+// UTF-8 ↔ codepoints (the decoder's output is valid UTF-8: it went through utf8_replace_invalid)
+std::u32string to_u32(const std::string& s) {
+    std::u32string o;
+    const unsigned char* p = (const unsigned char*)s.data();
+    for (size_t i = 0; i < s.size();) {
+        const unsigned c = p[i];
+        int len = c < 0x80 ? 1 : c < 0xE0 ? 2 : c < 0xF0 ? 3 : 4;
+        if (i + len > s.size()) len = 1;
+        char32_t cp = len == 1 ? c : len == 2 ? c & 0x1F : len == 3 ? c & 0x0F : c & 0x07;
+        for (int k = 1; k < len; k++) cp = (cp << 6) | (p[i + k] & 0x3F);
+        o += cp;
+        i += (size_t)len;
+    }
+    return o;
+}
+std::string to_utf8(const std::u32string& s) {
+    std::string o;
+    for (char32_t c : s) {
+        if (c < 0x80) o += (char)c;
+        else if (c < 0x800) o += (char)(0xC0 | (c >> 6)), o += (char)(0x80 | (c & 0x3F));
+        else if (c < 0x10000)
+            o += (char)(0xE0 | (c >> 12)), o += (char)(0x80 | ((c >> 6) & 0x3F)), o += (char)(0x80 | (c & 0x3F));
+        else
+            o += (char)(0xF0 | (c >> 18)), o += (char)(0x80 | ((c >> 12) & 0x3F)), o += (char)(0x80 | ((c >> 6) & 0x3F)),
+                o += (char)(0x80 | (c & 0x3F));
+    }
+    return o;
+}
+// Python str.isspace / str.strip() / str.splitlines() separators / ASCII str.lower()
+bool py_space(char32_t c) {
+    return (c >= 0x09 && c <= 0x0D) || (c >= 0x1C && c <= 0x20) || c == 0x85 || c == 0xA0 || c == 0x1680 ||
+           (c >= 0x2000 && c <= 0x200A) || c == 0x2028 || c == 0x2029 || c == 0x202F || c == 0x205F || c == 0x3000;
+}
+bool py_linebreak(char32_t c) {
+    return c == 0x0A || c == 0x0B || c == 0x0C || c == 0x0D || c == 0x1C || c == 0x1D || c == 0x1E || c == 0x85 ||
+           c == 0x2028 || c == 0x2029;
+}
+std::u32string strip(const std::u32string& s) {
+    size_t b = 0, e = s.size();
+    while (b < e && py_space(s[b])) b++;
+    while (e > b && py_space(s[e - 1])) e--;
+    return s.substr(b, e - b);
+}
+std::u32string lower_ascii(std::u32string s) {
+    for (auto& c : s)
+        if (c >= 'A' && c <= 'Z') c += 32;
+    return s;
+}
+
+// _detect_and_fix_repetitions (processing_qwen3_asr.py:310-380, threshold 20): runs of > 20 equal characters
+// collapse to one, then the first pattern of 1-20 characters repeated ≥ 20 times collapses to one copy (and the
+// rest of the string is fixed the same way)
+std::u32string fix_char_repeats(const std::u32string& s, size_t th) {
+    std::u32string r;
+    for (size_t i = 0; i < s.size();) {
+        size_t cnt = 1;
+        while (i + cnt < s.size() && s[i + cnt] == s[i]) cnt++;
+        if (cnt > th) r += s[i];
+        else r.append(s, i, cnt);
+        i += cnt;
+    }
+    return r;
+}
+std::u32string fix_pattern_repeats(const std::u32string& s, int64_t th, int64_t max_len = 20) {
+    const int64_t n = (int64_t)s.size(), min_rep = th * 2;
+    if (n < min_rep) return s;
+    std::u32string r;
+    int64_t i = 0;
+    bool found = false;
+    while (i <= n - min_rep) {
+        found = false;
+        for (int64_t k = 1; k <= max_len; k++) {
+            if (i + k * th > n) break;
+            bool valid = true;
+            for (int64_t rep = 1; rep < th && valid; rep++) valid = s.compare((size_t)(i + rep * k), (size_t)k, s, (size_t)i, (size_t)k) == 0;
+            if (valid) {
+                int64_t end = i + th * k;
+                while (end + k <= n && s.compare((size_t)end, (size_t)k, s, (size_t)i, (size_t)k) == 0) end += k;
+                r.append(s, (size_t)i, (size_t)k);
+                r += fix_pattern_repeats(s.substr((size_t)end), th, max_len);
+                i = n;
+                found = true;
+                break;
+            }
+        }
+        if (found) break;
+        r += s[(size_t)i];
+        i++;
+    }
+    if (!found) r.append(s, (size_t)std::min(i, n), std::u32string::npos);
+    return r;
+}
+}  // namespace
+
+// Qwen3-ASR output → (language, transcription).  transcribe.cpp's own parser is not available (third-party, absent:
+// SURVEY §8(c)); this restates the in-container Qwen3-ASR reference parser _parse_single_output
+// (transformers/models/qwen3_asr/processing_qwen3_asr.py:159-196, "like the original implementation"): strip, keep
+// what follows "assistant\n", the repetition fix, split at the first "<asr_text>" (none: all of it is the text, no
+// language), "language none" (any case) → no language, else the first non-empty line of the prefix with its
+// "language " prefix (any case) removed.  "" = no language (the server then reports "unknown",
+// qwen3_asr_server.py:327).  Lower-casing is ASCII-only.
 void Tokenizer::parse(const std::string& raw, std::string& language, std::string& text) {
-    static const char* tag = "<asr_text>";
-    size_t at = raw.find(tag);
-    if (at == std::string::npos) {
-        language.clear();
-        text = raw;
+    language.clear();
+    text.clear();
+    std::u32string t = strip(to_u32(raw));
+    if (t.empty()) return;
+    static const std::u32string kAssistant = U"assistant\n", kMarker = U"<asr_text>", kLang = U"language ";
+    if (size_t a = t.find(kAssistant); a != std::u32string::npos) t = t.substr(a + kAssistant.size());
+    t = fix_pattern_repeats(fix_char_repeats(t, 20), 20);
+    const size_t at = t.find(kMarker);
+    if (at == std::u32string::npos) {
+        text = to_utf8(strip(t));
         return;
     }
-    std::string head = raw.substr(0, at);
-    text = raw.substr(at + strlen(tag));
-    const std::string pre = "language ";
-    size_t p = head.find(pre);
-    language = p == std::string::npos ? head : head.substr(p + pre.size());
-    // trim
-    while (!language.empty() && (language.back() == ' ' || language.back() == '\n')) language.pop_back();
-    while (!language.empty() && (language[0] == ' ' || language[0] == '\n')) language.erase(0, 1);
-    if (language == "None") language.clear();
+    const std::u32string prefix = strip(t.substr(0, at));
+    text = to_utf8(strip(t.substr(at + kMarker.size())));
+    if (lower_ascii(prefix) == U"language none") return;
+    for (size_t b = 0; b < prefix.size();) {
+        size_t e = b;
+        while (e < prefix.size() && !py_linebreak(prefix[e])) e++;
+        const std::u32string line = strip(prefix.substr(b, e - b));
+        b = e + (e < prefix.size() && prefix[e] == 0x0D && e + 1 < prefix.size() && prefix[e + 1] == 0x0A ? 2 : 1);
+        if (line.empty()) continue;
+        if (lower_ascii(line).compare(0, kLang.size(), kLang) == 0) language = to_utf8(strip(line.substr(kLang.size())));
+        else language = to_utf8(line);
+        break;
+    }
 }
 
 std::vector<int32_t> Tokenizer::encode(const std::string& text) const {

@@ -41,7 +41,7 @@ class Result(C.Structure):
     _fields_ = [("text", C.c_char_p), ("language", C.c_char_p), ("raw", C.c_char_p),
                 ("tokens", C.POINTER(C.c_int32)), ("n_tokens", C.c_int32), ("n_audio_tokens", C.c_int32),
                 ("n_prompt", C.c_int32), ("ms_mel", C.c_double), ("ms_encoder", C.c_double),
-                ("ms_prefill", C.c_double), ("ms_decode", C.c_double)]
+                ("ms_prefill", C.c_double), ("ms_decode", C.c_double), ("truncated", C.c_int32)]
 
 
 class RunOpts(C.Structure):
@@ -102,7 +102,10 @@ SIGNATURES = {
     "qasr_vad_close": (None, [P]),
     "qasr_utf8_replace_invalid": (C.c_int, [C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)]),
     "qasr_decode_pcm_s16le": (C.c_int, [C.c_char_p, SZ, P, SZ, C.POINTER(SZ)]),
-    "qasr_resample_linear": (C.c_int, [P, SZ, I32, P, SZ, C.POINTER(SZ)]),
+    "qasr_resample_linear": (C.c_int, [P, SZ, C.c_double, P, SZ, C.POINTER(SZ)]),
+    "qasr_audio_load_path": (C.c_int, [C.c_char_p, P, SZ, C.POINTER(SZ)]),
+    "qasr_parse_transcript": (C.c_int, [C.c_char_p, SZ, C.c_char_p, SZ, C.POINTER(SZ), C.c_char_p, SZ,
+                                        C.POINTER(SZ)]),
     "qasr_op_quant_rows": (C.c_int, [P, I32, I32, I32, P, P, P]),
     "qasr_op_repack_q8": (C.c_int, [P, I64, P, P, P]),
     "qasr_op_linear_q8": (C.c_int, [P, P, I32, P, P, I32, I32, P, P, P, I32, I32, I32, P]),

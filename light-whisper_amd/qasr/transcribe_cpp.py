@@ -38,6 +38,7 @@ def _take_result(r: Result) -> SimpleNamespace:
         tokens=toks,
         n_audio_tokens=r.n_audio_tokens,
         n_prompt=r.n_prompt,
+        truncated=bool(r.truncated),
         timings_ms={"mel": r.ms_mel, "encoder": r.ms_encoder, "prefill": r.ms_prefill, "decode": r.ms_decode},
     )
     _lib.load().qasr_result_free(C.byref(r))

@@ -227,6 +227,35 @@ CFG_INT_KEYS = ["n_mels", "conv_ch", "enc_d", "enc_layers", "enc_heads", "enc_ff
                 "proj_out", "txt_h", "txt_layers", "txt_heads", "txt_kv_heads", "head_dim", "txt_ffn", "vocab"]
 CFG_FLOAT_KEYS = ["rope_theta", "rms_eps", "ln_eps"]
 
+# Qwen2-tokenizer special ids the pinned checkpoints use (chat prompt, EOS; the engine's default_hparams)
+QWEN_SPECIAL = dict(tok_im_start=151644, tok_im_end=151645, tok_system=8948, tok_user=872, tok_assistant=77091,
+                    tok_newline=198, tok_audio_start=151669, tok_audio_end=151670, tok_audio_pad=151676,
+                    tok_eos0=151645, tok_eos1=151643, tok_asr_text=151704)
+
+
+def arch_config(arch: str) -> dict:
+    """Hyper-parameters of the two pinned checkpoints (hf_cache_utils.py:11-26) — the same
+    values as the engine's default_hparams (model.cpp)."""
+    cfg = dict(n_mels=128, conv_ch=480, n_window=50, n_window_infer=800, txt_layers=28, txt_heads=16, txt_kv_heads=8,
+               head_dim=128, vocab=151936, rope_theta=1e6, rms_eps=1e-6, ln_eps=1e-5)
+    if arch == "qwen3-asr-0.6b":
+        cfg.update(enc_d=896, enc_layers=18, enc_heads=14, enc_ffn=3584, txt_h=1024, txt_ffn=3072)
+    elif arch == "qwen3-asr-1.7b":
+        cfg.update(enc_d=1024, enc_layers=24, enc_heads=16, enc_ffn=4096, txt_h=2048, txt_ffn=6144)
+    else:
+        raise ValueError(arch)
+    cfg["proj_out"] = cfg["txt_h"]
+    return cfg
+
+
+def chat_prompt(n_audio: int, sp: dict = QWEN_SPECIAL, context=()) -> list:
+    """The engine's chat prompt (processing_qwen3_asr.py:534-553) with n_audio audio placeholders."""
+    return ([sp["tok_im_start"], sp["tok_system"], sp["tok_newline"]] + list(context)
+            + [sp["tok_im_end"], sp["tok_newline"], sp["tok_im_start"], sp["tok_user"], sp["tok_newline"],
+               sp["tok_audio_start"]] + [sp["tok_audio_pad"]] * n_audio
+            + [sp["tok_audio_end"], sp["tok_im_end"], sp["tok_newline"], sp["tok_im_start"], sp["tok_assistant"],
+               sp["tok_newline"]])
+
 
 class Model:
     """Oracle model: either bound to numpy tensors (GGUF-style names) or synthetic (seeded)."""
@@ -301,6 +330,14 @@ class Model:
                 a = np.ctypeslib.as_array((C.c_uint16 * int(np.prod(shape))).from_address(p)).copy().reshape(shape)
             out[name] = a
         return out
+
+    def export_one(self, name: str) -> np.ndarray:
+        """one bound tensor in GGUF storage form, flattened to bytes (as Model.export_tensor returns it)"""
+        kind, shape = self.tensor_specs()[name]
+        p = lib().orc_model_get(self.h, name.encode())
+        assert p, name
+        n = shape[0] * shape[1] // QK * QBYTES if kind == "q8" else int(np.prod(shape)) * (4 if kind == "f32" else 2)
+        return np.ctypeslib.as_array((C.c_uint8 * n).from_address(p)).copy()
 
     def audio_tokens(self, t_valid: int) -> int:
         return lib().orc_audio_tokens(int(t_valid))

@@ -14,6 +14,18 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs on the GPU box via gpurun)")
 
 
+def record(test: str, **observed):
+    """Append the errors a parity test observed to $QASR_PARITY_LOG (JSON lines) — the evidence the bounds written
+    in the tests are set from (about 2x the observed values)."""
+    import json
+
+    path = os.environ.get("QASR_PARITY_LOG")
+    if path:
+        with open(path, "a") as f:
+            f.write(json.dumps({"test": test, **{k: (float(v) if hasattr(v, "__float__") else v)
+                                                 for k, v in observed.items()}}) + "\n")
+
+
 @pytest.fixture(scope="session")
 def torch_dev():
     import torch

@@ -16,6 +16,13 @@ Sources — every fixture is data (inputs + expected outputs); no reference sour
   * hf_tiny.npz        — transformers 5.15 qwen3_asr (the in-container restatement of the model math, NOT the
                          reference engine) on a tiny seeded config: log-mel, encoder/projector outputs and
                          decoder logits, with weights from the shared synthetic generator (Q8_0 dequantised).
+  * parse.json         — (language, transcription) from transformers' Qwen3-ASR output parser
+                         (processing_qwen3_asr.py:159-196, the in-container restatement; transcribe.cpp's own
+                         parser is absent, so parity with it stays unpinned) on hand-written and seeded cases.
+  * wav/*.wav + wav_expected.npz — path-mode inputs (qwen3_asr_server.py:256-267): the reference's own
+                         Qwen3ASRServer._load_audio run on these files with soundfile (absent here) replaced by a
+                         stub that restates libsndfile's WAV decoding (integer PCM / 2^(bits-1), u8 − 128, float32
+                         as is); the channel mean and _resample are the reference's code.
 
 Usage: python tests/golden/make_golden.py   (needs /root/reference + transformers; not run on the GPU box)
 """
@@ -93,7 +100,7 @@ sys.path.insert(0, %r)
 import server_common, qwen3_asr_server
 rng = np.random.default_rng(7)
 out = {"decode": [], "resample": []}
-for n, sr in [(1, 16000), (160, 16000), (3201, 8000), (16000, 44100)]:
+for n, sr in [(1, 16000), (160, 16000), (3201, 8000), (16000, 44100), (480, 16000.5)]:
     pcm = rng.integers(-32768, 32768, size=n).astype("<i2")
     payload = base64.b64encode(pcm.tobytes()).decode()
     audio, dur = server_common.decode_inline_audio(payload, "pcm_s16le", sr)
@@ -107,7 +114,8 @@ for payload, fmt, sr in [("", "pcm_s16le", 16000), ("AAE=", "pcm_s16le", 0), ("A
     except Exception as e:
         errs.append({"payload": payload, "format": fmt, "sample_rate": sr, "error": str(e)})
 out["decode_errors"] = errs
-for n, sr in [(100, 8000), (441, 44100), (1000, 22050), (16000, 48000), (5, 16000), (0, 8000), (7, 96000)]:
+for n, sr in [(100, 8000), (441, 44100), (1000, 22050), (16000, 48000), (5, 16000), (0, 8000), (7, 96000),
+              (1000, 16000.5), (441, 44100.7), (800, 8000.25), (3, 15999.9)]:
     x = rng.standard_normal(n).astype(np.float32)
     y = qwen3_asr_server.Qwen3ASRServer._resample(x, sr)
     out["resample"].append({"x": x.astype(float).tolist(), "sr": sr, "y": np.asarray(y, np.float32).astype(float).tolist()})
@@ -409,7 +417,145 @@ def make_hf_tiny():
     print("hf_tiny.npz", {k: v.shape for k, v in out.items()})
 
 
+# ---------------------------------------------------------------------------------------------- transcript parse
+def make_parse():
+    from transformers.models.qwen3_asr.processing_qwen3_asr import _parse_single_output
+
+    cases = ["language English<asr_text>Hello world.", "language None<asr_text>", "LANGUAGE NONE<asr_text> tail ",
+             "language Chinese<asr_text>你好，世界。", "\n\n  language Japanese\nsecond line<asr_text> こんにちは ",
+             "no tag at all  ", "Chinese<asr_text>text", "language <asr_text>abc", "language  <asr_text>x",
+             "system\nassistant\nlanguage English<asr_text>after assistant", "", "   \n\t ", "<asr_text>only text",
+             "language German<asr_text>a<asr_text>b", "Language French\r\nfoo<asr_text> bar",
+             "language English<asr_text>" + "a" * 25 + "b", "language English<asr_text>" + "哈" * 21 + "结束",
+             "x" * 20 + "y", "language English<asr_text>" + "ab" * 25 + "c",
+             "language English<asr_text>pre " + "la " * 30 + "post",
+             "language Chinese<asr_text>" + "我们" * 20 + "然后" + "好" * 30,
+             "　language Korean　<asr_text>　텍스트　", "language English x<asr_text>y"]
+    rng = np.random.default_rng(3)
+    alpha = ["a", "b", " ", "\n", "language ", "<asr_text>", "None", "你", "assistant\n", "ab", "ABC"]
+    for _ in range(150):
+        k = int(rng.integers(1, 12))
+        parts = [alpha[int(i)] for i in rng.integers(0, len(alpha), size=k)]
+        reps = int(rng.integers(0, 3))
+        if reps:
+            parts.append(alpha[int(rng.integers(0, len(alpha)))] * int(rng.integers(15, 45)))
+        cases.append("".join(parts))
+    out = []
+    for c in cases:
+        r = _parse_single_output(c)
+        out.append({"raw": c, "language": r["language"] or "", "text": r["transcription"]})
+    json.dump(out, open(os.path.join(HERE, "parse.json"), "w"), ensure_ascii=False)
+    print("parse.json", len(out))
+
+
+# ---------------------------------------------------------------------------------------------- path-mode WAV
+def _wav_bytes(frames: np.ndarray, rate: int, fmt: int, bits: int, extensible=False) -> bytes:
+    """RIFF/WAVE: frames [n][ch] already in the sample type's integer/float domain"""
+    import struct
+
+    ch = frames.shape[1]
+    if bits == 24:
+        v = frames.astype("<i4").reshape(-1)
+        data = np.stack([(v & 0xFF), (v >> 8) & 0xFF, (v >> 16) & 0xFF], 1).astype(np.uint8).tobytes()
+    else:
+        dt = {8: np.uint8, 16: "<i2", 32: "<f4" if fmt == 3 else "<i4"}[bits]
+        data = frames.astype(dt).tobytes()
+    ba = ch * bits // 8
+    if extensible:
+        sub = struct.pack("<HII", bits, (1 << ch) - 1, fmt) + b"\x00\x00\x00\x00\x10\x00\x80\x00\x00\xaa\x00\x38\x9b\x71"
+        fmt_chunk = struct.pack("<HHIIHHH", 0xFFFE, ch, rate, rate * ba, ba, bits, 22) + sub
+    else:
+        fmt_chunk = struct.pack("<HHIIHH", fmt, ch, rate, rate * ba, ba, bits)
+    body = b"WAVE" + b"fmt " + struct.pack("<I", len(fmt_chunk)) + fmt_chunk
+    body += b"LIST" + struct.pack("<I", 4) + b"INFO"   # an unrelated chunk before the data
+    body += b"data" + struct.pack("<I", len(data)) + data + (b"\x00" if len(data) % 2 else b"")
+    return b"RIFF" + struct.pack("<I", len(body)) + body
+
+
+def make_wav():
+    rng = np.random.default_rng(11)
+    wdir = os.path.join(HERE, "wav")
+    os.makedirs(wdir, exist_ok=True)
+    specs = [  # name, rate, channels, fmt, bits, seconds, extensible
+        ("pcm16_stereo_44k1", 44100, 2, 1, 16, 0.6, False),
+        ("pcm24_mono_48k", 48000, 1, 1, 24, 0.55, False),
+        ("float32_mono_16k", 16000, 1, 3, 32, 0.7, False),
+        ("pcm8_mono_8k", 8000, 1, 1, 8, 0.8, False),
+        ("pcm32_stereo_22k05", 22050, 2, 1, 32, 0.6, False),
+        ("pcm16_ext_3ch_16k", 16000, 3, 1, 16, 0.3, True),
+    ]
+    for name, rate, ch, fmt, bits, secs, ext in specs:
+        n = int(rate * secs)
+        x = (0.4 * np.sin(2 * np.pi * 220 * np.arange(n)[:, None] / rate + np.arange(ch)) +
+             0.05 * rng.standard_normal((n, ch)))
+        if fmt == 3:
+            fr = x.astype(np.float32)
+        elif bits == 8:
+            fr = np.clip(np.round(x * 127 + 128), 0, 255)
+        else:
+            fr = np.clip(np.round(x * (2 ** (bits - 1) - 1)), -(2 ** (bits - 1)), 2 ** (bits - 1) - 1)
+        open(os.path.join(wdir, name + ".wav"), "wb").write(_wav_bytes(fr, rate, fmt, bits, ext))
+    # a 4-bit IMA ADPCM header: refused (an error reply), never a division by zero
+    import struct
+
+    adpcm = struct.pack("<HHIIHHHH", 0x11, 1, 16000, 8000, 256, 4, 2, 505)
+    body = b"WAVE" + b"fmt " + struct.pack("<I", len(adpcm)) + adpcm + b"data" + struct.pack("<I", 512) + bytes(512)
+    open(os.path.join(wdir, "adpcm4_mono_16k.wav"), "wb").write(b"RIFF" + struct.pack("<I", len(body)) + body)
+    open(os.path.join(wdir, "not_a_wav.wav"), "wb").write(b"OggS" + bytes(60))
+    code = r"""
+import json, os, struct, sys, types
+import numpy as np
+sys.path.insert(0, %r)
+sf = types.ModuleType("soundfile")
+def read(path, dtype="float32", always_2d=True):
+    d = open(path, "rb").read()
+    if d[:4] != b"RIFF" or d[8:12] != b"WAVE":
+        raise RuntimeError("Error opening %%r: Format not recognised." %% path)
+    pos, fmt = 12, None
+    while pos + 8 <= len(d):
+        cid, sz = d[pos:pos + 4], struct.unpack("<I", d[pos + 4:pos + 8])[0]
+        b = pos + 8
+        if cid == b"fmt ":
+            fmt, ch, rate = struct.unpack("<HHI", d[b:b + 8]); bits = struct.unpack("<H", d[b + 14:b + 16])[0]
+            if fmt == 0xFFFE: fmt = struct.unpack("<H", d[b + 24:b + 26])[0]
+        elif cid == b"data":
+            raw = d[b:b + sz]
+            if fmt == 3: x = np.frombuffer(raw, "<f4").astype(np.float32)
+            elif bits == 16: x = np.frombuffer(raw, "<i2").astype(np.float32) / np.float32(2 ** 15)
+            elif bits == 32: x = (np.frombuffer(raw, "<i4").astype(np.float32) / np.float32(2 ** 31)).astype(np.float32)
+            elif bits == 8: x = (np.frombuffer(raw, np.uint8).astype(np.float32) - 128) / np.float32(128)
+            elif bits == 24:
+                u = np.frombuffer(raw, np.uint8).reshape(-1, 3).astype(np.int32)
+                v = ((u[:, 0] << 8) | (u[:, 1] << 16) | (u[:, 2] << 24)) >> 8
+                x = v.astype(np.float32) / np.float32(2 ** 23)
+            else: raise RuntimeError("unsupported")
+            return x.reshape(-1, ch).astype(np.float32), rate
+        pos = b + sz + (sz & 1)
+    raise RuntimeError("no data")
+sf.read = read
+sys.modules["soundfile"] = sf
+import qwen3_asr_server
+srv = qwen3_asr_server.Qwen3ASRServer.__new__(qwen3_asr_server.Qwen3ASRServer)
+out = {}
+wdir = %r
+for f in sorted(os.listdir(wdir)):
+    if f.startswith(("adpcm", "not_a")): continue
+    audio, dur, mode = srv._load_audio(os.path.join(wdir, f), None, None, None)
+    out[f] = {"audio": np.asarray(audio, np.float32).astype(float).tolist(), "duration": dur, "mode": mode}
+print(json.dumps(out))
+""" % (REF_RES, wdir)
+    env = dict(os.environ, LIGHT_WHISPER_DATA_DIR=tempfile.mkdtemp())
+    res = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env, check=True)
+    data = json.loads(res.stdout.strip().splitlines()[-1])
+    arrs = {}
+    for k, v in data.items():
+        arrs[k + "__audio"] = np.asarray(v["audio"], np.float32)
+        arrs[k + "__duration"] = np.float64(v["duration"])
+    np.savez_compressed(os.path.join(HERE, "wav_expected.npz"), **arrs)
+    print("wav_expected.npz", {k: len(v["audio"]) for k, v in data.items()})
+
+
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["vad_post", "audio_io", "protocol", "dfsmn", "hf_tiny"]
+    which = sys.argv[1:] or ["vad_post", "audio_io", "protocol", "dfsmn", "hf_tiny", "parse", "wav"]
     for w in which:
         globals()[f"make_{w}"]()

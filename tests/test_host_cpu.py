@@ -111,3 +111,54 @@ def test_utf8_replace_matches_python():
     for b in cases:
         _lib.check(lib.qasr_utf8_replace_invalid(b, len(b), buf, 512, C.byref(n)))
         assert buf.raw[: n.value] == b.decode("utf-8", "replace").encode(), b
+
+
+def test_parse_transcript_matches_restatement():
+    """qasr_parse_transcript (what result.language / result.text carry, qwen3_asr_server.py:326-327) against the
+    in-container Qwen3-ASR parser (transformers processing_qwen3_asr.py:159-196, golden parse.json): "language None",
+    multi-line prefixes, no tag, text after "assistant\\n", the repetition fix.  Parity with transcribe.cpp's own
+    parser stays unpinned (absent)."""
+    lib = _lib.load()
+    cases = json.load(open(os.path.join(G, "parse.json"), encoding="utf-8"))
+    assert len(cases) > 150
+    for c in cases:
+        raw = c["raw"].encode("utf-8")
+        ln, tn = C.c_size_t(), C.c_size_t()
+        _lib.check(lib.qasr_parse_transcript(raw, len(raw), None, 0, C.byref(ln), None, 0, C.byref(tn)))
+        lb, tb = C.create_string_buffer(ln.value + 1), C.create_string_buffer(tn.value + 1)
+        _lib.check(lib.qasr_parse_transcript(raw, len(raw), lb, ln.value, C.byref(ln), tb, tn.value, C.byref(tn)))
+        got = (lb.raw[: ln.value].decode("utf-8"), tb.raw[: tn.value].decode("utf-8"))
+        assert got == (c["language"], c["text"]), c["raw"]
+
+
+def _load_path(path):
+    lib = _lib.load()
+    n = C.c_size_t()
+    rc = lib.qasr_audio_load_path(path.encode(), None, 0, C.byref(n))
+    if rc != 0:
+        return rc, lib.qasr_last_error().decode()
+    out = np.empty(max(1, n.value), np.float32)
+    _lib.check(lib.qasr_audio_load_path(path.encode(), out.ctypes.data_as(C.c_void_p), out.size, C.byref(n)))
+    return 0, out[: n.value]
+
+
+def test_audio_load_path_matches_reference():
+    """Path-mode input (qwen3_asr_server.py:256-267): 16/24/32-bit PCM, 8-bit, float32, stereo and 3-channel
+    WAVE_FORMAT_EXTENSIBLE files at 8-48 kHz → the reference _load_audio's samples (channel mean + _resample),
+    bit for bit (golden wav_expected.npz; soundfile's decoding restated, see make_golden.py)."""
+    exp = np.load(os.path.join(G, "wav_expected.npz"))
+    names = sorted({k.split("__")[0] for k in exp.files})
+    assert len(names) == 6
+    for name in names:
+        rc, got = _load_path(os.path.join(G, "wav", name))
+        assert rc == 0, got
+        ref = exp[name + "__audio"]
+        assert got.size == ref.size and np.array_equal(got, ref), (name, np.abs(got - ref).max())
+        assert got.size / 16000.0 == float(exp[name + "__duration"])
+
+
+def test_audio_load_path_errors():
+    rc, msg = _load_path(os.path.join(G, "wav", "adpcm4_mono_16k.wav"))
+    assert rc == 3 and "Unsupported WAV sample format" in msg      # refused, not a division by zero
+    rc, msg = _load_path(os.path.join(G, "wav", "not_a_wav.wav"))
+    assert rc == 3 and msg.endswith("Format not recognised.")

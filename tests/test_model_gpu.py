@@ -8,6 +8,7 @@ import numpy as np
 import pytest
 
 import oracle
+from conftest import record
 from make_golden import TINY, TINY_SEED
 
 pytestmark = pytest.mark.gpu
@@ -86,9 +87,12 @@ def test_encoder(gpu, orc, golden, tag):
     emb, enc = s.encode(mel, tv, want_enc=True)
     remb, renc = orc.encode(mel, tv, want_enc=True)
     assert emb.shape == remb.shape
-    assert rel_err(enc, renc) < 2e-2 and rel_err(emb, remb) < 2e-2
+    record(f"tiny_encoder[{tag}]", enc_rel=rel_err(enc, renc), emb_rel=rel_err(emb, remb),
+           emb_vs_hf_rel=rel_err(emb, golden[f"{tag}__proj"]))
+    # observed on MI355X (r2, tags a/b/c): enc 3.3-4.1e-3, emb 1.16-1.48e-2 rel, vs HF 1.15-1.25e-2
+    assert rel_err(enc, renc) < 8e-3 and rel_err(emb, remb) < 3e-2
     # the transformers restatement (float weights, no activation quantisation): quantisation-level agreement
-    assert rel_err(emb, golden[f"{tag}__proj"]) < 6e-2
+    assert rel_err(emb, golden[f"{tag}__proj"]) < 2.5e-2
 
 
 def test_prefill_logits(gpu, orc, golden):
@@ -100,7 +104,8 @@ def test_prefill_logits(gpu, orc, golden):
     x[ids == SPECIAL["tok_audio_pad"]] = orc.encode(golden["b__mel"], int(golden["b__t_valid"]))
     ref = kv.forward(x, all_logits=True)
     got = s.prefill_logits(x)
-    assert rel_err(got, ref) < 2e-2
+    record("tiny_prefill_logits", logits_rel=rel_err(got, ref), argmax_agree=(got.argmax(1) == ref.argmax(1)).mean())
+    assert rel_err(got, ref) < 6e-3     # observed (r2): 2.8e-3
     assert (got.argmax(1) == ref.argmax(1)).mean() >= 0.95
 
 
@@ -119,7 +124,8 @@ def test_forced_decode_logits(gpu, orc, golden):
     toks, ref = _greedy_oracle(orc, audio, 12)
     got = s.forced_logits(audio, toks[:-1])     # logits before each of the 12 tokens
     assert got.shape == ref.shape
-    assert rel_err(got, ref) < 3e-2
+    record("tiny_forced_logits", logits_rel=rel_err(got, ref))
+    assert rel_err(got, ref) < 7e-3     # observed (r2): 3.4e-3
     top2 = np.sort(ref, 1)[:, -2:]
     clear = (top2[:, 1] - top2[:, 0]) > 0.02 * np.abs(ref).max()
     assert (got.argmax(1) == ref.argmax(1))[clear].all()
@@ -280,7 +286,8 @@ def test_mxfp8_precision_mode(golden, torch_dev):
         s.close()
         assert len(toks) > 0
         span = np.abs(ref).max()
-        assert np.abs(got - ref).max() < 0.1 * span
+        record("tiny_mxfp8", logits_rel_vs_q8=np.abs(got - ref).max() / span)
+        assert np.abs(got - ref).max() < 2.5e-2 * span     # observed (r2): 1.15e-2
         top2 = np.sort(ref, 1)[:, -2:]
         clear = (top2[:, 1] - top2[:, 0]) > 0.1 * span
         assert (got.argmax(1) == ref.argmax(1))[clear].all()
@@ -317,8 +324,52 @@ def test_hotword_context_prompt_matches_oracle(gpu, orc, golden):
         assert all(b.n_prompt == len(p) and b.tokens == batch[0].tokens for b in batch)
     finally:
         s.set_context([])
-    assert rel_err(got, ref) < 3e-2
+    record("tiny_hotword_forced_logits", logits_rel=rel_err(got, ref))
+    assert rel_err(got, ref) < 7e-3     # observed (r2): 3.1e-3
     top2 = np.sort(ref, 1)[:, -2:]
     clear = (top2[:, 1] - top2[:, 0]) > 0.02 * np.abs(ref).max()
     assert (got.argmax(1) == ref.argmax(1))[clear].all()
     assert s.run(audio, max_new_tokens=6).tokens == before
+
+
+def test_precision_switch_on_live_session(golden, torch_dev):
+    """set_precision on a model whose session has captured decode graphs: the session re-captures —
+    q8 → mxfp8 gives a fresh mxfp8 session's tokens, and back to q8 the original tokens (no replay of graphs that
+    read the freed fp8 images)."""
+    from qasr.transcribe_cpp import Model
+
+    m = Model.synthetic(arch=None, seed=TINY_SEED, hparams=tiny_hparams())
+    try:
+        audios = [golden["a__audio"], golden["b__audio"], golden["c__audio"]] * 2   # 6 rows: GEMM path + graphs
+        s = m.session(kv_type="f16", n_ctx=2048)
+        q8 = [r.tokens for r in s.run_batch(audios, max_new_tokens=8)]
+        m.set_precision("mxfp8")
+        live = [r.tokens for r in s.run_batch(audios, max_new_tokens=8)]
+        s2 = m.session(kv_type="f16", n_ctx=2048)
+        fresh = [r.tokens for r in s2.run_batch(audios, max_new_tokens=8)]
+        s2.close()
+        assert live == fresh
+        m.set_precision("q8")
+        assert [r.tokens for r in s.run_batch(audios, max_new_tokens=8)] == q8
+        s.close()
+    finally:
+        m.close()
+
+
+def test_single_run_decodes_to_eos_or_n_ctx(torch_dev, golden):
+    """one utterance without a cap decodes until EOS or n_ctx (the reference's session.run; ADVICE r1: the old
+    64 + 32·s default cut long outputs silently) and says when the budget, not EOS, ended it"""
+    from qasr.transcribe_cpp import Model
+
+    m = Model.synthetic(arch=None, seed=TINY_SEED, hparams=tiny_hparams())
+    try:
+        s = m.session(kv_type="f16", n_ctx=256)
+        audio = golden["a__audio"]
+        full = s.run(audio)
+        assert full.n_prompt + len(full.tokens) == 256 or not full.truncated
+        capped = s.run(audio, max_new_tokens=5)
+        assert capped.tokens == full.tokens[:5]
+        assert capped.truncated == (len(full.tokens) > 5)
+        s.close()
+    finally:
+        m.close()

@@ -80,3 +80,45 @@ def test_models_not_downloaded_without_fake(tmp_path):
     first = json.loads(res.stdout.splitlines()[0])
     assert first == {"success": False, "error": "Qwen3-ASR Q8 模型未下载: Qwen3-ASR-0.6B-Q8_0.gguf",
                      "type": "models_not_downloaded", "engine": "qwen3-asr-0.6b"}
+
+
+def test_path_mode_requests(tmp_path):
+    """audio_path requests (qwen3_asr_server.py:256-267, the app's WAV fallback funasr_service.rs:1296-1323): the reply
+    carries input_mode "path" and the duration of the decoded 16 kHz audio; an undecodable file is a
+    transcription_error reply and the server keeps serving."""
+    import numpy as np
+
+    gdir = os.path.join(os.path.dirname(__file__), "golden")
+    exp = np.load(os.path.join(gdir, "wav_expected.npz"))
+    names = sorted({k.split("__")[0] for k in exp.files})
+    reqs = [json.dumps({"action": "transcribe", "audio_path": os.path.join(gdir, "wav", n), "request_id": i})
+            for i, n in enumerate(names)]
+    reqs.append(json.dumps({"action": "transcribe", "audio_path": os.path.join(gdir, "wav", "adpcm4_mono_16k.wav"),
+                            "request_id": 50}))
+    reqs.append(json.dumps({"action": "status", "request_id": 51}))
+    res = _run_engine(reqs + ['{"action": "exit"}'], {"LIGHT_WHISPER_DATA_DIR": str(tmp_path)})
+    lines = [json.loads(ln) for ln in res.stdout.splitlines() if ln.strip()]
+    replies = {r.get("request_id"): r for r in lines[1:]}
+    for i, n in enumerate(names):
+        r = replies[i]
+        assert r["success"] is True and r["input_mode"] == "path", r
+        assert r["duration"] == float(exp[n + "__duration"])
+    bad = replies[50]
+    assert bad["success"] is False and bad["type"] == "transcription_error" and bad["input_mode"] == "path"
+    assert "Unsupported WAV sample format" in bad["error"]
+    assert replies[51]["success"] is True
+
+
+def test_fractional_sample_rate(tmp_path):
+    """a float sample_rate is used as given (decode_inline_audio duration, `_resample` target length), not truncated"""
+    import base64
+
+    import numpy as np
+
+    pcm = (np.arange(16000) % 200 - 100).astype("<i2")
+    b64 = base64.b64encode(pcm.tobytes()).decode()
+    req = json.dumps({"action": "transcribe", "audio_base64": b64, "audio_format": "pcm_s16le",
+                      "sample_rate": 16000.5, "request_id": 1})
+    res = _run_engine([req, '{"action": "exit"}'], {"LIGHT_WHISPER_DATA_DIR": str(tmp_path)})
+    r = json.loads(res.stdout.splitlines()[1])
+    assert r["success"] is True and r["duration"] == 16000 / 16000.5

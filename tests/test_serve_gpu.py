@@ -1,0 +1,147 @@
+"""`engine serve` with the real HIP backend (the process the Rust app spawns: funasr_service.rs:917-972 →
+engine.py:45-57 → server_common.BaseASRServer.run :339-437 → Qwen3ASRServer.transcribe_audio, qwen3_asr_server.py:
+269-353).  QASR_SYNTHETIC=1 gives the seeded 0.6B weights (no GGUF is provisioned); FireRedVAD, the crop, the
+decode and the reply are the production code.
+
+Checked: the init line; a transcribe whose speech FireRedVAD accepts → vad_segments > 0 and the reply's text equal
+to Session.run on the same cropped samples (the in-process C ABI, qwen3_asr_server.py:321,326); hot_words accepted
+and ignored (the reference ignores them); stats; a short interim replay (interim.rs:135-156: the last
+≤12 s re-sent each tick) followed by the final request; exit.
+"""
+import base64
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from bench import recording
+
+pytestmark = pytest.mark.gpu
+
+ENGINE = "qwen3-asr-0.6b"
+MAX_NEW = 48
+
+
+class Engine:
+    def __init__(self, tmp_path, extra=None):
+        from qasr import _lib
+
+        env = {k: v for k, v in os.environ.items() if k not in ("QASR_PROTOCOL_TEST_FAKE",)}
+        # synthetic weights rarely emit EOS: cap the natural decode (the reference decodes to EOS or n_ctx)
+        env.update(QASR_SYNTHETIC="1", QASR_MAX_NEW_TOKENS=str(MAX_NEW), LIGHT_WHISPER_DATA_DIR=str(tmp_path),
+                   HF_HUB_CACHE=str(tmp_path / "hf"), **(extra or {}))
+        self.p = subprocess.Popen([_lib.ENGINE_PATH, "serve", "--engine", ENGINE], stdin=subprocess.PIPE,
+                                  stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True, env=env)
+        self.init = json.loads(self.p.stdout.readline())
+
+    def ask(self, obj):
+        self.p.stdin.write(json.dumps(obj) + "\n")
+        self.p.stdin.flush()
+        line = self.p.stdout.readline()
+        assert line, "engine closed stdout"
+        return line, json.loads(line)
+
+    def close(self):
+        if self.p.poll() is None:
+            try:
+                self.ask({"action": "exit", "request_id": 99})
+            finally:
+                self.p.wait(timeout=30)
+
+
+def pcm_request(audio_i16, rid, hot_words=None):
+    req = {"action": "transcribe", "audio_base64": base64.b64encode(audio_i16.astype("<i2").tobytes()).decode(),
+           "audio_format": "pcm_s16le", "sample_rate": 16000, "request_id": rid}
+    if hot_words is not None:
+        req["hot_words"] = hot_words
+    return req
+
+
+@pytest.fixture(scope="module")
+def ref(torch_dev):
+    """in-process engine pieces on the same weights: the synthetic 0.6B model (seed 0, as QASR_SYNTHETIC) + VAD"""
+    from qasr.firered_vad import FireRedVad
+    from qasr.transcribe_cpp import Model
+
+    m = Model.synthetic(ENGINE, seed=0)
+    s = m.session(kv_type="f16", n_ctx=32768)
+    v = FireRedVad()
+    yield s, v
+    v.close()
+    s.close()
+    m.close()
+
+
+def expected(ref, audio_i16):
+    """what transcribe_audio replies for this PCM: FireRedVAD crop → session.run → .strip()"""
+    s, v = ref
+    a = audio_i16.astype(np.float32) / 32768.0
+    segs = v.speech_timestamps(a)
+    if not segs:
+        return None, 0
+    st, en = max(0, segs[0]["start"]), min(a.size, segs[-1]["end"])
+    return s.run(a[st:en], max_new_tokens=MAX_NEW).text.strip(), len(segs)
+
+
+def speech_clip(seconds, seed):
+    return np.clip(np.round(recording(seconds, seed) * 32768.0), -32768, 32767).astype(np.int16)
+
+
+def test_serve_real_backend(ref, tmp_path):
+    e = Engine(tmp_path)
+    try:
+        init = e.init
+        assert init["success"] is True and init["model_loaded"] is True
+        # qwen3_asr_server.py:208-223 key order; gpu_name / gpu_memory_total from hipGetDeviceProperties
+        assert list(init) == ["success", "message", "model_loaded", "engine", "backend", "device", "gpu_name",
+                              "gpu_memory_total"]
+        assert init["engine"] == ENGINE and init["backend"] == "hip" and init["gpu_name"]
+        assert init["gpu_memory_total"] > 0
+        audio = speech_clip(4.0, 3)
+        want, nseg = expected(ref, audio)
+        assert nseg > 0, "FireRedVAD must accept the test clip"
+        _, r = e.ask(pcm_request(audio, 1))
+        assert r["success"] is True and r["request_id"] == 1
+        assert r["vad_segments"] == nseg and r["input_mode"] == "memory" and r["backend"] == "hip"
+        assert r["text"] == want and r["raw_text"] == want
+        assert 0 < r["speech_duration"] <= 4.0 and r["duration"] == 4.0
+        # hot_words are accepted and ignored: the same reply (timings aside)
+        _, r2 = e.ask(pcm_request(audio, 2, hot_words=["Kubernetes", "张三", "ROCm"] * 30))
+        assert r2["text"] == want and r2["vad_segments"] == nseg
+        _, st = e.ask({"action": "stats", "request_id": 3})
+        assert st["stats"]["transcription_count"] == 2 and st["stats"]["vad_calls"] == 2
+        assert st["stats"]["backend"] == "hip" and st["request_id"] == 3
+        # silence: VAD-rejected, Qwen not run
+        _, r3 = e.ask(pcm_request(np.zeros(16000, np.int16), 4))
+        assert r3["vad_segments"] == 0 and r3["text"] == "" and r3["inference_ms"] == 0.0
+        _, st = e.ask({"action": "stats", "request_id": 5})
+        assert st["stats"]["vad_rejected"] == 1 and st["stats"]["transcription_count"] == 2
+    finally:
+        e.close()
+    assert e.p.returncode == 0
+
+
+def test_serve_interim_replay(ref, tmp_path):
+    """C3 in miniature: a recording growing in 0.7 s steps, each tick re-sends the last ≤12 s (interim.rs:135-146),
+    then the final request; every reply is the in-process result on the same crop."""
+    e = Engine(tmp_path)
+    try:
+        full = speech_clip(14.0, 4)
+        ticks = [int(t * 16000) for t in (0.7, 1.4, 2.1, 5.6, 9.8, 14.0)]
+        for i, end in enumerate(ticks):
+            win = full[max(0, end - 12 * 16000):end]
+            line, r = e.ask(pcm_request(win, 100 + i, hot_words=["热词"]))
+            assert r["success"] is True and r["request_id"] == 100 + i, line
+            if win.size < 8000:
+                assert r["text"] == "" and "vad_segments" not in r
+                continue
+            want, nseg = expected(ref, win)
+            assert r["vad_segments"] == nseg
+            assert r["text"] == (want or "")
+        _, fin = e.ask(pcm_request(full, 200))
+        want, nseg = expected(ref, full)
+        assert nseg > 0 and fin["vad_segments"] == nseg and fin["text"] == want
+    finally:
+        e.close()
