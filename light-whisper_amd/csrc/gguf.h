@@ -43,6 +43,7 @@ class GgufFile {
     std::string get_str(const std::string& key, const std::string& def) const;
     const GgufTensor* tensor(const std::string& name) const;
     const std::map<std::string, GgufTensor>& tensors() const { return tensors_; }
+    const std::map<std::string, GgufValue>& metadata() const { return kv_; }
     uint32_t version() const { return version_; }
 
    private:

@@ -761,6 +761,111 @@ __global__ __launch_bounds__(256 * KG, 2 / KG) void k_gemm_q8d(const int8_t* __r
     gemm_epilogue<TI, TJ>(acc, M, N, m0, n0, arow, bcol, fr, fq, bias, res, y, ldy, epi, yq, yd);
 }
 
+// ------------------------------------------------------------------------------------------------ GEMM (decode, K over waves)
+// Decode-sized Q8 W8A8 GEMM (a decode step's M ≤ 256 rows; every weight byte is read once per step).  One workgroup
+// owns a (16·TI)×(16·TJ) output tile over the WHOLE K and its NW waves split K into equal slices: each wave loads its
+// fragments straight from global memory into registers (no LDS staging, no barrier inside the loop — every wave is an
+// independent load stream, so a CU keeps NW waves' fragments in flight instead of one pipelined K loop), multiplies
+// with v_mfma_i32_16x16x32_i8 (one MFMA = the exact int32 sum of one Q8 block) and rescales into f32 as the other Q8
+// GEMMs do ((float)sum · (d_x·d_w), fma).  The NW partial tiles are summed once through LDS, in wave order, and wave
+// i < TI runs the shared epilogue for row fragment i.  No split-K atomics, no output memset, one launch.
+// Lane (fr, kh) holds row / column fr of a 16-row fragment and bytes [8kh, 8kh + 8) of each block: an 8-byte load per
+// fragment and block (4 lanes cover a row's 32-byte block; the G blocks of a load group cover its 128-byte line).
+template <int TI, int TJ, int NW>
+__global__ __launch_bounds__(64 * NW) void k_gemm_q8_ks(const int8_t* __restrict__ X, const float* __restrict__ Xd,
+                                                        int M, const int8_t* __restrict__ W,
+                                                        const __half* __restrict__ Wsc, int N, int K,
+                                                        const float* __restrict__ bias, const float* res, float* y,
+                                                        int ldy, int epi, int8_t* __restrict__ yq,
+                                                        float* __restrict__ yd) {
+    constexpr int BM = 16 * TI, BN = 16 * TJ, G = 4;   // G blocks per load group
+    // dynamic LDS: the tile's activation scales [nb][BM] (block-major, so a lane's 4 rows of one block are one
+    // ds_read_b128) during the K loop, then the NW partial tiles [NW][TI·TJ][64] float4 (host sizes the max)
+    extern __shared__ float4 smem_ks[];
+    float* sas = (float*)smem_ks;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM;
+    const int nb = K / QK, per = nb / NW, b0 = wave * per;   // host: nb % (NW·G) == 0
+    const int fr = lane & 15, kh = lane >> 4, fq = 4 * kh;
+    for (int idx = threadIdx.x; idx < nb * BM; idx += 64 * NW) {
+        const int row = idx / nb, blk = idx % nb;   // consecutive threads read consecutive blocks of a row
+        sas[blk * BM + row] = Xd[(size_t)min(m0 + row, M - 1) * nb + blk];
+    }
+    const int8_t* ap[TI];
+    const int8_t* bp[TJ];
+    const __half* sbp[TJ];
+#pragma unroll
+    for (int i = 0; i < TI; i++) ap[i] = X + (size_t)min(m0 + 16 * i + fr, M - 1) * K + 8 * kh;
+#pragma unroll
+    for (int j = 0; j < TJ; j++) {
+        const int c = min(n0 + 16 * j + fr, N - 1);
+        bp[j] = W + (size_t)c * K + 8 * kh;
+        sbp[j] = Wsc + (size_t)c * nb;
+    }
+    float acc[TI][TJ][4];
+#pragma unroll
+    for (int i = 0; i < TI; i++)
+#pragma unroll
+        for (int j = 0; j < TJ; j++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) acc[i][j][r] = 0.f;
+    __syncthreads();
+    for (int g0 = b0; g0 < b0 + per; g0 += G) {
+        long a[G][TI], b[G][TJ];
+        uint2 sb[TJ];
+#pragma unroll
+        for (int g = 0; g < G; g++) {
+#pragma unroll
+            for (int j = 0; j < TJ; j++) b[g][j] = __builtin_nontemporal_load((const long*)(bp[j] + 32 * (g0 + g)));
+#pragma unroll
+            for (int i = 0; i < TI; i++) a[g][i] = *(const long*)(ap[i] + 32 * (g0 + g));
+        }
+#pragma unroll
+        for (int j = 0; j < TJ; j++) sb[j] = *(const uint2*)(sbp[j] + g0);
+#pragma unroll
+        for (int g = 0; g < G; g++) {
+            float sw[TJ];
+#pragma unroll
+            for (int j = 0; j < TJ; j++) {
+                const uint32_t h2 = g < 2 ? sb[j].x : sb[j].y;
+                sw[j] = __half2float(__ushort_as_half((unsigned short)((g & 1) ? h2 >> 16 : h2 & 0xffff)));
+            }
+#pragma unroll
+            for (int i = 0; i < TI; i++) {
+                const float4 sx = *(const float4*)(sas + (g0 + g) * BM + 16 * i + fq);
+                const float sxr[4] = {sx.x, sx.y, sx.z, sx.w};
+#pragma unroll
+                for (int j = 0; j < TJ; j++) {
+                    const v4i c = __builtin_amdgcn_mfma_i32_16x16x32_i8(a[g][i], b[g][j], v4i{0, 0, 0, 0}, 0, 0, 0);
+#pragma unroll
+                    for (int r = 0; r < 4; r++) acc[i][j][r] = fmaf((float)c[r], sxr[r] * sw[j], acc[i][j][r]);
+                }
+            }
+        }
+    }
+    __syncthreads();   // the scale image is dead: its LDS takes the partial tiles
+    float4* red = smem_ks;   // [NW][TI·TJ][64]
+#pragma unroll
+    for (int i = 0; i < TI; i++)
+#pragma unroll
+        for (int j = 0; j < TJ; j++)
+            red[(wave * TI * TJ + i * TJ + j) * 64 + lane] = make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+    __syncthreads();
+    if (wave >= TI) return;
+    float out[1][TJ][4];
+#pragma unroll
+    for (int j = 0; j < TJ; j++) {
+        float4 t = red[(wave * TJ + j) * 64 + lane];
+#pragma unroll
+        for (int w = 1; w < NW; w++) {
+            const float4 v = red[(w * TI * TJ + wave * TJ + j) * 64 + lane];
+            t.x += v.x, t.y += v.y, t.z += v.z, t.w += v.w;
+        }
+        out[0][j][0] = t.x, out[0][j][1] = t.y, out[0][j][2] = t.z, out[0][j][3] = t.w;
+    }
+    gemm_epilogue<1, TJ>(out, M, N, m0, n0, 16 * wave, 0, fr, fq, bias, res, y, ldy, epi, yq, yd);
+}
+
 // ------------------------------------------------------------------------------------------------ GEMM (f16 operands)
 // Same contract as k_gemm_q8d, with the int8 operands carried as f16 (every Q8 value is exact in f16):
 // v_mfma_f32_16x16x32_f16 returns each block's exact integer sum already in f32, so the per-block rescale is
@@ -925,15 +1030,44 @@ static void launch_gemm_dma(dim3 grid, hipStream_t s, const int8_t* xq, const fl
 
 // GEMM configurations: 0..3 register-staged kernel (any K % 32 == 0), 4..11 LDS-DMA kernel, 2×2 waves, stages of
 // 64 (4..7) or 128 (8..11) K (K % bk == 0); 12..13 LDS-DMA, 4×1 waves (64-column wave tiles), K-128 stages.
-struct GemmCfg { int bm, bn, bk; bool dma; };
+struct GemmCfg { int bm, bn, bk; bool dma; int ks = 0; };   // ks: waves of the K-over-waves decode kernel (bk unused)
 static const GemmCfg kGemmCfgs[] = {
     {128, 128, 128, false}, {64, 128, 128, false}, {64, 64, 128, false}, {32, 64, 128, false},   // 0..3
     {128, 128, 64, true}, {64, 128, 64, true}, {64, 64, 64, true}, {128, 64, 64, true},          // 4..7
     {128, 128, 128, true}, {64, 128, 128, true}, {64, 64, 128, true}, {128, 64, 128, true},      // 8..11
     {64, 64, 128, true}, {128, 64, 128, true},                                                   // 12..13 4×1 waves
     {64, 64, 128, true}, {64, 64, 128, true},                        // 14..15 = 10 / 12 with two K groups (8 waves)
+    // decode-sized tiles with deep rings, meant for full-K (no split-K) launches of ≥ 256 workgroups
+    {32, 32, 128, true}, {32, 64, 128, true}, {64, 32, 128, true},   // 16..18 rings of 8 / 6 / 6
+    {64, 64, 128, true}, {64, 64, 128, true},                        // 19..20 = 14 / 15 (two K groups) with rings of 6
+    {64, 64, 128, true}, {64, 64, 128, true}, {32, 128, 128, true},  // 21..23 2×2 / 4×1 waves ring 6, 2×2 (16×64) ring 4
+    // 24..30 decode kernel k_gemm_q8_ks<TI, TJ, NW>: full K per workgroup, K split over NW waves
+    {32, 16, 0, false, 16}, {32, 32, 0, false, 16}, {64, 16, 0, false, 16}, {64, 32, 0, false, 8},
+    {16, 64, 0, false, 16}, {32, 64, 0, false, 8}, {64, 64, 0, false, 8},
 };
 constexpr int kNumGemmCfgs = sizeof(kGemmCfgs) / sizeof(kGemmCfgs[0]);
+
+template <int TI, int TJ, int NW>
+static void launch_ks(hipStream_t s, const int8_t* xq, const float* xd, int M, const Q8Mat& W, const float* bias,
+                      const float* res, float* y, int ldy, int epi, int8_t* yq, float* yd) {
+    const dim3 grid(cdiv(W.N, 16 * TJ), cdiv(M, 16 * TI));
+    const size_t lds = std::max<size_t>((size_t)(W.K / QK) * 16 * TI * 4, (size_t)NW * TI * TJ * 64 * 16);
+    QASR_CHECK(lds <= 160 * 1024, QASR_E_INVALID, "gemm_q8: decode tile's LDS exceeds 160 KB");
+    k_gemm_q8_ks<TI, TJ, NW><<<grid, 64 * NW, lds, s>>>(xq, xd, M, W.qs, W.sc, W.N, W.K, bias, res, y, ldy, epi, yq, yd);
+}
+
+static void launch_ks_cfg(int cfg, hipStream_t s, const int8_t* xq, const float* xd, int M, const Q8Mat& W,
+                          const float* bias, const float* res, float* y, int ldy, int epi, int8_t* yq, float* yd) {
+    switch (cfg) {
+        case 24: launch_ks<2, 1, 16>(s, xq, xd, M, W, bias, res, y, ldy, epi, yq, yd); break;
+        case 25: launch_ks<2, 2, 16>(s, xq, xd, M, W, bias, res, y, ldy, epi, yq, yd); break;
+        case 26: launch_ks<4, 1, 16>(s, xq, xd, M, W, bias, res, y, ldy, epi, yq, yd); break;
+        case 27: launch_ks<4, 2, 8>(s, xq, xd, M, W, bias, res, y, ldy, epi, yq, yd); break;
+        case 28: launch_ks<1, 4, 16>(s, xq, xd, M, W, bias, res, y, ldy, epi, yq, yd); break;
+        case 29: launch_ks<2, 4, 8>(s, xq, xd, M, W, bias, res, y, ldy, epi, yq, yd); break;
+        default: launch_ks<4, 4, 8>(s, xq, xd, M, W, bias, res, y, ldy, epi, yq, yd); break;
+    }
+}
 
 static void launch_cfg(int cfg, dim3 grid, hipStream_t s, const int8_t* xq, const float* xd, int M, const Q8Mat& W,
                        const float* bias, const float* res, float* y, int ldy, int epi, int sps, int8_t* yq,
@@ -955,7 +1089,15 @@ static void launch_cfg(int cfg, dim3 grid, hipStream_t s, const int8_t* xq, cons
         case 12: launch_gemm_dma<4, 1, 1, 4, 3, 128>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
         case 13: launch_gemm_dma<4, 1, 2, 4, 3, 128>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
         case 14: launch_gemm_dma<2, 2, 2, 2, 3, 128, 2>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
-        default: launch_gemm_dma<4, 1, 1, 4, 3, 128, 2>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
+        case 15: launch_gemm_dma<4, 1, 1, 4, 3, 128, 2>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
+        case 16: launch_gemm_dma<2, 2, 1, 1, 8, 128>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
+        case 17: launch_gemm_dma<2, 2, 1, 2, 6, 128>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
+        case 18: launch_gemm_dma<2, 2, 2, 1, 6, 128>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
+        case 19: launch_gemm_dma<2, 2, 2, 2, 6, 128, 2>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
+        case 20: launch_gemm_dma<4, 1, 1, 4, 6, 128, 2>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
+        case 21: launch_gemm_dma<2, 2, 2, 2, 6, 128>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
+        case 22: launch_gemm_dma<4, 1, 1, 4, 6, 128>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
+        default: launch_gemm_dma<2, 2, 1, 4, 4, 128>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
     }
 }
 
@@ -1164,7 +1306,10 @@ void gemm_mx(const uint8_t* x8, const uint8_t* xs, int M, const Q8Mat& W, const 
     int cfg = force_cfg;
     if (cfg < 0)
         cfg = M > 256 ? ((W.K <= 1024 || (W.N <= 2048 && W.K <= 2048)) ? 4 : 0) : W.N >= 32768 ? (M > 128 ? 0 : 2) : 1;
-    if (epi == EPI_SWIGLU && cfg == 1) cfg = 2;
+    // the SwiGLU epilogue needs 64-column wave tiles (TJ = 4): cfg 0 / 2 / 3; 64×64 → 64×128, 128×64 → 128×128
+    if (epi == EPI_SWIGLU && (cfg == 1 || cfg == 4)) cfg = cfg == 1 ? 2 : 0;
+    QASR_CHECK(epi != EPI_SWIGLU || cfg == 0 || cfg == 2 || cfg == 3, QASR_E_INVALID,
+               "gemm_mx: SwiGLU epilogue needs a 64-column wave tile");
     const int bm = cfg == 0 || cfg == 3 || cfg == 4 ? 128 : 64, bn = cfg == 0 || cfg == 2 || cfg == 3 ? 128 : 64;
     const int steps = W.K / 128, tiles = cdiv(W.N, bn) * cdiv(M, bm);
     const bool can_split = (epi == EPI_STORE || epi == EPI_RESID) && ldy == W.N && (epi != EPI_RESID || res == y);
@@ -1209,7 +1354,11 @@ void gemm_q8(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const flo
         return;
     }
     ProfScope ps(s, "gemm_q8", 2.0 * M * W.N * W.K, q8_bytes(M, W, epi));
-    auto usable = [&](int c) { return !kGemmCfgs[c].dma || W.K % kGemmCfgs[c].bk == 0; };
+    auto usable = [&](int c) {
+        const GemmCfg& g = kGemmCfgs[c];
+        if (g.ks) return W.K % (QK * 4 * g.ks) == 0 && (epi != EPI_GELU_Q8 || g.bn % 32 == 0);
+        return !g.dma || W.K % g.bk == 0;
+    };
     int pick;
     if (W.K % 64 == 0) {
         // measured on the engine's shapes (tools/gemm_tune.py, profiles/): 128×128 tiles with K-64 stages on prefill
@@ -1232,10 +1381,17 @@ void gemm_q8(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const flo
     }
     if (force_cfg >= 0 && force_cfg < kNumGemmCfgs && usable(force_cfg)) pick = force_cfg;
     const GemmCfg& cf = kGemmCfgs[pick];
+    if (cf.ks) {   // decode kernel: one launch over the whole K, no split-K, no memset
+        QASR_CHECK(epi != EPI_SWIGLU || (cf.bn == 64 && W.N % 64 == 0 && yq && yd), QASR_E_INVALID,
+                   "gemm_q8: SwiGLU epilogue needs a 64-column wave tile");
+        QASR_CHECK(epi != EPI_GELU_Q8 || (W.N % 32 == 0 && yq && yd), QASR_E_INVALID, "gemm_q8: GELU+Q8 epilogue shape");
+        launch_ks_cfg(pick, s, xq, xd, M, W, bias, res, y, ldy, epi, yq, yd);
+        return;
+    }
     const int steps = cf.dma ? W.K / cf.bk : cdiv(W.K, GBK);
     if (epi == EPI_SWIGLU) {
         QASR_CHECK(W.N % 64 == 0 && yq && yd, QASR_E_INVALID, "gemm_q8: SwiGLU epilogue needs N % 64 == 0");
-        QASR_CHECK(cf.bn == 128 || pick == 12 || pick == 13 || pick == 15, QASR_E_INVALID,
+        QASR_CHECK(cf.bn == 128 || pick == 12 || pick == 13 || pick == 15 || pick == 20 || pick == 22, QASR_E_INVALID,
                    "gemm_q8: SwiGLU epilogue needs a 64-column wave tile");
         dim3 grid(cdiv(W.N, cf.bn), cdiv(M, cf.bm), 1);
         launch_cfg(pick, grid, s, xq, xd, M, W, bias, res, y, ldy, epi, steps, yq, yd);

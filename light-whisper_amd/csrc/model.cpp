@@ -374,74 +374,256 @@ std::unique_ptr<Model> make_synthetic_shell(const qasr_hparams& hp, const std::s
 }
 
 // ----------------------------------------------------------------------------------------------- GGUF
-// Metadata keys and tensor names of this engine's GGUF convention (DESIGN.md §tensor names).  The text
-// decoder uses llama.cpp's qwen3 names; audio tensors use the "a." prefix.  Every tensor is validated
-// against the shape implied by the metadata before upload.
+// The pinned checkpoints (Qwen3-ASR-{0.6B,1.7B}-Q8_0.gguf, hf_cache_utils.py:11-26, opened by transcribe_cpp.Model at
+// qwen3_asr_server.py:122) are not in this container, so their tensor names and metadata keys are unknown.  The
+// loader therefore resolves every logical tensor through a table of candidate names — this engine's exporter
+// (llama.cpp-style text names, "a." audio prefix), the original qwen_asr / HF state-dict names ("thinker.audio_tower.*",
+// "thinker.model.*", "model.language_model.*", "model.multi_modal_projector.linear_{1,2}") and llama.cpp mtmd-style
+// audio names — validates each one's shape, derives every hyper-parameter a shape determines from the shapes, and fails
+// loudly (QASR_E_FORMAT, the server's init_error) on a tensor it cannot map, a tensor it needs but cannot find, a
+// shape or type it does not support, and missing required metadata (RoPE base, RMSNorm epsilon).
+namespace {
+
+bool starts(const std::string& s, const char* p) { return s.compare(0, strlen(p), p) == 0; }
+
+std::vector<std::string> name_candidates(const std::string& canon) {
+    std::vector<std::string> out = {canon};
+    static const char* AP[] = {"thinker.audio_tower.", "model.audio_tower.", "audio_tower.", "audio."};
+    static const char* TP[] = {"thinker.model.", "model.language_model.", "language_model.model.", "model.",
+                               "language_model."};
+    auto audio = [&](const std::string& tail) {
+        for (const char* p : AP) out.push_back(p + tail);
+    };
+    auto text = [&](const std::string& tail) {
+        for (const char* p : TP) out.push_back(p + tail);
+    };
+    const size_t dot = canon.rfind('.');
+    const std::string leaf = canon.substr(dot + 1);   // weight / bias
+    int l = -1, i = -1;
+    char part[64] = {0};
+    if (sscanf(canon.c_str(), "a.conv%d.%*s", &i) == 1 && canon.compare(0, 7, "a.conv_") != 0) {
+        audio("conv2d" + std::to_string(i) + "." + leaf);
+        out.push_back("a.conv2d." + std::to_string(i) + "." + leaf);
+    } else if (canon == "a.conv_out.weight") {
+        audio("conv_out.weight");
+        out.push_back("a.conv_out.weight");
+    } else if (sscanf(canon.c_str(), "a.blk.%d.%63[^.]", &l, part) == 2) {
+        const std::string p = part, L = "layers." + std::to_string(l) + ".";
+        static const std::pair<const char*, const char*> m[] = {
+            {"ln1", "self_attn_layer_norm"}, {"ln2", "final_layer_norm"}, {"attn_q", "self_attn.q_proj"},
+            {"attn_k", "self_attn.k_proj"}, {"attn_v", "self_attn.v_proj"}, {"attn_out", "self_attn.out_proj"},
+            {"ffn_up", "fc1"}, {"ffn_down", "fc2"}};
+        for (auto& kv : m)
+            if (p == kv.first) audio(L + kv.second + "." + leaf);
+        if (p == "attn_out") out.push_back("a.blk." + std::to_string(l) + ".attn_output." + leaf);
+    } else if (starts(canon, "a.ln_post.")) {
+        audio("ln_post." + leaf);
+        out.push_back("a.post_ln." + leaf);
+    } else if (starts(canon, "a.proj1.") || starts(canon, "a.proj2.")) {
+        const char k = canon[6];
+        audio(std::string("proj") + k + "." + leaf);
+        out.push_back(std::string("model.multi_modal_projector.linear_") + k + "." + leaf);
+        out.push_back(std::string("multi_modal_projector.linear_") + k + "." + leaf);
+        out.push_back(std::string("mm.a.mlp.") + k + "." + leaf);
+    } else if (canon == "token_embd.weight") {
+        text("embed_tokens.weight");
+    } else if (canon == "output_norm.weight") {
+        text("norm.weight");
+    } else if (canon == "output.weight") {
+        out.push_back("thinker.lm_head.weight");
+        out.push_back("lm_head.weight");
+    } else if (sscanf(canon.c_str(), "blk.%d.%63[^.]", &l, part) == 2) {
+        const std::string p = part, L = "layers." + std::to_string(l) + ".";
+        static const std::pair<const char*, const char*> m[] = {
+            {"attn_norm", "input_layernorm"}, {"ffn_norm", "post_attention_layernorm"},
+            {"attn_q_norm", "self_attn.q_norm"}, {"attn_k_norm", "self_attn.k_norm"}, {"attn_q", "self_attn.q_proj"},
+            {"attn_k", "self_attn.k_proj"}, {"attn_v", "self_attn.v_proj"}, {"attn_output", "self_attn.o_proj"},
+            {"ffn_gate", "mlp.gate_proj"}, {"ffn_up", "mlp.up_proj"}, {"ffn_down", "mlp.down_proj"}};
+        for (auto& kv : m)
+            if (p == kv.first) text(L + kv.second + "." + leaf);
+    }
+    return out;
+}
+
+// Tensors a checkpoint may carry that the engine recomputes (the encoder's sinusoid position table, modeling_
+// qwen3_asr.py:245-263, a non-persistent buffer some exporters still write; llama.cpp's RoPE frequency table)
+bool ignorable_tensor(const std::string& n) {
+    return n.find("positional_embedding") != std::string::npos || n == "rope_freqs.weight" ||
+           n.find("rotary_emb.inv_freq") != std::string::npos;
+}
+
+struct GgufResolver {
+    const GgufFile& f;
+    std::map<std::string, std::string> used;   // file name → logical name
+    explicit GgufResolver(const GgufFile& g) : f(g) {}
+    const GgufTensor* find(const std::string& canon) {
+        for (const std::string& c : name_candidates(canon))
+            if (const GgufTensor* t = f.tensor(c)) {
+                auto it = used.find(c);
+                QASR_CHECK(it == used.end() || it->second == canon, QASR_E_FORMAT,
+                           "GGUF tensor " + c + " maps to both " + it->second + " and " + canon);
+                used[c] = canon;
+                return t;
+            }
+        return nullptr;
+    }
+    const GgufTensor* need(const std::string& canon) {
+        const GgufTensor* t = find(canon);
+        QASR_CHECK(t, QASR_E_FORMAT, "GGUF is missing tensor " + canon + " (looked for: " + join(name_candidates(canon)) + ")");
+        return t;
+    }
+    static std::string join(const std::vector<std::string>& v) {
+        std::string s;
+        for (auto& x : v) s += (s.empty() ? "" : ", ") + x;
+        return s;
+    }
+    int count_layers(const char* fmt) {
+        int n = 0;
+        while (find(nm(fmt, n))) n++;
+        return n;
+    }
+};
+
+int64_t nelem(const GgufTensor* t) {
+    int64_t n = 1;
+    for (auto d : t->dims) n *= d;
+    return n;
+}
+
+// metadata value by exact key (any of `keys`) or by unique suffix; nullptr when absent
+const GgufValue* meta(const GgufFile& f, std::initializer_list<const char*> keys, std::initializer_list<const char*> suffixes) {
+    for (const char* k : keys)
+        if (const GgufValue* v = f.get(k)) return v;
+    const GgufValue* hit = nullptr;
+    std::string hit_key;
+    for (const auto& kv : f.metadata())
+        for (const char* sfx : suffixes) {
+            const size_t n = strlen(sfx);
+            if (kv.first.size() >= n && kv.first.compare(kv.first.size() - n, n, sfx) == 0) {
+                QASR_CHECK(!hit || hit_key == kv.first, QASR_E_FORMAT,
+                           "GGUF metadata is ambiguous: " + hit_key + " and " + kv.first);
+                hit = &kv.second, hit_key = kv.first;
+            }
+        }
+    return hit;
+}
+bool numeric(const GgufValue* v) { return v && v->type != 8 && v->type != 9; }
+
+}  // namespace
+
 std::unique_ptr<Model> load_gguf_model(const std::string& path, bool shell) {
     GgufFile f(path);
-    qasr_hparams hp;
-    default_hparams("qwen3-asr-1.7b", &hp);
+    GgufResolver R(f);
     const std::string A = f.get_str("general.architecture", "qwen3-asr");
-    auto gi = [&](const char* k, int def) { return (int)f.get_int(A + "." + k, def); };
-    auto gf = [&](const char* k, float def) { return (float)f.get_float(A + "." + k, def); };
-    hp.n_mels = gi("audio.n_mels", 128);
-    hp.conv_ch = gi("audio.conv_channels", 480);
-    hp.enc_d = gi("audio.embedding_length", hp.enc_d);
-    hp.enc_layers = gi("audio.block_count", hp.enc_layers);
-    hp.enc_heads = gi("audio.attention.head_count", hp.enc_heads);
-    hp.enc_ffn = gi("audio.feed_forward_length", hp.enc_ffn);
-    hp.n_window = gi("audio.n_window", 50);
-    hp.n_window_infer = gi("audio.n_window_infer", 800);
-    hp.txt_h = gi("embedding_length", hp.txt_h);
-    hp.proj_out = gi("audio.projection_dim", hp.txt_h);
-    hp.txt_layers = gi("block_count", hp.txt_layers);
-    hp.txt_heads = gi("attention.head_count", hp.txt_heads);
-    hp.txt_kv_heads = gi("attention.head_count_kv", hp.txt_kv_heads);
-    hp.head_dim = gi("attention.key_length", hp.head_dim);
-    hp.txt_ffn = gi("feed_forward_length", hp.txt_ffn);
-    hp.rope_theta = gf("rope.freq_base", hp.rope_theta);
-    hp.rms_eps = gf("attention.layer_norm_rms_epsilon", hp.rms_eps);
-    hp.ln_eps = gf("audio.attention.layer_norm_epsilon", hp.ln_eps);
-    const GgufValue* toks = f.get("tokenizer.ggml.tokens");
-    const GgufTensor* te = f.tensor("token_embd.weight");
-    QASR_CHECK(te, QASR_E_FORMAT, "GGUF has no token_embd.weight");
+    qasr_hparams hp;
+    memset(&hp, 0, sizeof hp);
+    // ---- hyper-parameters from the tensor shapes (GGUF dims: ne0 = row length K, ne1 = rows N)
+    const GgufTensor* conv1 = R.need("a.conv1.weight");
+    hp.conv_ch = (int)(nelem(conv1) / 9);
+    const GgufTensor* co = R.need("a.conv_out.weight");
+    QASR_CHECK(co->dims.size() == 2, QASR_E_FORMAT, "conv_out weight must be 2-D");
+    hp.enc_d = (int)co->dims[1];
+    const int F3 = (int)(co->dims[0] / std::max(1, hp.conv_ch));
+    hp.enc_layers = R.count_layers("a.blk.%d.attn_q.weight");
+    hp.enc_ffn = (int)R.need("a.blk.0.ffn_up.weight")->dims[1];
+    hp.proj_out = (int)R.need("a.proj2.weight")->dims[1];
+    const GgufTensor* te = R.need("token_embd.weight");
+    QASR_CHECK(te->dims.size() == 2, QASR_E_FORMAT, "token embedding must be 2-D");
+    hp.txt_h = (int)te->dims[0];
     hp.vocab = (int)te->dims[1];
-    hp.tok_im_start = gi("token.im_start", hp.tok_im_start);
-    hp.tok_im_end = gi("token.im_end", hp.tok_im_end);
-    hp.tok_system = gi("token.system", hp.tok_system);
-    hp.tok_user = gi("token.user", hp.tok_user);
-    hp.tok_assistant = gi("token.assistant", hp.tok_assistant);
-    hp.tok_newline = gi("token.newline", hp.tok_newline);
-    hp.tok_audio_start = gi("token.audio_start", hp.tok_audio_start);
-    hp.tok_audio_end = gi("token.audio_end", hp.tok_audio_end);
-    hp.tok_audio_pad = gi("token.audio_pad", hp.tok_audio_pad);
-    hp.tok_eos0 = gi("token.eos0", hp.tok_eos0);
-    hp.tok_eos1 = gi("token.eos1", hp.tok_eos1);
-    hp.tok_asr_text = gi("token.asr_text", hp.tok_asr_text);
+    hp.txt_layers = R.count_layers("blk.%d.attn_q.weight");
+    hp.head_dim = (int)nelem(R.need("blk.0.attn_q_norm.weight"));
+    hp.txt_heads = (int)(R.need("blk.0.attn_q.weight")->dims[1] / std::max(1, hp.head_dim));
+    hp.txt_kv_heads = (int)(R.need("blk.0.attn_k.weight")->dims[1] / std::max(1, hp.head_dim));
+    hp.txt_ffn = (int)R.need("blk.0.ffn_gate.weight")->dims[1];
+    // ---- scalars no shape determines
+    std::string assumed;
+    auto get_i = [&](const char* what, std::initializer_list<const char*> keys, std::initializer_list<const char*> sfx,
+                     int arch_value) {
+        const GgufValue* v = meta(f, keys, sfx);
+        if (numeric(v)) return (int)v->i;
+        assumed += std::string(assumed.empty() ? "" : ", ") + what + "=" + std::to_string(arch_value);
+        return arch_value;
+    };
+    auto need_f = [&](const char* what, std::initializer_list<const char*> keys, std::initializer_list<const char*> sfx) {
+        const GgufValue* v = meta(f, keys, sfx);
+        QASR_CHECK(numeric(v), QASR_E_FORMAT, std::string("GGUF metadata is missing ") + what);
+        return (float)v->f;
+    };
+    // the Qwen3-ASR audio encoder's fixed architecture (configuration_qwen3_asr.py: head_dim 64, n_window 50,
+    // n_window_infer 800, nn.LayerNorm eps 1e-5, 128 mel bins ⇔ 16 conv_out frequency rows) when the file is silent
+    hp.n_mels = get_i("n_mels", {}, {"audio.n_mels", "audio.num_mel_bins", "num_mel_bins"}, F3 == 16 ? 128 : 0);
+    hp.enc_heads = get_i("enc_heads", {}, {"audio.attention.head_count", "audio.encoder_attention_heads",
+                                           "encoder_attention_heads"}, hp.enc_d / 64);
+    hp.n_window = get_i("n_window", {}, {"audio.n_window", ".n_window"}, 50);
+    hp.n_window_infer = get_i("n_window_infer", {}, {"audio.n_window_infer", ".n_window_infer"}, 800);
+    hp.rope_theta = need_f("the RoPE base (*.rope.freq_base)", {}, {".rope.freq_base", ".rope_theta"});
+    hp.rms_eps = need_f("the RMSNorm epsilon (*.attention.layer_norm_rms_epsilon)", {},
+                        {".attention.layer_norm_rms_epsilon", ".rms_norm_eps"});
+    {
+        const GgufValue* v = meta(f, {}, {"audio.attention.layer_norm_epsilon", "audio.layer_norm_epsilon"});
+        if (numeric(v)) hp.ln_eps = (float)v->f;
+        else hp.ln_eps = 1e-5f, assumed += std::string(assumed.empty() ? "" : ", ") + "ln_eps=1e-5";
+    }
+    if (!assumed.empty())
+        fprintf(stderr, "qasr: %s: architecture values assumed (no metadata key): %s\n", path.c_str(), assumed.c_str());
+    QASR_CHECK(F3 * hp.conv_ch == co->dims[0] && (((hp.n_mels + 1) / 2 + 1) / 2 + 1) / 2 == F3, QASR_E_FORMAT,
+               "conv_out input width does not match the conv stack");
+    // ---- special tokens: metadata ids, else the canonical pieces of the Qwen2 vocabulary
+    const GgufValue* toks = f.get("tokenizer.ggml.tokens");
+    QASR_CHECK(toks && toks->arr_type == 8 && (int)toks->arr_s.size() >= hp.vocab, QASR_E_FORMAT,
+               "GGUF has no tokenizer vocabulary (tokenizer.ggml.tokens) covering the embedding rows");
+    std::map<std::string, int> piece_id;
+    for (int id = (int)toks->arr_s.size() - 1; id >= 0; id--) piece_id[toks->arr_s[id]] = id;   // lowest id wins
+    auto tok = [&](const char* key, const char* piece) {
+        const GgufValue* v = meta(f, {(A + ".token." + key).c_str()}, {});
+        if (numeric(v)) return (int)v->i;
+        auto it = piece_id.find(piece);
+        QASR_CHECK(it != piece_id.end(), QASR_E_FORMAT,
+                   std::string("GGUF vocabulary has no ") + piece + " token (nor metadata " + A + ".token." + key + ")");
+        return it->second;
+    };
+    hp.tok_im_start = tok("im_start", "<|im_start|>");
+    hp.tok_im_end = tok("im_end", "<|im_end|>");
+    hp.tok_system = tok("system", "system");
+    hp.tok_user = tok("user", "user");
+    hp.tok_assistant = tok("assistant", "assistant");
+    hp.tok_newline = tok("newline", "\xC4\x8A");   // "Ċ": the byte-level piece of "\n"
+    hp.tok_audio_start = tok("audio_start", "<|audio_start|>");
+    hp.tok_audio_end = tok("audio_end", "<|audio_end|>");
+    hp.tok_audio_pad = tok("audio_pad", "<|audio_pad|>");
+    hp.tok_eos0 = tok("eos0", "<|im_end|>");
+    hp.tok_eos1 = tok("eos1", "<|endoftext|>");
+    hp.tok_asr_text = tok("asr_text", "<asr_text>");
     validate(hp);
 
     auto mp = std::make_unique<Model>();
     Model& m = *mp;
     m.hp = hp;
     m.arch = f.get_str("general.name", "qwen3-asr");
-    const GgufTensor* out = f.tensor("output.weight");   // untied checkpoints carry their own vocabulary projection
-    if (out)
-        QASR_CHECK(out->type == GGML_Q8_0 && out->dims.size() == 2 && out->dims[0] == hp.txt_h && out->dims[1] == hp.vocab,
-                   QASR_E_FORMAT, "output.weight: shape mismatch");
+    const GgufTensor* out = R.find("output.weight");   // untied checkpoints carry their own vocabulary projection
     make_layout(m, out != nullptr);
+    // ---- every slot: resolve, check type and shape, upload
     hipStream_t s = nullptr;
     uint8_t* staging = nullptr;
     size_t staging_cap = 0;
     for (auto& kv : m.slots) {
-        if (shell) break;
         const std::string& name = kv.first;
         const TensorSlot& t = kv.second;
-        const GgufTensor* g = f.tensor(name);
-        QASR_CHECK(g, QASR_E_FORMAT, "GGUF is missing tensor " + name);
+        const GgufTensor* g = R.need(name);
         if (t.type == 8) {
-            QASR_CHECK(g->type == GGML_Q8_0, QASR_E_FORMAT, name + ": expected Q8_0");
+            QASR_CHECK(g->type == GGML_Q8_0, QASR_E_FORMAT,
+                       name + ": linear stored as ggml type " + std::to_string(g->type) + "; only Q8_0 linears are supported");
             QASR_CHECK(g->dims.size() == 2 && g->dims[0] == t.cols && g->dims[1] == t.rows, QASR_E_FORMAT,
                        name + ": shape mismatch");
+        } else if (t.type == 0) {
+            QASR_CHECK((g->type == GGML_F32 || g->type == GGML_F16) && nelem(g) == t.rows, QASR_E_FORMAT,
+                       name + ": expected an f32 / f16 vector of " + std::to_string(t.rows));
+        } else {
+            QASR_CHECK(g->type == GGML_F16 && nelem(g) == t.rows, QASR_E_FORMAT, name + ": expected an f16 conv kernel");
+        }
+        if (shell) continue;
+        if (t.type == 8) {
             if (g->nbytes > staging_cap) {
                 if (staging) QASR_HIP(hipFree(staging));
                 staging_cap = g->nbytes;
@@ -451,10 +633,12 @@ std::unique_ptr<Model> load_gguf_model(const std::string& path, bool shell) {
             repack_q8(staging, t.rows * (t.cols / QK), (int8_t*)t.base + t.row0 * t.ld, t.sc + t.row0 * (t.ld / QK), s);
             QASR_HIP(hipStreamSynchronize(s));
         } else if (t.type == 0) {
-            QASR_CHECK(g->type == GGML_F32 && (int64_t)(g->nbytes / 4) == t.rows, QASR_E_FORMAT, name + ": expected f32");
-            QASR_HIP(hipMemcpy(t.base, g->data, g->nbytes, hipMemcpyHostToDevice));
+            std::vector<float> v((size_t)t.rows);
+            if (g->type == GGML_F32) memcpy(v.data(), g->data, v.size() * 4);
+            else
+                for (size_t i = 0; i < v.size(); i++) v[i] = __half2float(((const __half*)g->data)[i]);   // exact
+            QASR_HIP(hipMemcpy(t.base, v.data(), v.size() * 4, hipMemcpyHostToDevice));
         } else {
-            QASR_CHECK(g->type == GGML_F16 && (int64_t)(g->nbytes / 2) == t.rows, QASR_E_FORMAT, name + ": expected f16");
             __half* tmp = nullptr;
             QASR_HIP(hipMalloc(&tmp, g->nbytes));
             QASR_HIP(hipMemcpy(tmp, g->data, g->nbytes, hipMemcpyHostToDevice));
@@ -464,18 +648,17 @@ std::unique_ptr<Model> load_gguf_model(const std::string& path, bool shell) {
         }
     }
     if (staging) QASR_HIP(hipFree(staging));
+    for (const auto& kv : f.tensors())
+        QASR_CHECK(R.used.count(kv.first) || ignorable_tensor(kv.first), QASR_E_FORMAT,
+                   "GGUF tensor " + kv.first + " is not mapped to any Qwen3-ASR tensor");
     finalize_layout(m, s, !shell);
     build_tables(m, s);
     m.weights_pending = shell;
-    if (toks && toks->arr_type == 8 && (int)toks->arr_s.size() >= hp.vocab) {
-        m.tok.pieces = toks->arr_s;
-        m.tok.is_special.assign(m.tok.pieces.size(), 0);
-        if (const GgufValue* tt = f.get("tokenizer.ggml.token_type"))
-            for (size_t i = 0; i < tt->arr_i.size() && i < m.tok.is_special.size(); i++)
-                m.tok.is_special[i] = tt->arr_i[i] == 3 || tt->arr_i[i] == 4;  // CONTROL / USER_DEFINED
-    } else {
-        make_tokenizer_synthetic(m);
-    }
+    m.tok.pieces = toks->arr_s;
+    m.tok.is_special.assign(m.tok.pieces.size(), 0);
+    if (const GgufValue* tt = f.get("tokenizer.ggml.token_type"))
+        for (size_t i = 0; i < tt->arr_i.size() && i < m.tok.is_special.size(); i++)
+            m.tok.is_special[i] = tt->arr_i[i] == 3 || tt->arr_i[i] == 4;  // CONTROL / USER_DEFINED
     return mp;
 }
 

@@ -373,3 +373,83 @@ def test_single_run_decodes_to_eos_or_n_ctx(torch_dev, golden):
         s.close()
     finally:
         m.close()
+
+
+def _vocab(hp, real_specials):
+    """tiny vocabulary: synthetic pieces; special ids carry the Qwen2 piece strings when real_specials (the loader
+    must then resolve them from the vocabulary alone)"""
+    names = {"tok_im_start": "<|im_start|>", "tok_im_end": "<|im_end|>", "tok_system": "system", "tok_user": "user",
+             "tok_assistant": "assistant", "tok_newline": "Ċ", "tok_audio_start": "<|audio_start|>",
+             "tok_audio_end": "<|audio_end|>", "tok_audio_pad": "<|audio_pad|>", "tok_eos1": "<|endoftext|>",
+             "tok_asr_text": "<asr_text>", "tok_eos0": "<|im_end|>"}
+    special = {v: k for k, v in SPECIAL.items()}
+    pieces = [("%s" % names[special[i]] if real_specials else f"<|{special[i]}|>") if i in special
+              else "abcdefghij"[i % 10] * (1 + i % 3) + str(i) for i in range(hp["vocab"])]
+    types = [3 if i in special and not pieces[i].isalpha() else 1 for i in range(hp["vocab"])]
+    return pieces, types
+
+
+@pytest.mark.parametrize("names", ["hf-thinker", "hf"])
+def test_gguf_naming_conventions_and_types(gpu, golden, torch_dev, tmp_path, names):
+    """GGUF loader: the same model exported under the original qwen_asr ("thinker.*") and the
+    transformers ("model.language_model.*", "model.multi_modal_projector.*") tensor names, with llama.cpp's text-model
+    metadata only (no audio / special-token keys: the audio hyper-parameters come from the tensor shapes, the special
+    tokens from the vocabulary's piece strings) and some vectors stored as F16, loads to the image of the same model
+    exported in this engine's convention with those vectors f16-rounded, and decodes the same tokens."""
+    import torch
+
+    from gguf_export import export_gguf
+    from qasr.transcribe_cpp import Model
+
+    m, _ = gpu
+    hp = m.hparams
+    pieces, types = _vocab(hp, real_specials=True)
+    f16 = ("a.blk.0.ln1.weight", "a.blk.1.ffn_up.bias", "blk.0.attn_norm.weight", "blk.1.attn_q_norm.weight",
+           "output_norm.weight")
+    pa, pb = str(tmp_path / "engine.gguf"), str(tmp_path / f"{names}.gguf")
+    export_gguf(m, pa, tokens=pieces, token_types=types, f16_round=f16)
+    export_gguf(m, pb, tokens=pieces, token_types=types, names=names, f16_vectors=f16, untied=(names == "hf"))
+    a, b = Model(pa, backend="hip"), Model(pb, backend="hip")
+    try:
+        assert b.hparams == a.hparams == hp
+        ta, tb = a.tensor_table(), b.tensor_table()
+        if names == "hf":
+            assert tb.pop("output.weight") == ta["token_embd.weight"]
+        assert ta == tb
+        if names != "hf":
+            assert torch.equal(_blob(a, torch_dev), _blob(b, torch_dev))
+        sa, sb = a.session(kv_type="f16", n_ctx=2048), b.session(kv_type="f16", n_ctx=2048)
+        assert _tokens(sa, golden) == _tokens(sb, golden)
+        sa.close()
+        sb.close()
+    finally:
+        a.close()
+        b.close()
+
+
+def test_gguf_loader_fails_loudly(gpu, torch_dev, tmp_path):
+    """unmapped tensors, missing required metadata and missing tensors are init errors (QASR_E_FORMAT), not defaults"""
+    from gguf_export import export_gguf
+    from qasr import _lib
+    from qasr.transcribe_cpp import Model
+
+    m, _ = gpu
+    pieces, types = _vocab(m.hparams, real_specials=True)
+    cases = [
+        (dict(names="hf", extra_tensors=[("audio_tower.mystery.weight", [1.0, 2.0])]), "not mapped"),
+        (dict(names="hf", drop_keys=("qwen3.rope.freq_base",)), "RoPE base"),
+        (dict(names="hf", drop_keys=("qwen3.attention.layer_norm_rms_epsilon",)), "RMSNorm epsilon"),
+    ]
+    for i, (kw, msg) in enumerate(cases):
+        path = str(tmp_path / f"bad{i}.gguf")
+        export_gguf(m, path, tokens=pieces, token_types=types, **kw)
+        with pytest.raises(_lib.QasrError) as e:
+            Model(path, backend="hip")
+        assert e.value.code == 3 and msg in str(e.value), str(e.value)
+    # a vocabulary without the chat-template pieces and no token metadata: the prompt cannot be built
+    path = str(tmp_path / "novocab.gguf")
+    plain, ptypes = _vocab(m.hparams, real_specials=False)
+    export_gguf(m, path, tokens=plain, token_types=ptypes, names="hf-thinker")
+    with pytest.raises(_lib.QasrError) as e:
+        Model(path, backend="hip")
+    assert "<|im_start|>" in str(e.value)

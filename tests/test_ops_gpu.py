@@ -138,9 +138,11 @@ def _linear_case(torch_dev, m, n, k, path, epi, seed=0, exact=False):
     return host(y), ref.astype(np.float32)
 
 
-# path: 1 GEMV, 2 auto, 16 + cfg (+ 16·splits) forces a GEMM configuration (kernels_q8.hip kGemmCfgs: 0..3 register-
-# staged, 4..10 LDS-DMA)
-GEMM_PATHS = [1, 2, 3, 4, 5] + [16 + c for c in range(16)] + [16 + 4 + 32 * 2, 16 + 9 + 32 * 4, 16 + 10 + 32 * 3]
+# path: 1 GEMV, 2 auto, 16 + cfg (+ 32·splits) forces a GEMM configuration (kernels_q8.hip kGemmCfgs: 0..3 register-
+# staged, 4..23 LDS-DMA, 24..30 the decode kernel with K split over waves; a configuration whose K granule does not
+# divide K falls back to the heuristic)
+GEMM_PATHS = ([1, 2, 3, 4, 5] + [16 + c for c in range(31)] + [16 + 4 + 32 * 2, 16 + 9 + 32 * 4, 16 + 10 + 32 * 3,
+                                                                 16 + 16 + 32, 16 + 21 + 32])
 
 
 @pytest.mark.parametrize("path", GEMM_PATHS)
@@ -165,8 +167,8 @@ def test_linear_q8_vs_oracle(torch_dev, path, epi, m, n, k):
     assert np.abs(y - ref).max() <= 2e-5 * scale * np.sqrt(k / 256)
 
 
-@pytest.mark.parametrize("cfg", [-1, 0, 2, 4, 5, 10, 14])
-@pytest.mark.parametrize("m,n,k", [(37, 320, 2048), (300, 1024, 1024), (9, 64, 96)])
+@pytest.mark.parametrize("cfg", [-1, 0, 2, 4, 5, 10, 14, 17, 23, 25, 27, 29, 30])
+@pytest.mark.parametrize("m,n,k", [(37, 320, 2048), (300, 1024, 1024), (9, 64, 96), (70, 256, 2048)])
 def test_linear_fused_epilogues(torch_dev, m, n, k, cfg):
     """GELU + Q8 quantisation (encoder up-projection, projector) and f16 store (encoder QKV) in the GEMM epilogue"""
     import torch
@@ -243,8 +245,8 @@ def _il16(f):
     return np.where(r < f, 32 * (r // 16) + r % 16, 32 * ((r - f) // 16) + 16 + (r - f) % 16)
 
 
-@pytest.mark.parametrize("cfg", [-1, 1, 4, 5, 8, 9, 12, 13, 15])
-@pytest.mark.parametrize("m,f,k", [(3, 256, 512), (40, 512, 1024), (300, 1024, 512)])
+@pytest.mark.parametrize("cfg", [-1, 1, 4, 5, 8, 9, 12, 13, 15, 20, 22, 23, 28, 29, 30])
+@pytest.mark.parametrize("m,f,k", [(3, 256, 512), (40, 512, 1024), (300, 1024, 512), (70, 512, 2048)])
 def test_gemm_swiglu_q8(torch_dev, m, f, k, cfg):
     """fused gate-up GEMM + SwiGLU + Q8 epilogue vs the oracle's linear_q8 of gate and up"""
     import torch

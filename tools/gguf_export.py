@@ -27,6 +27,48 @@ _FLOAT_KEYS = {"rope.freq_base": "rope_theta", "attention.layer_norm_rms_epsilon
                "audio.attention.layer_norm_epsilon": "ln_eps"}
 
 
+_AUDIO_LAYER = {"ln1": "self_attn_layer_norm", "ln2": "final_layer_norm", "attn_q": "self_attn.q_proj",
+                "attn_k": "self_attn.k_proj", "attn_v": "self_attn.v_proj", "attn_out": "self_attn.out_proj",
+                "ffn_up": "fc1", "ffn_down": "fc2"}
+_TEXT_LAYER = {"attn_norm": "input_layernorm", "ffn_norm": "post_attention_layernorm", "attn_q_norm": "self_attn.q_norm",
+               "attn_k_norm": "self_attn.k_norm", "attn_q": "self_attn.q_proj", "attn_k": "self_attn.k_proj",
+               "attn_v": "self_attn.v_proj", "attn_output": "self_attn.o_proj", "ffn_gate": "mlp.gate_proj",
+               "ffn_up": "mlp.up_proj", "ffn_down": "mlp.down_proj"}
+
+
+def convention_name(canon: str, names: str) -> str:
+    """This engine's tensor name → the same tensor in another naming convention: "engine" (as is), "hf-thinker"
+    (the original qwen_asr state dict: thinker.audio_tower.* / thinker.model.* / thinker.lm_head) or "hf"
+    (transformers' Qwen3ASRForConditionalGeneration: model.audio_tower.*, model.multi_modal_projector.linear_{1,2},
+    model.language_model.*, lm_head)."""
+    if names == "engine":
+        return canon
+    ap, tp, lm = (("thinker.audio_tower.", "thinker.model.", "thinker.lm_head.weight") if names == "hf-thinker" else
+                  ("model.audio_tower.", "model.language_model.", "lm_head.weight"))
+    parts = canon.split(".")
+    leaf = parts[-1]
+    if canon.startswith("a.conv") and not canon.startswith("a.conv_out"):
+        return f"{ap}conv2d{parts[1][4:]}.{leaf}"
+    if canon == "a.conv_out.weight":
+        return ap + "conv_out.weight"
+    if canon.startswith("a.blk."):
+        return f"{ap}layers.{parts[2]}.{_AUDIO_LAYER[parts[3]]}.{leaf}"
+    if canon.startswith("a.ln_post."):
+        return f"{ap}ln_post.{leaf}"
+    if canon.startswith("a.proj"):
+        k = parts[1][4]
+        return f"{ap}proj{k}.{leaf}" if names == "hf-thinker" else f"model.multi_modal_projector.linear_{k}.{leaf}"
+    if canon == "token_embd.weight":
+        return tp + "embed_tokens.weight"
+    if canon == "output_norm.weight":
+        return tp + "norm.weight"
+    if canon == "output.weight":
+        return lm
+    if canon.startswith("blk."):
+        return f"{tp}layers.{parts[1]}.{_TEXT_LAYER[parts[2]]}.{leaf}"
+    raise KeyError(canon)
+
+
 def _s(x: str) -> bytes:
     b = x.encode()
     return struct.pack("<Q", len(b)) + b
@@ -37,18 +79,35 @@ def _kv(key: str, vtype: int, payload: bytes) -> bytes:
 
 
 def export_gguf(model, path: str, name: str = "qwen3-asr-custom", tokens: list[str] | None = None,
-                token_types: list[int] | None = None, untied: bool = False) -> None:
+                token_types: list[int] | None = None, untied: bool = False, names: str = "engine",
+                f16_vectors: tuple = (), f16_round: tuple = (), drop_keys: tuple = (),
+                extra_tensors: tuple = ()) -> None:
     """`model`: a qasr.transcribe_cpp.Model.  `tokens`: optional vocabulary pieces (tokenizer.ggml.tokens);
-    `untied`: also write output.weight (a copy of token_embd) to exercise the untied-checkpoint layout."""
+    `untied`: also write output.weight (a copy of token_embd) to exercise the untied-checkpoint layout.
+    `names`: tensor naming convention (convention_name); the "hf*" conventions write llama.cpp's text-model metadata
+    keys (qwen3.rope.freq_base, qwen3.attention.layer_norm_rms_epsilon) and no audio / special-token keys, so the
+    loader must derive the audio hyper-parameters from the shapes and the special tokens from the vocabulary.
+    `f16_vectors`: f32 tensors to store as F16 (rounded); `f16_round`: f32 tensors rounded to f16 but stored as F32
+    (the same values: the loader must give identical models); `drop_keys`: metadata keys to omit;
+    `extra_tensors`: (name, f32 values) written as well (negative tests)."""
+    import numpy as np
+
     hp = model.hparams
     table = model.tensor_table()
-    arch = "qwen3-asr"
+    arch = "qwen3-asr" if names == "engine" else "qwen3asr"
     kvs = [_kv("general.architecture", GT_STR, _s(arch)), _kv("general.name", GT_STR, _s(name)),
            _kv("general.alignment", GT_U32, struct.pack("<I", ALIGN))]
-    for k, f in _INT_KEYS.items():
-        kvs.append(_kv(f"{arch}.{k}", GT_I32, struct.pack("<i", int(hp[f]))))
-    for k, f in _FLOAT_KEYS.items():
-        kvs.append(_kv(f"{arch}.{k}", GT_F32, struct.pack("<f", float(hp[f]))))
+    if names == "engine":
+        ints, floats = {f"{arch}.{k}": f for k, f in _INT_KEYS.items()}, {f"{arch}.{k}": f for k, f in _FLOAT_KEYS.items()}
+    else:
+        ints = {"qwen3.block_count": "txt_layers", "qwen3.embedding_length": "txt_h"}
+        floats = {"qwen3.rope.freq_base": "rope_theta", "qwen3.attention.layer_norm_rms_epsilon": "rms_eps"}
+    for k, f in ints.items():
+        if k not in drop_keys:
+            kvs.append(_kv(k, GT_I32, struct.pack("<i", int(hp[f]))))
+    for k, f in floats.items():
+        if k not in drop_keys:
+            kvs.append(_kv(k, GT_F32, struct.pack("<f", float(hp[f]))))
     if tokens is not None:
         kvs.append(_kv("tokenizer.ggml.tokens", GT_ARR,
                        struct.pack("<IQ", GT_STR, len(tokens)) + b"".join(_s(t) for t in tokens)))
@@ -70,8 +129,19 @@ def export_gguf(model, path: str, name: str = "qwen3-asr-custom", tokens: list[s
             nbytes, dims = rows * 2, (3, 3, cin, rows // (9 * cin))
         data = model.export_tensor(src, nbytes).tobytes()
         assert len(data) == nbytes, tname
-        infos.append(_s(tname) + struct.pack("<I", len(dims)) + b"".join(struct.pack("<Q", d) for d in dims)
-                     + struct.pack("<IQ", gtype, off))
+        if gtype == 0 and tname in f16_vectors:      # stored as F16 (rounded)
+            data, gtype = np.frombuffer(data, np.float32).astype(np.float16).tobytes(), 1
+        elif gtype == 0 and tname in f16_round:      # the same rounded values, stored as F32
+            data = np.frombuffer(data, np.float32).astype(np.float16).astype(np.float32).tobytes()
+        infos.append(_s(convention_name(tname, names)) + struct.pack("<I", len(dims))
+                     + b"".join(struct.pack("<Q", d) for d in dims) + struct.pack("<IQ", gtype, off))
+        pad = (-len(data)) % ALIGN
+        blobs.append(data + b"\0" * pad)
+        off += len(data) + pad
+
+    for tname, values in extra_tensors:
+        data = np.asarray(values, np.float32).tobytes()
+        infos.append(_s(tname) + struct.pack("<I", 1) + struct.pack("<Q", len(data) // 4) + struct.pack("<IQ", 0, off))
         pad = (-len(data)) % ALIGN
         blobs.append(data + b"\0" * pad)
         off += len(data) + pad
