@@ -327,8 +327,15 @@ def main():
                                     f"{world} rank(s) + probability all-gather, {c5_info.get('segments')} speech "
                                     f"segments ({c5_info.get('speech_s')} s) LPT-sharded, {FORCE_TPS} forced "
                                     f"tokens/audio-s"),
-                       "model": args.arch, "segments_per_rank": SEG_PER_RANK,
-                       "audio_s_per_rank": round(audio_s, 1), "parallelism": f"dp{world}"},
+                       "model": args.arch, "parallelism": f"dp{world}",
+                       **({"segments_per_rank": SEG_PER_RANK, "audio_s_per_rank": round(audio_s, 1)}
+                          if args.workload == "c4" else
+                          # C5: value counts the whole recording; ASR runs only on the VAD-kept speech
+                          {"recording_s": args.c5_seconds, "segments": c5_info.get("segments"),
+                           "speech_s": c5_info.get("speech_s"),
+                           "silence_fraction": (round(1 - c5_info["speech_s"] / args.c5_seconds, 3)
+                                                if c5_info.get("speech_s") is not None else None),
+                           "rank0_segments": c5_info.get("rank0_segments")})},
             "roofline": roof,
             "cpu_baseline": cpu,
             "collectives": collectives,

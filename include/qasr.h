@@ -125,6 +125,13 @@ QASR_API int qasr_session_run(qasr_session* s, const float* pcm16k, size_t n, in
    n = 0 restores the reference's prompt.  qasr_model_tokenize: UTF-8 → ids by greedy longest match over the
    byte-level vocabulary (decodes back to the same text; not the canonical BPE segmentation). */
 QASR_API int qasr_session_set_context(qasr_session* s, const int32_t* ids, int32_t n);
+/* Streaming decode (the app's interim loop re-sends the last ≤ 12 s every 140-460 ms, interim.rs:
+   135-156): on = 1 makes the session's single-utterance runs draft their continuation from its earlier transcripts
+   (prompt lookup: the tokens that followed the same bigram before) and verify each draft in one teacher-forced pass;
+   the accepted tokens are greedy's (up to near-ties of f32 summation order).  stats: passes, draft tokens proposed,
+   draft tokens accepted, tokens emitted. */
+QASR_API int qasr_session_set_draft(qasr_session* s, int32_t on);
+QASR_API int qasr_session_draft_stats(const qasr_session* s, int64_t* stats /* [4] */);
 QASR_API int qasr_model_tokenize(const qasr_model* m, const char* text, size_t len, int32_t* ids, size_t cap,
                                 size_t* n_out);
 /* ids → UTF-8 text (the transcript decoder: byte-level pieces, invalid sequences replaced as Python does) */

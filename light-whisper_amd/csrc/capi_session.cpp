@@ -227,6 +227,21 @@ QASR_API int qasr_session_set_context(qasr_session* s, const int32_t* ids, int32
     });
 }
 
+QASR_API int qasr_session_set_draft(qasr_session* s, int32_t on) {
+    return guard([&] {
+        QASR_CHECK(s, QASR_E_INVALID, "null argument");
+        s->s->set_draft(on != 0);
+    });
+}
+
+QASR_API int qasr_session_draft_stats(const qasr_session* s, int64_t* stats) {
+    return guard([&] {
+        QASR_CHECK(s && stats, QASR_E_INVALID, "null argument");
+        const Session::DraftStats& d = s->s->draft_stats();
+        stats[0] = d.passes, stats[1] = d.proposed, stats[2] = d.accepted, stats[3] = d.tokens;
+    });
+}
+
 QASR_API int qasr_session_run_opts(qasr_session* s, const float* pcm16k, size_t n, const qasr_run_opts* opts,
                                    qasr_result* out) {
     return guard([&] {

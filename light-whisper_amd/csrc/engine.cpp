@@ -108,7 +108,7 @@ Scratch::~Scratch() {
 Session::Session(Model* m, int n_ctx) : m_(m), n_ctx_(n_ctx) {
     QASR_CHECK(n_ctx > 32, QASR_E_INVALID, "n_ctx too small");
     QASR_HIP(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking));
-    QASR_HIP(hipHostMalloc(&pin_cnt_, 64, hipHostMallocDefault));
+    QASR_HIP(hipHostMalloc(&pin_cnt_, 256, hipHostMallocDefault));   // counters [0, 8), draft tokens [8, 24)
     for (auto& e : step_ev_) QASR_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     rope_n_ = n_ctx;
     std::vector<float> tab((size_t)n_ctx * m->hp.head_dim);
@@ -125,6 +125,7 @@ Session::~Session() {
     if (rope_) (void)hipFree(rope_);
     if (pin_) (void)hipHostFree(pin_);
     for (auto& g : graphs_) (void)hipGraphExecDestroy(g.second);
+    for (auto& g : draft_graphs_) (void)hipGraphExecDestroy(g.second);
     for (auto& e : step_ev_)
         if (e) (void)hipEventDestroy(e);
     if (pin_cnt_) (void)hipHostFree(pin_cnt_);
@@ -412,6 +413,124 @@ void Session::decode_step(const DecState& ds, int B, bool sizing) {
     QASR_HIP(hipMemcpyAsync(pin_cnt_, ds.counters, 4 * sizeof(int), hipMemcpyDeviceToHost, st_));
 }
 
+// ------------------------------------------------------------------------------------------ draft decode
+// One verify pass over B rows whose ids / positions / KV slots / key ranges sit in S_DTAB (5 tables of 16): embed →
+// 28 layers (the decode path: fused q/k-norm + RoPE + KV write, per-row attention over each row's own causal range)
+// → lm_head → argmax → token ids to the pinned host words [8, 8 + B).  Capturable like decode_step.
+void Session::draft_step(int B) {
+    const qasr_hparams& h = m_->hp;
+    int* tab = (int*)sc_.get(S_DTAB, (size_t)6 * 16 * sizeof(int));
+    float* x = (float*)sc_.get(S_X, (size_t)16 * h.txt_h * sizeof(float));
+    embed_rows(tab, B, m_->tok_embd, nullptr, x, st_);
+    decoder_layers(x, B, tab + 16, tab + 32, tab + 48, tab + 64, 0);
+    float* logits = (float*)sc_.get(S_LOGITS, (size_t)16 * h.vocab * sizeof(float));
+    lm_head_rows(x, B, h.txt_h, logits);
+    int* d_tok = (int*)sc_.get(S_TOK, (size_t)16 * sizeof(int));
+    argmax_rows(logits, B, h.vocab, d_tok, st_, sc_.get(S_ARGP, argmax_scratch_bytes(16)));
+    QASR_HIP(hipMemcpyAsync((int*)pin_cnt_ + 8, d_tok, (size_t)B * sizeof(int), hipMemcpyDeviceToHost, st_));
+}
+
+// Prompt-lookup decoding of one utterance (toks holds the first, prefill-chosen token).  Each pass feeds the last
+// accepted token and a draft — the tokens that followed the most recent earlier occurrence of the last two (else one)
+// accepted tokens in the session's history — and accepts greedy's tokens up to and including the first that departs
+// from the draft.  Row i's logits predict the token after row i's input, so an accepted prefix is exactly what one
+// greedy step per token would emit; KV rows written for rejected draft tokens sit past the accepted length and are
+// rewritten by the next pass.  A draft that keeps failing at its first token shrinks (to none: a plain greedy step).
+void Session::draft_decode(int n_prompt, int base, int budget, int dummy, std::vector<int32_t>& toks, bool& eos) {
+    const qasr_hparams& h = m_->hp;
+    constexpr int RMAX = 16;
+    int max_draft = RMAX - 1;
+    int* tab = (int*)sc_.get(S_DTAB, (size_t)6 * RMAX * sizeof(int));
+    int* hb = (int*)pinned((size_t)6 * RMAX * sizeof(int));
+    // bucket graphs hold scratch / KV / weight pointers: retire them whenever any of those moved
+    auto refresh = [&] {
+        const uint64_t key[3] = {sc_.epoch, kv_epoch_, m_->precision_gen};
+        if (memcmp(key, draft_key_, sizeof key) != 0) {
+            for (auto& g : draft_graphs_) (void)hipGraphExecDestroy(g.second);
+            draft_graphs_.clear();
+            memcpy(draft_key_, key, sizeof key);
+        }
+    };
+    refresh();
+    auto lookup = [&](std::vector<int32_t>& draft, int cap) {
+        draft.clear();
+        if (cap <= 0 || history_.empty()) return;
+        const int n = (int)toks.size();
+        for (int order = std::min(2, n); order >= 1 && draft.empty(); order--) {
+            for (int j = (int)history_.size() - order - 1; j >= 0; j--) {   // leaves ≥ 1 token to propose
+                bool match = true;
+                for (int k = 0; k < order && match; k++) match = history_[j + k] == toks[n - order + k];
+                if (!match) continue;
+                for (int k = j + order; k < (int)history_.size() && (int)draft.size() < cap; k++) draft.push_back(history_[k]);
+                break;
+            }
+        }
+    };
+    std::vector<int32_t> draft;
+    eos = false;
+    const bool graphs = !prof_enabled() && !getenv("QASR_NO_GRAPH");
+    while ((int)toks.size() < budget) {
+        const int pos = n_prompt + (int)toks.size() - 1;   // position of the last accepted token
+        lookup(draft, std::min(max_draft, budget - (int)toks.size() - 1));
+        const int R = 1 + (int)draft.size();
+        const int B = R <= 1 ? 1 : R <= 2 ? 2 : R <= 4 ? 4 : R <= 8 ? 8 : 16;
+        for (int i = 0; i < B; i++) {
+            const bool real = i < R;
+            hb[i] = real ? (i == 0 ? toks.back() : draft[i - 1]) : 0;
+            hb[16 + i] = real ? pos + i : 0;
+            hb[32 + i] = real ? base + pos + i : dummy;
+            hb[48 + i] = real ? base : dummy;
+            hb[64 + i] = real ? pos + i + 1 : 1;
+        }
+        QASR_HIP(hipMemcpyAsync(tab, hb, (size_t)80 * sizeof(int), hipMemcpyHostToDevice, st_));
+        auto it = draft_graphs_.find(B);
+        if (graphs && it != draft_graphs_.end()) {
+            QASR_HIP(hipGraphLaunch(it->second, st_));
+        } else {
+            draft_step(B);   // eager: also sizes the scratch this bucket needs before its graph is captured
+            refresh();       // (a growth retires the other buckets' graphs)
+            if (graphs) {
+                QASR_HIP(hipStreamSynchronize(st_));
+                hipGraph_t g;
+                QASR_HIP(hipStreamBeginCapture(st_, hipStreamCaptureModeRelaxed));
+                sc_.capturing = true;
+                try {
+                    draft_step(B);
+                } catch (...) {
+                    sc_.capturing = false;
+                    (void)hipStreamEndCapture(st_, &g);
+                    throw;
+                }
+                sc_.capturing = false;
+                QASR_HIP(hipStreamEndCapture(st_, &g));
+                hipGraphExec_t ex;
+                QASR_HIP(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
+                (void)hipGraphDestroy(g);
+                draft_graphs_.emplace(B, ex);
+            }
+        }
+        QASR_HIP(hipStreamSynchronize(st_));
+        const int* got = (const int*)pin_cnt_ + 8;
+        dstats_.passes++;
+        dstats_.proposed += R - 1;
+        int acc = 0;
+        for (int i = 0; i < R; i++) {
+            const int t = got[i];
+            if (t == h.tok_eos0 || t == h.tok_eos1) {
+                eos = true;
+                break;
+            }
+            toks.push_back(t);
+            if ((int)toks.size() >= budget) break;
+            if (i < R - 1 && t != draft[i]) break;   // row i + 1 was fed a token greedy did not choose
+            if (i < R - 1) acc++;
+        }
+        dstats_.accepted += acc;
+        max_draft = acc == 0 && R > 1 ? max_draft / 2 : std::min(RMAX - 1, std::max(max_draft * 2, 1));
+        if (eos) break;
+    }
+}
+
 // ------------------------------------------------------------------------------------------ batch run
 void Session::run_batch(const float* dpcm, const std::vector<int64_t>& off, const std::vector<int64_t>& len,
                         int max_new, int force_tps, std::vector<UttResult>& out, StageTimes* times) {
@@ -551,6 +670,31 @@ void Session::run_batch(const float* dpcm, const std::vector<int64_t>& off, cons
         dec_accept(ds, count, tab + 5 * count, d_tok, st_);
         QASR_HIP(hipMemcpyAsync(pin_cnt_, ds.counters, 4 * sizeof(int), hipMemcpyDeviceToHost, st_));
         QASR_HIP(hipStreamSynchronize(st_));
+    }
+    if (count == 1 && draft_ && force_tps <= 0) {   // streaming: prompt-lookup drafts from earlier transcripts
+        std::vector<int32_t> toks;
+        bool eos = false;
+        {
+            Timer tdd(st_, times ? &times->decode : nullptr);
+            int* hs = (int*)pinned(4 * sizeof(int));
+            QASR_HIP(hipMemcpyAsync(hs, ds.out, sizeof(int), hipMemcpyDeviceToHost, st_));
+            QASR_HIP(hipMemcpyAsync(hs + 1, ds.gen, sizeof(int), hipMemcpyDeviceToHost, st_));
+            QASR_HIP(hipMemcpyAsync(hs + 2, ds.done, sizeof(int), hipMemcpyDeviceToHost, st_));
+            QASR_HIP(hipStreamSynchronize(st_));
+            const int first = hs[0], gen = hs[1], done = hs[2];
+            if (gen > 0) toks.push_back(first);
+            eos = gen == 0;   // the prompt's first choice was EOS
+            if (!done) draft_decode(n_prompt[0], base[0], budget[0], (int)slots, toks, eos);
+        }
+        out[0].tokens = toks;
+        out[0].truncated = !eos && (int)toks.size() >= budget[0];
+        history_.insert(history_.end(), toks.begin(), toks.end());
+        if (history_.size() > 8192) history_.erase(history_.begin(), history_.end() - 8192);
+        dstats_.tokens += (int64_t)toks.size();
+        UttResult& r = out[0];
+        r.raw = m_->tok.decode(r.tokens.data(), (int)r.tokens.size());
+        Tokenizer::parse(r.raw, r.language, r.text);
+        return;
     }
     // continuous-batching greedy decode: rows = a bucket of the active count (padding rows are dummies); the
     // bound is the active count read back one step late, which never undercounts because it only decreases

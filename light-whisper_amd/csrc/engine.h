@@ -62,6 +62,14 @@ class Session {
     int n_ctx() const { return n_ctx_; }
     // system-prompt context tokens for the following runs (hot-word biasing; empty = the reference's prompt)
     void set_context(const std::vector<int32_t>& ids) { context_ = ids; }
+    // streaming decode: single-utterance runs draft their continuation from the session's previous
+    // transcripts (prompt-lookup: the tokens that followed the same bigram last time) and verify a whole draft in one
+    // teacher-forced pass; the accepted tokens are exactly greedy's (up to near-ties of f32 summation order)
+    void set_draft(bool on) { draft_ = on; }
+    struct DraftStats {
+        int64_t passes = 0, proposed = 0, accepted = 0, tokens = 0;
+    };
+    const DraftStats& draft_stats() const { return dstats_; }
     hipStream_t stream() const { return st_; }
 
    private:
@@ -77,6 +85,9 @@ class Session {
                         bool dense = false);
     void ensure_kv(int64_t slots);
     void decode_step(const DecState& ds, int B, bool sizing);
+    // one verify pass of B rows (last accepted token + draft, padded): tables in S_DTAB, argmax → pinned host
+    void draft_step(int B);
+    void draft_decode(int n_prompt, int base, int budget, int dummy, std::vector<int32_t>& toks, bool& eos);
     void lm_head_rows(const float* x, int rows, int ldx, float* logits);
     void mx_ws(int64_t rows, int64_t kmax);
     template <class T>
@@ -100,6 +111,11 @@ class Session {
     void* pin_cnt_ = nullptr;
     hipEvent_t step_ev_[2] = {nullptr, nullptr};
     std::map<int, hipGraphExec_t> graphs_;
+    std::map<int, hipGraphExec_t> draft_graphs_;
+    uint64_t draft_key_[3] = {~0ull, ~0ull, ~0ull};
+    bool draft_ = false;
+    std::vector<int32_t> history_;   // previous transcripts (the lookup corpus), oldest first
+    DraftStats dstats_;
     uint64_t graph_key_[3] = {~0ull, ~0ull, ~0ull};   // scratch epoch, KV epoch, model precision generation
     uint64_t kv_epoch_ = 0;
     int ucap_ = 0;

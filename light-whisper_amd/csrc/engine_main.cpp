@@ -285,6 +285,10 @@ struct Server {
             }
             if (rc != QASR_OK) return fail(qasr_last_error());
             if (qasr_session_open(model, "f16", 32768, &session) != QASR_OK) return fail(qasr_last_error());
+            // interim requests re-send overlapping windows: draft each decode from the earlier transcripts (greedy's
+            // tokens, verified in one pass; QASR_STREAM_DRAFT=0 turns it off)
+            const char* sd = getenv("QASR_STREAM_DRAFT");
+            qasr_session_set_draft(session, !(sd && std::string(sd) == "0"));
             if (qasr_vad_open(nullptr, &vad) != QASR_OK) return fail(qasr_last_error());
             backend = "hip";
             device = "hip";

@@ -1345,6 +1345,31 @@ static void gemm_mx_q8in(const int8_t* xq, const float* xd, int M, const Q8Mat& 
     gemm_mx(x8, xs, M, W, bias, res, y, ldy, epi, s, yq, yd, y_zeroed, -1);
 }
 
+// Decode-step table (M = the step's row bucket ≤ 256, K % 128 == 0): configuration and split-K count per row range,
+// from tools/dec_gemm_sweep.py with cold weights on MI355X (profiles/r2_dec_gemm_sweep.log) — every configuration ×
+// split count timed per shape; the winners per class of the decoder's shapes: QKV (plain store, K ≤ 2048), the
+// attention output projection (residual, K ≤ 2048) and the down projection (residual, K > 2048).
+struct DecPick { int m_max, cfg, splits; };
+static const DecPick kDecQkv[] = {{16, 17, 6}, {32, 16, 4}, {64, 18, 4}, {128, 14, 2}, {256, 14, 1}};
+static const DecPick kDecO[] = {{64, 16, 4}, {128, 18, 4}, {192, 15, 3}, {256, 14, 2}};
+static const DecPick kDecDown[] = {{32, 16, 8}, {64, 15, 8}, {96, 10, 8}, {128, 14, 4}, {192, 10, 8}, {256, 15, 4}};
+
+static bool dec_table_pick(int M, const Q8Mat& W, int epi, int& cfg, int& splits) {
+    if (M > 256 || W.K % 128 != 0 || W.N >= 32768) return false;
+    const DecPick* t = nullptr;
+    int n = 0;
+    if (epi == EPI_STORE && W.K <= 2048) t = kDecQkv, n = sizeof(kDecQkv) / sizeof(DecPick);
+    else if (epi == EPI_RESID && W.K <= 2048) t = kDecO, n = sizeof(kDecO) / sizeof(DecPick);
+    else if (epi == EPI_RESID) t = kDecDown, n = sizeof(kDecDown) / sizeof(DecPick);
+    if (!t) return false;
+    for (int i = 0; i < n; i++)
+        if (M <= t[i].m_max) {
+            cfg = t[i].cfg, splits = t[i].splits;
+            return true;
+        }
+    return false;
+}
+
 // force_cfg: -1 auto, else an index into kGemmCfgs (a DMA config on K % 64 != 0 falls back to auto);
 // force_splits: split-K (0 = heuristic).
 void gemm_q8(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const float* bias, const float* res, float* y,
@@ -1370,6 +1395,10 @@ void gemm_q8(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const flo
         else if (M > 256) pick = 4;
         else if (epi == EPI_SWIGLU) pick = !k128 ? 5 : M > 128 ? 12 : 15;
         else pick = !k128 ? 6 : W.N <= 4096 ? 14 : 10;
+        if (force_cfg < 0 && force_splits <= 0) {
+            int c, sp;
+            if (dec_table_pick(M, W, epi, c, sp)) pick = c, force_splits = sp;
+        }
     } else {
         const int first = M <= 32 ? 3 : M <= 64 ? 1 : 0, last = M <= 32 ? 3 : 2;
         pick = last;

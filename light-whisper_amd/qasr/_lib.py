@@ -104,6 +104,8 @@ SIGNATURES = {
     "qasr_decode_pcm_s16le": (C.c_int, [C.c_char_p, SZ, P, SZ, C.POINTER(SZ)]),
     "qasr_resample_linear": (C.c_int, [P, SZ, C.c_double, P, SZ, C.POINTER(SZ)]),
     "qasr_audio_load_path": (C.c_int, [C.c_char_p, P, SZ, C.POINTER(SZ)]),
+    "qasr_session_set_draft": (C.c_int, [P, I32]),
+    "qasr_session_draft_stats": (C.c_int, [P, C.POINTER(C.c_int64)]),
     "qasr_parse_transcript": (C.c_int, [C.c_char_p, SZ, C.c_char_p, SZ, C.POINTER(SZ), C.c_char_p, SZ,
                                         C.POINTER(SZ)]),
     "qasr_op_quant_rows": (C.c_int, [P, I32, I32, I32, P, P, P]),

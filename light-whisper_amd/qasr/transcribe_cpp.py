@@ -202,6 +202,15 @@ class Session:
         check(_lib.load().qasr_session_set_context(self._h, a.ctypes.data_as(C.c_void_p) if a.size else None,
                                                    int(a.size)))
 
+    def set_draft(self, on: bool = True):
+        """streaming decode: draft from this session's earlier transcripts, verify in one pass (greedy's tokens)"""
+        check(_lib.load().qasr_session_set_draft(self._h, 1 if on else 0))
+
+    def draft_stats(self) -> dict:
+        st = (C.c_int64 * 4)()
+        check(_lib.load().qasr_session_draft_stats(self._h, st))
+        return dict(zip(("passes", "proposed", "accepted", "tokens"), list(st)))
+
     def forced_logits(self, audio, forced) -> np.ndarray:
         a = _f32(audio)
         f = np.ascontiguousarray(forced, dtype=np.int32)

@@ -453,3 +453,32 @@ def test_gguf_loader_fails_loudly(gpu, torch_dev, tmp_path):
     with pytest.raises(_lib.QasrError) as e:
         Model(path, backend="hip")
     assert "<|im_start|>" in str(e.value)
+
+
+def test_streaming_draft_equals_greedy(torch_dev, golden):
+    """a session drafting from its earlier transcripts (prompt lookup, one verify pass
+    per draft) emits greedy's tokens — growing windows like the interim loop's, and a repeated window, whose whole
+    transcript is accepted as one draft.  A divergence is allowed only at a near-tie of the single-row logits."""
+    from qasr.transcribe_cpp import Model
+
+    m = Model.synthetic(arch=None, seed=TINY_SEED, hparams=tiny_hparams())
+    try:
+        ref, drf = m.session(kv_type="f16", n_ctx=2048), m.session(kv_type="f16", n_ctx=2048)
+        drf.set_draft(True)
+        audio = np.concatenate([golden["c__audio"], golden["b__audio"]])
+        windows = [audio[:n] for n in (16000, 24000, 32000, audio.size)] + [audio, audio]
+        for w in windows:
+            want = ref.run(w, max_new_tokens=40).tokens
+            got = drf.run(w, max_new_tokens=40).tokens
+            n = min(len(got), len(want))
+            div = next((i for i in range(n) if got[i] != want[i]), n)
+            if div < n or len(got) != len(want):
+                lg = ref.forced_logits(w, np.array(want[:max(div, 1)], np.int32))
+                top2 = np.sort(lg[div])[-2:]
+                assert top2[1] - top2[0] < 0.02 * np.abs(lg[div]).max(), f"draft diverges at {div} without a near-tie"
+        st = drf.draft_stats()
+        assert st["accepted"] >= 30 and st["passes"] < st["tokens"], st   # the repeats are accepted in bulk
+        ref.close()
+        drf.close()
+    finally:
+        m.close()

@@ -1,0 +1,78 @@
+#!/usr/bin/env python3
+"""Sweep every Q8 GEMM configuration × split-K count on the decode shapes with COLD weights (a ring of weight copies
+larger than the Infinity Cache, as in a decode step that streams 28 layers) and print the best few per (shape, M)
+next to the heuristic.  Tuning aid for gemm_q8's decode table (kernels_q8.hip).  GPU.
+usage: python tools/dec_gemm_sweep.py [out.json]"""
+import json
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "light-whisper_amd"))
+from qasr import _lib  # noqa: E402
+
+SHAPES = [("qkv", 4096, 2048, 0), ("o", 2048, 2048, 1), ("down", 2048, 6144, 1), ("gu", 12288, 2048, 3)]
+MS = [int(x) for x in os.environ.get("MS", "16,32,64,96,128,160,192,224,256").split(",")]
+CFGS = list(range(4, 31))
+SPLITS = [1, 2, 3, 4, 6, 8]
+SWIGLU_CFGS = [4, 5, 8, 9, 12, 13, 15, 20, 22, 23, 28, 29, 30]
+
+
+def main():
+    lib = _lib.load()
+    dev = torch.device("cuda:0")
+    result = {}
+    for tag, N, K, epi in SHAPES:
+        copies = max(2, int(768e6 // (N * K * 1.0625)) + 1)
+        wq = [torch.randint(-127, 128, (N, K), dtype=torch.int8, device=dev) for _ in range(copies)]
+        ws = [(torch.rand(N, K // 32, device=dev) * 0.01).half() for _ in range(copies)]
+        for M in MS:
+            xq = torch.randint(-127, 128, (M, K), dtype=torch.int8, device=dev)
+            xd = torch.rand(M, K // 32, device=dev) * 0.01
+            y = torch.zeros(M, N, device=dev)
+            hq = torch.empty(M, N // 2, dtype=torch.int8, device=dev)
+            hd = torch.empty(M, N // 64, device=dev)
+            combos = [(-1, 0)] + ([(c, 0) for c in SWIGLU_CFGS] if epi == 3 else
+                                  [(c, s) for c in CFGS for s in (SPLITS if c < 24 else [0])])
+            times = []
+            for cfg, sp in combos:
+                def run(i):
+                    if epi == 3:
+                        _lib.check(lib.qasr_op_gemm_swiglu_q8_cfg(xq.data_ptr(), xd.data_ptr(), M, wq[i].data_ptr(),
+                                                                  ws[i].data_ptr(), N, K, hq.data_ptr(), hd.data_ptr(),
+                                                                  cfg, None))
+                        return
+                    path = 2 if cfg < 0 else 16 + cfg + 32 * sp
+                    # a store GEMM with split-K clears y inside gemm_q8 (hipMemsetAsync): timed as part of it
+                    _lib.check(lib.qasr_op_linear_q8(xq.data_ptr(), xd.data_ptr(), M, wq[i].data_ptr(),
+                                                     ws[i].data_ptr(), N, K, None,
+                                                     y.data_ptr() if epi == 1 else None, y.data_ptr(), N, epi, path,
+                                                     None))
+                try:
+                    run(0)
+                except _lib.QasrError:
+                    continue
+                torch.cuda.synchronize()
+                n = copies * max(1, 16 // copies)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for i in range(n):
+                    run(i % copies)
+                e1.record()
+                torch.cuda.synchronize()
+                times.append((round(e0.elapsed_time(e1) / n * 1e3, 2), cfg, sp))
+            heur = next(t for t in times if t[1] < 0)
+            best = sorted(times)[:6]
+            result[f"{tag}:{M}"] = {"heuristic_us": heur[0], "best": best}
+            print(f"{tag:5s} M={M:4d} heuristic {heur[0]:7.1f}us | best " +
+                  "  ".join(f"{t:6.1f}us c{c}s{s}" for t, c, s in best), flush=True)
+        del wq, ws
+        torch.cuda.empty_cache()
+    if len(sys.argv) > 1:
+        json.dump(result, open(sys.argv[1], "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()
