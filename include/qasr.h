@@ -252,6 +252,15 @@ QASR_API int qasr_op_linear_q8h(const void* xq16, const float* xd, int32_t M, co
                                 int32_t N, int32_t K, const float* bias, const float* res, float* y, int32_t ldy,
                                 int32_t epi, int32_t cfg, void* stream);
 QASR_API int qasr_op_swiglu_q8_interleaved(const float* gu, int32_t M, int32_t F, int8_t* q, float* d, void* stream);
+/* The 1–4-row decoder GEMV (about one workgroup per CU) with the row operations around it fused; bit-identical to
+   the separate launches.  pro 0: activations = the Q8 rows xq [M][K] / xd [M][K/32], K ≤ 6144; pro 1: activations
+   = Q8(RMSNorm(src)·nw), src rows of K floats at stride ld_src, K ≤ 4096.  epi 0 store / 1 residual into y (y may
+   alias res), or 3 (pro 1 only): W = gate/up interleaved by 16 (qasr_op_interleave_gate_up), N % 64 == 0, output
+   h = Q8(silu(g)·u) rows hq [M][N/2] / hd [M][N/64].  M ≤ 4. */
+QASR_API int qasr_op_gemv_fused(int32_t pro, const float* src, int32_t ld_src, const float* nw, float eps, int32_t M,
+                                const int8_t* xq, const float* xd, const int8_t* wqs, const void* wsc, int32_t N,
+                                int32_t K, const float* res, float* y, int32_t ldy, int32_t epi, int8_t* hq,
+                                float* hd, void* stream);
 QASR_API int qasr_op_qk_norm_rope(const float* qkv, int32_t rows, int32_t nh, int32_t nkv, int32_t hd,
                                   const int32_t* pos, const int32_t* slot, const float* qnw, const float* knw,
                                   const float* rope_cs, float eps, void* qout, void* kc, void* vc, void* stream);
@@ -285,6 +294,11 @@ QASR_API int qasr_op_conv3x3_gelu(const void* in, int32_t n_chunks, int32_t Hi, 
                                   const float* bias, int32_t C, void* out, int32_t out_mode, void* stream);
 QASR_API int qasr_op_fbank(const float* pcm, int64_t n, float* feats /*[T][80]*/, void* stream);
 QASR_API int qasr_stream_sync(void* stream);
+
+/* Deterministic mode (process-wide, default off): GEMMs never split K across workgroups, so every run of the same
+   input gives bit-identical logits (split-K partial sums land by float atomics in a run-dependent order, a
+   last-ulp difference that can flip a near-tie).  Sessions re-capture their step graphs after a switch. */
+QASR_API int qasr_set_deterministic(int32_t on);
 
 /* -------------------------------------------------------------------------------------------- profiling */
 /* live per-kernel-class timing (hipEvents on each instrumented launch's stream) + algorithmic FLOPs/bytes;

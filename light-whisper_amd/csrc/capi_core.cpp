@@ -47,9 +47,14 @@ QASR_API int qasr_set_device(int device) {
 
 }  // extern "C"
 
+#include "kernels.h"
 #include "prof.h"
 
 extern "C" {
+
+QASR_API int qasr_set_deterministic(int32_t on) {
+    return guard([&] { qasr::set_deterministic(on != 0); });
+}
 
 QASR_API int qasr_prof_enable(int on) {
     return guard([&] { qasr::prof_set(on != 0); });

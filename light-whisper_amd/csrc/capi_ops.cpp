@@ -189,6 +189,22 @@ QASR_API int qasr_op_swiglu_q8_interleaved(const float* gu, int32_t M, int32_t F
     });
 }
 
+QASR_API int qasr_op_gemv_fused(int32_t pro, const float* src, int32_t ld_src, const float* nw, float eps, int32_t M,
+                                const int8_t* xq, const float* xd, const int8_t* wqs, const void* wsc, int32_t N,
+                                int32_t K, const float* res, float* y, int32_t ldy, int32_t epi, int8_t* hq,
+                                float* hd, void* stream) {
+    return guard([&] {
+        QASR_CHECK(N > 0 && (epi == EPI_SWIGLU || (y && ldy >= N)), QASR_E_INVALID, "gemv_fused: bad shape");
+        Q8Mat W;
+        W.qs = (int8_t*)wqs;
+        W.sc = (__half*)wsc;
+        W.N = N;
+        W.K = K;
+        gemv_fused(pro, xq, xd, src, ld_src, nw, eps, M, W, res, y, ldy, epi, hq, hd, S(stream));
+        launched();
+    });
+}
+
 QASR_API int qasr_op_qk_norm_rope(const float* qkv, int32_t rows, int32_t nh, int32_t nkv, int32_t hd,
                                   const int32_t* pos, const int32_t* slot, const float* qnw, const float* knw,
                                   const float* rope_cs, float eps, void* qout, void* kc, void* vc, void* stream) {

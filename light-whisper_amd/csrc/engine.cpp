@@ -330,15 +330,25 @@ void Session::decoder_layers(float* x, int rows, const int* d_pos, const int* d_
     const float scale = 1.0f / sqrtf((float)hd);
     const size_t layer_kv = (size_t)kv_slots_ * KD;
     const bool fuse_qk = !dense && hd == 128 && (nh / nkv == 2 || nh / nkv == 4) && !getenv("QASR_NO_QK_FUSE");
+    // GEMV row counts: the norms and the SwiGLU run inside the GEMVs' prologues (5 launches per layer, not 8)
+    const bool gv = !fused && dec_fuse_ && gemv_fused_ok(GV_RMS, rows, H) && gemv_fused_ok(GV_NONE, rows, F) &&
+                    gemv_fused_ok(GV_NONE, rows, QD);
+    int8_t* hq2 = gv ? (int8_t*)sc_.get(S_HQ, (size_t)rows * F) : nullptr;   // the SwiGLU epilogue's Q8 rows
+    float* hd2 = gv ? (float*)sc_.get(S_HD, (size_t)rows * (F / QK) * sizeof(float)) : nullptr;
     for (int l = 0; l < h.txt_layers; l++) {
         const DecLayer& L = m_->dec[l];
         __half* kc = kc_ + (size_t)l * layer_kv;
         __half* vc = vc_ + (size_t)l * layer_kv;
         // decode-sized steps: the norm launch also clears the QKV output, so the split-K QKV GEMM needs no memset
         const bool zq = rows <= 256;
-        rmsnorm_q8(x, rows, H, H, L.attn_norm, h.rms_eps, xq, xd, st_, zq ? qkv : nullptr,
-                   zq ? (int64_t)rows * (QD + 2 * KD) : 0);
-        linear_q8(xq, xd, rows, L.qkv, nullptr, nullptr, qkv, QD + 2 * KD, EPI_STORE, st_, zq);
+        if (gv) {
+            gemv_fused(GV_RMS, nullptr, nullptr, x, H, L.attn_norm, h.rms_eps, rows, L.qkv, nullptr, qkv, QD + 2 * KD,
+                       EPI_STORE, nullptr, nullptr, st_);
+        } else {
+            rmsnorm_q8(x, rows, H, H, L.attn_norm, h.rms_eps, xq, xd, st_, zq ? qkv : nullptr,
+                       zq ? (int64_t)rows * (QD + 2 * KD) : 0);
+            linear_q8(xq, xd, rows, L.qkv, nullptr, nullptr, qkv, QD + 2 * KD, EPI_STORE, st_, zq);
+        }
         if (fuse_qk) {   // decode rows: q/k norm + RoPE + KV write inside the attention kernel
             const QkFuse fz{qkv, d_pos, d_slot, L.q_norm, L.k_norm, rope_, h.rms_eps, kc, vc};
             attention_decode_fused(fz, KD, d_kvs, d_kvl, rows, nh, nkv, hd, scale, xq, xd, st_, total_keys);
@@ -346,6 +356,14 @@ void Session::decoder_layers(float* x, int rows, const int* d_pos, const int* d_
             qk_norm_rope(qkv, rows, nh, nkv, hd, d_pos, d_slot, L.q_norm, L.k_norm, rope_, h.rms_eps, qh, kc, vc, st_);
             attention(qh, QD, kc, vc, KD, d_kvs, d_kvl, rows, nh, nkv, hd, scale, nullptr, xq, xd, st_, total_keys,
                       dense);
+        }
+        if (gv) {   // O-projection + residual; norm + gate/up + SwiGLU + Q8; down-projection + residual
+            gemv_fused(GV_NONE, xq, xd, nullptr, 0, nullptr, 0.f, rows, L.o, x, x, H, EPI_RESID, nullptr, nullptr, st_);
+            gemv_fused(GV_RMS, nullptr, nullptr, x, H, L.ffn_norm, h.rms_eps, rows, L.gu, nullptr, nullptr, 0,
+                       EPI_SWIGLU, hq2, hd2, st_);
+            gemv_fused(GV_NONE, hq2, hd2, nullptr, 0, nullptr, 0.f, rows, L.down, x, x, H, EPI_RESID, nullptr, nullptr,
+                       st_);
+            continue;
         }
         linear_q8(xq, xd, rows, L.o, nullptr, x, x, H, EPI_RESID, st_);
         rmsnorm_q8(x, rows, H, H, L.ffn_norm, h.rms_eps, xq, xd, st_);
@@ -444,7 +462,7 @@ void Session::draft_decode(int n_prompt, int base, int budget, int dummy, std::v
     int* hb = (int*)pinned((size_t)6 * RMAX * sizeof(int));
     // bucket graphs hold scratch / KV / weight pointers: retire them whenever any of those moved
     auto refresh = [&] {
-        const uint64_t key[3] = {sc_.epoch, kv_epoch_, m_->precision_gen};
+        const uint64_t key[4] = {sc_.epoch, kv_epoch_, m_->precision_gen, deterministic_gen()};
         if (memcmp(key, draft_key_, sizeof key) != 0) {
             for (auto& g : draft_graphs_) (void)hipGraphExecDestroy(g.second);
             draft_graphs_.clear();
@@ -714,7 +732,7 @@ void Session::run_batch(const float* dpcm, const std::vector<int64_t>& off, cons
         QASR_HIP(hipEventRecord(step_ev_[0], st_));
     }
     // captured step graphs hold scratch, KV and weight pointers: any reallocation or precision change retires them
-    const uint64_t key[3] = {sc_.epoch, kv_epoch_, m_->precision_gen};
+    const uint64_t key[4] = {sc_.epoch, kv_epoch_, m_->precision_gen, deterministic_gen()};
     if (memcmp(key, graph_key_, sizeof key) != 0) {
         for (auto& g : graphs_) (void)hipGraphExecDestroy(g.second);
         graphs_.clear();

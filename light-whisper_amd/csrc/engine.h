@@ -112,11 +112,14 @@ class Session {
     hipEvent_t step_ev_[2] = {nullptr, nullptr};
     std::map<int, hipGraphExec_t> graphs_;
     std::map<int, hipGraphExec_t> draft_graphs_;
-    uint64_t draft_key_[3] = {~0ull, ~0ull, ~0ull};
+    uint64_t draft_key_[4] = {~0ull, ~0ull, ~0ull, ~0ull};
     bool draft_ = false;
+    // 1–4-row decode: norms / SwiGLU fused into the GEMV prologues (QASR_NO_DEC_FUSE=1: the separate launches,
+    // for A/B parity and timing; read once per session, so captured step graphs stay consistent)
+    bool dec_fuse_ = getenv("QASR_NO_DEC_FUSE") == nullptr;
     std::vector<int32_t> history_;   // previous transcripts (the lookup corpus), oldest first
     DraftStats dstats_;
-    uint64_t graph_key_[3] = {~0ull, ~0ull, ~0ull};   // scratch epoch, KV epoch, model precision generation
+    uint64_t graph_key_[4] = {~0ull, ~0ull, ~0ull, ~0ull};   // scratch epoch, KV epoch, precision gen, determinism gen
     uint64_t kv_epoch_ = 0;
     int ucap_ = 0;
 };

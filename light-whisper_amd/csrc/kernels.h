@@ -31,6 +31,20 @@ void linear_q8(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const f
 constexpr int kGemvRows = 4;
 void gemv_q8(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const float* bias, const float* res, float* y,
              int ldy, int epi, hipStream_t s, int cols = 0);
+// the 1–4-row decoder GEMVs, about one workgroup per CU, with the row operations around them fused (bit-identical to
+// the separate rmsnorm_q8 / gemv_q8 / swiglu_q8 launches): pro GV_RMS: activations = Q8(RMSNorm(src rows, stride
+// ld_src floats)·nw), K ≤ 4096; GV_NONE: the Q8 rows xq / xd, K ≤ 6144.  epi EPI_STORE / EPI_RESID into y, or
+// EPI_SWIGLU (GV_RMS only; W = interleaved gate/up, N % 64 == 0): h = Q8(silu(g)·u) into yq [M][N/2] / yd [M][N/64].
+enum GvPro : int { GV_NONE = 0, GV_RMS = 1 };
+bool gemv_fused_ok(int pro, int M, int K);
+void gemv_fused(int pro, const int8_t* xq, const float* xd, const float* src, int ld_src, const float* nw, float eps,
+                int M, const Q8Mat& W, const float* res, float* y, int ldy, int epi, int8_t* yq, float* yd,
+                hipStream_t s);
+// deterministic mode (process-wide): GEMMs never split K over workgroups (split-K sums land by float atomics, whose
+// order varies run to run); deterministic_gen() changes on every switch so captured step graphs are re-captured
+void set_deterministic(bool on);
+bool deterministic();
+uint64_t deterministic_gen();
 // force_cfg: index into kernels_q8.hip kGemmCfgs (-1 = heuristic); force_splits: split-K (0 = heuristic)
 void gemm_q8(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const float* bias, const float* res, float* y,
              int ldy, int epi, hipStream_t s, int force_cfg = -1, int force_splits = 0, int8_t* yq = nullptr,

@@ -4,6 +4,7 @@
 
 #include "kernels.h"
 #include "qk_rope.h"
+#include "rowops.h"
 #include "xlane.h"
 
 namespace qasr {
@@ -45,20 +46,6 @@ __device__ __forceinline__ void load32(const float* p, float* v) {
 // block is 8 consecutive lanes' chunks: its amax is three DPP steps, each lane packs its 4 int8 into one
 // dword (coalesced stores), the block's first lane writes the scale.  Rows up to RW_MAX·256 elements.
 constexpr int RW_MAX = 16;
-
-__device__ __forceinline__ float amax8(float v) { return max8(v); }
-
-__device__ __forceinline__ void quant4_store(float4 v, int c, int lane, int8_t* qrow, float* drow) {
-    const float am = amax8(fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
-    const float dd = am / 127.f;
-    int32_t w = 0;
-    if (am != 0.f) {
-        w = ((int)roundf(v.x / dd) & 0xff) | (((int)roundf(v.y / dd) & 0xff) << 8) |
-            (((int)roundf(v.z / dd) & 0xff) << 16) | (((int)roundf(v.w / dd) & 0xff) << 24);
-    }
-    ((int32_t*)qrow)[c] = w;
-    if ((lane & 7) == 0) drow[c >> 3] = __half2float(f2h(dd));
-}
 
 template <int KC>
 __global__ __launch_bounds__(256) void k_rmsnorm_q8(const float* __restrict__ x, int M, int H, int ldx,
@@ -103,37 +90,11 @@ __global__ __launch_bounds__(256) void k_rmsnorm_q8_wg(const float* __restrict__
                                                        float* __restrict__ d, float4* __restrict__ zero,
                                                        int64_t nzero4) {
     __shared__ float part[4];
-    const int tid = threadIdx.x, lane = tid & 63, row = blockIdx.x;
+    const int tid = threadIdx.x, row = blockIdx.x;
     // optional: clear the next split-K GEMM's output (saves a memset launch per layer)
     for (int64_t i = (int64_t)row * 256 + tid; i < nzero4; i += (int64_t)gridDim.x * 256)
         zero[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-    const int nc = H / 4;
-    const float4* xr = (const float4*)(x + (size_t)row * ldx);
-    const float4* g4 = (const float4*)w;
-    float4 v[KC], gw[KC];
-#pragma unroll
-    for (int k = 0; k < KC; k++) {
-        const int c = tid + 256 * k;
-        v[k] = c < nc ? xr[c] : make_float4(0.f, 0.f, 0.f, 0.f);
-        gw[k] = c < nc ? g4[c] : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-    float ss = 0.f;
-#pragma unroll
-    for (int k = 0; k < KC; k++) ss += v[k].x * v[k].x + v[k].y * v[k].y + v[k].z * v[k].z + v[k].w * v[k].w;
-    ss = wsum(ss);
-    if (lane == 0) part[tid >> 6] = ss;
-    __syncthreads();
-    ss = (part[0] + part[1]) + (part[2] + part[3]);
-    const float inv = 1.0f / sqrtf(ss / (float)H + eps);
-#pragma unroll
-    for (int k = 0; k < KC; k++) {
-        const int c = tid + 256 * k;
-        if (256 * k + (tid & ~7) < nc) {   // 8-thread blocks are all in or all out (nc % 8 == 0)
-            const float4 g = gw[k];
-            const float4 y = make_float4(v[k].x * inv * g.x, v[k].y * inv * g.y, v[k].z * inv * g.z, v[k].w * inv * g.w);
-            quant4_store(y, c, lane, q + (size_t)row * H, d + (size_t)row * (H / 32));
-        }
-    }
+    rms_row_q8_wg<KC>(x + (size_t)row * ldx, H, w, eps, q + (size_t)row * H, d + (size_t)row * (H / 32), part);
 }
 
 void rmsnorm_q8(const float* x, int M, int H, int ldx, const float* w, float eps, int8_t* q, float* d, hipStream_t s,
@@ -204,7 +165,7 @@ __global__ __launch_bounds__(256) void k_layernorm_q8(const float* __restrict__ 
         }
         if (q) {
             if (c < nc) quant4_store(o, c, lane, q + (size_t)row * H, d + (size_t)row * (H / 32));
-            else amax8(0.f);
+            else max8(0.f);
         }
     }
 }
@@ -254,24 +215,8 @@ __global__ __launch_bounds__(256) void k_swiglu_q8_lane(const float* __restrict_
                                                         int8_t* __restrict__ q, float* __restrict__ d, int interleaved) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= (int64_t)M * F) return;     // F % 32 == 0: a 32-lane group never straddles the bound
-    const int m = (int)(i / F), f = (int)(i % F), b = f >> 5, j = f & 31;
-    const float* row = gu + (size_t)m * 2 * F;
-    float g, u;
-    if (interleaved) {   // h columns 32b..32b+31 = [g 16 | u 16 | g 16 | u 16] at 64b
-        const int c = 64 * b + (j < 16 ? j : j + 16);
-        g = row[c];
-        u = row[c + 16];
-    } else {
-        g = row[f];
-        u = row[F + f];
-    }
-    const float v = g / (1.f + expf(-g)) * u;
-    float amax = fabsf(v);
-#pragma unroll
-    for (int o = 16; o >= 1; o >>= 1) amax = fmaxf(amax, __shfl_xor(amax, o));
-    const float dd = amax / 127.f;
-    q[(size_t)m * F + f] = (int8_t)(amax == 0.f ? 0 : (int)roundf(v / dd));
-    if (j == 0) d[(size_t)m * (F / 32) + b] = __half2float(f2h(dd));
+    const int m = (int)(i / F), f = (int)(i % F);
+    swiglu_lane_q8(gu + (size_t)m * 2 * F, F, f, interleaved != 0, q + (size_t)m * F, d + (size_t)m * (F / 32));
 }
 
 void swiglu_q8(const float* gu, int M, int F, int8_t* q, float* d, hipStream_t s, bool interleaved) {

@@ -5,10 +5,12 @@
 //   activation block (32): d = amax/127 (f32), q = roundf(x/d) (IEEE division), d kept as f16
 //   block dot: exact int32 Σ q_w·q_x, contribution (float)sum · (d_w·d_x), f32 accumulation.
 #include <algorithm>
+#include <atomic>
 #include <type_traits>
 
 #include "kernels.h"
 #include "lds_dma.h"
+#include "rowops.h"
 #include "xlane.h"
 
 namespace qasr {
@@ -248,6 +250,223 @@ void gemv_q8(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const flo
     else if (M <= 4) gemv_launch<4>(cols, xq, xd, M, W, bias, res, y, ldy, epi, s);
     else gemv_launch<8>(std::min(cols, 2), xq, xd, M, W, bias, res, y, ldy, epi, s);
 }
+
+// ------------------------------------------------------------------------------------------------ fused decode GEMV
+// The 1–4-row decoder's weight-streaming launches with the row operations that feed or follow them folded in (at
+// batch 1 a separate norm or SwiGLU launch costs ~2 µs of a ~33 µs layer, tools/graph_cost.py).  About one
+// workgroup per CU: a wave owns CPW output columns and issues every 16-byte weight load of them first (T = ⌈K/1024⌉
+// chunks per lane per column, lane l reading bytes 16(l + 64t); chunks past K clamped and dropped as in k_gemv_q8),
+// so the workgroup's whole weight slice is in flight while it builds its activation rows:
+//   GV_RMS:  Q8(RMSNorm(src row)·nw) into LDS by rms_row_q8_wg (rmsnorm_q8's per-row-workgroup arithmetic), once
+//            per workgroup (a prologue in every workgroup of a column-group grid costs more than the launch it saves);
+//   GV_NONE: the Q8 rows as given (global memory).
+// SWI: the workgroup's 64 columns are one h block of the interleaved gate/up matrix, whose SwiGLU + Q8
+// (swiglu_q8_block: swiglu_q8's lane arithmetic) is the epilogue, into yq [M][N/2] / yd [M][N/64].
+// The dot products, their order and the store / residual epilogue are k_gemv_q8's, so the outputs are bit-identical
+// to the separate launches (tests/test_ops_gpu.py::test_gemv_fused_*).
+template <int MR, int CPW, int T, int PRO, bool SWI, int NWV>
+__global__ __launch_bounds__(64 * NWV) void k_gemv_wide(const int8_t* __restrict__ W, const __half* __restrict__ Wsc,
+                                                        int N, int K, int M, const int8_t* __restrict__ X,
+                                                        const float* __restrict__ Xd, const float* __restrict__ src,
+                                                        int ld_src, const float* __restrict__ nw, float eps,
+                                                        const float* res, float* y, int ldy, int epi,
+                                                        int8_t* __restrict__ yq, float* __restrict__ yd) {
+    static_assert(!SWI || CPW * NWV == 64, "SwiGLU epilogue: one 64-column h block per workgroup");
+    extern __shared__ __align__(16) unsigned char gv_smem[];
+    __shared__ float part[MR][4];
+    __shared__ float gub[SWI ? MR : 1][64];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int n0 = (blockIdx.x * NWV + wv) * CPW;
+    const int nb = K / QK;
+    // the norm rows' loads go out first (measured: 0.8 µs less than behind the weight stream, whose loads a wave's
+    // in-order completion would make them wait for)
+    constexpr int RK = PRO == GV_RMS ? T : 1;
+    float4 rv[PRO == GV_RMS ? MR : 1][RK], rg[RK];
+    if constexpr (PRO == GV_RMS) {
+        if (tid < 256) {
+#pragma unroll
+            for (int m = 0; m < MR; m++)
+                if (m < M) rms_row_load<RK>(src + (size_t)m * ld_src, K, nw, rv[m], rg);
+        }
+    }
+    int4 w[CPW][T];
+    float dw[CPW][T];
+#pragma unroll
+    for (int c = 0; c < CPW; c++) {
+        const int n = min(n0 + c, N - 1);
+#pragma unroll
+        for (int t = 0; t < T; t++) {
+            const int kc = min(16 * (lane + 64 * t), K - 16);
+            const v4i wv4 = __builtin_nontemporal_load((const v4i*)(W + (size_t)n * K + kc));
+            w[c][t] = make_int4(wv4.x, wv4.y, wv4.z, wv4.w);
+            dw[c][t] = __half2float(Wsc[(size_t)n * nb + (kc >> 5)]);
+        }
+    }
+    const int8_t* xq = X;
+    const float* xd = Xd;
+    if constexpr (PRO == GV_RMS) {
+        int8_t* sq = (int8_t*)gv_smem;
+        float* sd = (float*)(gv_smem + (size_t)MR * K);
+#pragma unroll
+        for (int m = 0; m < MR; m++)   // M is uniform: every thread meets the barriers inside
+            if (m < M)
+                rms_row_q8_finish<RK>(rv[m], rg, K, eps, sq + (size_t)m * K, sd + (size_t)m * nb, part[m], tid < 256);
+        __syncthreads();
+        xq = sq;
+        xd = sd;
+    }
+    const bool even = (lane & 1) == 0;
+    float acc[CPW][MR];
+#pragma unroll
+    for (int c = 0; c < CPW; c++)
+#pragma unroll
+        for (int m = 0; m < MR; m++) acc[c][m] = 0.f;
+#pragma unroll
+    for (int t = 0; t < T; t++) {
+        const int k = 16 * (lane + 64 * t);
+        const bool in = k < K;
+        const int kc = min(k, K - 16), blk = kc >> 5;
+        int4 x[MR];
+        float dx[MR];
+#pragma unroll
+        for (int m = 0; m < MR; m++) {
+            const int mm = min(m, M - 1);
+            x[m] = *(const int4*)(xq + (size_t)mm * K + kc);
+            dx[m] = xd[(size_t)mm * nb + blk];
+        }
+#pragma unroll
+        for (int c = 0; c < CPW; c++) {
+#pragma unroll
+            for (int m = 0; m < MR; m++) {
+                int p = __builtin_amdgcn_sdot4(w[c][t].x, x[m].x, 0, false);
+                p = __builtin_amdgcn_sdot4(w[c][t].y, x[m].y, p, false);
+                p = __builtin_amdgcn_sdot4(w[c][t].z, x[m].z, p, false);
+                p = __builtin_amdgcn_sdot4(w[c][t].w, x[m].w, p, false);
+                p += __builtin_amdgcn_update_dpp(0, p, 0xB1, 0xf, 0xf, false);   // + lane ^ 1
+                acc[c][m] += (even && in) ? (float)p * (dw[c][t] * dx[m]) : 0.f;
+            }
+        }
+    }
+    if constexpr (SWI) {
+#pragma unroll
+        for (int c = 0; c < CPW; c++)
+#pragma unroll
+            for (int m = 0; m < MR; m++) {
+                const float v = wave_sum(acc[c][m]);
+                if (lane == 0 && m < M) gub[m][wv * CPW + c] = v;
+            }
+        __syncthreads();
+        const int m = 2 * wv + (lane >> 5), j = lane & 31;   // rows 2w, 2w+1 on wave w's lane halves
+        if (m < M)   // uniform over each 32-lane group
+            swiglu_q8_block(gub[m], j, yq + (size_t)m * (N / 2) + 32 * blockIdx.x + j,
+                            yd + (size_t)m * (N / 64) + blockIdx.x);
+    } else {
+#pragma unroll
+        for (int c = 0; c < CPW; c++) {
+#pragma unroll
+            for (int m = 0; m < MR; m++) {
+                const float v = wave_sum(acc[c][m]);
+                const int n = n0 + c;
+                if (lane == 0 && m < M && n < N) y[(size_t)m * ldy + n] = epi_apply(epi, v, m, n, nullptr, res, ldy);
+            }
+        }
+    }
+}
+
+struct GvArgs {
+    const Q8Mat* W;
+    int M;
+    const int8_t* xq;
+    const float* xd;
+    const float* src;
+    int ld_src;
+    const float* nw;
+    float eps;
+    const float* res;
+    float* y;
+    int ldy, epi;
+    int8_t* yq;
+    float* yd;
+};
+
+template <int MR, int CPW, int T, int PRO, bool SWI, int NWV>
+static void gv_go(const GvArgs& a, hipStream_t s) {
+    const Q8Mat& W = *a.W;
+    const dim3 g(cdiv(W.N, NWV * CPW));
+    const size_t lds = PRO == GV_RMS ? (size_t)MR * W.K + (size_t)MR * (W.K / QK) * sizeof(float) : 0;
+    k_gemv_wide<MR, CPW, T, PRO, SWI, NWV><<<g, 64 * NWV, lds, s>>>(W.qs, W.sc, W.N, W.K, a.M, a.xq, a.xd, a.src,
+                                                                    a.ld_src, a.nw, a.eps, a.res, a.y, a.ldy, a.epi,
+                                                                    a.yq, a.yd);
+}
+
+template <int MR, int CPW, int PRO>
+static void gv_t(int T, const GvArgs& a, hipStream_t s) {
+    switch (T) {
+        case 1: gv_go<MR, CPW, 1, PRO, false, 4>(a, s); break;
+        case 2: gv_go<MR, CPW, 2, PRO, false, 4>(a, s); break;
+        case 3: gv_go<MR, CPW, 3, PRO, false, 4>(a, s); break;
+        case 4: gv_go<MR, CPW, 4, PRO, false, 4>(a, s); break;
+        default:
+            if constexpr (PRO == GV_NONE) gv_go<MR, CPW, 6, PRO, false, 4>(a, s);
+            break;
+    }
+}
+
+template <int MR>
+static void gv_mr(int pro, bool swi, int cpw, int T, const GvArgs& a, hipStream_t s) {
+    if (swi) {
+        switch (T) {
+            case 1: gv_go<MR, 8, 1, GV_RMS, true, 8>(a, s); break;
+            case 2: gv_go<MR, 8, 2, GV_RMS, true, 8>(a, s); break;
+            case 3: gv_go<MR, 8, 3, GV_RMS, true, 8>(a, s); break;
+            default: gv_go<MR, 8, 4, GV_RMS, true, 8>(a, s); break;
+        }
+    } else if (pro == GV_RMS) {
+        if (cpw == 4) gv_t<MR, 4, GV_RMS>(T, a, s);
+        else if (cpw == 2) gv_t<MR, 2, GV_RMS>(T, a, s);
+        else gv_t<MR, 1, GV_RMS>(T, a, s);
+    } else {
+        if (cpw == 4) gv_t<MR, 4, GV_NONE>(T, a, s);
+        else if (cpw == 2) gv_t<MR, 2, GV_NONE>(T, a, s);
+        else gv_t<MR, 1, GV_NONE>(T, a, s);
+    }
+}
+
+bool gemv_fused_ok(int pro, int M, int K) {
+    if (M < 1 || M > kGemvRows || K % QK != 0 || K < QK) return false;
+    return pro == GV_RMS ? K <= 4096 : K <= 6144;
+}
+
+void gemv_fused(int pro, const int8_t* xq, const float* xd, const float* src, int ld_src, const float* nw, float eps,
+                int M, const Q8Mat& W, const float* res, float* y, int ldy, int epi, int8_t* yq, float* yd,
+                hipStream_t s) {
+    const bool swi = epi == EPI_SWIGLU;
+    ProfScope ps(s, pro == GV_RMS ? (swi ? "gemv_q8_rms_swiglu" : "gemv_q8_rms") : "gemv_q8_wide",
+                 2.0 * M * W.N * W.K, q8_bytes(M, W, swi ? EPI_STORE : epi));
+    QASR_CHECK(pro == GV_RMS || pro == GV_NONE, QASR_E_INVALID, "gemv_fused: unknown prologue");
+    QASR_CHECK(gemv_fused_ok(pro, M, W.K), QASR_E_INVALID, "gemv_fused: rows or K out of range");
+    QASR_CHECK(pro != GV_RMS || (nw && ld_src % 4 == 0 && ((uintptr_t)src & 15) == 0), QASR_E_INVALID,
+               "gemv_fused: norm rows must be 16-byte aligned float rows with a weight");
+    QASR_CHECK(pro != GV_NONE || (xq && xd), QASR_E_INVALID, "gemv_fused: Q8 rows missing");
+    QASR_CHECK(epi == EPI_STORE || (epi == EPI_RESID && res) || (swi && pro == GV_RMS && W.N % 64 == 0 && yq && yd),
+               QASR_E_INVALID, "gemv_fused: epilogue (SwiGLU needs the norm prologue, N % 64 == 0 and yq / yd)");
+    const int T = cdiv(W.K, 1024);
+    // columns per wave: about one workgroup of four waves per CU on the decoder shapes (N 1,024–4,096)
+    const int cpw = W.N >= 4096 ? 4 : W.N >= 2048 ? 2 : 1;
+    const GvArgs a{&W, M, xq, xd, src, ld_src, nw, eps, res, y, ldy, epi, yq, yd};
+    if (M <= 1) gv_mr<1>(pro, swi, cpw, T, a, s);
+    else if (M <= 2) gv_mr<2>(pro, swi, cpw, T, a, s);
+    else gv_mr<4>(pro, swi, cpw, T, a, s);
+}
+
+static std::atomic<int> g_det{0};
+static std::atomic<uint64_t> g_det_gen{0};
+void set_deterministic(bool on) {
+    if (g_det.exchange(on ? 1 : 0) != (on ? 1 : 0)) g_det_gen++;
+}
+bool deterministic() { return g_det.load(std::memory_order_relaxed) != 0; }
+uint64_t deterministic_gen() { return g_det_gen.load(); }
+
 
 // ------------------------------------------------------------------------------------------------ GEMM (MFMA)
 // Tile (32·TI)×(32·TJ), 256 threads = 2×2 waves, each wave (16·TI)×(16·TJ) built from
@@ -1315,6 +1534,7 @@ void gemm_mx(const uint8_t* x8, const uint8_t* xs, int M, const Q8Mat& W, const 
     const bool can_split = (epi == EPI_STORE || epi == EPI_RESID) && ldy == W.N && (epi != EPI_RESID || res == y);
     int splits = 1;
     if (tiles < 256 && can_split) splits = std::max(1, std::min(std::min(cdiv(512, tiles), steps / 2), 8));
+    if (deterministic()) splits = 1;
     const int sps = cdiv(steps, splits);
     splits = cdiv(steps, sps);
     if (splits > 1 && epi == EPI_STORE && !y_zeroed) QASR_HIP(hipMemsetAsync(y, 0, (size_t)M * ldy * sizeof(float), s));
@@ -1433,6 +1653,7 @@ void gemm_q8(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const flo
     int splits = 1;
     if (tiles < 256 && can_split) splits = std::max(1, std::min(std::min(cdiv(512, tiles), steps / 2), 8));
     if (force_splits > 0) splits = can_split ? std::min(force_splits, steps) : 1;
+    if (deterministic()) splits = 1;
     const int sps = cdiv(steps, splits);
     splits = cdiv(steps, sps);
     if (splits > 1 && epi == EPI_STORE && !y_zeroed)

@@ -118,6 +118,7 @@ SIGNATURES = {
     "qasr_op_gemm_swiglu_q8": (C.c_int, [P, P, I32, P, P, I32, I32, P, P, P]),
     "qasr_op_gemm_swiglu_q8_cfg": (C.c_int, [P, P, I32, P, P, I32, I32, P, P, I32, P]),
     "qasr_op_swiglu_q8_interleaved": (C.c_int, [P, I32, I32, P, P, P]),
+    "qasr_op_gemv_fused": (C.c_int, [I32, P, I32, P, F32, I32, P, P, P, P, I32, I32, P, P, I32, I32, P, P, P]),
     "qasr_op_qk_norm_rope": (C.c_int, [P, I32, I32, I32, I32, P, P, P, P, P, F32, P, P, P, P]),
     "qasr_op_q8_to_mx": (C.c_int, [P, P, I32, C.c_int64, P, P, P]),
     "qasr_op_gemm_mx": (C.c_int, [P, P, I32, P, P, I32, I32, P, P, P, I32, I32, P, P, I32, P]),
@@ -136,6 +137,7 @@ SIGNATURES = {
     "qasr_op_fbank": (C.c_int, [P, I64, P, P]),
     "qasr_stream_sync": (C.c_int, [P]),
     "qasr_prof_enable": (C.c_int, [C.c_int]),
+    "qasr_set_deterministic": (C.c_int, [I32]),
     "qasr_prof_reset": (C.c_int, []),
     "qasr_prof_report": (C.c_int, [C.c_char_p, SZ, C.POINTER(SZ)]),
 }

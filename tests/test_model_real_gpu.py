@@ -149,6 +149,44 @@ def test_real_greedy_run_matches_oracle(pair):
     assert div >= min(8, n)
 
 
+def test_real_decode_fusion_bit_identical(pair, monkeypatch):
+    """the 1–4-row decode with the norms / SwiGLU in the GEMV prologues (default) against the separate launches
+    (QASR_NO_DEC_FUSE=1): teacher-forced logits equal bit for bit, and 40 forced decode steps give the same tokens
+    (verdict r1 item 5: tokens identical to the previous build)"""
+    from qasr import _lib
+
+    arch, m, s, _ = pair
+    monkeypatch.setenv("QASR_NO_DEC_FUSE", "1")
+    s2 = m.session(kv_type="f16", n_ctx=4096)
+    monkeypatch.delenv("QASR_NO_DEC_FUSE")
+    # the prefill / encoder GEMMs split K with float atomics (run-to-run last-ulp noise): compare without
+    _lib.check(_lib.load().qasr_set_deterministic(1))
+    try:
+        audio = clip(5.0, 16)
+        forced = np.array([900 + 41 * i for i in range(5)], np.int32)
+        assert np.array_equal(s.forced_logits(audio, forced), s2.forced_logits(audio, forced))
+        a = s.run(audio, force_tokens_per_s=8).tokens
+        b = s2.run(audio, force_tokens_per_s=8).tokens
+        assert len(a) == 41 and a == b
+    finally:
+        _lib.check(_lib.load().qasr_set_deterministic(0))
+        s2.close()
+
+
+def test_real_deterministic_mode_repeats(pair):
+    """deterministic mode: two runs of the same request give bit-identical logits"""
+    from qasr import _lib
+
+    arch, _, s, _ = pair
+    audio = clip(2.0, 17)
+    forced = np.array([700, 701], np.int32)
+    _lib.check(_lib.load().qasr_set_deterministic(1))
+    try:
+        assert np.array_equal(s.forced_logits(audio, forced), s.forced_logits(audio, forced))
+    finally:
+        _lib.check(_lib.load().qasr_set_deterministic(0))
+
+
 def test_real_batch_equals_single_and_oracle(pair):
     """1.7B: 8 segments of 1-4.5 s decoded together (rows > 4: MFMA decode GEMMs, step graphs, shrinking batch) give
     the tokens of the 8 single runs (GEMV path); segment 0 also against the oracle.  A divergence is allowed only at

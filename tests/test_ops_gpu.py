@@ -282,6 +282,90 @@ def test_gemm_swiglu_q8(torch_dev, m, f, k, cfg):
     assert (np.abs(host(q2).astype(int) - qr) <= 1).all()
 
 
+def _q8_weights(torch_dev, n, k, seed):
+    qs, sc = q8_split(oracle.synth_q8(seed, "gv", n, k, 0.05), n, k)
+    return dev(qs, torch_dev), dev(sc, torch_dev)
+
+
+@pytest.mark.parametrize("m,n,k,epi", [(1, 4096, 2048, 0), (1, 2048, 1024, 1), (2, 12288, 2048, 0),
+                                       (4, 6144, 1024, 1), (1, 40000, 1024, 0), (3, 512, 4096, 0),
+                                       (1, 384, 256, 1), (2, 100, 896, 0)])
+def test_gemv_fused_rms(torch_dev, m, n, k, epi):
+    """norm-in-prologue GEMV == rmsnorm_q8 then the GEMV, bit for bit (the decode fusion's parity contract)"""
+    import torch
+
+    rng = np.random.default_rng(11)
+    x = dev((rng.standard_normal((m, k)) * 3).astype(np.float32), torch_dev)
+    w = dev((1 + 0.1 * rng.standard_normal(k)).astype(np.float32), torch_dev)
+    res = dev(rng.standard_normal((m, n)).astype(np.float32), torch_dev)
+    wq, ws = _q8_weights(torch_dev, n, k, 3)
+    q = empty((m, k), torch.int8, torch_dev)
+    d = empty((m, k // 32), torch.float32, torch_dev)
+    y0, y1 = res.clone(), res.clone()
+    _lib.check(L().qasr_op_rmsnorm_q8(ptr(x), m, k, ptr(w), 1e-6, ptr(q), ptr(d), None))
+    _lib.check(L().qasr_op_linear_q8(ptr(q), ptr(d), m, ptr(wq), ptr(ws), n, k, None, ptr(y0), ptr(y0), n, epi, 1,
+                                     None))
+    _lib.check(L().qasr_op_gemv_fused(1, ptr(x), k, ptr(w), 1e-6, m, None, None, ptr(wq), ptr(ws), n, k, ptr(y1),
+                                      ptr(y1), n, epi, None, None, None))
+    assert np.array_equal(host(y0), host(y1))
+
+
+@pytest.mark.parametrize("m,n,k,epi", [(1, 2048, 6144, 1), (4, 1024, 3072, 1), (1, 2048, 2048, 1), (2, 1024, 2048, 0),
+                                       (3, 4096, 5120, 1), (1, 300, 96, 0)])
+def test_gemv_fused_q8_rows(torch_dev, m, n, k, epi):
+    """the per-CU GEMV on given Q8 rows (O / down projections) == gemv_q8, bit for bit"""
+    import torch
+
+    rng = np.random.default_rng(13)
+    xq = dev(rng.integers(-127, 128, (m, k), dtype=np.int8), torch_dev)
+    xd = dev((rng.random((m, k // 32)) * 0.02).astype(np.float32), torch_dev)
+    res = dev(rng.standard_normal((m, n)).astype(np.float32), torch_dev)
+    wq, ws = _q8_weights(torch_dev, n, k, 5)
+    y0, y1 = res.clone(), res.clone()
+    _lib.check(L().qasr_op_linear_q8(ptr(xq), ptr(xd), m, ptr(wq), ptr(ws), n, k, None, ptr(y0), ptr(y0), n, epi, 1,
+                                     None))
+    _lib.check(L().qasr_op_gemv_fused(0, None, 0, None, 0.0, m, ptr(xq), ptr(xd), ptr(wq), ptr(ws), n, k, ptr(y1),
+                                      ptr(y1), n, epi, None, None, None))
+    assert np.array_equal(host(y0), host(y1))
+
+
+@pytest.mark.parametrize("m,f,k", [(1, 6144, 2048), (4, 3072, 1024), (2, 256, 256), (3, 512, 4096)])
+def test_gemv_fused_swiglu(torch_dev, m, f, k):
+    """norm + interleaved gate/up GEMV + SwiGLU + Q8 in one launch == rmsnorm_q8, the GEMV into f32 gate/up rows and
+    swiglu_q8 (interleaved), bit for bit"""
+    import torch
+
+    rng = np.random.default_rng(12)
+    x = dev((rng.standard_normal((m, k)) * 3).astype(np.float32), torch_dev)
+    w = dev((1 + 0.1 * rng.standard_normal(k)).astype(np.float32), torch_dev)
+    wq, ws = _q8_weights(torch_dev, 2 * f, k, 4)
+    _lib.check(L().qasr_op_interleave_gate_up(ptr(wq), ptr(ws), 2 * f, k, None))
+    q = empty((m, k), torch.int8, torch_dev)
+    d = empty((m, k // 32), torch.float32, torch_dev)
+    gu = empty((m, 2 * f), torch.float32, torch_dev)
+    h0, hd0 = empty((m, f), torch.int8, torch_dev), empty((m, f // 32), torch.float32, torch_dev)
+    h1, hd1 = empty((m, f), torch.int8, torch_dev), empty((m, f // 32), torch.float32, torch_dev)
+    _lib.check(L().qasr_op_rmsnorm_q8(ptr(x), m, k, ptr(w), 1e-6, ptr(q), ptr(d), None))
+    _lib.check(L().qasr_op_linear_q8(ptr(q), ptr(d), m, ptr(wq), ptr(ws), 2 * f, k, None, None, ptr(gu), 2 * f, 0, 1,
+                                     None))
+    _lib.check(L().qasr_op_swiglu_q8_interleaved(ptr(gu), m, f, ptr(h0), ptr(hd0), None))
+    _lib.check(L().qasr_op_gemv_fused(1, ptr(x), k, ptr(w), 1e-6, m, None, None, ptr(wq), ptr(ws), 2 * f, k, None,
+                                      None, 0, 3, ptr(h1), ptr(hd1), None))
+    assert np.array_equal(host(h0), host(h1)) and np.array_equal(host(hd0), host(hd1))
+
+
+def test_gemv_fused_rejects_bad_shapes(torch_dev):
+    import torch
+
+    x = empty((8, 8192), torch.float32, torch_dev)
+    y = empty((8, 64), torch.float32, torch_dev)
+    for pro, m, k, epi in ((1, 5, 1024, 0), (1, 1, 8192, 0), (0, 1, 8192, 0), (3, 1, 1024, 0), (1, 1, 100, 0),
+                           (0, 1, 1024, 3)):
+        with pytest.raises(_lib.QasrError):
+            _lib.check(L().qasr_op_gemv_fused(pro, ptr(x), 2 * k, ptr(x), 1e-6, m, ptr(x), ptr(x), ptr(x), ptr(x), 64,
+                                              k, None, ptr(y), 64, epi, ptr(x), ptr(x), None))
+
+
 @pytest.mark.parametrize("m", [1, 4, 40])
 def test_swiglu_q8(torch_dev, m):
     """lane-per-element kernel (M <= 16) and thread-per-block kernel (larger M)"""
