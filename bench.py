@@ -126,6 +126,46 @@ def traffic_per_launch(kernel):
         return round(json.load(f)["per_launch_bytes"])
 
 
+# bench kernel class (ProfScope names) → tools/pmc_classes.py classes it spans
+PMC_CLASSES = {"gemm_q8": ("gemm_q8_prefill", "gemm_q8_decode"), "gemm_mx": ("gemm_mx",),
+               "attention": ("attention_decode", "attention_tile"), "gemv_q8": ("gemv_q8",)}
+
+
+def pmc_evidence(kernel):
+    """MFMA-busy and HBM traffic of `kernel`'s class from the newest committed per-class counter passes of this bench
+    command (profiles/*pmc_classes*.json, tools/pmc_round.sh → tools/pmc_classes.py; raw SQ/GRBM/TCC counters
+    summed over the classes it spans): MFMA busy = SQ_VALU_MFMA_BUSY_CYCLES / (1,024 SIMDs × GRBM_GUI_ACTIVE/8),
+    HBM = 2·FETCH_SIZE + WRITE_SIZE (gfx950 FETCH_SIZE counts half of 16-B streaming reads).  None if absent."""
+    import glob
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_classes*.json")))
+    names = PMC_CLASSES.get(kernel, (kernel,))
+    if not files:
+        return None
+    with open(files[-1]) as f:
+        pmc = json.load(f)
+    busy = grbm = fetch = write = time_ns = launches = 0.0
+    found = []
+    for c in names:
+        if c not in pmc:
+            continue
+        found.append(c)
+        raw = pmc[c]["raw"]
+        busy += raw.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0)
+        grbm += raw.get("GRBM_GUI_ACTIVE", 0.0)
+        fetch += raw.get("FETCH_SIZE", 0.0)
+        write += raw.get("WRITE_SIZE", 0.0)
+        time_ns += pmc[c]["avg_us"] * 1e3 * pmc[c]["launches_per_pass"]
+        launches += pmc[c]["launches_per_pass"]
+    if not found:
+        return None
+    hbm_bytes = (2 * fetch + write) * 1024
+    return {"source": os.path.relpath(files[-1], ROOT), "classes": found,
+            "mfma_busy": round(busy / (1024 * grbm / 8), 4) if grbm else None,
+            "hbm_gbps": round(hbm_bytes / time_ns, 1) if time_ns else None,
+            "hbm_bytes_per_launch": round(hbm_bytes / launches) if launches else None}
+
+
 def main():
     global SEG_PER_RANK
     ap = argparse.ArgumentParser()
@@ -298,6 +338,12 @@ def main():
                         "frac": round(ach / 8000.0, 4), "traffic": None,
                         "avg_launch_us": round(avg_s * 1e6, 2), "launches": p["count"],
                         "measured_on": "one instrumented step after the timed region (HIP events per launch)"}
+            # hardware-counter evidence for the same kernel class (north_star: "rocprof HBM GB/s and MFMA-busy")
+            ev = pmc_evidence(name)
+            if ev:
+                roof["mfma_busy"], roof["hbm_gbps"] = ev["mfma_busy"], ev["hbm_gbps"]
+                roof["traffic"] = ev["hbm_bytes_per_launch"]   # the newest counter passes supersede older ones
+                roof["pmc"] = ev
             roof["breakdown_ms"] = {k: round(v["ms"], 3) for k, v in sorted(prof.items(), key=lambda kv: -kv[1]["ms"])}
         cpu = None
         if not args.no_cpu_baseline:

@@ -7,6 +7,8 @@
 #include <string.h>
 
 #include <algorithm>
+#include <cstdio>
+#include <map>
 #include <chrono>
 
 #include "capi_util.h"
@@ -739,8 +741,12 @@ void Session::run_batch(const float* dpcm, const std::vector<int64_t>& off, cons
         memcpy(graph_key_, key, sizeof key);
     }
     int step = 1;
+    // QASR_STEP_HIST=1: decode steps per row bucket on stderr (tuning aid for the decode GEMM shapes)
+    static const bool hist = getenv("QASR_STEP_HIST") != nullptr;
+    std::map<int, int> steps_per_bucket;
     while (bound > 0) {
         const int B = row_bucket(bound);
+        if (hist) steps_per_bucket[B]++;
         if (graphs) {
             auto it = graphs_.find(B);
             if (it == graphs_.end()) {
@@ -772,6 +778,11 @@ void Session::run_batch(const float* dpcm, const std::vector<int64_t>& off, cons
         step++;
     }
     QASR_HIP(hipStreamSynchronize(st_));
+    if (hist) {
+        fprintf(stderr, "decode steps per row bucket:");
+        for (auto& kv : steps_per_bucket) fprintf(stderr, " %d:%d", kv.first, kv.second);
+        fprintf(stderr, "\n");
+    }
     {
         std::vector<int> hb((size_t)6 * ucap_ + 16), ho((size_t)count * ld);
         QASR_HIP(hipMemcpyAsync(hb.data(), blk, hb.size() * sizeof(int), hipMemcpyDeviceToHost, st_));
