@@ -456,7 +456,9 @@ void Session::draft_step(int B) {
 // from the draft.  Row i's logits predict the token after row i's input, so an accepted prefix is exactly what one
 // greedy step per token would emit; KV rows written for rejected draft tokens sit past the accepted length and are
 // rewritten by the next pass.  A draft that keeps failing at its first token shrinks (to none: a plain greedy step).
-void Session::draft_decode(int n_prompt, int base, int budget, int dummy, std::vector<int32_t>& toks, bool& eos) {
+// forced: a fixed token count (force_tokens_per_s): EOS is emitted like any token, as by the batch loop.
+void Session::draft_decode(int n_prompt, int base, int budget, int dummy, std::vector<int32_t>& toks, bool& eos,
+                           bool forced) {
     const qasr_hparams& h = m_->hp;
     constexpr int RMAX = 16;
     int max_draft = RMAX - 1;
@@ -536,7 +538,7 @@ void Session::draft_decode(int n_prompt, int base, int budget, int dummy, std::v
         int acc = 0;
         for (int i = 0; i < R; i++) {
             const int t = got[i];
-            if (t == h.tok_eos0 || t == h.tok_eos1) {
+            if (!forced && (t == h.tok_eos0 || t == h.tok_eos1)) {
                 eos = true;
                 break;
             }
@@ -691,7 +693,7 @@ void Session::run_batch(const float* dpcm, const std::vector<int64_t>& off, cons
         QASR_HIP(hipMemcpyAsync(pin_cnt_, ds.counters, 4 * sizeof(int), hipMemcpyDeviceToHost, st_));
         QASR_HIP(hipStreamSynchronize(st_));
     }
-    if (count == 1 && draft_ && force_tps <= 0) {   // streaming: prompt-lookup drafts from earlier transcripts
+    if (count == 1 && draft_) {   // streaming: prompt-lookup drafts from earlier transcripts
         std::vector<int32_t> toks;
         bool eos = false;
         {
@@ -703,11 +705,11 @@ void Session::run_batch(const float* dpcm, const std::vector<int64_t>& off, cons
             QASR_HIP(hipStreamSynchronize(st_));
             const int first = hs[0], gen = hs[1], done = hs[2];
             if (gen > 0) toks.push_back(first);
-            eos = gen == 0;   // the prompt's first choice was EOS
-            if (!done) draft_decode(n_prompt[0], base[0], budget[0], (int)slots, toks, eos);
+            eos = gen == 0;   // the prompt's first choice was EOS (natural mode)
+            if (!done) draft_decode(n_prompt[0], base[0], budget[0], (int)slots, toks, eos, force_tps > 0);
         }
         out[0].tokens = toks;
-        out[0].truncated = !eos && (int)toks.size() >= budget[0];
+        out[0].truncated = force_tps <= 0 && !eos && (int)toks.size() >= budget[0];
         history_.insert(history_.end(), toks.begin(), toks.end());
         if (history_.size() > 8192) history_.erase(history_.begin(), history_.end() - 8192);
         dstats_.tokens += (int64_t)toks.size();

@@ -87,7 +87,8 @@ class Session {
     void decode_step(const DecState& ds, int B, bool sizing);
     // one verify pass of B rows (last accepted token + draft, padded): tables in S_DTAB, argmax → pinned host
     void draft_step(int B);
-    void draft_decode(int n_prompt, int base, int budget, int dummy, std::vector<int32_t>& toks, bool& eos);
+    void draft_decode(int n_prompt, int base, int budget, int dummy, std::vector<int32_t>& toks, bool& eos,
+                      bool forced);
     void lm_head_rows(const float* x, int rows, int ldx, float* logits);
     void mx_ws(int64_t rows, int64_t kmax);
     template <class T>

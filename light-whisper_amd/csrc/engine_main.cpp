@@ -526,6 +526,17 @@ struct Server {
         s.set("engine", Value::str(engine));
         s.set("backend", Value::str(backend));
         s.set("speculative_decoding", Value::boolean(false));
+        if (session) {   // this engine's prompt-lookup drafting of interim windows (an addition to the reference keys)
+            int64_t st[4] = {0, 0, 0, 0};
+            if (qasr_session_draft_stats(session, st) == QASR_OK) {
+                Value d = Value::object();
+                d.set("passes", Value::integer((int)st[0]));
+                d.set("proposed", Value::integer((int)st[1]));
+                d.set("accepted", Value::integer((int)st[2]));
+                d.set("tokens", Value::integer((int)st[3]));
+                s.set("prompt_lookup", d);
+            }
+        }
         Value ml = Value::object();
         ml.set("asr", Value::boolean(model != nullptr || (fake && initialized)));
         ml.set("vad", Value::boolean(vad != nullptr || (fake && initialized)));

@@ -482,3 +482,30 @@ def test_streaming_draft_equals_greedy(torch_dev, golden):
         drf.close()
     finally:
         m.close()
+
+
+def test_streaming_draft_forced_count(torch_dev, golden):
+    """the draft path under a forced token count (the C3 benchmark's QASR_FORCE_TOKENS_PER_S): exactly the forced
+    number of tokens, EOS emitted like any other token, greedy's tokens up to a near-tie"""
+    from qasr.transcribe_cpp import Model
+
+    m = Model.synthetic(arch=None, seed=TINY_SEED, hparams=tiny_hparams())
+    try:
+        ref, drf = m.session(kv_type="f16", n_ctx=2048), m.session(kv_type="f16", n_ctx=2048)
+        drf.set_draft(True)
+        audio = golden["c__audio"]
+        for w in (audio[:16000], audio[:24000], audio, audio):
+            want = ref.run(w, force_tokens_per_s=8).tokens
+            got = drf.run(w, force_tokens_per_s=8).tokens
+            assert len(got) == len(want) == int(round(8 * w.size / 16000)) + 1
+            div = next((i for i in range(len(want)) if got[i] != want[i]), len(want))
+            if div < len(want):
+                lg = ref.forced_logits(w, np.array(want[:max(div, 1)], np.int32))
+                top2 = np.sort(lg[div])[-2:]
+                assert top2[1] - top2[0] < 0.02 * np.abs(lg[div]).max(), f"draft diverges at {div} without a near-tie"
+        st = drf.draft_stats()
+        assert st["accepted"] > 0 and st["passes"] < st["tokens"], st
+        ref.close()
+        drf.close()
+    finally:
+        m.close()

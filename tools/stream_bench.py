@@ -29,7 +29,7 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-from bench import recording  # noqa: E402
+from bench import recording, speech_like  # noqa: E402
 
 SR = 16000
 MIN_INTERIM_S, MIN_GROWTH, WINDOW_S = 0.2, 1024, 12.0
@@ -89,12 +89,17 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--seconds", type=float, default=60.0)
     ap.add_argument("--engine", default="qwen3-asr-1.7b")
+    ap.add_argument("--speech-only", action="store_true",
+                    help="continuous speech-like audio (no pauses): every window is ~12 s of speech the VAD keeps, "
+                         "the full-load case (the default recording's pauses let the VAD trim windows)")
+    ap.add_argument("--draft", type=int, default=1, help="QASR_STREAM_DRAFT (prompt-lookup drafts, 1 = default on)")
     a = ap.parse_args()
-    audio = recording(a.seconds, seed=3)
+    audio = (speech_like(np.random.default_rng(3), int(a.seconds * SR)) if a.speech_only else
+             recording(a.seconds, seed=3))
     hot = [f"热词{i:03d}" for i in range(100)]
     with tempfile.TemporaryDirectory() as tmp:
         eng = Engine(a.engine, {"QASR_SYNTHETIC": "1", "QASR_FORCE_TOKENS_PER_S": "8", "HF_HUB_CACHE": tmp,
-                                "LIGHT_WHISPER_DATA_DIR": tmp})
+                                "LIGHT_WHISPER_DATA_DIR": tmp, "QASR_STREAM_DRAFT": str(a.draft)})
         assert eng.init.get("success"), eng.init
         eng.request(transcribe_req(audio[: 2 * SR], hot))   # first-request warm-up (graphs, buffers)
         clock, interval, last, lat, inf, vad, sizes, speech = 0.0, I_BASE, 0, [], [], [], [], []
@@ -119,10 +124,13 @@ def main():
             interval = adjust_interval(interval, dt * 1e3)
         fin, fin_s = eng.request(transcribe_req(audio, hot))
         fin_ms = fin_s * 1e3
+        stats, _ = eng.request({"action": "stats"})
         eng.close()
     lat = np.array(lat)
-    out = {"workload": f"C3 streaming: {a.seconds:g} s recording (seed 3), interim ticks (interim.rs policy), "
-                       f"≤12 s windows, 100 hot words, + final request",
+    out = {"workload": f"C3 streaming: {a.seconds:g} s " + ("continuous speech-like audio" if a.speech_only else
+                                                               "recording (seed 3)")
+                       + ", interim ticks (interim.rs policy), ≤12 s windows, 100 hot words, + final request",
+           "draft": bool(a.draft),
            "engine": a.engine, "weights": "synthetic (QASR_SYNTHETIC=1), 8 forced tokens/audio-s",
            "requests": int(lat.size), "mean_window_s": round(float(np.mean(sizes)), 2),
            "p50_ms": round(float(np.median(lat)), 2), "p95_ms": round(float(np.percentile(lat, 95)), 2),
@@ -133,7 +141,8 @@ def main():
            "final": {"audio_s": round(audio.size / SR, 1), "round_trip_ms": round(fin_ms, 1),
                      "inference_ms": fin.get("inference_ms"), "vad_ms": fin.get("vad_ms"),
                      "speech_duration": fin.get("speech_duration"),
-                     "rtf_inv": round(audio.size / SR / (fin_ms / 1e3), 1)}}
+                     "rtf_inv": round(audio.size / SR / (fin_ms / 1e3), 1)},
+           "prompt_lookup": stats.get("stats", {}).get("prompt_lookup")}
     print(json.dumps(out, ensure_ascii=False), flush=True)
 
 
