@@ -1173,20 +1173,35 @@ __global__ __launch_bounds__(256, 2) void k_gemm_q8h(const __half* __restrict__ 
         if (!active) continue;
         const char* st = smem + (s % NBUF) * STAGE;
         const int hsel = ((k_begin + s * BK) / QK) & 1;
-        float sb[TJ], sa[TI][4];
+        // OP (outer-product scales, as in k_gemm_q8d): d_x(row)·d_w(col) of one i-fragment's 16×16·TJ outputs from
+        // one v_mfma_f32_16x16x1_4b_f32 (exact: a product of two f16 values), so the rescale is ONE fma per output
+        // and block — the f16 MFMA already returns the exact integer block sum as f32 (no cvt): same values as
+        // k_gemm_q8d's cvt + fma, hence bit-identical outputs
+        constexpr bool OP = TJ <= 4;
+        float sb[TJ], sa[TI][4], sal[TI], sbl = 0.f;
         v8h a[TI], b[TJ];
+        if constexpr (OP) {
+            const int cl = min(lane, 16 * TJ - 1);
+            const uint32_t v = *(const uint32_t*)(st + OSB + 4 * (bcol + cl));
+            sbl = __half2float(__ushort_as_half((unsigned short)(hsel ? v >> 16 : v & 0xffff)));
+        } else {
 #pragma unroll
-        for (int j = 0; j < TJ; j++) {
-            const uint32_t v = *(const uint32_t*)(st + OSB + 4 * (bcol + 16 * j + fr));
-            sb[j] = __half2float(__ushort_as_half((unsigned short)(hsel ? v >> 16 : v & 0xffff)));
+            for (int j = 0; j < TJ; j++) {
+                const uint32_t v = *(const uint32_t*)(st + OSB + 4 * (bcol + 16 * j + fr));
+                sb[j] = __half2float(__ushort_as_half((unsigned short)(hsel ? v >> 16 : v & 0xffff)));
+            }
         }
 #pragma unroll
         for (int i = 0; i < TI; i++) {
             int off = (arow + 16 * i + fr) * 64 + foff;
             asm volatile("" : "+v"(off));
             a[i] = *(const v8h*)(st + off);
-            const float4 v = *(const float4*)(st + OSA + 4 * (arow + 16 * i + fq));
-            sa[i][0] = v.x, sa[i][1] = v.y, sa[i][2] = v.z, sa[i][3] = v.w;
+            if constexpr (OP) {
+                sal[i] = *(const float*)(st + OSA + 4 * (arow + 16 * i + fr));
+            } else {
+                const float4 v = *(const float4*)(st + OSA + 4 * (arow + 16 * i + fq));
+                sa[i][0] = v.x, sa[i][1] = v.y, sa[i][2] = v.z, sa[i][3] = v.w;
+            }
         }
 #pragma unroll
         for (int j = 0; j < TJ; j++) {
@@ -1195,22 +1210,36 @@ __global__ __launch_bounds__(256, 2) void k_gemm_q8h(const __half* __restrict__ 
             b[j] = *(const v8h*)(st + off);
         }
         constexpr int LAG = 3;
+        constexpr int NPR = LAG / TJ + 2;   // outer-product results live at once (ring)
         v4f c[LAG + 1];
+        v16f prod[NPR];
 #pragma unroll
         for (int q = 0; q < NF + LAG; q++) {
-            if (q < NF)
+            if (q < NF) {
+                if constexpr (OP) {
+                    if (q % TJ == 0) {
+                        const v16f z = {};
+                        prod[(q / TJ) % NPR] = __builtin_amdgcn_mfma_f32_16x16x1f32(sal[q / TJ], sbl, z, 0, 0, 0);
+                    }
+                }
                 c[q % (LAG + 1)] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[q / TJ], b[q % TJ], v4f{0.f, 0.f, 0.f, 0.f},
                                                                           0, 0, 0);
+            }
             if (q >= LAG) {
                 const int p = q - LAG, i = p / TJ, j = p % TJ;
 #pragma unroll
-                for (int r = 0; r < 4; r++) acc[i][j][r] = fmaf(c[p % (LAG + 1)][r], sa[i][r] * sb[j], acc[i][j][r]);
+                for (int r = 0; r < 4; r++) {
+                    if constexpr (OP)
+                        acc[i][j][r] = fmaf(c[p % (LAG + 1)][r], prod[(p / TJ) % NPR][4 * j + r], acc[i][j][r]);
+                    else
+                        acc[i][j][r] = fmaf(c[p % (LAG + 1)][r], sa[i][r] * sb[j], acc[i][j][r]);
+                }
             }
         }
 #pragma unroll
         for (int t = 0; t < NF; t++) {
             __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-            __builtin_amdgcn_sched_group_barrier(0x002, 8, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, OP ? 4 : 8, 0);
         }
     }
     if (!active) return;
