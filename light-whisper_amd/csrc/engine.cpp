@@ -314,7 +314,7 @@ void Session::encoder(FrontEnd& fe, float* enc_out_dbg) {
 
 // ------------------------------------------------------------------------------------------ decoder
 void Session::decoder_layers(float* x, int rows, const int* d_pos, const int* d_slot, const int* d_kvs,
-                             const int* d_kvl, int64_t total_keys, bool dense) {
+                             const int* d_kvl, int64_t total_keys, bool dense, bool rows_share_kv) {
     const qasr_hparams& h = m_->hp;
     const int H = h.txt_h, F = h.txt_ffn, nh = h.txt_heads, nkv = h.txt_kv_heads, hd = h.head_dim;
     const int QD = nh * hd, KD = nkv * hd;
@@ -331,7 +331,8 @@ void Session::decoder_layers(float* x, int rows, const int* d_pos, const int* d_
     float* hd_ = fused ? (float*)sc_.get(S_HD, (size_t)rows * (F / QK) * sizeof(float)) : nullptr;
     const float scale = 1.0f / sqrtf((float)hd);
     const size_t layer_kv = (size_t)kv_slots_ * KD;
-    const bool fuse_qk = !dense && hd == 128 && (nh / nkv == 2 || nh / nkv == 4) && !getenv("QASR_NO_QK_FUSE");
+    const bool fuse_qk = !dense && !rows_share_kv && hd == 128 && (nh / nkv == 2 || nh / nkv == 4) &&
+                         !getenv("QASR_NO_QK_FUSE");
     // GEMV row counts: the norms and the SwiGLU run inside the GEMVs' prologues (5 launches per layer, not 8)
     const bool gv = !fused && dec_fuse_ && gemv_fused_ok(GV_RMS, rows, H) && gemv_fused_ok(GV_NONE, rows, F) &&
                     gemv_fused_ok(GV_NONE, rows, QD);
@@ -442,7 +443,7 @@ void Session::draft_step(int B) {
     int* tab = (int*)sc_.get(S_DTAB, (size_t)6 * 16 * sizeof(int));
     float* x = (float*)sc_.get(S_X, (size_t)16 * h.txt_h * sizeof(float));
     embed_rows(tab, B, m_->tok_embd, nullptr, x, st_);
-    decoder_layers(x, B, tab + 16, tab + 32, tab + 48, tab + 64, 0);
+    decoder_layers(x, B, tab + 16, tab + 32, tab + 48, tab + 64, 0, /*dense=*/false, /*rows_share_kv=*/B > 1);
     float* logits = (float*)sc_.get(S_LOGITS, (size_t)16 * h.vocab * sizeof(float));
     lm_head_rows(x, B, h.txt_h, logits);
     int* d_tok = (int*)sc_.get(S_TOK, (size_t)16 * sizeof(int));

@@ -80,9 +80,11 @@ class Session {
     void front_end(const float* dpcm, const std::vector<int64_t>& off, const std::vector<int64_t>& len, FrontEnd& fe,
                    float* enc_out_dbg);
     void encoder(FrontEnd& fe, float* enc_out_dbg);
+    // rows_share_kv: rows are consecutive positions of ONE utterance (a draft verify pass), so row i attends the K/V
+    // rows 0…i-1 write in the same layer — the K/V write then runs as its own launch before the attention (the
+    // fused decode attention writes each row's K/V in its own workgroup, unordered against the others)
     void decoder_layers(float* x, int rows, const int* d_pos, const int* d_slot, const int* d_kvs, const int* d_kvl,
-                        int64_t total_keys,
-                        bool dense = false);
+                        int64_t total_keys, bool dense = false, bool rows_share_kv = false);
     void ensure_kv(int64_t slots);
     void decode_step(const DecState& ds, int B, bool sizing);
     // one verify pass of B rows (last accepted token + draft, padded): tables in S_DTAB, argmax → pinned host
