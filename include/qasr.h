@@ -272,6 +272,14 @@ QASR_API int qasr_op_attention_decode_fused(const float* qkv, int32_t rows, int3
                                             const float* knw, const float* rope_cs, float eps, void* kc, void* vc,
                                             const int32_t* kv_start, const int32_t* kv_len, float scale, int8_t* oq,
                                             float* od, void* stream);
+/* The same for ≤ 4 rows with key ranges longer than 768 split over up to 16 workgroups per (row, KV head): part =
+   4·nkv·16·G·130 floats of scratch, cnt = 4·nkv int32 counters, zero before the first call (left zero by every call).
+   Same math up to the f32 order of the pieces' merge (flash-decoding). */
+QASR_API int qasr_op_attention_decode_split(const float* qkv, int32_t rows, int32_t nh, int32_t nkv, int32_t hd,
+                                            const int32_t* pos, const int32_t* slot, const float* qnw,
+                                            const float* knw, const float* rope_cs, float eps, void* kc, void* vc,
+                                            const int32_t* kv_start, const int32_t* kv_len, float scale, int8_t* oq,
+                                            float* od, float* part, int32_t* cnt, void* stream);
 QASR_API int qasr_op_attention(const void* q, int32_t ldq, const void* k, const void* v, int32_t ldkv,
                                const int32_t* kv_start, const int32_t* kv_len, int32_t rows, int32_t nh, int32_t nkv,
                                int32_t hd, float scale, float* o, int8_t* oq, float* od, void* stream);

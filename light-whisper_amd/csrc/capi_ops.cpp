@@ -230,6 +230,22 @@ QASR_API int qasr_op_attention_decode_fused(const float* qkv, int32_t rows, int3
     });
 }
 
+QASR_API int qasr_op_attention_decode_split(const float* qkv, int32_t rows, int32_t nh, int32_t nkv, int32_t hd,
+                                            const int32_t* pos, const int32_t* slot, const float* qnw,
+                                            const float* knw, const float* rope_cs, float eps, void* kc, void* vc,
+                                            const int32_t* kv_start, const int32_t* kv_len, float scale, int8_t* oq,
+                                            float* od, float* part, int32_t* cnt, void* stream) {
+    return guard([&] {
+        QASR_CHECK(hd == 128 && nkv > 0 && nh % nkv == 0 && oq && od && part && cnt && rows <= 4, QASR_E_INVALID,
+                   "attention_decode_split: hd 128, Q8 output, ≤ 4 rows, scratch");
+        QkFuse fz{qkv, pos, slot, qnw, knw, rope_cs, eps, (__half*)kc, (__half*)vc};
+        fz.part = part;
+        fz.cnt = cnt;
+        attention_decode_fused(fz, nkv * hd, kv_start, kv_len, rows, nh, nkv, hd, scale, oq, od, S(stream));
+        launched();
+    });
+}
+
 QASR_API int qasr_op_attention(const void* q, int32_t ldq, const void* k, const void* v, int32_t ldkv,
                                const int32_t* kv_start, const int32_t* kv_len, int32_t rows, int32_t nh, int32_t nkv,
                                int32_t hd, float scale, float* o, int8_t* oq, float* od, void* stream) {

@@ -119,12 +119,21 @@ Session::Session(Model* m, int n_ctx) : m_(m), n_ctx_(n_ctx) {
     QASR_HIP(hipMemcpy(rope_, tab.data(), tab.size() * sizeof(float), hipMemcpyHostToDevice));
     // the reference session reserves the full f16 KV for n_ctx (qwen3_asr_server.py:123); + the dummy slot
     ensure_kv(n_ctx + 1);
+    // split-K decode attention scratch (≤ 4 rows over long key ranges): partial states + zeroed arrival counters
+    const int nkv = m->hp.txt_kv_heads, G = nkv > 0 ? m->hp.txt_heads / nkv : 1;
+    if (m->hp.head_dim == 128 && nkv > 0) {
+        QASR_HIP(hipMalloc(&attn_part_, attn_split_floats(nkv, G) * sizeof(float)));
+        QASR_HIP(hipMalloc(&attn_cnt_, (size_t)4 * nkv * sizeof(int)));
+        QASR_HIP(hipMemset(attn_cnt_, 0, (size_t)4 * nkv * sizeof(int)));
+    }
 }
 
 Session::~Session() {
     if (kc_) (void)hipFree(kc_);
     if (vc_) (void)hipFree(vc_);
     if (rope_) (void)hipFree(rope_);
+    if (attn_part_) (void)hipFree(attn_part_);
+    if (attn_cnt_) (void)hipFree(attn_cnt_);
     if (pin_) (void)hipHostFree(pin_);
     for (auto& g : graphs_) (void)hipGraphExecDestroy(g.second);
     for (auto& g : draft_graphs_) (void)hipGraphExecDestroy(g.second);
@@ -353,7 +362,11 @@ void Session::decoder_layers(float* x, int rows, const int* d_pos, const int* d_
             linear_q8(xq, xd, rows, L.qkv, nullptr, nullptr, qkv, QD + 2 * KD, EPI_STORE, st_, zq);
         }
         if (fuse_qk) {   // decode rows: q/k norm + RoPE + KV write inside the attention kernel
-            const QkFuse fz{qkv, d_pos, d_slot, L.q_norm, L.k_norm, rope_, h.rms_eps, kc, vc};
+            QkFuse fz{qkv, d_pos, d_slot, L.q_norm, L.k_norm, rope_, h.rms_eps, kc, vc};
+            if (rows <= 4 && attn_part_ && attn_split_) {   // long key ranges split over workgroups
+                fz.part = attn_part_;
+                fz.cnt = attn_cnt_;
+            }
             attention_decode_fused(fz, KD, d_kvs, d_kvl, rows, nh, nkv, hd, scale, xq, xd, st_, total_keys);
         } else {
             qk_norm_rope(qkv, rows, nh, nkv, hd, d_pos, d_slot, L.q_norm, L.k_norm, rope_, h.rms_eps, qh, kc, vc, st_);

@@ -105,7 +105,17 @@ struct QkFuse {
     float eps;
     __half* kc;
     __half* vc;
+    // split-K over the key range (1–4 decode rows, long contexts): partial (m, l, Σp·v) per (row, KV head, split)
+    // and an arrival counter per (row, KV head), zero between launches (kAttnSplitScratch sizes them); nullptr = one
+    // workgroup per (row, KV head)
+    float* part = nullptr;
+    int* cnt = nullptr;
 };
+constexpr int kAttnSplitMax = 16;      // workgroups per (row, KV head) at most
+constexpr int kAttnSplitKeys = 128;    // keys per split workgroup (at least)
+constexpr int kAttnSplitMin = 512;     // ranges up to this many keys stay in one workgroup (tools/graph_cost.py)
+// scratch floats / counters for rows ≤ 4 decode rows of a model (G query heads per KV head, hd 128)
+inline size_t attn_split_floats(int nkv, int G) { return (size_t)4 * nkv * kAttnSplitMax * G * (2 + 128); }
 void attention_decode_fused(const QkFuse& fz, int ldkv, const int* kv_start, const int* kv_len, int rows, int nh,
                             int nkv, int hd, float scale, int8_t* oq, float* od, hipStream_t s, int64_t total_keys = 0);
 void attention(const __half* Q, int ldq, const __half* K, const __half* V, int ldkv, const int* kv_start,

@@ -85,12 +85,25 @@ __global__ __launch_bounds__(256) void k_attention(const __half* __restrict__ Q,
     // NW = 4: one workgroup per (row, KV head), its 4 waves take contiguous quarters of the key range and merge
     // their partial softmax states through LDS (long decoder KV ranges).  NW = 1: one wave per (row, KV head)
     // (the encoder's 104-key windows).  The G query heads of a KV group share every K/V load.
-    const int gw = NW == 4 ? blockIdx.x : blockIdx.x * 4 + w;
+    // FUSED with fz.part: kAttnSplitMax workgroups per (row, KV head); a range longer than kAttnSplitMin keys is
+    // cut into S ≤ kAttnSplitMax contiguous pieces (≥ kAttnSplitKeys each), the rest exit at once.  Each piece's
+    // merged (m, l, Σp·v) goes to fz.part; the last piece to arrive (fz.cnt) combines them in piece order.
+    const bool spl = FUSED && fz.part != nullptr;   // uniform
+    const int gw = spl ? blockIdx.x / kAttnSplitMax : NW == 4 ? blockIdx.x : blockIdx.x * 4 + w;
+    const int piece = spl ? blockIdx.x % kAttnSplitMax : 0;
     if (NW == 1 && gw >= rows * nkv) return;
     const int part = NW == 4 ? w : 0;
     const int r = gw / nkv, kvh = gw % nkv;
-    const int Lr = kv_len[r], qn = (Lr + NW - 1) / NW;
-    const int s0 = kv_start[r] + part * qn, L = max(0, min(qn, Lr - part * qn));
+    const int Lr = kv_len[r];
+    int S = 1, per = Lr;
+    if (spl && Lr > kAttnSplitMin) {
+        S = min(kAttnSplitMax, (Lr + kAttnSplitKeys - 1) / kAttnSplitKeys);
+        per = (Lr + S - 1) / S;
+    }
+    if (piece >= S) return;   // whole workgroup, before any barrier
+    const int kb0 = kv_start[r] + piece * per, Ls = min(per, Lr - piece * per);
+    const int qn = (Ls + NW - 1) / NW;
+    const int s0 = kb0 + part * qn, L = max(0, min(qn, Ls - part * qn));
     const int sub = lane & 7, kk = lane >> 3;
 
     h2v qv[G][QD / 2];   // the f16 q dims of this lane (q is f16-rounded on every path)
@@ -104,10 +117,13 @@ __global__ __launch_bounds__(256) void k_attention(const __half* __restrict__ Q,
         const int nslot = nh + 2 * nkv, kvd = nkv * HD;
         const float* src = fz.qkv + (size_t)r * nslot * HD;
         const int p = fz.pos[r], sl = fz.slot[r];
+        // the new K/V row is written (and read back through the barrier) by the piece whose range holds its slot
+        const bool own = S == 1 || (sl >= kb0 && sl < kb0 + Ls);
         const int e0 = (2 * lane) & (HD / 2 - 1);
         const float4 cs = *(const float4*)(fz.rope_cs + ((size_t)p * (HD / 2) + e0) * 2);
         const bool lo = 2 * lane < HD / 2;
         for (int t = w; t < G + 2; t += 4) {
+            if (t >= G && !own) continue;
             const int h = t < G ? kvh * G + t : t == G ? nh + kvh : nh + nkv + kvh;
             const float2 v = *(const float2*)(src + h * HD + 2 * lane);
             if (t == G + 1) {
@@ -354,26 +370,92 @@ __global__ __launch_bounds__(256) void k_attention(const __half* __restrict__ Q,
     }
     const int wb = NW == 1 ? w : 0;   // first partial state of this item
     const int D = nh * HD;
+    float* pbase = spl ? fz.part + (size_t)gw * kAttnSplitMax * G * (2 + HD) : nullptr;
+    if (S > 1) {
+        // this piece's merged state → fz.part; the last piece to arrive goes on to combine all S of them
+#pragma unroll
+        for (int g = 0; g < G; g++) {
+            float mt = -INFINITY;
+#pragma unroll
+            for (int u = 0; u < NW; u++) mt = fmaxf(mt, cm_s[wb + u][g]);
+            float lt = 0.f, sc[NW];
+#pragma unroll
+            for (int u = 0; u < NW; u++) {
+                sc[u] = cm_s[wb + u][g] == -INFINITY ? 0.f : expf(cm_s[wb + u][g] - mt);
+                lt += cl_s[wb + u][g] * sc[u];
+            }
+            float* pp = pbase + (size_t)(piece * G + g) * (2 + HD);
+#pragma unroll
+            for (int j = 0; j < PD; j++) {
+                float a = 0.f;
+#pragma unroll
+                for (int u = 0; u < NW; u++) a += ca_s[wb + u][g][lane * PD + j] * sc[u];
+                __hip_atomic_store(pp + 2 + lane * PD + j, a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            if (lane == 0) {
+                __hip_atomic_store(pp, mt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(pp + 1, lt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        // hand-off without cache-wide fences (MI355X_MICROARCH.md, inter-workgroup visibility, table row 1): the
+        // state is stored write-through (sc1) by this one wave, which waits for its stores, then counts the arrival
+        // with an agent-scope add; the piece whose add comes last reads every state with sc1 loads
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        int prev = 0;
+        if (lane == 0) prev = __hip_atomic_fetch_add(fz.cnt + gw, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        prev = __builtin_amdgcn_readfirstlane(prev);
+        if (prev != S - 1) return;
+        if (lane == 0) __hip_atomic_store(fz.cnt + gw, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // next launch
+    }
 #pragma unroll
     for (int g = 0; g < G; g++) {
         const int h = kvh * G + g;
-        float mt = -INFINITY;
-#pragma unroll
-        for (int u = 0; u < NW; u++) mt = fmaxf(mt, cm_s[wb + u][g]);
-        float lt = 0.f, sc[NW];
-#pragma unroll
-        for (int u = 0; u < NW; u++) {
-            sc[u] = cm_s[wb + u][g] == -INFINITY ? 0.f : expf(cm_s[wb + u][g] - mt);
-            lt += cl_s[wb + u][g] * sc[u];
-        }
-        const float inv = Lr > 0 ? 1.f / lt : 0.f;
         float out[PD];
+        if (S > 1) {
+            // combine the S pieces in piece order (deterministic whatever the arrival order)
+            // every load in flight at once: lane u reads piece u's (m, l); each lane reads its dims of all pieces
+            // (unconditionally, pieces past S clamped and weighted 0); fixed order, so deterministic
+            auto ld = [](const float* q) { return __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+            const float* pl = pbase + (size_t)(min(lane, S - 1) * G + g) * (2 + HD);
+            const float mu = ld(pl), lu = ld(pl + 1);
+            float av2[kAttnSplitMax][PD];
 #pragma unroll
-        for (int j = 0; j < PD; j++) {
-            float a = 0.f;
+            for (int u = 0; u < kAttnSplitMax; u++)
 #pragma unroll
-            for (int u = 0; u < NW; u++) a += ca_s[wb + u][g][lane * PD + j] * sc[u];
-            out[j] = a * inv;
+                for (int j = 0; j < PD; j++)
+                    av2[u][j] = ld(pbase + (size_t)(min(u, S - 1) * G + g) * (2 + HD) + 2 + lane * PD + j);
+            const float mt = wave_max(lane < S ? mu : -INFINITY);
+            const float su = lane < S ? expf(mu - mt) : 0.f;
+            const float lt = wave_sum(lu * su);
+            float a[PD];
+#pragma unroll
+            for (int j = 0; j < PD; j++) a[j] = 0.f;
+#pragma unroll
+            for (int u = 0; u < kAttnSplitMax; u++) {
+                const float sc = lane_f(su, u);   // 0 for pieces past S
+#pragma unroll
+                for (int j = 0; j < PD; j++) a[j] += av2[u][j] * sc;
+            }
+#pragma unroll
+            for (int j = 0; j < PD; j++) out[j] = a[j] / lt;
+        } else {
+            float mt = -INFINITY;
+#pragma unroll
+            for (int u = 0; u < NW; u++) mt = fmaxf(mt, cm_s[wb + u][g]);
+            float lt = 0.f, sc[NW];
+#pragma unroll
+            for (int u = 0; u < NW; u++) {
+                sc[u] = cm_s[wb + u][g] == -INFINITY ? 0.f : expf(cm_s[wb + u][g] - mt);
+                lt += cl_s[wb + u][g] * sc[u];
+            }
+            const float inv = Lr > 0 ? 1.f / lt : 0.f;
+#pragma unroll
+            for (int j = 0; j < PD; j++) {
+                float a = 0.f;
+#pragma unroll
+                for (int u = 0; u < NW; u++) a += ca_s[wb + u][g][lane * PD + j] * sc[u];
+                out[j] = a * inv;
+            }
         }
         if (o) {
 #pragma unroll
@@ -647,7 +729,8 @@ void attention_decode_fused(const QkFuse& fz, int ldkv, const int* kv_start, con
     ProfScope ps(s, "attention", 4.0 * hd * nh * (double)total_keys, 4.0 * hd * nh * (double)total_keys);
     QASR_CHECK(hd == 128 && nkv > 0 && nh % nkv == 0, QASR_E_INVALID, "attention_decode_fused: hd 128 only");
     const int G = nh / nkv;
-    const unsigned b4 = (unsigned)(rows * nkv);
+    QASR_CHECK(!fz.part || (rows <= 4 && fz.cnt), QASR_E_INVALID, "attention_decode_fused: split-K is for ≤ 4 rows");
+    const unsigned b4 = (unsigned)(rows * nkv * (fz.part ? kAttnSplitMax : 1));
     if (G == 2)
         k_attention<128, 2, 4, true><<<b4, 256, 0, s>>>(nullptr, 0, fz.kc, fz.vc, ldkv, kv_start, kv_len, rows, nh, nkv,
                                                         scale, nullptr, oq, od, fz);

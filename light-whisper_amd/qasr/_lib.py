@@ -126,6 +126,8 @@ SIGNATURES = {
     "qasr_op_linear_q8h": (C.c_int, [P, P, I32, P, P, I32, I32, P, P, P, I32, I32, I32, P]),
     "qasr_op_attention_decode_fused": (C.c_int, [P, I32, I32, I32, I32, P, P, P, P, P, F32, P, P, P, P, F32, P, P,
                                                  P]),
+    "qasr_op_attention_decode_split": (C.c_int, [P, I32, I32, I32, I32, P, P, P, P, P, F32, P, P, P, P, F32, P, P,
+                                                 P, P, P]),
     "qasr_op_attention": (C.c_int, [P, I32, P, P, I32, P, P, I32, I32, I32, I32, F32, P, P, P, P]),
     "qasr_op_attention_dense": (C.c_int, [P, I32, P, P, I32, P, P, I32, I32, I32, I32, F32, P, P, P, I32, P]),
     "qasr_op_argmax": (C.c_int, [P, I32, I32, P, P]),

@@ -107,10 +107,13 @@ def test_real_prefill_logits(pair):
     got = s.prefill_logits(x)
     e = rel_err(got, ref)
     agree = float((got.argmax(1) == ref.argmax(1)).mean())
-    record(f"real_prefill_logits[{arch}]", logits_rel=e, argmax_agree=agree, rows=len(ids))
-    # observed (r2): 8.8e-3 / 8.1e-3 rel, argmax 0.979 / 1.0 of 48 rows (0.6B / 1.7B)
+    clear = np.array([not _near_tie(r) for r in ref])
+    record(f"real_prefill_logits[{arch}]", logits_rel=e, argmax_agree=agree, rows=len(ids), clear_rows=int(clear.sum()))
+    # observed (r2): 7.5e-3-8.8e-3 rel; argmax on all 48 rows 0.94-1.0 from run to run — synthetic weights leave
+    # near-ties among 151,936 logits, and the split-K GEMMs' atomic order varies per run — so the argmax is
+    # required on the rows with a clear margin (top-2 gap > 2 % of the range), as for the decode logits
     assert e < 1.8e-2
-    assert agree >= 0.95
+    assert (got.argmax(1) == ref.argmax(1))[clear].all()
 
 
 def test_real_forced_decode_logits(pair):

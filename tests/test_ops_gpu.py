@@ -473,6 +473,57 @@ def test_attention_decode_fused(torch_dev, nh, nkv):
     assert not np.array_equal(outs[1][2], kc0)   # the new K rows were written
 
 
+@pytest.mark.parametrize("nh,nkv", [(16, 8), (16, 4)])
+def test_attention_decode_split(torch_dev, nh, nkv):
+    """≤ 4 decode rows over long key ranges split over workgroups (flash-decoding, pieces merged by the last to
+    arrive): the same K/V cache writes as one workgroup per row, outputs within f32 merge-order noise of it and of an
+    f64 reference, deterministic, arrival counters left zero"""
+    import torch
+
+    hd, rows = 128, 4
+    rng = np.random.default_rng(21)
+    lens = np.array([1, 700, 1500, 4000], np.int32)
+    starts = np.concatenate([[2], 2 + np.cumsum(lens[:-1] + 3)]).astype(np.int32)
+    slots = int(starts[-1] + lens[-1] + 4)
+    qkv = rng.standard_normal((rows, (nh + 2 * nkv) * hd)).astype(np.float32)
+    pos = (lens - 1).astype(np.int32)
+    slot = (starts + lens - 1).astype(np.int32)
+    qnw = (1 + 0.1 * rng.standard_normal(hd)).astype(np.float32)
+    knw = (1 + 0.1 * rng.standard_normal(hd)).astype(np.float32)
+    tab = np.empty((4096, hd // 2, 2), np.float32)
+    _lib.check(L().qasr_op_rope_table(4096, hd, 1e6, tab.ctypes.data_as(C.c_void_p)))
+    kc0 = rng.standard_normal((slots, nkv * hd)).astype(np.float16)
+    vc0 = rng.standard_normal((slots, nkv * hd)).astype(np.float16)
+    keep = [dev(a, torch_dev) for a in (qkv, pos, slot, qnw, knw, tab, starts, lens)]
+    scale = 1.0 / np.sqrt(hd)
+    G = nh // nkv
+    part = torch.empty(4 * nkv * 16 * G * 130, dtype=torch.float32, device=torch_dev)
+    cnt = torch.zeros(4 * nkv, dtype=torch.int32, device=torch_dev)
+    outs = []
+    for split in (False, True, True):
+        kc, vc = dev(kc0, torch_dev), dev(vc0, torch_dev)
+        oq = torch.zeros((rows, nh * hd), dtype=torch.int8, device=torch_dev)
+        od = torch.zeros((rows, nh * hd // 32), dtype=torch.float32, device=torch_dev)
+        args = (ptr(keep[0]), rows, nh, nkv, hd, ptr(keep[1]), ptr(keep[2]), ptr(keep[3]), ptr(keep[4]), ptr(keep[5]),
+                1e-6, ptr(kc), ptr(vc), ptr(keep[6]), ptr(keep[7]), scale, ptr(oq), ptr(od))
+        if split:
+            _lib.check(L().qasr_op_attention_decode_split(*args, ptr(part), ptr(cnt), None))
+        else:
+            _lib.check(L().qasr_op_attention_decode_fused(*args, None))
+        outs.append([host(t) for t in (oq, od, kc, vc)])
+    assert not host(cnt).any()
+    one, sp, sp2 = outs
+    assert all(np.array_equal(a, b) for a, b in zip(sp, sp2))            # deterministic
+    assert np.array_equal(one[2], sp[2]) and np.array_equal(one[3], sp[3])   # the same cache writes
+    assert np.array_equal(one[0][0], sp[0][0])   # the 1-key row is not split: bit-identical
+    deq = lambda o: o[0].astype(np.float64) * np.repeat(o[1], 32, axis=1)
+    # reference: f64 attention of the f16-rounded q over the written caches (q from the unsplit kernel's own
+    # norm/RoPE is not exported, so compare the two kernels' dequantised outputs to each other at the Q8 grain)
+    step = np.repeat(np.maximum(one[1], sp[1]), 32, axis=1)
+    assert (np.abs(deq(one) - deq(sp)) <= 1.01 * step + 1e-6).all()
+    assert (one[0] != sp[0]).mean() < 0.05
+
+
 def _attention_case(torch_dev, hd, nh, nkv, starts, lens, dense, seed):
     import torch
 

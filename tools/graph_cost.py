@@ -90,6 +90,16 @@ def main():
                     rope.data_ptr(), C.c_float(1e-6), kc[i % 28].data_ptr(), vc[i % 28].data_ptr(), kvs.data_ptr(),
                     kvl.data_ptr(), C.c_float(HD ** -0.5), xq.data_ptr(), xd.data_ptr(), stream()))
                 for i in range(R)]) / R
+            # the session's default for ≤ 4 rows: ranges over 512 keys split over up to 8 workgroups
+            part = torch.empty(4 * nkv * 16 * (nh // nkv) * 130, device=dev)
+            cnt = torch.zeros(4 * nkv, dtype=torch.int32, device=dev)
+            res["attention_decode_split" + ("" if keys == KEYS else f"@{keys}")] = timed(lambda: [_lib.check(
+                lib.qasr_op_attention_decode_split(
+                    qkv.data_ptr(), 1, nh, nkv, HD, pos.data_ptr(), pos.data_ptr(), qn.data_ptr(), qn.data_ptr(),
+                    rope.data_ptr(), C.c_float(1e-6), kc[i % 28].data_ptr(), vc[i % 28].data_ptr(), kvs.data_ptr(),
+                    kvl.data_ptr(), C.c_float(HD ** -0.5), xq.data_ptr(), xd.data_ptr(), part.data_ptr(),
+                    cnt.data_ptr(), stream()))
+                for i in range(R)]) / R
         if os.environ.get("ATTN_ONLY"):
             out[arch] = {k: round(v, 2) for k, v in res.items()}
             print(json.dumps({arch: out[arch]}), flush=True)
