@@ -120,7 +120,7 @@ class Session {
     // 1–4-row decode: norms / SwiGLU fused into the GEMV prologues (QASR_NO_DEC_FUSE=1: the separate launches,
     // for A/B parity and timing; read once per session, so captured step graphs stay consistent)
     bool dec_fuse_ = getenv("QASR_NO_DEC_FUSE") == nullptr;
-    // ≤ 4-row decode attention over > kAttnSplitMin keys split over workgroups (QASR_NO_ATTN_SPLIT=1: one per row and
+    // ≤ 4-row decode attention over > QkFuse::split_min keys split over workgroups (QASR_NO_ATTN_SPLIT=1: one per row and
     // KV head); the scratch is the session's own (allocated with it, counters zeroed)
     bool attn_split_ = getenv("QASR_NO_ATTN_SPLIT") == nullptr;
     float* attn_part_ = nullptr;

@@ -110,10 +110,12 @@ struct QkFuse {
     // workgroup per (row, KV head)
     float* part = nullptr;
     int* cnt = nullptr;
+    // ranges up to split_min keys stay in one workgroup; longer ones get pieces of ≥ split_keys keys
+    // (tools/graph_cost.py, profiles/r2_attn_split_min_sweep.jsonl: 300 / 400 keys 9.7 → 8.0 / 8.2 µs at 256)
+    int split_min = 256;
+    int split_keys = 128;
 };
 constexpr int kAttnSplitMax = 16;      // workgroups per (row, KV head) at most
-constexpr int kAttnSplitKeys = 128;    // keys per split workgroup (at least)
-constexpr int kAttnSplitMin = 512;     // ranges up to this many keys stay in one workgroup (tools/graph_cost.py)
 // scratch floats / counters for rows ≤ 4 decode rows of a model (G query heads per KV head, hd 128)
 inline size_t attn_split_floats(int nkv, int G) { return (size_t)4 * nkv * kAttnSplitMax * G * (2 + 128); }
 void attention_decode_fused(const QkFuse& fz, int ldkv, const int* kv_start, const int* kv_len, int rows, int nh,

@@ -67,7 +67,7 @@ __device__ __forceinline__ float qk_dot16(const h2v* qh, int4 a, int4 b) {
     return part;
 }
 
-template <int HD, int G, int NW, bool FUSED = false>
+template <int HD, int G, int NW, bool FUSED = false, int CK = 64>
 __global__ __launch_bounds__(256) void k_attention(const __half* __restrict__ Q, int ldq, const __half* K,
                                                    const __half* V, int ldkv,
                                                    const int* __restrict__ kv_start, const int* __restrict__ kv_len,
@@ -85,8 +85,8 @@ __global__ __launch_bounds__(256) void k_attention(const __half* __restrict__ Q,
     // NW = 4: one workgroup per (row, KV head), its 4 waves take contiguous quarters of the key range and merge
     // their partial softmax states through LDS (long decoder KV ranges).  NW = 1: one wave per (row, KV head)
     // (the encoder's 104-key windows).  The G query heads of a KV group share every K/V load.
-    // FUSED with fz.part: kAttnSplitMax workgroups per (row, KV head); a range longer than kAttnSplitMin keys is
-    // cut into S ≤ kAttnSplitMax contiguous pieces (≥ kAttnSplitKeys each), the rest exit at once.  Each piece's
+    // FUSED with fz.part: kAttnSplitMax workgroups per (row, KV head); a range longer than fz.split_min keys is
+    // cut into S ≤ kAttnSplitMax contiguous pieces (≥ fz.split_keys each), the rest exit at once.  Each piece's
     // merged (m, l, Σp·v) goes to fz.part; the last piece to arrive (fz.cnt) combines them in piece order.
     const bool spl = FUSED && fz.part != nullptr;   // uniform
     const int gw = spl ? blockIdx.x / kAttnSplitMax : NW == 4 ? blockIdx.x : blockIdx.x * 4 + w;
@@ -96,8 +96,8 @@ __global__ __launch_bounds__(256) void k_attention(const __half* __restrict__ Q,
     const int r = gw / nkv, kvh = gw % nkv;
     const int Lr = kv_len[r];
     int S = 1, per = Lr;
-    if (spl && Lr > kAttnSplitMin) {
-        S = min(kAttnSplitMax, (Lr + kAttnSplitKeys - 1) / kAttnSplitKeys);
+    if (spl && Lr > fz.split_min) {
+        S = min(kAttnSplitMax, (Lr + fz.split_keys - 1) / fz.split_keys);
         per = (Lr + S - 1) / S;
     }
     if (piece >= S) return;   // whole workgroup, before any barrier
@@ -176,20 +176,27 @@ __global__ __launch_bounds__(256) void k_attention(const __half* __restrict__ Q,
 #pragma unroll
         for (int j = 0; j < 8; j++) av[g][j] = 0.f;
     if constexpr (DEC) {
+        // C keys per chunk and wave: K as C/8 row groups of 8 lanes × 32 B, V as C/4 groups of 16 lanes × 16 B.
+        // CK = 64 kernels run a wave with ≤ 32 keys in 32-key chunks (half the clamped re-reads; the registers are
+        // sized by the 64-key path anyway); CK = 32 kernels (many rows: occupancy 4, not 3) only in 32-key chunks.
+        static_assert(CK == 32 || CK == 64, "k_attention: decode chunk of 32 or 64 keys");
         const __half* vbase16 = V + (size_t)kvh * HD + vd;
-        for (int c0 = 0; c0 < L; c0 += 64) {
-            const int n = min(64, L - c0);
+        auto run = [&](auto ckc) {
+        constexpr int C = decltype(ckc)::value;
+        constexpr int KU8 = C / 8, VU4 = C / 4;
+        for (int c0 = 0; c0 < L; c0 += C) {
+            const int n = min(C, L - c0);
             const __half* kc = kbase + (size_t)(s0 + c0) * ldkv;
             const __half* vc = vbase16 + (size_t)(s0 + c0) * ldkv;
-            int4 ka[8], kb[8], vr[16];
+            int4 ka[KU8], kb[KU8], vr[VU4];
 #pragma unroll
-            for (int u = 0; u < 8; u++) {
+            for (int u = 0; u < KU8; u++) {
                 const int j = min(8 * u + kk, n - 1);   // rows past n re-read row n-1 (their scores are dropped)
                 ka[u] = *(const int4*)(kc + (size_t)j * ldkv);
                 kb[u] = *(const int4*)(kc + (size_t)j * ldkv + 8);
             }
 #pragma unroll
-            for (int u = 0; u < 8; u++) {
+            for (int u = 0; u < KU8; u++) {
                 const int j = 8 * u + kk;
 #pragma unroll
                 for (int g = 0; g < G; g++) {
@@ -200,7 +207,7 @@ __global__ __launch_bounds__(256) void k_attention(const __half* __restrict__ Q,
             wave_sync_lds();
             // the V loads fly while the softmax runs (issued after the scores so K and V are never live together)
 #pragma unroll
-            for (int u = 0; u < 16; u++) {
+            for (int u = 0; u < VU4; u++) {
                 const int j = min(4 * u + vg, n - 1);   // rows past n: weight p = 0
                 vr[u] = *(const int4*)(vc + (size_t)j * ldkv);
             }
@@ -210,7 +217,7 @@ __global__ __launch_bounds__(256) void k_attention(const __half* __restrict__ Q,
                 const float mnew = fmaxf(m[g], wave_max(x));
                 const float alpha = expf(m[g] - mnew);
                 const float p = lane < n ? expf(x - mnew) : 0.f;
-                lsum[g] = lsum[g] * alpha + wave_sum(p);
+                lsum[g] = fmaf(lsum[g], alpha, wave_sum(p));
                 m[g] = mnew;
                 sp[w][g][lane] = p;
 #pragma unroll
@@ -218,7 +225,7 @@ __global__ __launch_bounds__(256) void k_attention(const __half* __restrict__ Q,
             }
             wave_sync_lds();
 #pragma unroll
-            for (int u = 0; u < 16; u++) {
+            for (int u = 0; u < VU4; u++) {
                 const uint32_t* hv = (const uint32_t*)&vr[u];
 #pragma unroll
                 for (int g = 0; g < G; g++) {
@@ -232,6 +239,9 @@ __global__ __launch_bounds__(256) void k_attention(const __half* __restrict__ Q,
             }
             wave_sync_lds();
         }
+        };
+        if (CK == 32 || L <= 32) run(std::integral_constant<int, 32>{});
+        else run(std::integral_constant<int, CK>{});
 #pragma unroll
         for (int g = 0; g < G; g++)
 #pragma unroll
@@ -336,7 +346,9 @@ __global__ __launch_bounds__(256) void k_attention(const __half* __restrict__ Q,
         }
         wave_sync_lds();
     }
-    // merge the NW partial states (m, l, acc) of this row's key ranges
+    // merge the NW partial states (m, l, acc) of this row's key ranges.  Every multiply-add of the decode softmax
+    // and merges is an explicit fmaf: left to contraction, each instantiation's SLP packing decides mul+add (two
+    // roundings, v_pk_*) or fma (one), and the fused and unfused kernels then differ in the last bit
     if constexpr (NW == 1) {
 #pragma unroll
         for (int g = 0; g < G; g++) {
@@ -382,14 +394,14 @@ __global__ __launch_bounds__(256) void k_attention(const __half* __restrict__ Q,
 #pragma unroll
             for (int u = 0; u < NW; u++) {
                 sc[u] = cm_s[wb + u][g] == -INFINITY ? 0.f : expf(cm_s[wb + u][g] - mt);
-                lt += cl_s[wb + u][g] * sc[u];
+                lt = fmaf(cl_s[wb + u][g], sc[u], lt);
             }
             float* pp = pbase + (size_t)(piece * G + g) * (2 + HD);
 #pragma unroll
             for (int j = 0; j < PD; j++) {
                 float a = 0.f;
 #pragma unroll
-                for (int u = 0; u < NW; u++) a += ca_s[wb + u][g][lane * PD + j] * sc[u];
+                for (int u = 0; u < NW; u++) a = fmaf(ca_s[wb + u][g][lane * PD + j], sc[u], a);
                 __hip_atomic_store(pp + 2 + lane * PD + j, a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
             if (lane == 0) {
@@ -434,7 +446,7 @@ __global__ __launch_bounds__(256) void k_attention(const __half* __restrict__ Q,
             for (int u = 0; u < kAttnSplitMax; u++) {
                 const float sc = lane_f(su, u);   // 0 for pieces past S
 #pragma unroll
-                for (int j = 0; j < PD; j++) a[j] += av2[u][j] * sc;
+                for (int j = 0; j < PD; j++) a[j] = fmaf(av2[u][j], sc, a[j]);
             }
 #pragma unroll
             for (int j = 0; j < PD; j++) out[j] = a[j] / lt;
@@ -446,14 +458,14 @@ __global__ __launch_bounds__(256) void k_attention(const __half* __restrict__ Q,
 #pragma unroll
             for (int u = 0; u < NW; u++) {
                 sc[u] = cm_s[wb + u][g] == -INFINITY ? 0.f : expf(cm_s[wb + u][g] - mt);
-                lt += cl_s[wb + u][g] * sc[u];
+                lt = fmaf(cl_s[wb + u][g], sc[u], lt);
             }
             const float inv = Lr > 0 ? 1.f / lt : 0.f;
 #pragma unroll
             for (int j = 0; j < PD; j++) {
                 float a = 0.f;
 #pragma unroll
-                for (int u = 0; u < NW; u++) a += ca_s[wb + u][g][lane * PD + j] * sc[u];
+                for (int u = 0; u < NW; u++) a = fmaf(ca_s[wb + u][g][lane * PD + j], sc[u], a);
                 out[j] = a * inv;
             }
         }
@@ -717,8 +729,23 @@ static void launch_attention(int G, int rows, hipStream_t s, const __half* Q, in
     const unsigned b4 = (unsigned)(rows * nkv), b1 = (unsigned)cdiv(rows * nkv, 4);
     switch (G) {
         case 1: k_attention<HD, 1, 1><<<b1, 256, 0, s>>>(Q, ldq, K, V, ldkv, kv_start, kv_len, rows, nh, nkv, scale, o, oq, od); break;
-        case 2: k_attention<HD, 2, 4><<<b4, 256, 0, s>>>(Q, ldq, K, V, ldkv, kv_start, kv_len, rows, nh, nkv, scale, o, oq, od); break;
-        case 4: k_attention<HD, 4, 4><<<b4, 256, 0, s>>>(Q, ldq, K, V, ldkv, kv_start, kv_len, rows, nh, nkv, scale, o, oq, od); break;
+        // the fused decode kernel's chunk policy (attention_decode_fused), so the two paths stay bit-identical
+        case 2:
+            if (HD == 128 && rows >= 192)
+                k_attention<HD, 2, 4, false, 32><<<b4, 256, 0, s>>>(Q, ldq, K, V, ldkv, kv_start, kv_len, rows, nh, nkv,
+                                                                     scale, o, oq, od);
+            else
+                k_attention<HD, 2, 4><<<b4, 256, 0, s>>>(Q, ldq, K, V, ldkv, kv_start, kv_len, rows, nh, nkv, scale, o,
+                                                         oq, od);
+            break;
+        case 4:
+            if (HD == 128 && rows >= 192)
+                k_attention<HD, 4, 4, false, 32><<<b4, 256, 0, s>>>(Q, ldq, K, V, ldkv, kv_start, kv_len, rows, nh, nkv,
+                                                                     scale, o, oq, od);
+            else
+                k_attention<HD, 4, 4><<<b4, 256, 0, s>>>(Q, ldq, K, V, ldkv, kv_start, kv_len, rows, nh, nkv, scale, o,
+                                                         oq, od);
+            break;
         default: throw Error(QASR_E_INVALID, "attention: query heads per KV head must be 1, 2 or 4");
     }
 }
@@ -731,9 +758,19 @@ void attention_decode_fused(const QkFuse& fz, int ldkv, const int* kv_start, con
     const int G = nh / nkv;
     QASR_CHECK(!fz.part || (rows <= 4 && fz.cnt), QASR_E_INVALID, "attention_decode_fused: split-K is for ≤ 4 rows");
     const unsigned b4 = (unsigned)(rows * nkv * (fz.part ? kAttnSplitMax : 1));
-    if (G == 2)
+    // many rows (≥ 192: ≥ 1,536 workgroups) → the 32-key-chunk kernel, 103 VGPRs and 4 waves per SIMD instead of 3
+    // (tools/attn_batch.py, profiles/r2_attn_batch_chunk.jsonl: 256 rows 35.9 → 31.2 µs); fewer rows → the 64-key
+    // kernel, which still runs its ≤ 32-key waves in 32-key chunks (1 key 6.35 → 5.37 µs)
+    const bool ck32 = rows >= 192;
+    if (G == 2 && ck32)
+        k_attention<128, 2, 4, true, 32><<<b4, 256, 0, s>>>(nullptr, 0, fz.kc, fz.vc, ldkv, kv_start, kv_len, rows, nh,
+                                                            nkv, scale, nullptr, oq, od, fz);
+    else if (G == 2)
         k_attention<128, 2, 4, true><<<b4, 256, 0, s>>>(nullptr, 0, fz.kc, fz.vc, ldkv, kv_start, kv_len, rows, nh, nkv,
                                                         scale, nullptr, oq, od, fz);
+    else if (G == 4 && ck32)
+        k_attention<128, 4, 4, true, 32><<<b4, 256, 0, s>>>(nullptr, 0, fz.kc, fz.vc, ldkv, kv_start, kv_len, rows, nh,
+                                                            nkv, scale, nullptr, oq, od, fz);
     else if (G == 4)
         k_attention<128, 4, 4, true><<<b4, 256, 0, s>>>(nullptr, 0, fz.kc, fz.vc, ldkv, kv_start, kv_len, rows, nh, nkv,
                                                         scale, nullptr, oq, od, fz);

@@ -426,15 +426,16 @@ def test_qk_norm_rope(torch_dev, nh, nkv, hd):
             assert np.abs(vh[slot[r], h * hd:(h + 1) * hd] - vref).max() < 2e-3 * np.abs(vref).max()
 
 
-@pytest.mark.parametrize("nh,nkv", [(16, 8), (16, 4)])
-def test_attention_decode_fused(torch_dev, nh, nkv):
+@pytest.mark.parametrize("nh,nkv,rows", [(16, 8, 5), (16, 4, 5), (16, 8, 200), (16, 4, 200)])
+def test_attention_decode_fused(torch_dev, nh, nkv, rows):
     """decode attention with the q/k norm + RoPE + KV write fused in == qk_norm_rope then attention, bit for bit
-    (Q8 output rows and both caches), over short and long key ranges"""
+    (Q8 output rows and both caches), over short and long key ranges; 200 rows take both kernels' 32-key-chunk
+    form (≥ 192 rows)"""
     import torch
 
-    hd, rows = 128, 5
+    hd = 128
     rng = np.random.default_rng(11)
-    lens = np.array([1, 7, 40, 130, 300], np.int32)
+    lens = np.resize(np.array([1, 7, 40, 130, 300], np.int32), rows)
     starts = np.concatenate([[3], 3 + np.cumsum(lens[:-1] + 2)]).astype(np.int32)
     slots = int(starts[-1] + lens[-1] + 4)
     qkv = rng.standard_normal((rows, (nh + 2 * nkv) * hd)).astype(np.float32)
@@ -565,6 +566,16 @@ def _attention_case(torch_dev, hd, nh, nkv, starts, lens, dense, seed):
 def test_attention(torch_dev, hd, nh, nkv, dense):
     """ragged per-row ranges (incl. a 1-key row) on both kernels"""
     _attention_case(torch_dev, hd, nh, nkv, [0, 10, 100, 0, 300], [1, 57, 300, 513, 104], dense, hd + nh)
+
+
+@pytest.mark.parametrize("nh,nkv", [(16, 8), (16, 4)])
+def test_attention_decode_many_rows(torch_dev, nh, nkv):
+    """≥ 192 decode rows take the 32-key-chunk kernel: ragged ranges (1 … 300 keys) against the f64 reference"""
+    rng = np.random.default_rng(5)
+    lens = rng.integers(1, 300, 200)
+    lens[:4] = [1, 31, 32, 33]
+    starts = rng.integers(0, 200, 200)
+    _attention_case(torch_dev, 128, nh, nkv, starts.tolist(), lens.tolist(), False, 3)
 
 
 @pytest.mark.parametrize("hd,nh,nkv", [(128, 16, 8), (64, 16, 16)])

@@ -117,20 +117,22 @@ def main():
                                     ("gemv_lm_head", V, H, 0, 0)):
             nbytes = N * K * 1.0625
             n = max(28 if "lm_head" not in tag else 4, math.ceil(600e6 / nbytes))
-            wq = [torch.randint(-127, 128, (N, K), dtype=torch.int8, device=dev) for _ in range(n)]
-            ws = [(torch.rand(N, K // 32, device=dev) * 0.01).half() for _ in range(n)]
+            # WARM=1: one weight copy re-read by every launch (Infinity-Cache / L2 resident), the cold chain's contrast
+            ncopy = 1 if os.environ.get("WARM") else n
+            wq = [torch.randint(-127, 128, (N, K), dtype=torch.int8, device=dev) for _ in range(ncopy)]
+            ws = [(torch.rand(N, K // 32, device=dev) * 0.01).half() for _ in range(ncopy)]
 
             def chain():
                 for i in range(n):
                     if pro:
                         _lib.check(lib.qasr_op_gemv_fused(
                             0 if pro == 1 else 1, src.data_ptr(), K, nw.data_ptr(), 1e-6, 1, xq.data_ptr(),
-                            xd.data_ptr(), wq[i].data_ptr(), ws[i].data_ptr(), N, K,
+                            xd.data_ptr(), wq[i % ncopy].data_ptr(), ws[i % ncopy].data_ptr(), N, K,
                             y.data_ptr() if epi == 1 else None, y.data_ptr(), N, epi, hq.data_ptr(), hd.data_ptr(),
                             stream()))
                         continue
-                    _lib.check(lib.qasr_op_linear_q8(xq.data_ptr(), xd.data_ptr(), 1, wq[i].data_ptr(),
-                                                     ws[i].data_ptr(), N, K, None,
+                    _lib.check(lib.qasr_op_linear_q8(xq.data_ptr(), xd.data_ptr(), 1, wq[i % ncopy].data_ptr(),
+                                                     ws[i % ncopy].data_ptr(), N, K, None,
                                                      y.data_ptr() if epi == 1 else None, y.data_ptr(), N, epi, 1,
                                                      stream()))
             us = timed(chain) / n
