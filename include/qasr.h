@@ -132,6 +132,17 @@ QASR_API int qasr_session_set_context(qasr_session* s, const int32_t* ids, int32
    draft tokens accepted, tokens emitted. */
 QASR_API int qasr_session_set_draft(qasr_session* s, int32_t on);
 QASR_API int qasr_session_draft_stats(const qasr_session* s, int64_t* stats /* [4] */);
+/* Streaming encoder cache: on = 1 makes a single-utterance run whose samples extend the previous
+   run's (bitwise: the interim loop's growing window, interim.rs:135-156) reuse the audio-embedding rows of the
+   previous run's complete 8-chunk attention windows (104 tokens each) when the window's log-mel maximum is unchanged
+   — the condition under which those rows are functions of the same samples (Whisper-style normalisation uses the
+   window's maximum; the conv stack is per 1 s chunk, the encoder attention per window) — and encodes only the rest.
+   Sliding windows (a start that moves) never qualify.  stats: runs, windows reused, windows encoded. */
+QASR_API int qasr_session_set_encoder_cache(qasr_session* s, int32_t on);
+QASR_API int qasr_session_encoder_cache_stats(const qasr_session* s, int64_t* stats /* [3] */);
+/* The audio-embedding rows (projector output, [tokens][text hidden] f32) of the session's last run — a test /
+   debugging hook (transcribe.cpp exposes no equivalent).  out = NULL: *n_out = the float count only. */
+QASR_API int qasr_session_audio_embeds(qasr_session* s, float* out, size_t cap, size_t* n_out);
 QASR_API int qasr_model_tokenize(const qasr_model* m, const char* text, size_t len, int32_t* ids, size_t cap,
                                 size_t* n_out);
 /* ids → UTF-8 text (the transcript decoder: byte-level pieces, invalid sequences replaced as Python does) */
@@ -227,10 +238,18 @@ QASR_API int qasr_op_interleave_gate_up(int8_t* qs, void* sc, int32_t N, int32_t
 /* h = silu(x·Wgᵀ)·(x·Wuᵀ) quantised to Q8 rows (hq [M][N/2], hd [M][N/64]) in the GEMM epilogue; W interleaved */
 QASR_API int qasr_op_gemm_swiglu_q8(const int8_t* xq, const float* xd, int32_t M, const int8_t* wqs, const void* wsc,
                                     int32_t N, int32_t K, int8_t* hq, float* hd, void* stream);
-/* Same, with the GEMM configuration forced (kernels_q8.hip kGemmCfgs index; -1 = heuristic) — tuning and tests. */
+/* Same, with the GEMM configuration forced (kernels_q8.hip kGemmCfgs index + 32 × split-K count; -1 = heuristic)
+   — tuning and tests.  Split-K needs a fix-up workspace (qasr_op_set_gemm_fixup). */
 QASR_API int qasr_op_gemm_swiglu_q8_cfg(const int8_t* xq, const float* xd, int32_t M, const int8_t* wqs,
                                         const void* wsc, int32_t N, int32_t K, int8_t* hq, float* hd, int32_t cfg,
                                         void* stream);
+/* Register (this thread) the split-K fix-up workspace the op-level Q8 GEMMs use: part_bytes of device memory for
+   partial tiles and ncnt device uint32 arrival counters, ZEROED by the caller (the kernels leave them zero).  With
+   it, every split-K GEMM stores partial tiles and the tile's last workgroup adds them in split order and runs the
+   full epilogue (deterministic, any epilogue); without it (part = NULL) split-K adds with f32 atomics.  Sessions
+   register their own for the decode steps (used there for the SwiGLU epilogue and in deterministic mode).  Not in
+   the reference (an engine-internal tuning / test hook). */
+QASR_API int qasr_op_set_gemm_fixup(void* part, int64_t part_bytes, void* cnt, int32_t ncnt);
 /* Q8 GEMM with a fused output epilogue (M > 8, the MFMA path): epi 4 = erf-GELU(acc + bias) quantised to Q8 rows
    (yq [M][N] int8, yd [M][N/32] f32 block scales; y unused), epi 5 = f16(acc + bias) into y (__half, row stride
    ldy).  cfg: GEMM configuration (-1 = heuristic). */

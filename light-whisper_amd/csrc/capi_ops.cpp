@@ -176,8 +176,16 @@ QASR_API int qasr_op_gemm_swiglu_q8_cfg(const int8_t* xq, const float* xd, int32
         W.sc = (__half*)wsc;
         W.N = N;
         W.K = K;
-        gemm_q8(xq, xd, M, W, nullptr, nullptr, nullptr, N, EPI_SWIGLU, S(stream), cfg, 0, hq, hd);
+        gemm_q8(xq, xd, M, W, nullptr, nullptr, nullptr, N, EPI_SWIGLU, S(stream), cfg < 0 ? -1 : cfg % 32,
+                cfg < 0 ? 0 : cfg / 32, hq, hd);
         launched();
+    });
+}
+
+QASR_API int qasr_op_set_gemm_fixup(void* part, int64_t part_bytes, void* cnt, int32_t ncnt) {
+    return guard([&] {
+        QASR_CHECK(part_bytes >= 0 && ncnt >= 0, QASR_E_INVALID, "set_gemm_fixup: bad size");
+        set_gemm_fixup((float*)part, (size_t)part_bytes / sizeof(float), (unsigned*)cnt, ncnt, true);
     });
 }
 

@@ -242,6 +242,31 @@ QASR_API int qasr_session_draft_stats(const qasr_session* s, int64_t* stats) {
     });
 }
 
+QASR_API int qasr_session_set_encoder_cache(qasr_session* s, int32_t on) {
+    return guard([&] {
+        QASR_CHECK(s, QASR_E_INVALID, "null argument");
+        s->s->set_enc_cache(on != 0);
+    });
+}
+
+QASR_API int qasr_session_encoder_cache_stats(const qasr_session* s, int64_t* stats) {
+    return guard([&] {
+        QASR_CHECK(s && stats, QASR_E_INVALID, "null argument");
+        const Session::EncCacheStats& e = s->s->enc_cache_stats();
+        stats[0] = e.runs, stats[1] = e.windows_reused, stats[2] = e.windows_computed;
+    });
+}
+
+QASR_API int qasr_session_audio_embeds(qasr_session* s, float* out, size_t cap, size_t* n_out) {
+    return guard([&] {
+        QASR_CHECK(s && n_out, QASR_E_INVALID, "null argument");
+        const std::vector<float> e = s->s->last_audio_embeds();
+        *n_out = e.size();
+        QASR_CHECK(!out || cap >= e.size(), QASR_E_CAPACITY, "audio_embeds: buffer too small");
+        if (out) std::copy(e.begin(), e.end(), out);
+    });
+}
+
 QASR_API int qasr_session_run_opts(qasr_session* s, const float* pcm16k, size_t n, const qasr_run_opts* opts,
                                    qasr_result* out) {
     return guard([&] {

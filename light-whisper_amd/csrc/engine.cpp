@@ -7,6 +7,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <climits>
 #include <cstdio>
 #include <map>
 #include <chrono>
@@ -126,6 +127,17 @@ Session::Session(Model* m, int n_ctx) : m_(m), n_ctx_(n_ctx) {
         QASR_HIP(hipMalloc(&attn_cnt_, (size_t)4 * nkv * sizeof(int)));
         QASR_HIP(hipMemset(attn_cnt_, 0, (size_t)4 * nkv * sizeof(int)));
     }
+    // split-K fix-up of the decode GEMMs: up to kFixSplits partial tiles of 256 rows × the widest decoder weight
+    const qasr_hparams& hp = m->hp;
+    const size_t widest = (size_t)std::max(std::max(2 * hp.txt_ffn, hp.txt_h),
+                                           (hp.txt_heads + 2 * hp.txt_kv_heads) * hp.head_dim);
+    const char* nofix = getenv("QASR_NO_FIXUP");
+    if (!nofix || atoi(nofix) == 0) {
+        fix_floats_ = (size_t)256 * ((widest + 127) / 128 * 128) * kFixSplits;
+        QASR_HIP(hipMalloc(&fix_part_, fix_floats_ * sizeof(float)));
+        QASR_HIP(hipMalloc(&fix_cnt_, (size_t)kFixCounters * sizeof(unsigned)));
+        QASR_HIP(hipMemset(fix_cnt_, 0, (size_t)kFixCounters * sizeof(unsigned)));
+    }
 }
 
 Session::~Session() {
@@ -134,6 +146,9 @@ Session::~Session() {
     if (rope_) (void)hipFree(rope_);
     if (attn_part_) (void)hipFree(attn_part_);
     if (attn_cnt_) (void)hipFree(attn_cnt_);
+    if (fix_part_) (void)hipFree(fix_part_);
+    if (ec_emb_) (void)hipFree(ec_emb_);
+    if (fix_cnt_) (void)hipFree(fix_cnt_);
     if (pin_) (void)hipHostFree(pin_);
     for (auto& g : graphs_) (void)hipGraphExecDestroy(g.second);
     for (auto& g : draft_graphs_) (void)hipGraphExecDestroy(g.second);
@@ -229,6 +244,27 @@ void Session::front_end(const float* dpcm, const std::vector<int64_t>& off, cons
     float* melx = (float*)sc_.get(S_MELX, (size_t)chunks * nm * 100 * sizeof(float));
     mel_frames(dpcm, d_utts, d_work, (int)work.size(), nm, m_->dft_basis, m_->mel_filters, lm, d_umax, st_);
     mel_normalize(d_utts, count, chunks, d_cu, nm, lm, d_umax, melx, st_);
+    // encoder cache (single-utterance runs of run_host): the leading windows the sample prefix allows are reused when
+    // this window's mel maximum equals the cached one (then their normalised mel frames, conv chunks and windowed
+    // encoder rows are functions of the same samples); the conv stack and the encoder run on the remaining chunks
+    fe.skip_tokens = 0;
+    if (ec_run_) {
+        QASR_HIP(hipMemcpyAsync((unsigned*)pin_cnt_ + 32, d_umax, sizeof(unsigned), hipMemcpyDeviceToHost, st_));
+        QASR_HIP(hipStreamSynchronize(st_));
+        ec_umax_new_ = ((const unsigned*)pin_cnt_)[32];
+        // (ec_cand_ ≤ the windows the previous run stored; run_host marks them invalid while this run overwrites them)
+        const int reuse = ec_umax_new_ == ec_umax_ && m_->precision_gen == ec_prec_ ? ec_cand_ : 0;
+        const int per = h.n_window_infer / 100;   // chunks per attention window
+        if (reuse > 0 && per * reuse < chunks) {
+            const int c0 = per * reuse;
+            fe.skip_tokens = 13 * c0;
+            melx += (size_t)c0 * nm * 100;
+            chunks -= c0;
+            valid_idx.erase(valid_idx.begin(), valid_idx.begin() + fe.skip_tokens);
+            for (int& v : valid_idx) v -= fe.skip_tokens;
+        }
+    }
+    const int n_out = fe.total_tokens - fe.skip_tokens;
     // conv stack
     const int H1 = (nm + 1) / 2, W1 = 50, H2 = (H1 + 1) / 2, W2 = 25;
     __half* a1 = (__half*)sc_.get(S_A1, (size_t)chunks * H1 * W1 * C * sizeof(__half));
@@ -238,6 +274,7 @@ void Session::front_end(const float* dpcm, const std::vector<int64_t>& off, cons
     conv3x3_gelu(a1, chunks, H1, W1, m_->conv_w[1], m_->conv_b[1], C, a2, 0, st_);
     conv3x3_gelu(a2, chunks, H2, W2, m_->conv_w[2], m_->conv_b[2], C, a3, 1, st_);
     const int rows = chunks * 13, K = C * F3;
+    StableOrderScope order(ec_run_);   // encoder-cache runs: rows independent of the row count (bit-exact reuse)
     int8_t* xq = (int8_t*)sc_.get(S_XQ, (size_t)rows * K);
     float* xd = (float*)sc_.get(S_XD, (size_t)rows * (K / QK) * sizeof(float));
     quant_rows(a3, rows, K, K, xq, xd, st_);
@@ -245,19 +282,23 @@ void Session::front_end(const float* dpcm, const std::vector<int64_t>& off, cons
     mx_ws(rows, K);
     linear_q8(xq, xd, rows, m_->conv_out, nullptr, nullptr, proj, d, EPI_STORE, st_);
     int* d_valid = upload(S_VALID, valid_idx);
-    float* hs = (float*)sc_.get(S_HS, (size_t)fe.total_tokens * d * sizeof(float));
-    add_posemb_gather(proj, chunks, 13, d, m_->pos_emb, d_valid, fe.total_tokens, hs, st_);
+    float* hs = (float*)sc_.get(S_HS, (size_t)n_out * d * sizeof(float));
+    add_posemb_gather(proj, chunks, 13, d, m_->pos_emb, d_valid, n_out, hs, st_);
     QASR_HIP(hipGetLastError());
 }
 
 // windowed bidirectional encoder + ln_post + projector → S_EMB [tokens][H]
 void Session::encoder(FrontEnd& fe, float* enc_out_dbg) {
     const qasr_hparams& h = m_->hp;
-    const int N = fe.total_tokens, d = h.enc_d, F = h.enc_ffn, H = h.txt_h;
+    // fe.skip_tokens (one utterance): its leading cached rows are not encoded; the rest starts on a window boundary,
+    // so encoding it as an utterance of its own gives the same windows
+    const int skip = fe.skip_tokens, N = fe.total_tokens - skip, d = h.enc_d, F = h.enc_ffn, H = h.txt_h;
+    QASR_CHECK(skip == 0 || fe.n_tok.size() == 1, QASR_E_INTERNAL, "encoder cache: one utterance");
+    StableOrderScope order(ec_run_);   // encoder-cache runs: rows independent of the row count (bit-exact reuse)
     // attention windows (get_audio_cu_seqlens, modeling_qwen3_asr.py:276-315)
     std::vector<int> kvs(N), kvl(N);
     for (size_t u = 0; u < fe.n_tok.size(); u++) {
-        const int n = fe.n_tok[u];
+        const int n = fe.n_tok[u] - skip;
         // all chunks but the last are full → max post-CNN length is 13 unless the utterance is one partial chunk
         const int maxlen = n >= 13 ? 13 : n;
         const int window = maxlen * (h.n_window_infer / 100);
@@ -316,9 +357,43 @@ void Session::encoder(FrontEnd& fe, float* enc_out_dbg) {
         linear_q8(xq, xd, N, m_->proj1, m_->proj1_b, nullptr, ff, d, EPI_GELU, st_);
         quant_rows(ff, N, d, d, xq, xd, st_);
     }
-    float* emb = (float*)sc_.get(S_EMB, (size_t)N * H * sizeof(float));
-    linear_q8(xq, xd, N, m_->proj2, m_->proj2_b, nullptr, emb, H, EPI_STORE, st_);
+    float* emb = (float*)sc_.get(S_EMB, (size_t)(skip + N) * H * sizeof(float));
+    linear_q8(xq, xd, N, m_->proj2, m_->proj2_b, nullptr, emb + (size_t)skip * H, H, EPI_STORE, st_);
+    if (skip > 0)
+        QASR_HIP(hipMemcpyAsync(emb, ec_emb_, (size_t)skip * H * sizeof(float), hipMemcpyDeviceToDevice, st_));
+    last_audio_tokens_ = skip + N;
     QASR_HIP(hipGetLastError());
+}
+
+// encoder cache update after a single-utterance run of n samples: keep the embedding rows of its complete windows
+// (every frame of their chunks inside the samples: frame t reads samples up to 160·t + 199)
+void Session::enc_cache_store(int64_t n, int total_tokens) {
+    const qasr_hparams& h = m_->hp;
+    const int per = h.n_window_infer / 100;
+    int w = 0;
+    while (16000LL * (per * (w + 1) - 1) + 16040 <= n && 13 * per * (w + 1) <= total_tokens) w++;
+    const size_t bytes = (size_t)w * 13 * per * h.txt_h * sizeof(float);
+    if (bytes > ec_cap_) {
+        QASR_HIP(hipStreamSynchronize(st_));   // this run's reuse copy may still read the old buffer
+        if (ec_emb_) QASR_HIP(hipFree(ec_emb_));
+        ec_emb_ = nullptr;
+        ec_cap_ = 0;
+        QASR_HIP(hipMalloc(&ec_emb_, bytes));
+        ec_cap_ = bytes;
+    }
+    if (bytes) QASR_HIP(hipMemcpyAsync(ec_emb_, sc_.get(S_EMB, 0), bytes, hipMemcpyDeviceToDevice, st_));
+    ec_windows_ = w;
+    ec_umax_ = ec_umax_new_;
+    ec_prec_ = m_->precision_gen;
+}
+
+std::vector<float> Session::last_audio_embeds() {
+    std::vector<float> out((size_t)last_audio_tokens_ * m_->hp.txt_h);
+    if (!out.empty()) {
+        QASR_HIP(hipMemcpyAsync(out.data(), sc_.get(S_EMB, 0), out.size() * sizeof(float), hipMemcpyDeviceToHost, st_));
+        QASR_HIP(hipStreamSynchronize(st_));
+    }
+    return out;
 }
 
 // ------------------------------------------------------------------------------------------ decoder
@@ -328,6 +403,7 @@ void Session::decoder_layers(float* x, int rows, const int* d_pos, const int* d_
     const int H = h.txt_h, F = h.txt_ffn, nh = h.txt_heads, nkv = h.txt_kv_heads, hd = h.head_dim;
     const int QD = nh * hd, KD = nkv * hd;
     const int kmax = std::max(std::max(H, QD), F);
+    FixupScope fixup(rows <= 256 ? fix_part_ : nullptr, fix_floats_, fix_cnt_, kFixCounters);
     int8_t* xq = (int8_t*)sc_.get(S_XQ, (size_t)rows * kmax);
     float* xd = (float*)sc_.get(S_XD, (size_t)rows * (kmax / QK) * sizeof(float));
     float* qkv = (float*)sc_.get(S_QKV, (size_t)rows * (QD + 2 * KD) * sizeof(float));
@@ -488,18 +564,29 @@ void Session::draft_decode(int n_prompt, int base, int budget, int dummy, std::v
         }
     };
     refresh();
+    // the continuation of the last bigram (else unigram) in the previous transcripts.  Within the latest transcript —
+    // the previous window of the same speech, in step with this decode (a few tokens ahead where the window's start
+    // moved) — the occurrence nearest the current position, so a repeated n-gram does not cut the draft short at its
+    // last occurrence; else the most recent occurrence anywhere.
     auto lookup = [&](std::vector<int32_t>& draft, int cap) {
         draft.clear();
         if (cap <= 0 || history_.empty()) return;
-        const int n = (int)toks.size();
+        const int n = (int)toks.size(), H = (int)history_.size();
         for (int order = std::min(2, n); order >= 1 && draft.empty(); order--) {
-            for (int j = (int)history_.size() - order - 1; j >= 0; j--) {   // leaves ≥ 1 token to propose
-                bool match = true;
-                for (int k = 0; k < order && match; k++) match = history_[j + k] == toks[n - order + k];
-                if (!match) continue;
-                for (int k = j + order; k < (int)history_.size() && (int)draft.size() < cap; k++) draft.push_back(history_[k]);
-                break;
+            auto match = [&](int j) {
+                for (int k = 0; k < order; k++)
+                    if (history_[j + k] != toks[n - order + k]) return false;
+                return true;
+            };
+            int best = -1, bd = INT_MAX;
+            for (int j = hist_last_; j + order < H; j++) {   // leaves ≥ 1 token to propose
+                const int d = std::abs(j - hist_last_ + order - n);
+                if (d < bd && match(j)) bd = d, best = j;
             }
+            for (int j = H - order - 1; best < 0 && j >= 0; j--)
+                if (match(j)) best = j;
+            if (best >= 0)
+                for (int k = best + order; k < H && (int)draft.size() < cap; k++) draft.push_back(history_[k]);
         }
     };
     std::vector<int32_t> draft;
@@ -583,6 +670,13 @@ void Session::run_batch(const float* dpcm, const std::vector<int64_t>& off, cons
     {
         Timer t(st_, times ? &times->encoder : nullptr);
         encoder(fe, nullptr);
+    }
+    if (ec_run_) {
+        ecstats_.runs++;
+        const int per = h.n_window_infer / 100;
+        ecstats_.windows_reused += fe.skip_tokens / (13 * per);
+        ecstats_.windows_computed += (fe.total_tokens - fe.skip_tokens + 13 * per - 1) / (13 * per);
+        enc_cache_store(len[0], fe.total_tokens);
     }
     // prompts, KV slots, generation budgets
     std::vector<int> n_prompt(count), base(count), row0(count), budget(count);
@@ -724,8 +818,13 @@ void Session::run_batch(const float* dpcm, const std::vector<int64_t>& off, cons
         }
         out[0].tokens = toks;
         out[0].truncated = force_tps <= 0 && !eos && (int)toks.size() >= budget[0];
+        hist_last_ = (int)history_.size();
         history_.insert(history_.end(), toks.begin(), toks.end());
-        if (history_.size() > 8192) history_.erase(history_.begin(), history_.end() - 8192);
+        if (history_.size() > 8192) {
+            const int cut = (int)history_.size() - 8192;
+            history_.erase(history_.begin(), history_.begin() + cut);
+            hist_last_ = std::max(0, hist_last_ - cut);
+        }
         dstats_.tokens += (int64_t)toks.size();
         UttResult& r = out[0];
         r.raw = m_->tok.decode(r.tokens.data(), (int)r.tokens.size());
@@ -829,7 +928,28 @@ void Session::run_host(const std::vector<const float*>& pcm, const std::vector<i
     float* d = (float*)sc_.get(S_PCM, (size_t)std::max<int64_t>(total, 1) * sizeof(float));
     for (size_t i = 0; i < len.size(); i++)
         QASR_HIP(hipMemcpyAsync(d + off[i], pcm[i], (size_t)len[i] * sizeof(float), hipMemcpyHostToDevice, st_));
-    run_batch(d, off, len, max_new, force_tps, out, times);
+    ec_run_ = enc_cache_ && len.size() == 1;
+    ec_cand_ = 0;
+    if (ec_run_ && ec_windows_ > 0) {
+        // windows whose chunks' frames all lie in the samples this run shares with the previous one (bitwise)
+        const int64_t m = std::min<int64_t>(len[0], (int64_t)ec_pcm_.size());
+        int64_t L = 0;
+        const size_t B = 4096;
+        while (L + (int64_t)B <= m && !memcmp(pcm[0] + L, ec_pcm_.data() + L, B * sizeof(float))) L += B;
+        while (L < m && !memcmp(pcm[0] + L, ec_pcm_.data() + L, sizeof(float))) L++;
+        const int per = m_->hp.n_window_infer / 100;
+        while (ec_cand_ < ec_windows_ && 16000LL * (per * (ec_cand_ + 1) - 1) + 16040 <= L) ec_cand_++;
+    }
+    if (ec_run_) ec_windows_ = 0;   // invalid until this run stores its own (an exception leaves it empty)
+    try {
+        run_batch(d, off, len, max_new, force_tps, out, times);
+    } catch (...) {
+        ec_run_ = false;
+        ec_windows_ = 0;
+        throw;
+    }
+    if (ec_run_) ec_pcm_.assign(pcm[0], pcm[0] + len[0]);
+    ec_run_ = false;
 }
 
 // ------------------------------------------------------------------------------------------ test stages

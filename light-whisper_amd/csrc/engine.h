@@ -70,11 +70,25 @@ class Session {
         int64_t passes = 0, proposed = 0, accepted = 0, tokens = 0;
     };
     const DraftStats& draft_stats() const { return dstats_; }
+    // streaming encoder cache: a single-utterance run whose samples extend the previous run's (the
+    // app's growing interim window) reuses the audio-embedding rows of the previous run's complete 8-chunk attention
+    // windows when the window's mel maximum is unchanged — those rows are then a function of the same samples
+    void set_enc_cache(bool on) {
+        enc_cache_ = on;
+        ec_windows_ = 0;
+    }
+    struct EncCacheStats {
+        int64_t runs = 0, windows_reused = 0, windows_computed = 0;
+    };
+    const EncCacheStats& enc_cache_stats() const { return ecstats_; }
+    // the audio-embedding rows (projector output, [tokens][H]) of the last single-utterance run (tests)
+    std::vector<float> last_audio_embeds();
     hipStream_t stream() const { return st_; }
 
    private:
     struct FrontEnd {
         int total_chunks = 0, total_tokens = 0;
+        int skip_tokens = 0;   // leading audio tokens taken from the encoder cache (not encoded)
         std::vector<int> n_tok, tok_base;
     };
     void front_end(const float* dpcm, const std::vector<int64_t>& off, const std::vector<int64_t>& len, FrontEnd& fe,
@@ -86,6 +100,7 @@ class Session {
     void decoder_layers(float* x, int rows, const int* d_pos, const int* d_slot, const int* d_kvs, const int* d_kvl,
                         int64_t total_keys, bool dense = false, bool rows_share_kv = false);
     void ensure_kv(int64_t slots);
+    void enc_cache_store(int64_t n, int total_tokens);
     void decode_step(const DecState& ds, int B, bool sizing);
     // one verify pass of B rows (last accepted token + draft, padded): tables in S_DTAB, argmax → pinned host
     void draft_step(int B);
@@ -125,8 +140,27 @@ class Session {
     bool attn_split_ = getenv("QASR_NO_ATTN_SPLIT") == nullptr;
     float* attn_part_ = nullptr;
     int* attn_cnt_ = nullptr;
+    // split-K fix-up workspace of the decode-step GEMMs (≤ 256 rows; QASR_NO_FIXUP=1: f32 atomics instead): partial
+    // tiles + per-tile arrival counters (zeroed once; the kernels leave them zero)
+    float* fix_part_ = nullptr;
+    size_t fix_floats_ = 0;
+    unsigned* fix_cnt_ = nullptr;
     std::vector<int32_t> history_;   // previous transcripts (the lookup corpus), oldest first
+    int hist_last_ = 0;              // where the latest transcript starts in history_
     DraftStats dstats_;
+    // encoder cache: the previous single-utterance run's samples, mel maximum, precision generation and the
+    // embedding rows of its ec_windows_ complete windows (ec_emb_, device); ec_cand_ = windows the current run's
+    // sample prefix allows (run_host → front_end), ec_umax_new_ = the current run's mel maximum
+    bool enc_cache_ = false;
+    std::vector<float> ec_pcm_;
+    unsigned ec_umax_ = 0, ec_umax_new_ = 0;
+    uint64_t ec_prec_ = 0;
+    int ec_windows_ = 0, ec_cand_ = 0;
+    bool ec_run_ = false;
+    float* ec_emb_ = nullptr;
+    size_t ec_cap_ = 0;
+    EncCacheStats ecstats_;
+    int last_audio_tokens_ = 0;
     uint64_t graph_key_[4] = {~0ull, ~0ull, ~0ull, ~0ull};   // scratch epoch, KV epoch, precision gen, determinism gen
     uint64_t kv_epoch_ = 0;
     int ucap_ = 0;

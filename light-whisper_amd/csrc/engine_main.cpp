@@ -289,6 +289,10 @@ struct Server {
             // tokens, verified in one pass; QASR_STREAM_DRAFT=0 turns it off)
             const char* sd = getenv("QASR_STREAM_DRAFT");
             qasr_session_set_draft(session, !(sd && std::string(sd) == "0"));
+            // and reuse the encoder windows a growing window shares with the previous request (QASR_STREAM_ENC_CACHE=0
+            // turns it off)
+            const char* ec = getenv("QASR_STREAM_ENC_CACHE");
+            qasr_session_set_encoder_cache(session, !(ec && std::string(ec) == "0"));
             if (qasr_vad_open(nullptr, &vad) != QASR_OK) return fail(qasr_last_error());
             backend = "hip";
             device = "hip";
@@ -535,6 +539,13 @@ struct Server {
                 d.set("accepted", Value::integer((int)st[2]));
                 d.set("tokens", Value::integer((int)st[3]));
                 s.set("prompt_lookup", d);
+            }
+            if (qasr_session_encoder_cache_stats(session, st) == QASR_OK) {
+                Value e = Value::object();
+                e.set("runs", Value::integer((int)st[0]));
+                e.set("windows_reused", Value::integer((int)st[1]));
+                e.set("windows_encoded", Value::integer((int)st[2]));
+                s.set("encoder_cache", e);
             }
         }
         Value ml = Value::object();

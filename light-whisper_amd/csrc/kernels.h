@@ -45,6 +45,15 @@ void gemv_fused(int pro, const int8_t* xq, const float* xd, const float* src, in
 void set_deterministic(bool on);
 bool deterministic();
 uint64_t deterministic_gen();
+// Row-count-independent summation order for the Q8 GEMMs in its scope (thread-local): one tile configuration with one
+// K group and no split for every M (and no GEMV rows), so a row's outputs are the same bits whatever other rows the
+// call carries — the streaming encoder cache reuses rows of an earlier, shorter run bit for bit.
+struct StableOrderScope {
+    explicit StableOrderScope(bool on);
+    ~StableOrderScope();
+    bool prev;
+};
+bool stable_order();
 // force_cfg: index into kernels_q8.hip kGemmCfgs (-1 = heuristic); force_splits: split-K (0 = heuristic)
 void gemm_q8(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const float* bias, const float* res, float* y,
              int ldy, int epi, hipStream_t s, int force_cfg = -1, int force_splits = 0, int8_t* yq = nullptr,
@@ -61,6 +70,17 @@ void gemm_mx(const uint8_t* x8, const uint8_t* xs, int M, const Q8Mat& W, const 
              float* y, int ldy, int epi, hipStream_t s, int8_t* yq = nullptr, float* yd = nullptr,
              bool y_zeroed = false, int force_cfg = -1);
 void set_mx_workspace(void* p, size_t bytes);
+// split-K fix-up workspace for gemm_q8 (thread-local): `floats` partial-tile floats and `ncnt` arrival counters that
+// are zero between launches (the kernels keep them so); nullptr = split-K adds with f32 atomics.  The fix-up serves
+// the SwiGLU epilogue and deterministic mode, or every split epilogue with all_epilogues (op-level tests / tuning).
+void set_gemm_fixup(float* part, size_t floats, unsigned* cnt, int ncnt, bool all_epilogues = false);
+constexpr int kFixSplits = 8, kFixCounters = 8192;
+struct FixupScope {   // registers a fix-up workspace for the calls in its scope, unregisters on exit (throws included)
+    FixupScope(float* part, size_t floats, unsigned* cnt, int ncnt) { set_gemm_fixup(part, floats, cnt, ncnt); }
+    ~FixupScope() { set_gemm_fixup(nullptr, 0, nullptr, 0); }
+    FixupScope(const FixupScope&) = delete;
+    FixupScope& operator=(const FixupScope&) = delete;
+};
 size_t mx_workspace_bytes(int64_t M, int64_t K);
 // rows of a [2F][K] gate|up matrix → interleaved by 16 (32j+t: t<16 gate 16j+t, else up 16j+t-16)
 int64_t gate_up_interleaved_row(int64_t r, int64_t F);

@@ -540,12 +540,7 @@ __global__ __launch_bounds__(256) void k_attn_tile(const __half* __restrict__ Q,
     const int myrow = SINGLE ? r0 : min(r0 + fr, rows - 1);
     const bool row_ok = SINGLE || r0 + fr < rows;
     const int st = kv_start[myrow], en = row_ok ? st + kv_len[myrow] : st;
-    int lo = row_ok && en > st ? st : INT_MAX, hi = row_ok ? en : INT_MIN;
-#pragma unroll
-    for (int off = 1; off < 16; off <<= 1) {
-        lo = min(lo, __shfl_xor(lo, off));
-        hi = max(hi, __shfl_xor(hi, off));
-    }
+    int lo = 0, hi = 0;
     // Q fragments (B operand of K·Qᵀ): lane (row fr, kh) holds Q[row][32c + 8kh .. +8]
     v8h qf[G][DC];
 #pragma unroll
@@ -580,7 +575,25 @@ __global__ __launch_bounds__(256) void k_attn_tile(const __half* __restrict__ Q,
             for (int c = 0; c < DC; c++)
                 kn[t][c] = *(const v8h*)(kbase + (size_t)min(c0 + 16 * t + fr, hi - 1) * ldkv + 32 * c + 8 * kh);
     };
-    if (lo < hi) load_chunk(lo);
+    // One pass per distinct range start among the tile's rows (encoder windows / packed utterances meeting inside a
+    // 16-row tile): the rows that share a start take every key in chunks aligned at THAT start, the others see the
+    // pass fully masked (state unchanged bit for bit: alpha 1, p 0).  A row's result is then independent of where its
+    // range sits relative to the tile — the streaming encoder cache recomputes a window as rows 0… of a shorter run.
+    // Tiles whose rows share one start (nearly all) run exactly one pass, as before.
+    bool pend = row_ok && en > st;
+    for (;;) {
+    int s0 = pend ? st : INT_MAX;
+#pragma unroll
+    for (int off = 1; off < 16; off <<= 1) s0 = min(s0, __shfl_xor(s0, off));
+    if (s0 == INT_MAX) break;
+    const bool in = pend && st == s0;
+    int e0 = in ? en : INT_MIN;
+#pragma unroll
+    for (int off = 1; off < 16; off <<= 1) e0 = max(e0, __shfl_xor(e0, off));
+    lo = s0;
+    hi = e0;
+    pend = pend && !in;
+    load_chunk(lo);
     for (int k0 = lo; k0 < hi; k0 += KC) {
         // ---- this chunk: V into the wave's LDS image, K fragments to registers; then prefetch the next chunk
 #pragma unroll
@@ -606,7 +619,7 @@ __global__ __launch_bounds__(256) void k_attn_tile(const __half* __restrict__ Q,
 #pragma unroll
                 for (int i = 0; i < 4; i++) {
                     const int key = k0 + 16 * t + 4 * kh + i;
-                    p[g][t][i] = (key >= st && key < en) ? sacc[i] * scale : -INFINITY;
+                    p[g][t][i] = (in && key >= st && key < en) ? sacc[i] * scale : -INFINITY;
                 }
             }
         }
@@ -679,6 +692,7 @@ __global__ __launch_bounds__(256) void k_attn_tile(const __half* __restrict__ Q,
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
     }
     // ---- normalise and store: acc[g][t][i] = O[row 4kh+i][dim 16t + fr] of head kvh·G + g
     const int D = nkv * G * HD;

@@ -465,6 +465,10 @@ void set_deterministic(bool on) {
     if (g_det.exchange(on ? 1 : 0) != (on ? 1 : 0)) g_det_gen++;
 }
 bool deterministic() { return g_det.load(std::memory_order_relaxed) != 0; }
+static thread_local bool g_stable = false;
+StableOrderScope::StableOrderScope(bool on) : prev(g_stable) { g_stable = on || prev; }
+StableOrderScope::~StableOrderScope() { g_stable = prev; }
+bool stable_order() { return g_stable; }
 uint64_t deterministic_gen() { return g_det_gen.load(); }
 
 
@@ -482,7 +486,7 @@ uint64_t deterministic_gen() { return g_det_gen.load(); }
 // Shared GEMM epilogue: the wave's (16·TI)×(16·TJ) f32 accumulators (lane: rows fq..fq+3 of each 16-row
 // fragment, column fr of each 16-column fragment) → bias / residual / GELU store, split-K f32 atomics, or the fused
 // SwiGLU + Q8 quantisation of interleaved gate/up columns.
-template <int TI, int TJ>
+template <int TI, int TJ, bool SUMMED = false>
 __device__ __forceinline__ void gemm_epilogue(const float (&acc)[TI][TJ][4], int M, int N, int m0, int n0, int arow,
                                               int bcol, int fr, int fq, const float* __restrict__ bias,
                                               const float* res, float* y, int ldy, int epi, int8_t* __restrict__ yq,
@@ -557,7 +561,7 @@ __device__ __forceinline__ void gemm_epilogue(const float (&acc)[TI][TJ][4], int
             }
         return;
     }
-    const bool split = gridDim.z > 1;
+    const bool split = !SUMMED && gridDim.z > 1;   // SUMMED: a split-K fix-up already added the partial tiles
 #pragma unroll
     for (int i = 0; i < TI; i++) {
 #pragma unroll
@@ -577,6 +581,89 @@ __device__ __forceinline__ void gemm_epilogue(const float (&acc)[TI][TJ][4], int
             }
         }
     }
+}
+
+// Split-K fix-up (no output atomics, any epilogue): the S = gridDim.z workgroups of a tile each store their partial
+// tile write-through (sc1) into `part`, wait for their stores, and one lane counts the arrival with an agent-scope
+// add (MI355X_MICROARCH.md, inter-workgroup visibility: one counter add per storing workgroup, the last adder's
+// workgroup reads after a barrier, sc1 loads); the workgroup whose add comes last resets the counter for the next
+// launch, adds the S partials in split order — the same sum whatever the arrival order, so the result is
+// deterministic — and runs the tile's full epilogue (bias, residual, SwiGLU + Q8, …).  Partial layout per tile:
+// [split][wave slot][i·TJ + j][r][lane] floats, 256-B contiguous per store instruction.  Every thread of the
+// workgroup calls this (it holds two barriers); `has` = this wave owns accumulators (K group 0, active rows).
+// Returns true in the workgroup that must run the epilogue, with acc replaced by the full sums.
+// `flag`: one LDS int the caller no longer uses (a static __shared__ here would grow the kernel's LDS past the
+// 3-workgroups-per-CU budget of the 3-stage decode tiles).
+template <int TI, int TJ>
+__device__ __forceinline__ bool splitk_fixup(float (&acc)[TI][TJ][4], bool has, int slot, int nslot, float* part,
+                                             unsigned* cnt, int* flag) {
+    constexpr int PER = TI * TJ * 4 * 64;   // floats per wave slot
+    const int S = gridDim.z, z = blockIdx.z, lane = threadIdx.x & 63;
+    const int tile = blockIdx.y * gridDim.x + blockIdx.x;
+    float* tp = part + (size_t)tile * S * nslot * PER + (size_t)slot * PER + lane;
+    if (has) {
+        float* p = tp + (size_t)z * nslot * PER;
+#pragma unroll
+        for (int i = 0; i < TI; i++)
+#pragma unroll
+            for (int j = 0; j < TJ; j++)
+#pragma unroll
+                for (int r = 0; r < 4; r++)
+                    __hip_atomic_store(p + ((i * TJ + j) * 4 + r) * 64, acc[i][j][r], __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned prev = __hip_atomic_fetch_add(cnt + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int last = prev == (unsigned)(S - 1);
+        if (last) __hip_atomic_store(cnt + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // next launch
+        *flag = last;
+    }
+    __syncthreads();
+    if (!*flag) return false;
+    if (!has) return true;
+    // the S partials in split order; every load of a batch of PB partials in flight at once (partials past S and
+    // this workgroup's own are not loaded: its own sums come from registers)
+    constexpr int F = TI * TJ * 4, PB = F >= 16 ? 4 : 8;
+    float own[F];
+#pragma unroll
+    for (int i = 0; i < TI; i++)
+#pragma unroll
+        for (int j = 0; j < TJ; j++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) own[(i * TJ + j) * 4 + r] = acc[i][j][r];
+    float sum[F];
+    for (int u0 = 0; u0 < S; u0 += PB) {
+        float v[PB][F];
+#pragma unroll
+        for (int b = 0; b < PB; b++) {
+            const int u = u0 + b;
+            if (u < S && u != z) {
+                const float* p = tp + (size_t)u * nslot * PER;
+#pragma unroll
+                for (int e = 0; e < F; e++)
+                    v[b][e] = __hip_atomic_load(p + e * 64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+#pragma unroll
+        for (int b = 0; b < PB; b++) {
+            const int u = u0 + b;
+            if (u >= S) break;
+#pragma unroll
+            for (int e = 0; e < F; e++) {
+                const float x = u == z ? own[e] : v[b][e];
+                sum[e] = u == 0 ? x : sum[e] + x;
+            }
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < TI; i++)
+#pragma unroll
+        for (int j = 0; j < TJ; j++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) acc[i][j][r] = sum[(i * TJ + j) * 4 + r];
+    return true;
 }
 
 constexpr int GBK = 128;     // K per step
@@ -767,7 +854,8 @@ __global__ __launch_bounds__(256 * KG, 2 / KG) void k_gemm_q8d(const int8_t* __r
                                                      const int8_t* __restrict__ W, const __half* __restrict__ Wsc,
                                                      int N, int K, const float* __restrict__ bias, const float* res,
                                                      float* y, int ldy, int epi, int steps_per_split,
-                                                     int8_t* __restrict__ yq, float* __restrict__ yd) {
+                                                     int8_t* __restrict__ yq, float* __restrict__ yd,
+                                                     float* fix_part, unsigned* fix_cnt) {
     static_assert(WM * WN == 4, "k_gemm_q8d: 4 waves per K group");
     static_assert(BK == 64 || BK == 128, "k_gemm_q8d: a stage is 2 or 4 Q8 blocks");
     // KG K groups of 4 waves share the tile: group g takes blocks [g·KB/KG, (g+1)·KB/KG) of every stage and the
@@ -965,8 +1053,8 @@ __global__ __launch_bounds__(256 * KG, 2 / KG) void k_gemm_q8d(const int8_t* __r
                     red[(i * TJ + j) * 64] = make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
         }
         __syncthreads();
-        if (kg == 1) return;
-        if (active) {
+        if (kg == 1 && (TI * TJ > 4 || !fix_part)) return;
+        if (kg == 0 && active) {
 #pragma unroll
             for (int i = 0; i < TI; i++)
 #pragma unroll
@@ -976,7 +1064,17 @@ __global__ __launch_bounds__(256 * KG, 2 / KG) void k_gemm_q8d(const int8_t* __r
                 }
         }
     }
-    if (!active) return;
+    // split-K fix-up (decode-sized tiles only, ≤ 64×64: the prefill tiles keep their register budget): the last
+    // workgroup of the tile adds the partials
+    if constexpr (TI * TJ <= 4) {
+        if (fix_part && gridDim.z > 1) {
+            if (!splitk_fixup<TI, TJ>(acc, kg == 0 && active, lw, 4, fix_part, fix_cnt, (int*)smem)) return;
+            if ((KG == 2 && kg != 0) || !active) return;
+            gemm_epilogue<TI, TJ, true>(acc, M, N, m0, n0, arow, bcol, fr, fq, bias, res, y, ldy, epi, yq, yd);
+            return;
+        }
+    }
+    if ((KG == 2 && kg != 0) || !active) return;
     gemm_epilogue<TI, TJ>(acc, M, N, m0, n0, arow, bcol, fr, fq, bias, res, y, ldy, epi, yq, yd);
 }
 
@@ -1271,9 +1369,9 @@ static void launch_gemm(dim3 grid, hipStream_t s, const int8_t* xq, const float*
 template <int WM, int WN, int TI, int TJ, int NBUF = 3, int BK = 64, int KG = 1>
 static void launch_gemm_dma(dim3 grid, hipStream_t s, const int8_t* xq, const float* xd, int M, const Q8Mat& W,
                             const float* bias, const float* res, float* y, int ldy, int epi, int sps, int8_t* yq,
-                            float* yd) {
+                            float* yd, float* fix_part, unsigned* fix_cnt) {
     k_gemm_q8d<WM, WN, TI, TJ, NBUF, BK, KG><<<grid, 256 * KG, 0, s>>>(xq, xd, M, W.qs, W.sc, W.N, W.K, bias, res, y, ldy, epi, sps, yq,
-                                                    yd);
+                                                    yd, fix_part, fix_cnt);
 }
 
 // GEMM configurations: 0..3 register-staged kernel (any K % 32 == 0), 4..11 LDS-DMA kernel, 2×2 waves, stages of
@@ -1319,33 +1417,33 @@ static void launch_ks_cfg(int cfg, hipStream_t s, const int8_t* xq, const float*
 
 static void launch_cfg(int cfg, dim3 grid, hipStream_t s, const int8_t* xq, const float* xd, int M, const Q8Mat& W,
                        const float* bias, const float* res, float* y, int ldy, int epi, int sps, int8_t* yq,
-                       float* yd) {
+                       float* yd, float* fp = nullptr, unsigned* fc = nullptr) {
     switch (cfg) {
         case 0: launch_gemm<4, 4>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
         case 1: launch_gemm<2, 4>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
         case 2: launch_gemm<2, 2>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
         case 3: launch_gemm<1, 2>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
-        case 4: launch_gemm_dma<2, 2, 4, 4, 3, 64>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
-        case 5: launch_gemm_dma<2, 2, 2, 4, 3, 64>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
-        case 6: launch_gemm_dma<2, 2, 2, 2, 3, 64>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
-        case 7: launch_gemm_dma<2, 2, 4, 2, 3, 64>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
-        case 8: launch_gemm_dma<2, 2, 4, 4, 2, 128>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
-        case 9: launch_gemm_dma<2, 2, 2, 4, 3, 128>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
-        case 10: launch_gemm_dma<2, 2, 2, 2, 3, 128>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
-        case 11: launch_gemm_dma<2, 2, 4, 2, 3, 128>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
+        case 4: launch_gemm_dma<2, 2, 4, 4, 3, 64>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd, fp, fc); break;
+        case 5: launch_gemm_dma<2, 2, 2, 4, 3, 64>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd, fp, fc); break;
+        case 6: launch_gemm_dma<2, 2, 2, 2, 3, 64>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd, fp, fc); break;
+        case 7: launch_gemm_dma<2, 2, 4, 2, 3, 64>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd, fp, fc); break;
+        case 8: launch_gemm_dma<2, 2, 4, 4, 2, 128>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd, fp, fc); break;
+        case 9: launch_gemm_dma<2, 2, 2, 4, 3, 128>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd, fp, fc); break;
+        case 10: launch_gemm_dma<2, 2, 2, 2, 3, 128>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd, fp, fc); break;
+        case 11: launch_gemm_dma<2, 2, 4, 2, 3, 128>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd, fp, fc); break;
         // 4×1 waves of 64 columns: the SwiGLU epilogue on 64-column workgroup tiles
-        case 12: launch_gemm_dma<4, 1, 1, 4, 3, 128>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
-        case 13: launch_gemm_dma<4, 1, 2, 4, 3, 128>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
-        case 14: launch_gemm_dma<2, 2, 2, 2, 3, 128, 2>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
-        case 15: launch_gemm_dma<4, 1, 1, 4, 3, 128, 2>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
-        case 16: launch_gemm_dma<2, 2, 1, 1, 8, 128>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
-        case 17: launch_gemm_dma<2, 2, 1, 2, 6, 128>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
-        case 18: launch_gemm_dma<2, 2, 2, 1, 6, 128>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
-        case 19: launch_gemm_dma<2, 2, 2, 2, 6, 128, 2>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
-        case 20: launch_gemm_dma<4, 1, 1, 4, 6, 128, 2>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
-        case 21: launch_gemm_dma<2, 2, 2, 2, 6, 128>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
-        case 22: launch_gemm_dma<4, 1, 1, 4, 6, 128>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
-        default: launch_gemm_dma<2, 2, 1, 4, 4, 128>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd); break;
+        case 12: launch_gemm_dma<4, 1, 1, 4, 3, 128>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd, fp, fc); break;
+        case 13: launch_gemm_dma<4, 1, 2, 4, 3, 128>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd, fp, fc); break;
+        case 14: launch_gemm_dma<2, 2, 2, 2, 3, 128, 2>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd, fp, fc); break;
+        case 15: launch_gemm_dma<4, 1, 1, 4, 3, 128, 2>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd, fp, fc); break;
+        case 16: launch_gemm_dma<2, 2, 1, 1, 8, 128>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd, fp, fc); break;
+        case 17: launch_gemm_dma<2, 2, 1, 2, 6, 128>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd, fp, fc); break;
+        case 18: launch_gemm_dma<2, 2, 2, 1, 6, 128>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd, fp, fc); break;
+        case 19: launch_gemm_dma<2, 2, 2, 2, 6, 128, 2>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd, fp, fc); break;
+        case 20: launch_gemm_dma<4, 1, 1, 4, 6, 128, 2>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd, fp, fc); break;
+        case 21: launch_gemm_dma<2, 2, 2, 2, 6, 128>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd, fp, fc); break;
+        case 22: launch_gemm_dma<4, 1, 1, 4, 6, 128>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd, fp, fc); break;
+        default: launch_gemm_dma<2, 2, 1, 4, 4, 128>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd, fp, fc); break;
     }
 }
 
@@ -1594,6 +1692,23 @@ static void gemm_mx_q8in(const int8_t* xq, const float* xd, int M, const Q8Mat& 
     gemm_mx(x8, xs, M, W, bias, res, y, ldy, epi, s, yq, yd, y_zeroed, -1);
 }
 
+// Split-K fix-up workspace (thread-local registration, like the MXFP8 workspace): partial tiles + one arrival
+// counter per tile, zero between launches.  Unregistered (or QASR_NO_FIXUP=1): split-K adds with f32 atomics.
+static thread_local float* g_fix_part = nullptr;
+static thread_local size_t g_fix_floats = 0;
+static thread_local unsigned* g_fix_cnt = nullptr;
+static thread_local int g_fix_ncnt = 0;
+static thread_local bool g_fix_all = false;
+void set_gemm_fixup(float* part, size_t floats, unsigned* cnt, int ncnt, bool all_epilogues) {
+    static const bool off = getenv("QASR_NO_FIXUP") && atoi(getenv("QASR_NO_FIXUP")) != 0;
+    const bool on = !off && part && cnt;
+    g_fix_part = on ? part : nullptr;
+    g_fix_floats = on ? floats : 0;
+    g_fix_cnt = on ? cnt : nullptr;
+    g_fix_ncnt = on ? ncnt : 0;
+    g_fix_all = on && all_epilogues;
+}
+
 // Decode-step table (M = the step's row bucket ≤ 256, K % 128 == 0): configuration and split-K count per row range,
 // from tools/dec_gemm_sweep.py with cold weights on MI355X (profiles/r2_dec_gemm_sweep.log) — every configuration ×
 // split count timed per shape; the winners per class of the decoder's shapes: QKV (plain store, K ≤ 2048), the
@@ -1602,6 +1717,8 @@ struct DecPick { int m_max, cfg, splits; };
 static const DecPick kDecQkv[] = {{16, 17, 6}, {32, 16, 4}, {64, 18, 4}, {128, 14, 2}, {256, 14, 1}};
 static const DecPick kDecO[] = {{64, 16, 4}, {128, 18, 4}, {192, 15, 3}, {256, 14, 2}};
 static const DecPick kDecDown[] = {{32, 16, 8}, {64, 15, 8}, {96, 10, 8}, {128, 14, 4}, {192, 10, 8}, {256, 15, 4}};
+// gate/up with the SwiGLU epilogue: split-K through the fix-up workspace pays off only at ≤ 32 rows
+static const DecPick kDecGu[] = {{16, 15, 2}, {32, 23, 2}};
 
 static bool dec_table_pick(int M, const Q8Mat& W, int epi, int& cfg, int& splits) {
     if (M > 256 || W.K % 128 != 0 || W.N >= 32768) return false;
@@ -1610,6 +1727,7 @@ static bool dec_table_pick(int M, const Q8Mat& W, int epi, int& cfg, int& splits
     if (epi == EPI_STORE && W.K <= 2048) t = kDecQkv, n = sizeof(kDecQkv) / sizeof(DecPick);
     else if (epi == EPI_RESID && W.K <= 2048) t = kDecO, n = sizeof(kDecO) / sizeof(DecPick);
     else if (epi == EPI_RESID) t = kDecDown, n = sizeof(kDecDown) / sizeof(DecPick);
+    else if (epi == EPI_SWIGLU && g_fix_part) t = kDecGu, n = sizeof(kDecGu) / sizeof(DecPick);
     if (!t) return false;
     for (int i = 0; i < n; i++)
         if (M <= t[i].m_max) {
@@ -1634,7 +1752,12 @@ void gemm_q8(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const flo
         return !g.dma || W.K % g.bk == 0;
     };
     int pick;
-    if (W.K % 64 == 0) {
+    if (g_stable && W.K % 128 == 0 && force_cfg < 0) {
+        // row-count-independent order: 64×64 tiles, K-128 stages, one K group, no split — every output is its blocks'
+        // fma chain in K order, the same for any M (StableOrderScope)
+        pick = 10;
+        force_splits = 1;
+    } else if (W.K % 64 == 0) {
         // measured on the engine's shapes (tools/gemm_tune.py, profiles/): 128×128 tiles with K-64 stages on prefill
         // / encoder shapes; 64×64 tiles with K-128 stages (+ split-K) on batched decode; the vocabulary projection
         // by row count; decode SwiGLU epilogue on 4×1 waves of 64 columns; two K groups (8 waves per tile) where
@@ -1667,6 +1790,26 @@ void gemm_q8(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const flo
         return;
     }
     const int steps = cf.dma ? W.K / cf.bk : cdiv(W.K, GBK);
+    const int tiles = cdiv(W.N, cf.bn) * cdiv(M, cf.bm);
+    // split-K through the fix-up workspace (any epilogue, deterministic): a forced / table split count of a DMA tile
+    auto fixup_ok = [&](int sp) {
+        return cf.dma && cf.bm * cf.bn <= 64 * 64 && sp > 1 && g_fix_part && tiles <= g_fix_ncnt &&
+               (size_t)tiles * sp * cf.bm * cf.bn <= g_fix_floats;
+    };
+    // The fix-up's serial tail (store → count → reload) costs more than f32 atomics on the plain-store / residual
+    // decode shapes (profiles/r2_dec_gemm_sweep_fixup.log), so those keep the atomics unless the sums must be
+    // deterministic; the SwiGLU epilogue (no atomic form) splits only through the fix-up.
+    const bool fix_epi = epi == EPI_SWIGLU || g_fix_all || deterministic();
+    if (force_splits > 1 && fix_epi && fixup_ok(std::min(force_splits, steps))) {
+        const int sps = cdiv(steps, std::min(force_splits, steps));
+        dim3 grid(cdiv(W.N, cf.bn), cdiv(M, cf.bm), cdiv(steps, sps));
+        if (epi == EPI_SWIGLU)
+            QASR_CHECK(W.N % 64 == 0 && yq && yd && (cf.bn == 128 || pick == 12 || pick == 13 || pick == 15 ||
+                                                     pick == 20 || pick == 22),
+                       QASR_E_INVALID, "gemm_q8: SwiGLU epilogue needs a 64-column wave tile");
+        launch_cfg(pick, grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd, g_fix_part, g_fix_cnt);
+        return;
+    }
     if (epi == EPI_SWIGLU) {
         QASR_CHECK(W.N % 64 == 0 && yq && yd, QASR_E_INVALID, "gemm_q8: SwiGLU epilogue needs N % 64 == 0");
         QASR_CHECK(cf.bn == 128 || pick == 12 || pick == 13 || pick == 15 || pick == 20 || pick == 22, QASR_E_INVALID,
@@ -1675,7 +1818,6 @@ void gemm_q8(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const flo
         launch_cfg(pick, grid, s, xq, xd, M, W, bias, res, y, ldy, epi, steps, yq, yd);
         return;
     }
-    const int tiles = cdiv(W.N, cf.bn) * cdiv(M, cf.bm);
     const bool can_split = (epi == EPI_STORE || epi == EPI_RESID) && ldy == W.N && (epi != EPI_RESID || res == y);
     if (epi == EPI_GELU_Q8)
         QASR_CHECK(W.N % 32 == 0 && yq && yd && cf.bn >= 64, QASR_E_INVALID, "gemm_q8: GELU+Q8 epilogue shape");
@@ -1720,7 +1862,7 @@ void interleave_gate_up(Q8Mat& W, hipStream_t s) {
 void linear_q8(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const float* bias, const float* res,
                float* y, int ldy, int epi, hipStream_t s, bool y_zeroed) {
     if (M <= 0) return;
-    if (M <= kGemvRows) gemv_q8(xq, xd, M, W, bias, res, y, ldy, epi, s);
+    if (M <= kGemvRows && !(g_stable && W.K % 128 == 0)) gemv_q8(xq, xd, M, W, bias, res, y, ldy, epi, s);
     else gemm_q8(xq, xd, M, W, bias, res, y, ldy, epi, s, -1, 0, nullptr, nullptr, y_zeroed);
 }
 

@@ -10,7 +10,7 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 PKG_ROOT = os.path.dirname(_HERE)                 # light-whisper_amd/
-LIB_PATH = os.path.join(PKG_ROOT, "libqasr.so")
+LIB_PATH = os.environ.get("QASR_LIB") or os.path.join(PKG_ROOT, "libqasr.so")   # QASR_LIB: A/B builds (tools)
 ENGINE_PATH = os.path.join(PKG_ROOT, "engine")
 REPO_ROOT = os.path.dirname(PKG_ROOT)
 VAD_ASSET = os.path.join(REPO_ROOT, "assets", "fireredvad_dfsmn.qvad")
@@ -106,6 +106,9 @@ SIGNATURES = {
     "qasr_audio_load_path": (C.c_int, [C.c_char_p, P, SZ, C.POINTER(SZ)]),
     "qasr_session_set_draft": (C.c_int, [P, I32]),
     "qasr_session_draft_stats": (C.c_int, [P, C.POINTER(C.c_int64)]),
+    "qasr_session_set_encoder_cache": (C.c_int, [P, I32]),
+    "qasr_session_encoder_cache_stats": (C.c_int, [P, C.POINTER(C.c_int64)]),
+    "qasr_session_audio_embeds": (C.c_int, [P, P, SZ, C.POINTER(SZ)]),
     "qasr_parse_transcript": (C.c_int, [C.c_char_p, SZ, C.c_char_p, SZ, C.POINTER(SZ), C.c_char_p, SZ,
                                         C.POINTER(SZ)]),
     "qasr_op_quant_rows": (C.c_int, [P, I32, I32, I32, P, P, P]),
@@ -117,6 +120,7 @@ SIGNATURES = {
     "qasr_op_interleave_gate_up": (C.c_int, [P, P, I32, I32, P]),
     "qasr_op_gemm_swiglu_q8": (C.c_int, [P, P, I32, P, P, I32, I32, P, P, P]),
     "qasr_op_gemm_swiglu_q8_cfg": (C.c_int, [P, P, I32, P, P, I32, I32, P, P, I32, P]),
+    "qasr_op_set_gemm_fixup": (C.c_int, [P, C.c_int64, P, I32]),
     "qasr_op_swiglu_q8_interleaved": (C.c_int, [P, I32, I32, P, P, P]),
     "qasr_op_gemv_fused": (C.c_int, [I32, P, I32, P, F32, I32, P, P, P, P, I32, I32, P, P, I32, I32, P, P, P]),
     "qasr_op_qk_norm_rope": (C.c_int, [P, I32, I32, I32, I32, P, P, P, P, P, F32, P, P, P, P]),

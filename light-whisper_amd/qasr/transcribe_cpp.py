@@ -211,6 +211,23 @@ class Session:
         check(_lib.load().qasr_session_draft_stats(self._h, st))
         return dict(zip(("passes", "proposed", "accepted", "tokens"), list(st)))
 
+    def set_encoder_cache(self, on: bool = True):
+        """streaming encoder cache: reuse the previous run's complete encoder windows when the samples extend it"""
+        check(_lib.load().qasr_session_set_encoder_cache(self._h, 1 if on else 0))
+
+    def encoder_cache_stats(self) -> dict:
+        st = (C.c_int64 * 3)()
+        check(_lib.load().qasr_session_encoder_cache_stats(self._h, st))
+        return dict(zip(("runs", "windows_reused", "windows_computed"), list(st)))
+
+    def audio_embeds(self) -> np.ndarray:
+        """the audio-embedding rows [tokens][hidden] of this session's last run"""
+        lib, n = _lib.load(), C.c_size_t(0)
+        check(lib.qasr_session_audio_embeds(self._h, None, 0, C.byref(n)))
+        out = np.empty(n.value, np.float32)
+        check(lib.qasr_session_audio_embeds(self._h, out.ctypes.data_as(C.c_void_p), n.value, C.byref(n)))
+        return out
+
     def forced_logits(self, audio, forced) -> np.ndarray:
         a = _f32(audio)
         f = np.ascontiguousarray(forced, dtype=np.int32)

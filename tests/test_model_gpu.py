@@ -509,3 +509,58 @@ def test_streaming_draft_forced_count(torch_dev, golden):
         drf.close()
     finally:
         m.close()
+
+
+def test_streaming_encoder_cache(torch_dev, golden):
+    """a growing interim window (same start, samples appended) reuses the embedding
+    rows of the previous run's complete 8-chunk encoder windows when its mel maximum is unchanged, and encodes only
+    the rest.  Cache runs use the row-count-independent GEMM order (StableOrderScope), so the result is bit-identical
+    to a full recompute (a fresh cache session's first run); against the default path (whose split-K / K-group
+    choices depend on the row count, and Q8 re-quantisation turns last-bit differences into ≈1e-2 element changes)
+    the embeddings agree within the encoder parity bound.  Greedy tokens equal up to a near-tie.  A moved start (the
+    sliding window) or a new maximum reuses nothing."""
+    from qasr.transcribe_cpp import Model
+
+    m = Model.synthetic(arch=None, seed=TINY_SEED, hparams=tiny_hparams())
+    H = TINY["txt_h"]
+    try:
+        ref, enc = m.session(kv_type="f16", n_ctx=2048), m.session(kv_type="f16", n_ctx=2048)
+        enc.set_encoder_cache(True)
+        audio = 0.5 * np.concatenate([golden["c__audio"], golden["b__audio"]]).astype(np.float32)
+        t = np.arange(4000, dtype=np.float32) / 16000
+        audio[8000:12000] += 0.9 * np.sin(2 * np.pi * 440 * t)   # the window's log-mel maximum, in its first second
+        louder = audio.copy()
+        louder[190000:194000] += 3.0 * np.sin(2 * np.pi * 440 * t)   # a new maximum near the end
+        cases = [(audio[:136000], 0), (audio[:160000], 1), (audio[:176000], 1), (audio[:176000], 1),
+                 (audio, 1), (louder, 0), (audio[16000:], 0)]
+        prev = None
+        for i, (w, reused) in enumerate(cases):
+            before = enc.encoder_cache_stats()["windows_reused"]
+            got = enc.run(w, max_new_tokens=24).tokens
+            assert enc.encoder_cache_stats()["windows_reused"] - before == reused, (i, enc.encoder_cache_stats())
+            e_got = enc.audio_embeds().reshape(-1, H)
+            fresh = m.session(kv_type="f16", n_ctx=2048)   # full recompute in the same (stable) order
+            fresh.set_encoder_cache(True)
+            fresh.run(w, max_new_tokens=1)
+            assert np.array_equal(e_got, fresh.audio_embeds().reshape(-1, H)), i
+            fresh.close()
+            if reused:
+                assert np.array_equal(e_got[:104 * reused], prev[:104 * reused])   # copied, not recomputed
+            prev = e_got
+            want = ref.run(w, max_new_tokens=24).tokens
+            e_ref = ref.audio_embeds().reshape(-1, H)
+            err = np.abs(e_got - e_ref).max() / np.abs(e_ref).max()
+            record(f"encoder_cache_case{i}", rel_err_vs_default_order=err)
+            assert err <= 3e-2, (i, err)
+            n = min(len(got), len(want))
+            div = next((k for k in range(n) if got[k] != want[k]), n)
+            if div < n or len(got) != len(want):
+                lg = ref.forced_logits(w, np.array(want[:max(div, 1)], np.int32))
+                top2 = np.sort(lg[div])[-2:]
+                assert top2[1] - top2[0] < 0.02 * np.abs(lg[div]).max(), f"case {i} diverges at {div} without a near-tie"
+        st = enc.encoder_cache_stats()
+        assert st["runs"] == len(cases) and st["windows_reused"] == 4, st
+        ref.close()
+        enc.close()
+    finally:
+        m.close()

@@ -652,3 +652,50 @@ def test_conv3x3_gelu(torch_dev, c, hi, wi, mode):
         got = got.reshape(n, wo, c, ho).transpose(0, 3, 1, 2).reshape(n * ho * wo, c)
     tol = (2e-3 if mode == 0 else 1e-4) * np.abs(ref).max() + 1e-3 * np.abs(ref)
     assert (np.abs(got - ref) <= tol).all(), np.abs(got - ref).max()
+
+
+@pytest.fixture
+def fixup(torch_dev):
+    """a registered split-K fix-up workspace (zeroed counters); unregistered afterwards"""
+    import torch
+
+    part = torch.empty(256 * 12288 * 8, dtype=torch.float32, device=torch_dev)
+    cnt = torch.zeros(8192, dtype=torch.int32, device=torch_dev)
+    _lib.check(L().qasr_op_set_gemm_fixup(ptr(part), part.numel() * 4, ptr(cnt), cnt.numel()))
+    yield cnt
+    _lib.check(L().qasr_op_set_gemm_fixup(None, 0, None, 0))
+
+
+# split-K through the fix-up workspace: decode-sized DMA tiles (≤ 64×64) × split counts
+FIXUP_PATHS = [16 + c + 32 * s for c in (6, 10, 12, 14, 15, 16, 17, 18, 19, 20, 21, 22) for s in (2, 3, 8)]
+
+
+@pytest.mark.parametrize("path", FIXUP_PATHS)
+@pytest.mark.parametrize("m,n,k", [(64, 128, 1024), (100, 192, 512), (32, 2048, 2048), (256, 4096, 2048)])
+def test_linear_q8_fixup_exact_integer(torch_dev, fixup, path, m, n, k):
+    y, ref = _linear_case(torch_dev, m, n, k, path, 0, seed=m + n, exact=True)
+    assert np.array_equal(y, ref)
+    assert not host(fixup).any()   # the last workgroup of every tile reset its counter
+
+
+@pytest.mark.parametrize("path", FIXUP_PATHS)
+@pytest.mark.parametrize("epi", [0, 1, 2])
+@pytest.mark.parametrize("m,n,k", [(37, 320, 2048), (24, 2048, 6144), (130, 1024, 1024)])
+def test_linear_q8_fixup_vs_oracle(torch_dev, fixup, path, epi, m, n, k):
+    """any epilogue on the summed tile (the residual and GELU are applied once, by the tile's last workgroup), and
+    the partial tiles are added in split order: repeats are bit-identical"""
+    y, ref = _linear_case(torch_dev, m, n, k, path, epi, seed=k + epi)
+    scale = np.abs(ref).max() + 1e-6
+    assert np.abs(y - ref).max() <= 2e-5 * scale * np.sqrt(k / 256)
+    for _ in range(2):
+        y2, _ = _linear_case(torch_dev, m, n, k, path, epi, seed=k + epi)
+        assert np.array_equal(y, y2)
+    assert not host(fixup).any()
+
+
+@pytest.mark.parametrize("cfg", [c + 32 * s for c in (12, 15, 20, 22) for s in (2, 4, 8)])
+@pytest.mark.parametrize("m,f,k", [(40, 512, 1024), (70, 512, 2048), (256, 1024, 2048)])
+def test_gemm_swiglu_q8_fixup(torch_dev, fixup, m, f, k, cfg):
+    """split-K gate-up GEMM: the SwiGLU + Q8 epilogue runs once per tile on the summed partials"""
+    test_gemm_swiglu_q8(torch_dev, m, f, k, cfg)
+    assert not host(fixup).any()

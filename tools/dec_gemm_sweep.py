@@ -24,7 +24,14 @@ def main():
     lib = _lib.load()
     dev = torch.device("cuda:0")
     result = {}
-    for tag, N, K, epi in SHAPES:
+    fix = os.environ.get("FIX", "1") == "1"   # split-K through the fix-up workspace (FIX=0: f32 atomics)
+    if fix:
+        part = torch.empty(256 * 12288 * 8, dtype=torch.float32, device=dev)
+        cnt = torch.zeros(8192, dtype=torch.int32, device=dev)
+        _lib.check(lib.qasr_op_set_gemm_fixup(part.data_ptr(), part.numel() * 4, cnt.data_ptr(), cnt.numel()))
+    shapes = [s for s in SHAPES if s[0] in os.environ.get("SHAPES", "qkv,o,down,gu").split(",")]
+    cfgs = [int(c) for c in os.environ["CFGS"].split(",")] if "CFGS" in os.environ else CFGS
+    for tag, N, K, epi in shapes:
         copies = max(2, int(768e6 // (N * K * 1.0625)) + 1)
         wq = [torch.randint(-127, 128, (N, K), dtype=torch.int8, device=dev) for _ in range(copies)]
         ws = [(torch.rand(N, K // 32, device=dev) * 0.01).half() for _ in range(copies)]
@@ -34,15 +41,15 @@ def main():
             y = torch.zeros(M, N, device=dev)
             hq = torch.empty(M, N // 2, dtype=torch.int8, device=dev)
             hd = torch.empty(M, N // 64, device=dev)
-            combos = [(-1, 0)] + ([(c, 0) for c in SWIGLU_CFGS] if epi == 3 else
-                                  [(c, s) for c in CFGS for s in (SPLITS if c < 24 else [0])])
+            combos = [(-1, 0)] + ([(c, s) for c in SWIGLU_CFGS for s in (SPLITS if fix and c < 24 else [0])]
+                                  if epi == 3 else [(c, s) for c in cfgs for s in (SPLITS if c < 24 else [0])])
             times = []
             for cfg, sp in combos:
                 def run(i):
                     if epi == 3:
                         _lib.check(lib.qasr_op_gemm_swiglu_q8_cfg(xq.data_ptr(), xd.data_ptr(), M, wq[i].data_ptr(),
                                                                   ws[i].data_ptr(), N, K, hq.data_ptr(), hd.data_ptr(),
-                                                                  cfg, None))
+                                                                  cfg + 32 * sp if cfg >= 0 else cfg, None))
                         return
                     path = 2 if cfg < 0 else 16 + cfg + 32 * sp
                     # a store GEMM with split-K clears y inside gemm_q8 (hipMemsetAsync): timed as part of it

@@ -93,13 +93,16 @@ def main():
                     help="continuous speech-like audio (no pauses): every window is ~12 s of speech the VAD keeps, "
                          "the full-load case (the default recording's pauses let the VAD trim windows)")
     ap.add_argument("--draft", type=int, default=1, help="QASR_STREAM_DRAFT (prompt-lookup drafts, 1 = default on)")
+    ap.add_argument("--enc-cache", type=int, default=1,
+                    help="QASR_STREAM_ENC_CACHE (encoder windows of growing interim windows reused, 1 = default on)")
     a = ap.parse_args()
     audio = (speech_like(np.random.default_rng(3), int(a.seconds * SR)) if a.speech_only else
              recording(a.seconds, seed=3))
     hot = [f"热词{i:03d}" for i in range(100)]
     with tempfile.TemporaryDirectory() as tmp:
         eng = Engine(a.engine, {"QASR_SYNTHETIC": "1", "QASR_FORCE_TOKENS_PER_S": "8", "HF_HUB_CACHE": tmp,
-                                "LIGHT_WHISPER_DATA_DIR": tmp, "QASR_STREAM_DRAFT": str(a.draft)})
+                                "LIGHT_WHISPER_DATA_DIR": tmp, "QASR_STREAM_DRAFT": str(a.draft),
+                                "QASR_STREAM_ENC_CACHE": str(a.enc_cache)})
         assert eng.init.get("success"), eng.init
         eng.request(transcribe_req(audio[: 2 * SR], hot))   # first-request warm-up (graphs, buffers)
         clock, interval, last, lat, inf, vad, sizes, speech = 0.0, I_BASE, 0, [], [], [], [], []
@@ -130,7 +133,7 @@ def main():
     out = {"workload": f"C3 streaming: {a.seconds:g} s " + ("continuous speech-like audio" if a.speech_only else
                                                                "recording (seed 3)")
                        + ", interim ticks (interim.rs policy), ≤12 s windows, 100 hot words, + final request",
-           "draft": bool(a.draft),
+           "draft": bool(a.draft), "encoder_cache": bool(a.enc_cache),
            "engine": a.engine, "weights": "synthetic (QASR_SYNTHETIC=1), 8 forced tokens/audio-s",
            "requests": int(lat.size), "mean_window_s": round(float(np.mean(sizes)), 2),
            "p50_ms": round(float(np.median(lat)), 2), "p95_ms": round(float(np.percentile(lat, 95)), 2),
@@ -142,7 +145,8 @@ def main():
                      "inference_ms": fin.get("inference_ms"), "vad_ms": fin.get("vad_ms"),
                      "speech_duration": fin.get("speech_duration"),
                      "rtf_inv": round(audio.size / SR / (fin_ms / 1e3), 1)},
-           "prompt_lookup": stats.get("stats", {}).get("prompt_lookup")}
+           "prompt_lookup": stats.get("stats", {}).get("prompt_lookup"),
+           "encoder_cache_stats": stats.get("stats", {}).get("encoder_cache")}
     print(json.dumps(out, ensure_ascii=False), flush=True)
 
 
