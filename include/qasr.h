@@ -133,11 +133,13 @@ QASR_API int qasr_session_set_context(qasr_session* s, const int32_t* ids, int32
 QASR_API int qasr_session_set_draft(qasr_session* s, int32_t on);
 QASR_API int qasr_session_draft_stats(const qasr_session* s, int64_t* stats /* [4] */);
 /* Streaming encoder cache: on = 1 makes a single-utterance run whose samples extend the previous
-   run's (bitwise: the interim loop's growing window, interim.rs:135-156) reuse the audio-embedding rows of the
-   previous run's complete 8-chunk attention windows (104 tokens each) when the window's log-mel maximum is unchanged
-   — the condition under which those rows are functions of the same samples (Whisper-style normalisation uses the
-   window's maximum; the conv stack is per 1 s chunk, the encoder attention per window) — and encodes only the rest.
-   Sliding windows (a start that moves) never qualify.  stats: runs, windows reused, windows encoded. */
+   run's (bitwise: the interim loop's growing window, interim.rs:135-156) and hold a complete 8-chunk attention
+   window run its encoder in a row-count-independent order, keep its complete windows' audio-embedding rows, and
+   reuse the previous run's (104 tokens each) when the window's log-mel maximum is unchanged — the condition under
+   which those rows are functions of the same samples (Whisper-style normalisation uses the window's maximum; the
+   conv stack is per 1 s chunk, the encoder attention per window) — encoding only the rest: bit-identical to a full
+   recompute in that order.  Other runs (a new utterance, a sliding window) are unaffected.  stats: growing runs,
+   windows reused, windows encoded by them. */
 QASR_API int qasr_session_set_encoder_cache(qasr_session* s, int32_t on);
 QASR_API int qasr_session_encoder_cache_stats(const qasr_session* s, int64_t* stats /* [3] */);
 /* The audio-embedding rows (projector output, [tokens][text hidden] f32) of the session's last run — a test /

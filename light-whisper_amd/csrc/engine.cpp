@@ -111,7 +111,8 @@ Scratch::~Scratch() {
 Session::Session(Model* m, int n_ctx) : m_(m), n_ctx_(n_ctx) {
     QASR_CHECK(n_ctx > 32, QASR_E_INVALID, "n_ctx too small");
     QASR_HIP(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking));
-    QASR_HIP(hipHostMalloc(&pin_cnt_, 256, hipHostMallocDefault));   // counters [0, 8), draft tokens [8, 24)
+    // counters [0, 8), draft tokens [8, 8 + kDraftRows), the encoder cache's mel-maximum read-back [60]
+    QASR_HIP(hipHostMalloc(&pin_cnt_, 256, hipHostMallocDefault));
     for (auto& e : step_ev_) QASR_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     rope_n_ = n_ctx;
     std::vector<float> tab((size_t)n_ctx * m->hp.head_dim);
@@ -249,9 +250,9 @@ void Session::front_end(const float* dpcm, const std::vector<int64_t>& off, cons
     // encoder rows are functions of the same samples); the conv stack and the encoder run on the remaining chunks
     fe.skip_tokens = 0;
     if (ec_run_) {
-        QASR_HIP(hipMemcpyAsync((unsigned*)pin_cnt_ + 32, d_umax, sizeof(unsigned), hipMemcpyDeviceToHost, st_));
+        QASR_HIP(hipMemcpyAsync((unsigned*)pin_cnt_ + 60, d_umax, sizeof(unsigned), hipMemcpyDeviceToHost, st_));
         QASR_HIP(hipStreamSynchronize(st_));
-        ec_umax_new_ = ((const unsigned*)pin_cnt_)[32];
+        ec_umax_new_ = ((const unsigned*)pin_cnt_)[60];
         // (ec_cand_ ≤ the windows the previous run stored; run_host marks them invalid while this run overwrites them)
         const int reuse = ec_umax_new_ == ec_umax_ && m_->precision_gen == ec_prec_ ? ec_cand_ : 0;
         const int per = h.n_window_infer / 100;   // chunks per attention window
@@ -419,8 +420,8 @@ void Session::decoder_layers(float* x, int rows, const int* d_pos, const int* d_
     const bool fuse_qk = !dense && !rows_share_kv && hd == 128 && (nh / nkv == 2 || nh / nkv == 4) &&
                          !getenv("QASR_NO_QK_FUSE");
     // GEMV row counts: the norms and the SwiGLU run inside the GEMVs' prologues (5 launches per layer, not 8)
-    const bool gv = !fused && dec_fuse_ && gemv_fused_ok(GV_RMS, rows, H) && gemv_fused_ok(GV_NONE, rows, F) &&
-                    gemv_fused_ok(GV_NONE, rows, QD);
+    const bool gv = rows <= gemv_layer_rows() && dec_fuse_ && gemv_fused_ok(GV_RMS, rows, H) &&
+                    gemv_fused_ok(GV_NONE, rows, F) && gemv_fused_ok(GV_NONE, rows, QD);
     int8_t* hq2 = gv ? (int8_t*)sc_.get(S_HQ, (size_t)rows * F) : nullptr;   // the SwiGLU epilogue's Q8 rows
     float* hd2 = gv ? (float*)sc_.get(S_HD, (size_t)rows * (F / QK) * sizeof(float)) : nullptr;
     for (int l = 0; l < h.txt_layers; l++) {
@@ -529,14 +530,15 @@ void Session::decode_step(const DecState& ds, int B, bool sizing) {
 // → lm_head → argmax → token ids to the pinned host words [8, 8 + B).  Capturable like decode_step.
 void Session::draft_step(int B) {
     const qasr_hparams& h = m_->hp;
-    int* tab = (int*)sc_.get(S_DTAB, (size_t)6 * 16 * sizeof(int));
-    float* x = (float*)sc_.get(S_X, (size_t)16 * h.txt_h * sizeof(float));
+    constexpr int R = kDraftRows;
+    int* tab = (int*)sc_.get(S_DTAB, (size_t)6 * R * sizeof(int));
+    float* x = (float*)sc_.get(S_X, (size_t)R * h.txt_h * sizeof(float));
     embed_rows(tab, B, m_->tok_embd, nullptr, x, st_);
-    decoder_layers(x, B, tab + 16, tab + 32, tab + 48, tab + 64, 0, /*dense=*/false, /*rows_share_kv=*/B > 1);
-    float* logits = (float*)sc_.get(S_LOGITS, (size_t)16 * h.vocab * sizeof(float));
+    decoder_layers(x, B, tab + R, tab + 2 * R, tab + 3 * R, tab + 4 * R, 0, /*dense=*/false, /*rows_share_kv=*/B > 1);
+    float* logits = (float*)sc_.get(S_LOGITS, (size_t)R * h.vocab * sizeof(float));
     lm_head_rows(x, B, h.txt_h, logits);
-    int* d_tok = (int*)sc_.get(S_TOK, (size_t)16 * sizeof(int));
-    argmax_rows(logits, B, h.vocab, d_tok, st_, sc_.get(S_ARGP, argmax_scratch_bytes(16)));
+    int* d_tok = (int*)sc_.get(S_TOK, (size_t)R * sizeof(int));
+    argmax_rows(logits, B, h.vocab, d_tok, st_, sc_.get(S_ARGP, argmax_scratch_bytes(R)));
     QASR_HIP(hipMemcpyAsync((int*)pin_cnt_ + 8, d_tok, (size_t)B * sizeof(int), hipMemcpyDeviceToHost, st_));
 }
 
@@ -550,7 +552,7 @@ void Session::draft_step(int B) {
 void Session::draft_decode(int n_prompt, int base, int budget, int dummy, std::vector<int32_t>& toks, bool& eos,
                            bool forced) {
     const qasr_hparams& h = m_->hp;
-    constexpr int RMAX = 16;
+    constexpr int RMAX = kDraftRows;
     int max_draft = RMAX - 1;
     int* tab = (int*)sc_.get(S_DTAB, (size_t)6 * RMAX * sizeof(int));
     int* hb = (int*)pinned((size_t)6 * RMAX * sizeof(int));
@@ -596,16 +598,16 @@ void Session::draft_decode(int n_prompt, int base, int budget, int dummy, std::v
         const int pos = n_prompt + (int)toks.size() - 1;   // position of the last accepted token
         lookup(draft, std::min(max_draft, budget - (int)toks.size() - 1));
         const int R = 1 + (int)draft.size();
-        const int B = R <= 1 ? 1 : R <= 2 ? 2 : R <= 4 ? 4 : R <= 8 ? 8 : 16;
+        const int B = R <= 1 ? 1 : R <= 2 ? 2 : R <= 4 ? 4 : R <= 8 ? 8 : R <= 16 ? 16 : 32;
         for (int i = 0; i < B; i++) {
             const bool real = i < R;
             hb[i] = real ? (i == 0 ? toks.back() : draft[i - 1]) : 0;
-            hb[16 + i] = real ? pos + i : 0;
-            hb[32 + i] = real ? base + pos + i : dummy;
-            hb[48 + i] = real ? base : dummy;
-            hb[64 + i] = real ? pos + i + 1 : 1;
+            hb[RMAX + i] = real ? pos + i : 0;
+            hb[2 * RMAX + i] = real ? base + pos + i : dummy;
+            hb[3 * RMAX + i] = real ? base : dummy;
+            hb[4 * RMAX + i] = real ? pos + i + 1 : 1;
         }
-        QASR_HIP(hipMemcpyAsync(tab, hb, (size_t)80 * sizeof(int), hipMemcpyHostToDevice, st_));
+        QASR_HIP(hipMemcpyAsync(tab, hb, (size_t)5 * RMAX * sizeof(int), hipMemcpyHostToDevice, st_));
         auto it = draft_graphs_.find(B);
         if (graphs && it != draft_graphs_.end()) {
             QASR_HIP(hipGraphLaunch(it->second, st_));
@@ -928,27 +930,35 @@ void Session::run_host(const std::vector<const float*>& pcm, const std::vector<i
     float* d = (float*)sc_.get(S_PCM, (size_t)std::max<int64_t>(total, 1) * sizeof(float));
     for (size_t i = 0; i < len.size(); i++)
         QASR_HIP(hipMemcpyAsync(d + off[i], pcm[i], (size_t)len[i] * sizeof(float), hipMemcpyHostToDevice, st_));
-    ec_run_ = enc_cache_ && len.size() == 1;
+    // encoder cache: only a window that GROWS the previous one (the previous samples are its prefix — the app's
+    // interim window before it reaches 12 s) and holds a complete encoder window runs in the fixed order, stores its
+    // windows and may reuse the previous run's; any other run (a new utterance, a sliding window) keeps the faster
+    // row-count-dependent GEMM choices and clears the cache
+    const bool single = enc_cache_ && len.size() == 1;
+    ec_run_ = false;
     ec_cand_ = 0;
-    if (ec_run_ && ec_windows_ > 0) {
-        // windows whose chunks' frames all lie in the samples this run shares with the previous one (bitwise)
+    if (single) {
         const int64_t m = std::min<int64_t>(len[0], (int64_t)ec_pcm_.size());
         int64_t L = 0;
         const size_t B = 4096;
         while (L + (int64_t)B <= m && !memcmp(pcm[0] + L, ec_pcm_.data() + L, B * sizeof(float))) L += B;
         while (L < m && !memcmp(pcm[0] + L, ec_pcm_.data() + L, sizeof(float))) L++;
         const int per = m_->hp.n_window_infer / 100;
-        while (ec_cand_ < ec_windows_ && 16000LL * (per * (ec_cand_ + 1) - 1) + 16040 <= L) ec_cand_++;
+        const auto frames_in = [&](int w, int64_t n) { return 16000LL * (per * w - 1) + 16040 <= n; };
+        ec_run_ = !ec_pcm_.empty() && L == (int64_t)ec_pcm_.size() && frames_in(1, len[0]);
+        // windows whose chunks' frames all lie in the samples this run shares with the previous one (bitwise)
+        while (ec_run_ && ec_cand_ < ec_windows_ && frames_in(ec_cand_ + 1, L)) ec_cand_++;
+        ec_windows_ = 0;   // invalid until this run stores its own (an exception or a non-growing run leaves it empty)
     }
-    if (ec_run_) ec_windows_ = 0;   // invalid until this run stores its own (an exception leaves it empty)
     try {
         run_batch(d, off, len, max_new, force_tps, out, times);
     } catch (...) {
         ec_run_ = false;
         ec_windows_ = 0;
+        ec_pcm_.clear();
         throw;
     }
-    if (ec_run_) ec_pcm_.assign(pcm[0], pcm[0] + len[0]);
+    if (single) ec_pcm_.assign(pcm[0], pcm[0] + len[0]);
     ec_run_ = false;
 }
 

@@ -166,6 +166,8 @@ class Session {
     int ucap_ = 0;
 };
 int row_bucket(int m);
+// rows of a draft verify pass at most (the last accepted token + up to kDraftRows − 1 proposed tokens)
+constexpr int kDraftRows = 32;
 
 // the chat prompt of one utterance (processing_qwen3_asr.py:534-553, empty system prompt); audio
 // placeholders are returned as -(audio_row + 1)

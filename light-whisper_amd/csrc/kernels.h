@@ -29,9 +29,13 @@ void linear_q8(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const f
 // rows up to which linear_q8 streams weights with the GEMV kernel; more rows take the MFMA GEMM and its fused
 // epilogues (tools/gemv_tune.py: at 8 rows the GEMM is faster on every decoder shape, at 4 the GEMV mostly is)
 constexpr int kGemvRows = 4;
+// rows up to which the decoder layer runs on the fused weight-streaming GEMVs (gemv_fused: norm prologue, SwiGLU
+// epilogue, 5 launches per layer) instead of the MFMA GEMMs (QASR_GV_ROWS overrides, for A/B timing)
+constexpr int kGemvWideRows = 8;
+int gemv_layer_rows();
 void gemv_q8(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const float* bias, const float* res, float* y,
              int ldy, int epi, hipStream_t s, int cols = 0);
-// the 1–4-row decoder GEMVs, about one workgroup per CU, with the row operations around them fused (bit-identical to
+// the 1–8-row decoder GEMVs, about one workgroup per CU, with the row operations around them fused (bit-identical to
 // the separate rmsnorm_q8 / gemv_q8 / swiglu_q8 launches): pro GV_RMS: activations = Q8(RMSNorm(src rows, stride
 // ld_src floats)·nw), K ≤ 4096; GV_NONE: the Q8 rows xq / xd, K ≤ 6144.  epi EPI_STORE / EPI_RESID into y, or
 // EPI_SWIGLU (GV_RMS only; W = interleaved gate/up, N % 64 == 0): h = Q8(silu(g)·u) into yq [M][N/2] / yd [M][N/64].

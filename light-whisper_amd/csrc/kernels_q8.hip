@@ -432,8 +432,14 @@ static void gv_mr(int pro, bool swi, int cpw, int T, const GvArgs& a, hipStream_
     }
 }
 
+int gemv_layer_rows() {
+    static const int r = getenv("QASR_GV_ROWS") ? std::max(1, std::min(kGemvWideRows, atoi(getenv("QASR_GV_ROWS"))))
+                                                 : kGemvWideRows;
+    return r;
+}
+
 bool gemv_fused_ok(int pro, int M, int K) {
-    if (M < 1 || M > kGemvRows || K % QK != 0 || K < QK) return false;
+    if (M < 1 || M > kGemvWideRows || K % QK != 0 || K < QK) return false;
     return pro == GV_RMS ? K <= 4096 : K <= 6144;
 }
 
@@ -456,7 +462,8 @@ void gemv_fused(int pro, const int8_t* xq, const float* xd, const float* src, in
     const GvArgs a{&W, M, xq, xd, src, ld_src, nw, eps, res, y, ldy, epi, yq, yd};
     if (M <= 1) gv_mr<1>(pro, swi, cpw, T, a, s);
     else if (M <= 2) gv_mr<2>(pro, swi, cpw, T, a, s);
-    else gv_mr<4>(pro, swi, cpw, T, a, s);
+    else if (M <= 4) gv_mr<4>(pro, swi, cpw, T, a, s);
+    else gv_mr<8>(pro, swi, cpw, T, a, s);
 }
 
 static std::atomic<int> g_det{0};

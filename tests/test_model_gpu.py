@@ -512,13 +512,13 @@ def test_streaming_draft_forced_count(torch_dev, golden):
 
 
 def test_streaming_encoder_cache(torch_dev, golden):
-    """a growing interim window (same start, samples appended) reuses the embedding
-    rows of the previous run's complete 8-chunk encoder windows when its mel maximum is unchanged, and encodes only
-    the rest.  Cache runs use the row-count-independent GEMM order (StableOrderScope), so the result is bit-identical
-    to a full recompute (a fresh cache session's first run); against the default path (whose split-K / K-group
-    choices depend on the row count, and Q8 re-quantisation turns last-bit differences into ≈1e-2 element changes)
-    the embeddings agree within the encoder parity bound.  Greedy tokens equal up to a near-tie.  A moved start (the
-    sliding window) or a new maximum reuses nothing."""
+    """a growing interim window (the previous request's samples are its prefix) with a
+    complete encoder window runs in the row-count-independent GEMM order, stores the embedding rows of its complete
+    8-chunk windows and reuses the previous run's when its mel maximum is unchanged, encoding only the rest.  The
+    reused result is bit-identical to a full recompute in the same order (a fresh session whose run also grows a
+    prefix, reusing nothing); against the default order (split-K / K-group choices depend on the row count, and Q8
+    re-quantisation turns last-bit differences into ≈1e-2 element changes) it agrees within the encoder parity
+    bound.  Greedy tokens equal up to a near-tie.  A first run, a new maximum or a moved start reuses nothing."""
     from qasr.transcribe_cpp import Model
 
     m = Model.synthetic(arch=None, seed=TINY_SEED, hparams=tiny_hparams())
@@ -531,21 +531,24 @@ def test_streaming_encoder_cache(torch_dev, golden):
         audio[8000:12000] += 0.9 * np.sin(2 * np.pi * 440 * t)   # the window's log-mel maximum, in its first second
         louder = audio.copy()
         louder[190000:194000] += 3.0 * np.sin(2 * np.pi * 440 * t)   # a new maximum near the end
-        cases = [(audio[:136000], 0), (audio[:160000], 1), (audio[:176000], 1), (audio[:176000], 1),
-                 (audio, 1), (louder, 0), (audio[16000:], 0)]
+        # (window, windows reused): the first run and its growth to 8.5 s store; then reuse while it grows
+        cases = [(audio[:130000], 0), (audio[:136000], 0), (audio[:160000], 1), (audio[:176000], 1),
+                 (audio[:176000], 1), (audio, 1), (louder, 0), (audio[16000:], 0)]
         prev = None
         for i, (w, reused) in enumerate(cases):
             before = enc.encoder_cache_stats()["windows_reused"]
             got = enc.run(w, max_new_tokens=24).tokens
             assert enc.encoder_cache_stats()["windows_reused"] - before == reused, (i, enc.encoder_cache_stats())
             e_got = enc.audio_embeds().reshape(-1, H)
-            fresh = m.session(kv_type="f16", n_ctx=2048)   # full recompute in the same (stable) order
-            fresh.set_encoder_cache(True)
-            fresh.run(w, max_new_tokens=1)
-            assert np.array_equal(e_got, fresh.audio_embeds().reshape(-1, H)), i
-            fresh.close()
             if reused:
                 assert np.array_equal(e_got[:104 * reused], prev[:104 * reused])   # copied, not recomputed
+                fresh = m.session(kv_type="f16", n_ctx=2048)   # full recompute in the same (fixed) order
+                fresh.set_encoder_cache(True)
+                fresh.run(w[:16000], max_new_tokens=1)
+                fresh.run(w, max_new_tokens=1)
+                assert fresh.encoder_cache_stats()["windows_reused"] == 0
+                assert np.array_equal(e_got, fresh.audio_embeds().reshape(-1, H)), i
+                fresh.close()
             prev = e_got
             want = ref.run(w, max_new_tokens=24).tokens
             e_ref = ref.audio_embeds().reshape(-1, H)
@@ -559,7 +562,7 @@ def test_streaming_encoder_cache(torch_dev, golden):
                 top2 = np.sort(lg[div])[-2:]
                 assert top2[1] - top2[0] < 0.02 * np.abs(lg[div]).max(), f"case {i} diverges at {div} without a near-tie"
         st = enc.encoder_cache_stats()
-        assert st["runs"] == len(cases) and st["windows_reused"] == 4, st
+        assert st["runs"] == 5 and st["windows_reused"] == 4, st   # runs = the growing runs (fixed order)
         ref.close()
         enc.close()
     finally:

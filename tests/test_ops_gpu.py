@@ -289,7 +289,7 @@ def _q8_weights(torch_dev, n, k, seed):
 
 @pytest.mark.parametrize("m,n,k,epi", [(1, 4096, 2048, 0), (1, 2048, 1024, 1), (2, 12288, 2048, 0),
                                        (4, 6144, 1024, 1), (1, 40000, 1024, 0), (3, 512, 4096, 0),
-                                       (1, 384, 256, 1), (2, 100, 896, 0)])
+                                       (1, 384, 256, 1), (2, 100, 896, 0), (8, 4096, 2048, 0), (6, 2048, 1024, 1)])
 def test_gemv_fused_rms(torch_dev, m, n, k, epi):
     """norm-in-prologue GEMV == rmsnorm_q8 then the GEMV, bit for bit (the decode fusion's parity contract)"""
     import torch
@@ -310,7 +310,7 @@ def test_gemv_fused_rms(torch_dev, m, n, k, epi):
     assert np.array_equal(host(y0), host(y1))
 
 
-@pytest.mark.parametrize("m,n,k,epi", [(1, 2048, 6144, 1), (4, 1024, 3072, 1), (1, 2048, 2048, 1), (2, 1024, 2048, 0),
+@pytest.mark.parametrize("m,n,k,epi", [(1, 2048, 6144, 1), (8, 2048, 6144, 1), (7, 2048, 2048, 0), (4, 1024, 3072, 1), (1, 2048, 2048, 1), (2, 1024, 2048, 0),
                                        (3, 4096, 5120, 1), (1, 300, 96, 0)])
 def test_gemv_fused_q8_rows(torch_dev, m, n, k, epi):
     """the per-CU GEMV on given Q8 rows (O / down projections) == gemv_q8, bit for bit"""
@@ -329,7 +329,8 @@ def test_gemv_fused_q8_rows(torch_dev, m, n, k, epi):
     assert np.array_equal(host(y0), host(y1))
 
 
-@pytest.mark.parametrize("m,f,k", [(1, 6144, 2048), (4, 3072, 1024), (2, 256, 256), (3, 512, 4096)])
+@pytest.mark.parametrize("m,f,k", [(1, 6144, 2048), (4, 3072, 1024), (2, 256, 256), (3, 512, 4096), (8, 6144, 2048),
+                                   (5, 3072, 1024)])
 def test_gemv_fused_swiglu(torch_dev, m, f, k):
     """norm + interleaved gate/up GEMV + SwiGLU + Q8 in one launch == rmsnorm_q8, the GEMV into f32 gate/up rows and
     swiglu_q8 (interleaved), bit for bit"""
@@ -359,7 +360,7 @@ def test_gemv_fused_rejects_bad_shapes(torch_dev):
 
     x = empty((8, 8192), torch.float32, torch_dev)
     y = empty((8, 64), torch.float32, torch_dev)
-    for pro, m, k, epi in ((1, 5, 1024, 0), (1, 1, 8192, 0), (0, 1, 8192, 0), (3, 1, 1024, 0), (1, 1, 100, 0),
+    for pro, m, k, epi in ((1, 9, 1024, 0), (1, 1, 8192, 0), (0, 1, 8192, 0), (3, 1, 1024, 0), (1, 1, 100, 0),
                            (0, 1, 1024, 3)):
         with pytest.raises(_lib.QasrError):
             _lib.check(L().qasr_op_gemv_fused(pro, ptr(x), 2 * k, ptr(x), 1e-6, m, ptr(x), ptr(x), ptr(x), ptr(x), 64,
