@@ -18,3 +18,5 @@ echo "bench done" >> $out/${tag}_progress.log
 timeout -k 10 300 python3 -u tools/stream_bench.py --speech-only --draft 1 > $out/${tag}_c3_draft.json 2> $out/${tag}_c3_draft.err || exit 1
 timeout -k 10 300 python3 -u tools/stream_bench.py --speech-only --draft 0 > $out/${tag}_c3_nodraft.json 2> $out/${tag}_c3_nodraft.err || exit 1
 echo "c3 done" >> $out/${tag}_progress.log
+timeout -k 10 300 python3 -u tools/latency.py > $out/${tag}_latency.jsonl 2> $out/${tag}_latency.err || exit 1
+echo "c2 done" >> $out/${tag}_progress.log
