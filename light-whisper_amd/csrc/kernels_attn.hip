@@ -67,7 +67,7 @@ __device__ __forceinline__ float qk_dot16(const h2v* qh, int4 a, int4 b) {
     return part;
 }
 
-template <int HD, int G, int NW, bool FUSED = false, int CK = 64, bool VE = false>
+template <int HD, int G, int NW, bool FUSED = false, int CK = 64>
 __global__ __launch_bounds__(256) void k_attention(const __half* __restrict__ Q, int ldq, const __half* K,
                                                    const __half* V, int ldkv,
                                                    const int* __restrict__ kv_start, const int* __restrict__ kv_len,
@@ -195,10 +195,6 @@ __global__ __launch_bounds__(256) void k_attention(const __half* __restrict__ Q,
                 ka[u] = *(const int4*)(kc + (size_t)j * ldkv);
                 kb[u] = *(const int4*)(kc + (size_t)j * ldkv + 8);
             }
-            if constexpr (VE) {   // V in flight with K (one round trip per chunk, K and V live together)
-#pragma unroll
-                for (int u = 0; u < VU4; u++) vr[u] = *(const int4*)(vc + (size_t)min(4 * u + vg, n - 1) * ldkv);
-            }
 #pragma unroll
             for (int u = 0; u < KU8; u++) {
                 const int j = 8 * u + kk;
@@ -209,13 +205,13 @@ __global__ __launch_bounds__(256) void k_attention(const __half* __restrict__ Q,
                 }
             }
             wave_sync_lds();
-            // the V loads fly while the softmax runs (issued after the scores so K and V are never live together)
-            if constexpr (!VE) {
+            // the V loads fly while the softmax runs (issued after the scores so K and V are never live together:
+            // issuing them with K costs the 32-key kernel its 4th wave per SIMD, 31.9 → 33.8 µs at 256 rows,
+            // profiles/r2s2_attn_v_early_ab.jsonl)
 #pragma unroll
-                for (int u = 0; u < VU4; u++) {
-                    const int j = min(4 * u + vg, n - 1);   // rows past n: weight p = 0
-                    vr[u] = *(const int4*)(vc + (size_t)j * ldkv);
-                }
+            for (int u = 0; u < VU4; u++) {
+                const int j = min(4 * u + vg, n - 1);   // rows past n: weight p = 0
+                vr[u] = *(const int4*)(vc + (size_t)j * ldkv);
             }
 #pragma unroll
             for (int g = 0; g < G; g++) {
@@ -782,11 +778,7 @@ void attention_decode_fused(const QkFuse& fz, int ldkv, const int* kv_start, con
     // (tools/attn_batch.py, profiles/r2_attn_batch_chunk.jsonl: 256 rows 35.9 → 31.2 µs); fewer rows → the 64-key
     // kernel, which still runs its ≤ 32-key waves in 32-key chunks (1 key 6.35 → 5.37 µs)
     const bool ck32 = rows >= 192;
-    static const bool ve = getenv("QASR_ATTN_VE") && *getenv("QASR_ATTN_VE") == '1';   // A/B: V loads with K
-    if (G == 2 && ck32 && ve)
-        k_attention<128, 2, 4, true, 32, true><<<b4, 256, 0, s>>>(nullptr, 0, fz.kc, fz.vc, ldkv, kv_start, kv_len, rows,
-                                                                  nh, nkv, scale, nullptr, oq, od, fz);
-    else if (G == 2 && ck32)
+    if (G == 2 && ck32)
         k_attention<128, 2, 4, true, 32><<<b4, 256, 0, s>>>(nullptr, 0, fz.kc, fz.vc, ldkv, kv_start, kv_len, rows, nh,
                                                             nkv, scale, nullptr, oq, od, fz);
     else if (G == 2)
