@@ -249,9 +249,14 @@ QASR_API int qasr_op_gemm_swiglu_q8_cfg(const int8_t* xq, const float* xd, int32
    partial tiles and ncnt device uint32 arrival counters, ZEROED by the caller (the kernels leave them zero).  With
    it, every split-K GEMM stores partial tiles and the tile's last workgroup adds them in split order and runs the
    full epilogue (deterministic, any epilogue); without it (part = NULL) split-K adds with f32 atomics.  Sessions
-   register their own for the decode steps (used there for the SwiGLU epilogue and in deterministic mode).  Not in
+   register their own for the decode steps (used there for the SwiGLU epilogue).  Not in
    the reference (an engine-internal tuning / test hook). */
 QASR_API int qasr_op_set_gemm_fixup(void* part, int64_t part_bytes, void* cnt, int32_t ncnt);
+/* Rows (0..64) up to which the Q8 GEMM's automatic choice streams the weights straight into the matrix core's operand
+   registers (k_gemm_q8_ws: decode rows, every weight byte read once, no LDS staging); 0 = never.  all_shapes = 0: only
+   on the wide decoder matrices where it is faster (QKV, gate/up); 1: every shape it supports (tests).  Process-wide;
+   default 16 rows (QASR_WS_ROWS).  Tuning / A/B hook, not in the reference. */
+QASR_API int qasr_op_set_gemm_ws_rows(int32_t rows, int32_t all_shapes);
 /* Q8 GEMM with a fused output epilogue (M > 8, the MFMA path): epi 4 = erf-GELU(acc + bias) quantised to Q8 rows
    (yq [M][N] int8, yd [M][N/32] f32 block scales; y unused), epi 5 = f16(acc + bias) into y (__half, row stride
    ldy).  cfg: GEMM configuration (-1 = heuristic). */

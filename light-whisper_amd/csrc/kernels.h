@@ -44,7 +44,7 @@ bool gemv_fused_ok(int pro, int M, int K);
 void gemv_fused(int pro, const int8_t* xq, const float* xd, const float* src, int ld_src, const float* nw, float eps,
                 int M, const Q8Mat& W, const float* res, float* y, int ldy, int epi, int8_t* yq, float* yd,
                 hipStream_t s);
-// deterministic mode (process-wide): GEMMs never split K over workgroups (split-K sums land by float atomics, whose
+// deterministic mode (process-wide): GEMMs never split K with float atomics (split-K sums landing by atomics, whose
 // order varies run to run); deterministic_gen() changes on every switch so captured step graphs are re-captured
 void set_deterministic(bool on);
 bool deterministic();
@@ -76,8 +76,11 @@ void gemm_mx(const uint8_t* x8, const uint8_t* xs, int M, const Q8Mat& W, const 
 void set_mx_workspace(void* p, size_t bytes);
 // split-K fix-up workspace for gemm_q8 (thread-local): `floats` partial-tile floats and `ncnt` arrival counters that
 // are zero between launches (the kernels keep them so); nullptr = split-K adds with f32 atomics.  The fix-up serves
-// the SwiGLU epilogue and deterministic mode, or every split epilogue with all_epilogues (op-level tests / tuning).
+// the SwiGLU epilogue (deterministic), or every split epilogue with all_epilogues (op-level tests / tuning).
 void set_gemm_fixup(float* part, size_t floats, unsigned* cnt, int ncnt, bool all_epilogues = false);
+// rows up to which gemm_q8's automatic choice takes the weight-streaming kernel (≤ 64; 0 = never); all_shapes: on
+// every shape it supports, not only the wide decoder matrices where it is faster (tests)
+void set_gemm_ws_rows(int rows, bool all_shapes = false);
 constexpr int kFixSplits = 8, kFixCounters = 8192;
 struct FixupScope {   // registers a fix-up workspace for the calls in its scope, unregisters on exit (throws included)
     FixupScope(float* part, size_t floats, unsigned* cnt, int ncnt) { set_gemm_fixup(part, floats, cnt, ncnt); }

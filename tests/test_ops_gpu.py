@@ -667,8 +667,8 @@ def fixup(torch_dev):
     _lib.check(L().qasr_op_set_gemm_fixup(None, 0, None, 0))
 
 
-# split-K through the fix-up workspace: decode-sized DMA tiles (≤ 64×64) × split counts
-FIXUP_PATHS = [16 + c + 32 * s for c in (6, 10, 12, 14, 15, 16, 17, 18, 19, 20, 21, 22) for s in (2, 3, 8)]
+# split-K through the fix-up workspace: the decode tiles with 64-column wave tiles (≤ 64×64) × split counts
+FIXUP_PATHS = [16 + c + 32 * s for c in (12, 15, 20, 22, 23) for s in (2, 3, 8)]
 
 
 @pytest.mark.parametrize("path", FIXUP_PATHS)
@@ -700,3 +700,43 @@ def test_gemm_swiglu_q8_fixup(torch_dev, fixup, m, f, k, cfg):
     """split-K gate-up GEMM: the SwiGLU + Q8 epilogue runs once per tile on the summed partials"""
     test_gemm_swiglu_q8(torch_dev, m, f, k, cfg)
     assert not host(fixup).any()
+
+
+@pytest.fixture
+def ws_all():
+    """the weight-streaming kernel on every shape it supports up to 64 rows (restored to the default afterwards)"""
+    _lib.check(L().qasr_op_set_gemm_ws_rows(64, 1))
+    yield
+    _lib.check(L().qasr_op_set_gemm_ws_rows(16, 0))
+
+
+# the decoder's shapes at decode row counts (1.7B / 0.6B widths): QKV store, O / down residual, K = 6,144
+@pytest.mark.parametrize("m", [5, 9, 16, 31, 33, 48, 64])
+@pytest.mark.parametrize("n,k,epi", [(4096, 2048, 0), (2048, 2048, 1), (2048, 6144, 1), (1024, 3072, 1), (384, 1024, 0)])
+def test_linear_q8_weight_stream(torch_dev, ws_all, m, n, k, epi):
+    """k_gemm_q8_ws (rows ≤ 64: weights straight into the MFMA operands, two zero-masked 16x16x64 MFMAs per two Q8
+    blocks) against the oracle, on the automatic path (path 2)"""
+    y, ref = _linear_case(torch_dev, m, n, k, 2, epi, seed=m + n + k)
+    scale = np.abs(ref).max() + 1e-6
+    assert np.abs(y - ref).max() <= 2e-5 * scale * np.sqrt(k / 256)
+    ye, refe = _linear_case(torch_dev, m, n, k, 2, 0, seed=m + k, exact=True)
+    assert np.array_equal(ye, refe)
+
+
+@pytest.mark.parametrize("m", [9, 16, 33, 64])
+@pytest.mark.parametrize("f,k", [(6144, 2048), (3072, 1024), (512, 1024)])
+def test_gemm_swiglu_q8_weight_stream(torch_dev, ws_all, m, f, k):
+    """the weight-streaming kernel's SwiGLU + Q8 epilogue (four 16-column groups = one 32-wide h block)"""
+    test_gemm_swiglu_q8(torch_dev, m, f, k, -1)
+
+
+def test_linear_q8_weight_stream_vs_gemm(torch_dev):
+    """the same decode GEMM with and without the weight-streaming kernel: equal up to f32 summation order"""
+    m, n, k = 16, 4096, 2048
+    y1, _ = _linear_case(torch_dev, m, n, k, 2, 0, seed=3)   # default: the weight stream at ≤ 16 rows
+    _lib.check(L().qasr_op_set_gemm_ws_rows(0, 0))
+    try:
+        y0, _ = _linear_case(torch_dev, m, n, k, 2, 0, seed=3)
+    finally:
+        _lib.check(L().qasr_op_set_gemm_ws_rows(16, 0))
+    assert np.abs(y1 - y0).max() <= 1e-5 * np.abs(y0).max()
