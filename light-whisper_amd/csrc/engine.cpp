@@ -945,7 +945,8 @@ void Session::run_host(const std::vector<const float*>& pcm, const std::vector<i
         while (L < m && !memcmp(pcm[0] + L, ec_pcm_.data() + L, sizeof(float))) L++;
         const int per = m_->hp.n_window_infer / 100;
         const auto frames_in = [&](int w, int64_t n) { return 16000LL * (per * w - 1) + 16040 <= n; };
-        ec_run_ = !ec_pcm_.empty() && L == (int64_t)ec_pcm_.size() && frames_in(1, len[0]);
+        // (Q8 precision only: the MXFP8 GEMMs have no row-count-independent order)
+        ec_run_ = !m_->mx() && !ec_pcm_.empty() && L == (int64_t)ec_pcm_.size() && frames_in(1, len[0]);
         // windows whose chunks' frames all lie in the samples this run shares with the previous one (bitwise)
         while (ec_run_ && ec_cand_ < ec_windows_ && frames_in(ec_cand_ + 1, L)) ec_cand_++;
         ec_windows_ = 0;   // invalid until this run stores its own (an exception or a non-growing run leaves it empty)
