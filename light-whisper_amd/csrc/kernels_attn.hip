@@ -778,6 +778,8 @@ void attention_decode_fused(const QkFuse& fz, int ldkv, const int* kv_start, con
     // (tools/attn_batch.py, profiles/r2_attn_batch_chunk.jsonl: 256 rows 35.9 → 31.2 µs); fewer rows → the 64-key
     // kernel, which still runs its ≤ 32-key waves in 32-key chunks (1 key 6.35 → 5.37 µs)
     const bool ck32 = rows >= 192;
+    // (a 5-waves-per-SIMD build of the 32-key kernel, 95 VGPRs, streamed the same: 31.1 against 31.5 µs at 256
+    // rows, profiles/r2s2_attn_occupancy_ab.jsonl — the kernel is not occupancy-bound)
     if (G == 2 && ck32)
         k_attention<128, 2, 4, true, 32><<<b4, 256, 0, s>>>(nullptr, 0, fz.kc, fz.vc, ldkv, kv_start, kv_len, rows, nh,
                                                             nkv, scale, nullptr, oq, od, fz);
