@@ -567,3 +567,43 @@ def test_streaming_encoder_cache(torch_dev, golden):
         enc.close()
     finally:
         m.close()
+
+
+def test_concurrent_sessions_match_sequential(torch_dev, golden):
+    """bench.py --streams: sessions of one model decoding on their own streams from concurrent host threads give the
+    tokens each gives alone (deterministic mode: no split-K atomics, so the comparison is exact)"""
+    import threading
+
+    from qasr import _lib
+    from qasr.transcribe_cpp import Model
+
+    m = Model.synthetic(arch=None, seed=TINY_SEED, hparams=tiny_hparams())
+    _lib.check(_lib.load().qasr_set_deterministic(1))
+    try:
+        rng = np.random.default_rng(9)
+        base = [golden["a__audio"], golden["b__audio"], golden["c__audio"]]
+        groups = [[b[: int(rng.integers(b.size // 2, b.size + 1))] for b in (base[(i + g) % 3] for i in range(12))]
+                  for g in range(3)]
+        sessions = [m.session(kv_type="f16", n_ctx=2048) for _ in groups]
+        alone = [[r.tokens for r in s.run_batch(a, force_tokens_per_s=8)] for s, a in zip(sessions, groups)]
+        for _ in range(2):
+            out, errs = [None] * len(groups), []
+
+            def work(g):
+                try:
+                    out[g] = [r.tokens for r in sessions[g].run_batch(groups[g], force_tokens_per_s=8)]
+                except Exception as e:
+                    errs.append(e)
+
+            th = [threading.Thread(target=work, args=(g,)) for g in range(len(groups))]
+            for t in th:
+                t.start()
+            for t in th:
+                t.join()
+            assert not errs, errs
+            assert out == alone
+        for s in sessions:
+            s.close()
+    finally:
+        _lib.check(_lib.load().qasr_set_deterministic(0))
+        m.close()
