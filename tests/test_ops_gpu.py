@@ -694,6 +694,37 @@ def test_linear_q8_fixup_vs_oracle(torch_dev, fixup, path, epi, m, n, k):
     assert not host(fixup).any()
 
 
+@pytest.mark.parametrize("path", [16 + 23 + 32 * 2, 16 + 15 + 32 * 8, 16 + 12 + 32 * 3])
+@pytest.mark.parametrize("m,n,k", [(256, 12288, 2048), (48, 4096, 2048)])
+def test_linear_q8_fixup_repeat_stress(torch_dev, fixup, path, m, n, k):
+    """400 back-to-back launches on one stream with no host sync in between: the arrival counters are reused by
+    every launch (the last workgroup of a tile resets its counter), so a missed reset or an early read of another
+    workgroup's partial would show as a differing repeat or a non-zero counter"""
+    import torch
+
+    rng = np.random.default_rng(m + n)
+    x = rng.standard_normal((m, k)).astype(np.float32)
+    blocks = oracle.synth_q8(m + k, "w", n, k, 0.05)
+    qs, sc = q8_split(blocks, n, k)
+    xq = empty((m, k), torch.int8, torch_dev)
+    xdd = empty((m, k // 32), torch.float32, torch_dev)
+    xt = dev(x, torch_dev)
+    _lib.check(L().qasr_op_quant_rows(ptr(xt), m, k, k, ptr(xq), ptr(xdd), None))
+    wq, ws = dev(qs, torch_dev), dev(sc, torch_dev)
+    reps = 400
+    ys = torch.empty((reps, m, n), dtype=torch.float32, device=torch_dev)
+    for r in range(reps):
+        _lib.check(L().qasr_op_linear_q8(ptr(xq), ptr(xdd), m, ptr(wq), ptr(ws), n, k, None, None, ptr(ys[r]), n, 0,
+                                         path, None))
+    torch.cuda.synchronize()
+    assert bool((ys == ys[0]).all())
+    assert not host(fixup).any()
+    ref = oracle.linear_q8(x, blocks, n, None) if m * n <= 48 * 4096 else None
+    if ref is not None:
+        scale = np.abs(ref).max() + 1e-6
+        assert np.abs(host(ys[0]) - ref).max() <= 2e-5 * scale * np.sqrt(k / 256)
+
+
 @pytest.mark.parametrize("cfg", [c + 32 * s for c in (12, 15, 20, 22) for s in (2, 4, 8)])
 @pytest.mark.parametrize("m,f,k", [(40, 512, 1024), (70, 512, 2048), (256, 1024, 2048)])
 def test_gemm_swiglu_q8_fixup(torch_dev, fixup, m, f, k, cfg):
