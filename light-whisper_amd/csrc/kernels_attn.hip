@@ -81,6 +81,7 @@ __global__ __launch_bounds__(256) void k_attention(const __half* __restrict__ Q,
     __shared__ float sp[4][G][CH];
     __shared__ float cm_s[4][G], cl_s[4][G];
     __shared__ float ca_s[4][G][HD];
+    __shared__ __align__(16) __half2 kn[FUSED ? HD / 2 : 1];   // FUSED: the new K row (f16), see the K preload
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     // NW = 4: one workgroup per (row, KV head), its 4 waves take contiguous quarters of the key range and merge
     // their partial softmax states through LDS (long decoder KV ranges).  NW = 1: one wave per (row, KV head)
@@ -105,6 +106,29 @@ __global__ __launch_bounds__(256) void k_attention(const __half* __restrict__ Q,
     const int qn = (Ls + NW - 1) / NW;
     const int s0 = kb0 + part * qn, L = max(0, min(qn, Ls - part * qn));
     const int sub = lane & 7, kk = lane >> 3;
+    constexpr bool DEC = HD == 128 && NW == 4;
+    // FUSED decode: the first chunk's K loads go out before the q/k prologue (they do not wait for its barrier).
+    // Only the new row (slot sl_new, written by the prologue) would be stale: its lanes take it from LDS (kn).
+    constexpr int KP = DEC ? CK / 8 : 1;
+    int4 ka[KP], kb[KP];   // the decode chunk loop's K registers (chunk 0 preloaded when FUSED)
+    int sl_new = -1;
+    // (G = 2 only: with 4 query heads the preload costs a wave per SIMD; the 64-key kernel preloads only ranges
+    // of ≤ 32 keys per wave, which it runs as one 32-key chunk)
+    constexpr bool PRE = FUSED && DEC && G == 2;
+    const bool pre = PRE && (CK == 32 || L <= 32);   // uniform
+    if (pre) {
+        const int C0 = 32;
+        const int n0 = min(C0, L);
+        const __half* kc = K + (size_t)kvh * HD + sub * QD + (size_t)s0 * ldkv;
+#pragma unroll
+        for (int u = 0; u < KP; u++) {
+            if (8 * u < C0 && n0 > 0) {
+                const int j = min(8 * u + kk, n0 - 1);
+                ka[u] = *(const int4*)(kc + (size_t)j * ldkv);
+                kb[u] = *(const int4*)(kc + (size_t)j * ldkv + 8);
+            }
+        }
+    }
 
     h2v qv[G][QD / 2];   // the f16 q dims of this lane (q is f16-rounded on every path)
     if constexpr (FUSED) {
@@ -119,6 +143,7 @@ __global__ __launch_bounds__(256) void k_attention(const __half* __restrict__ Q,
         const int p = fz.pos[r], sl = fz.slot[r];
         // the new K/V row is written (and read back through the barrier) by the piece whose range holds its slot
         const bool own = S == 1 || (sl >= kb0 && sl < kb0 + Ls);
+        sl_new = own ? sl : -1;
         const int e0 = (2 * lane) & (HD / 2 - 1);
         const float4 cs = *(const float4*)(fz.rope_cs + ((size_t)p * (HD / 2) + e0) * 2);
         const bool lo = 2 * lane < HD / 2;
@@ -138,6 +163,7 @@ __global__ __launch_bounds__(256) void k_attention(const __half* __restrict__ Q,
                 qs[t][2 * lane + 1] = back.y;
             } else {
                 *(__half2*)(fz.kc + (size_t)sl * kvd + kvh * HD + 2 * lane) = hv;
+                kn[lane] = hv;
             }
         }
         __syncthreads();
@@ -168,7 +194,6 @@ __global__ __launch_bounds__(256) void k_attention(const __half* __restrict__ Q,
     // decoder rows (hd 128, 4 waves): 64-key chunks whose K and V loads are all issued together (one memory round
     // trip per chunk instead of one per 8 keys); PV with 16 lanes per key (16-B V loads, dims 8·(lane&15)..+8,
     // key group lane>>4), the 4 key groups summed once at the end
-    constexpr bool DEC = HD == 128 && NW == 4;
     const int vg = lane >> 4, vd = 8 * (lane & 15);
     float av[G][8];
 #pragma unroll
@@ -188,12 +213,26 @@ __global__ __launch_bounds__(256) void k_attention(const __half* __restrict__ Q,
             const int n = min(C, L - c0);
             const __half* kc = kbase + (size_t)(s0 + c0) * ldkv;
             const __half* vc = vbase16 + (size_t)(s0 + c0) * ldkv;
-            int4 ka[KU8], kb[KU8], vr[VU4];
+            static_assert(KU8 <= KP, "k_attention: chunk wider than the K registers");
+            int4 vr[VU4];
+            if (!pre || c0 > 0) {
 #pragma unroll
-            for (int u = 0; u < KU8; u++) {
-                const int j = min(8 * u + kk, n - 1);   // rows past n re-read row n-1 (their scores are dropped)
-                ka[u] = *(const int4*)(kc + (size_t)j * ldkv);
-                kb[u] = *(const int4*)(kc + (size_t)j * ldkv + 8);
+                for (int u = 0; u < KU8; u++) {
+                    const int j = min(8 * u + kk, n - 1);   // rows past n re-read row n-1 (their scores are dropped)
+                    ka[u] = *(const int4*)(kc + (size_t)j * ldkv);
+                    kb[u] = *(const int4*)(kc + (size_t)j * ldkv + 8);
+                }
+            }
+            if constexpr (FUSED) {
+                if (sl_new >= s0 + c0 && sl_new < s0 + c0 + n) {   // this chunk holds the new row
+#pragma unroll
+                    for (int u = 0; u < KU8; u++) {
+                        if (s0 + c0 + min(8 * u + kk, n - 1) == sl_new) {
+                            ka[u] = *(const int4*)(kn + sub * (QD / 2));
+                            kb[u] = *(const int4*)(kn + sub * (QD / 2) + 4);
+                        }
+                    }
+                }
             }
 #pragma unroll
             for (int u = 0; u < KU8; u++) {
