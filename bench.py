@@ -166,6 +166,34 @@ def pmc_evidence(kernel):
             "hbm_bytes_per_launch": round(hbm_bytes / launches) if launches else None}
 
 
+def launch_ranks(argv, n, dry_run=False):
+    """`bench.py --gpus N` started without WORLD_SIZE (N > 1): run N fresh child ranks under torch.distributed.run
+    (127.0.0.1 rendezvous) and return their exit code.  Called BEFORE this process touches the GPU (counting devices
+    does not initialise HIP on this image); the parent never execs, it waits for the launcher child.  Fewer visible
+    devices than N fails loudly unless QASR_DIST_BACKEND=gloo (the rehearsal mode where ranks share cards)."""
+    import socket
+    import subprocess
+
+    backend = os.environ.get("QASR_DIST_BACKEND", "nccl")
+    if not dry_run and backend != "gloo":
+        import torch
+
+        have = torch.cuda.device_count()
+        if have < n:
+            print(f"bench.py: --gpus {n} requested but only {have} GPU(s) visible "
+                  f"(QASR_DIST_BACKEND=gloo rehearses N ranks on fewer cards)", file=sys.stderr, flush=True)
+            return 2
+    with socket.socket() as s:   # a free rendezvous port
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+    if dry_run:
+        print(json.dumps({"launch": cmd}), flush=True)
+        return 0
+    return subprocess.call(cmd, env=dict(os.environ))
+
+
 def main():
     global SEG_PER_RANK
     ap = argparse.ArgumentParser()
@@ -184,14 +212,28 @@ def main():
                          "(seed 2) VAD-segmented across the ranks (halo-sharded FireRedVAD, probability "
                          "all-gather), segments LPT-sharded for ASR — strong scaling")
     ap.add_argument("--c5-seconds", type=float, default=3600.0)
+    ap.add_argument("--dry-run-launch", action="store_true",
+                    help="print the multi-rank launch command that --gpus N > 1 would run, and exit (tests)")
     args = ap.parse_args()
     if args.precision is None:
         args.precision = "mxfp8" if args.workload == "c5" else "q8"
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # one process per GPU: spawn the ranks (this process stays off the GPU and exits with their code)
+        argv = [a for a in sys.argv[1:] if a != "--dry-run-launch"]
+        sys.exit(launch_ranks(argv, args.gpus, dry_run=args.dry_run_launch))
+    if args.dry_run_launch:
+        print(json.dumps({"launch": None, "world": int(os.environ.get("WORLD_SIZE", "1"))}), flush=True)
+        return
 
     SEG_PER_RANK = args.segments
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr, flush=True)
+        sys.exit(2)
 
     import torch
     import torch.distributed as dist

@@ -127,19 +127,22 @@ QASR_API int qasr_session_run(qasr_session* s, const float* pcm16k, size_t n, in
 QASR_API int qasr_session_set_context(qasr_session* s, const int32_t* ids, int32_t n);
 /* Streaming decode (the app's interim loop re-sends the last ≤ 12 s every 140-460 ms, interim.rs:
    135-156): on = 1 makes the session's single-utterance runs draft their continuation from its earlier transcripts
-   (prompt lookup: the tokens that followed the same bigram before) and verify each draft in one teacher-forced pass;
-   the accepted tokens are greedy's (up to near-ties of f32 summation order).  stats: passes, draft tokens proposed,
-   draft tokens accepted, tokens emitted. */
+   (prompt lookup: the tokens that followed the same bigram before) and verify each draft in one teacher-forced pass
+   whose every row runs the arithmetic of a 1-row decode step, so the accepted tokens are greedy's BIT FOR BIT (the
+   transcript does not depend on the session's history).  stats: passes, draft tokens proposed, draft tokens
+   accepted, tokens emitted.  set_draft_noise (benchmark / test hook, not in the reference): each proposed token is
+   replaced by a random id with probability rate (acceptance below the 100 % of degenerate synthetic transcripts). */
 QASR_API int qasr_session_set_draft(qasr_session* s, int32_t on);
+QASR_API int qasr_session_set_draft_noise(qasr_session* s, float rate, uint64_t seed);
 QASR_API int qasr_session_draft_stats(const qasr_session* s, int64_t* stats /* [4] */);
-/* Streaming encoder cache: on = 1 makes a single-utterance run whose samples extend the previous
-   run's (bitwise: the interim loop's growing window, interim.rs:135-156) and hold a complete 8-chunk attention
-   window run its encoder in a row-count-independent order, keep its complete windows' audio-embedding rows, and
-   reuse the previous run's (104 tokens each) when the window's log-mel maximum is unchanged — the condition under
-   which those rows are functions of the same samples (Whisper-style normalisation uses the window's maximum; the
-   conv stack is per 1 s chunk, the encoder attention per window) — encoding only the rest: bit-identical to a full
-   recompute in that order.  Other runs (a new utterance, a sliding window) are unaffected.  stats: growing runs,
-   windows reused, windows encoded by them. */
+/* Streaming encoder cache: every single-utterance run encodes in a row-count-independent GEMM
+   order (cache on or off), so a complete 8-chunk attention window's audio-embedding rows are a function of its
+   samples and the request's log-mel maximum (Whisper-style normalisation; the conv stack is per 1 s chunk, the
+   encoder attention per window).  on = 1 keeps the complete windows of each run (≥ one window) and reuses the
+   previous run's (104 tokens each) whose frames lie in the samples both share bitwise (the interim loop's growing
+   window, interim.rs:135-156) when the mel maximum is the same bits — encoding only the rest, bit-identical to the
+   cache-off result.  A sliding window shares no prefix and reuses nothing.  stats: runs that took part, windows
+   reused, windows encoded by them. */
 QASR_API int qasr_session_set_encoder_cache(qasr_session* s, int32_t on);
 QASR_API int qasr_session_encoder_cache_stats(const qasr_session* s, int64_t* stats /* [3] */);
 /* The audio-embedding rows (projector output, [tokens][text hidden] f32) of the session's last run — a test /
@@ -162,9 +165,13 @@ QASR_API int qasr_run_batch_device(qasr_session* s, const float* dev_pcm, const 
                                    qasr_result* out);
 QASR_API void qasr_result_free(qasr_result* r);
 QASR_API void qasr_session_close(qasr_session* s);
-/* teacher-forced logits for parity tests: prompt (with audio placeholders) + forced continuation */
+/* teacher-forced logits for parity tests: prompt (with audio placeholders) + forced continuation, one decode step
+   per token; _verify: the continuation (≤ 32 tokens) in ONE draft verify pass of the streaming decode (same output
+   layout) — the exact-row contract says both are the same bits */
 QASR_API int qasr_session_forced_logits(qasr_session* s, const float* pcm16k, size_t n, const int32_t* forced,
                                         int32_t n_forced, float* logits_out /* [n_forced+1][vocab] */);
+QASR_API int qasr_session_forced_logits_verify(qasr_session* s, const float* pcm16k, size_t n, const int32_t* forced,
+                                               int32_t n_forced, float* logits_out /* [n_forced+1][vocab] */);
 /* the stages of one utterance, for layer-level parity tests (host outputs) */
 QASR_API int qasr_session_mel(qasr_session* s, const float* pcm16k, size_t n, float* mel_out /*[n_mels][t_pad]*/,
                               int32_t* t_valid, int32_t* t_pad);
@@ -329,10 +336,13 @@ QASR_API int qasr_op_conv3x3_gelu(const void* in, int32_t n_chunks, int32_t Hi, 
 QASR_API int qasr_op_fbank(const float* pcm, int64_t n, float* feats /*[T][80]*/, void* stream);
 QASR_API int qasr_stream_sync(void* stream);
 
-/* Deterministic mode (process-wide, default off): GEMMs never split K across workgroups, so every run of the same
-   input gives bit-identical logits (split-K partial sums land by float atomics in a run-dependent order, a
-   last-ulp difference that can flip a near-tie).  Sessions re-capture their step graphs after a switch. */
+/* Deterministic mode (process-wide, DEFAULT ON; QASR_ATOMICS=1 in the environment starts the process with it off):
+   GEMMs never add split-K partial sums with float atomics (whose landing order varies run to run, a last-ulp
+   difference that can flip a near-tie) — splits go through the ordered fix-up or do not happen — so every run of
+   the same input gives bit-identical logits and tokens.  on = 0 is a throughput A/B knob only.  Sessions
+   re-capture their step graphs after a switch.  qasr_get_deterministic reports the current mode. */
 QASR_API int qasr_set_deterministic(int32_t on);
+QASR_API int qasr_get_deterministic(int32_t* on);
 
 /* -------------------------------------------------------------------------------------------- profiling */
 /* live per-kernel-class timing (hipEvents on each instrumented launch's stream) + algorithmic FLOPs/bytes;

@@ -56,6 +56,13 @@ QASR_API int qasr_set_deterministic(int32_t on) {
     return guard([&] { qasr::set_deterministic(on != 0); });
 }
 
+QASR_API int qasr_get_deterministic(int32_t* on) {
+    return guard([&] {
+        QASR_CHECK(on, QASR_E_INVALID, "qasr_get_deterministic: null pointer");
+        *on = qasr::deterministic() ? 1 : 0;
+    });
+}
+
 QASR_API int qasr_prof_enable(int on) {
     return guard([&] { qasr::prof_set(on != 0); });
 }

@@ -251,8 +251,8 @@ QASR_API int qasr_op_attention_decode_split(const float* qkv, int32_t rows, int3
                                             const int32_t* kv_start, const int32_t* kv_len, float scale, int8_t* oq,
                                             float* od, float* part, int32_t* cnt, void* stream) {
     return guard([&] {
-        QASR_CHECK(hd == 128 && nkv > 0 && nh % nkv == 0 && oq && od && part && cnt && rows <= 4, QASR_E_INVALID,
-                   "attention_decode_split: hd 128, Q8 output, ≤ 4 rows, scratch");
+        QASR_CHECK(hd == 128 && nkv > 0 && nh % nkv == 0 && oq && od && part && cnt && rows <= kExactRows,
+                   QASR_E_INVALID, "attention_decode_split: hd 128, Q8 output, ≤ 32 rows, scratch");
         QkFuse fz{qkv, pos, slot, qnw, knw, rope_cs, eps, (__half*)kc, (__half*)vc};
         fz.part = part;
         fz.cnt = cnt;
@@ -307,7 +307,8 @@ QASR_API int qasr_op_synth_q8(uint64_t seed, const char* name, int64_t N, int64_
                               void* stream) {
     return guard([&] {
         QASR_CHECK(K % QK == 0, QASR_E_INVALID, "synth_q8: K must be a multiple of 32");
-        synth_q8(smix(seed ^ fnv1a(name)), N * (K / QK), sigma / 73.6f, qs, (__half*)sc, S(stream));
+        synth_q8(smix(seed ^ fnv1a(name)), N * (K / QK), sigma / 73.6f, qs, (__half*)sc, S(stream),
+                 strcmp(name, "token_embd.weight") == 0 ? K / QK : 0);
         launched();
     });
 }

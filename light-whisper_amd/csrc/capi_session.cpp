@@ -234,6 +234,13 @@ QASR_API int qasr_session_set_draft(qasr_session* s, int32_t on) {
     });
 }
 
+QASR_API int qasr_session_set_draft_noise(qasr_session* s, float rate, uint64_t seed) {
+    return guard([&] {
+        QASR_CHECK(s && rate >= 0.f && rate <= 1.f, QASR_E_INVALID, "bad arguments");
+        s->s->set_draft_noise(rate, seed);
+    });
+}
+
 QASR_API int qasr_session_draft_stats(const qasr_session* s, int64_t* stats) {
     return guard([&] {
         QASR_CHECK(s && stats, QASR_E_INVALID, "null argument");
@@ -330,6 +337,17 @@ QASR_API int qasr_session_forced_logits(qasr_session* s, const float* pcm16k, si
         QASR_CHECK(s && pcm16k && logits_out && n_forced >= 0, QASR_E_INVALID, "bad arguments");
         std::vector<float> lg;
         s->s->forced_logits_host(pcm16k, (int64_t)n, forced, n_forced, lg);
+        memcpy(logits_out, lg.data(), lg.size() * sizeof(float));
+    });
+}
+
+QASR_API int qasr_session_forced_logits_verify(qasr_session* s, const float* pcm16k, size_t n, const int32_t* forced,
+                                               int32_t n_forced, float* logits_out) {
+    return guard([&] {
+        QASR_CHECK(s && pcm16k && logits_out && n_forced >= 0 && n_forced <= kDraftRows, QASR_E_INVALID,
+                   "bad arguments (n_forced ≤ 32)");
+        std::vector<float> lg;
+        s->s->forced_logits_host(pcm16k, (int64_t)n, forced, n_forced, lg, /*one_pass=*/true);
         memcpy(logits_out, lg.data(), lg.size() * sizeof(float));
     });
 }

@@ -62,6 +62,25 @@ __host__ __device__ inline uint64_t smix(uint64_t z) {
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
     return z ^ (z >> 31);
 }
+
+// Row gain of the synthetic vocabulary table (token_embd, the tied lm_head): g = 2^(e/8) with e ≈ 5.77·n, n an
+// Irwin-Hall(12) normal from the row's hashes — a log-normal spread of row norms (σ ≈ 0.5 in ln), as real embedding
+// tables have, so the synthetic logits have a dominant top entry (a clear top-2 margin on ≥ 90 % of rows instead of
+// the ≈ 78 % of i.i.d. rows).  Integer arithmetic and an exact power-of-two table: the same bits on the host
+// (oracle/qasr_oracle.c orc_synth_q8) and the device (k_synth_q8).
+__host__ __device__ inline float synth_row_gain(uint64_t base, int64_t row) {
+    const uint64_t g = smix(base ^ 0x6A09E667F3BCC909ull);
+    int64_t sum = 0;
+    for (int i = 0; i < 3; i++) {
+        const uint64_t h = smix(g + 3 * (uint64_t)row + (uint64_t)i);
+        for (int j = 0; j < 4; j++) sum += (int64_t)((h >> (16 * j)) & 0xffff);
+    }
+    const int64_t num = (sum - 6 * 65536) * 577 / 100;
+    const int64_t e = (num + 32768 >= 0) ? (num + 32768) / 65536 : -((-(num + 32768) + 65535) / 65536);
+    const float frac[8] = {0x1.000000p+0f, 0x1.172b84p+0f, 0x1.306fe0p+0f, 0x1.4bfdaep+0f,
+                           0x1.6a09e6p+0f, 0x1.8ace54p+0f, 0x1.ae89fap+0f, 0x1.d5818ep+0f};
+    return ldexpf(frac[e & 7], (int)(e >> 3));
+}
 inline uint64_t fnv1a(const char* s) {
     uint64_t h = 0xcbf29ce484222325ull;
     for (const unsigned char* p = (const unsigned char*)s; *p; p++) {

@@ -124,9 +124,9 @@ Session::Session(Model* m, int n_ctx) : m_(m), n_ctx_(n_ctx) {
     // split-K decode attention scratch (≤ 4 rows over long key ranges): partial states + zeroed arrival counters
     const int nkv = m->hp.txt_kv_heads, G = nkv > 0 ? m->hp.txt_heads / nkv : 1;
     if (m->hp.head_dim == 128 && nkv > 0) {
-        QASR_HIP(hipMalloc(&attn_part_, attn_split_floats(nkv, G) * sizeof(float)));
-        QASR_HIP(hipMalloc(&attn_cnt_, (size_t)4 * nkv * sizeof(int)));
-        QASR_HIP(hipMemset(attn_cnt_, 0, (size_t)4 * nkv * sizeof(int)));
+        QASR_HIP(hipMalloc(&attn_part_, attn_split_floats(kExactRows, nkv, G) * sizeof(float)));
+        QASR_HIP(hipMalloc(&attn_cnt_, (size_t)kExactRows * nkv * sizeof(int)));
+        QASR_HIP(hipMemset(attn_cnt_, 0, (size_t)kExactRows * nkv * sizeof(int)));
     }
     // split-K fix-up of the decode GEMMs: up to kFixSplits partial tiles of 256 rows × the widest decoder weight
     const qasr_hparams& hp = m->hp;
@@ -250,11 +250,13 @@ void Session::front_end(const float* dpcm, const std::vector<int64_t>& off, cons
     // encoder rows are functions of the same samples); the conv stack and the encoder run on the remaining chunks
     fe.skip_tokens = 0;
     if (ec_run_) {
+        // the mel maximum reaches the pinned word with the stream (run_host keeps it once the run has synchronised);
+        // only a run with reusable windows waits for it here
         QASR_HIP(hipMemcpyAsync((unsigned*)pin_cnt_ + 60, d_umax, sizeof(unsigned), hipMemcpyDeviceToHost, st_));
-        QASR_HIP(hipStreamSynchronize(st_));
-        ec_umax_new_ = ((const unsigned*)pin_cnt_)[60];
+        if (ec_cand_ > 0) QASR_HIP(hipStreamSynchronize(st_));
+        const unsigned umax_new = ((volatile const unsigned*)pin_cnt_)[60];
         // (ec_cand_ ≤ the windows the previous run stored; run_host marks them invalid while this run overwrites them)
-        const int reuse = ec_umax_new_ == ec_umax_ && m_->precision_gen == ec_prec_ ? ec_cand_ : 0;
+        const int reuse = ec_cand_ > 0 && umax_new == ec_umax_ && m_->precision_gen == ec_prec_ ? ec_cand_ : 0;
         const int per = h.n_window_infer / 100;   // chunks per attention window
         if (reuse > 0 && per * reuse < chunks) {
             const int c0 = per * reuse;
@@ -275,7 +277,9 @@ void Session::front_end(const float* dpcm, const std::vector<int64_t>& off, cons
     conv3x3_gelu(a1, chunks, H1, W1, m_->conv_w[1], m_->conv_b[1], C, a2, 0, st_);
     conv3x3_gelu(a2, chunks, H2, W2, m_->conv_w[2], m_->conv_b[2], C, a3, 1, st_);
     const int rows = chunks * 13, K = C * F3;
-    StableOrderScope order(ec_run_);   // encoder-cache runs: rows independent of the row count (bit-exact reuse)
+    // one utterance: the row-count-independent GEMM order, so its audio-embedding rows are the same bits whether a
+    // window is computed in this run or reused from the encoder cache (cache on == cache off, bit for bit)
+    StableOrderScope order(count == 1);
     int8_t* xq = (int8_t*)sc_.get(S_XQ, (size_t)rows * K);
     float* xd = (float*)sc_.get(S_XD, (size_t)rows * (K / QK) * sizeof(float));
     quant_rows(a3, rows, K, K, xq, xd, st_);
@@ -295,7 +299,7 @@ void Session::encoder(FrontEnd& fe, float* enc_out_dbg) {
     // so encoding it as an utterance of its own gives the same windows
     const int skip = fe.skip_tokens, N = fe.total_tokens - skip, d = h.enc_d, F = h.enc_ffn, H = h.txt_h;
     QASR_CHECK(skip == 0 || fe.n_tok.size() == 1, QASR_E_INTERNAL, "encoder cache: one utterance");
-    StableOrderScope order(ec_run_);   // encoder-cache runs: rows independent of the row count (bit-exact reuse)
+    StableOrderScope order(fe.n_tok.size() == 1);   // one utterance: rows independent of the row count (front_end)
     // attention windows (get_audio_cu_seqlens, modeling_qwen3_asr.py:276-315)
     std::vector<int> kvs(N), kvl(N);
     for (size_t u = 0; u < fe.n_tok.size(); u++) {
@@ -383,8 +387,7 @@ void Session::enc_cache_store(int64_t n, int total_tokens) {
         ec_cap_ = bytes;
     }
     if (bytes) QASR_HIP(hipMemcpyAsync(ec_emb_, sc_.get(S_EMB, 0), bytes, hipMemcpyDeviceToDevice, st_));
-    ec_windows_ = w;
-    ec_umax_ = ec_umax_new_;
+    ec_windows_ = w;   // (ec_umax_: run_host, once the run has synchronised)
     ec_prec_ = m_->precision_gen;
 }
 
@@ -417,11 +420,17 @@ void Session::decoder_layers(float* x, int rows, const int* d_pos, const int* d_
     float* hd_ = fused ? (float*)sc_.get(S_HD, (size_t)rows * (F / QK) * sizeof(float)) : nullptr;
     const float scale = 1.0f / sqrtf((float)hd);
     const size_t layer_kv = (size_t)kv_slots_ * KD;
-    const bool fuse_qk = !dense && !rows_share_kv && hd == 128 && (nh / nkv == 2 || nh / nkv == 4) &&
-                         !getenv("QASR_NO_QK_FUSE");
+    const bool fuse_qk = !dense && hd == 128 && (nh / nkv == 2 || nh / nkv == 4) && !getenv("QASR_NO_QK_FUSE");
+    // exact rows (a draft verify pass): every row runs the arithmetic of a 1-row decode step — the fused GEMVs in
+    // row groups against the same weight registers, the same per-row decode attention (split over the key range like a
+    // single row) — so the accepted tokens are greedy's bit for bit, whatever the draft
+    const bool exact = rows_share_kv && rows <= kExactRows;
+    const bool gv_shapes = gemv_fused_ok(GV_RMS, rows, H) && gemv_fused_ok(GV_NONE, rows, F) &&
+                           gemv_fused_ok(GV_NONE, rows, QD);
     // GEMV row counts: the norms and the SwiGLU run inside the GEMVs' prologues (5 launches per layer, not 8)
-    const bool gv = rows <= gemv_layer_rows() && dec_fuse_ && gemv_fused_ok(GV_RMS, rows, H) &&
-                    gemv_fused_ok(GV_NONE, rows, F) && gemv_fused_ok(GV_NONE, rows, QD);
+    const bool gv = gv_shapes && (exact || (rows <= gemv_layer_rows() && dec_fuse_));
+    QASR_CHECK(!rows_share_kv || (exact && gv), QASR_E_INTERNAL,
+               "decoder: a verify pass needs the exact-row path (≤ kExactRows rows, GEMV shapes)");
     int8_t* hq2 = gv ? (int8_t*)sc_.get(S_HQ, (size_t)rows * F) : nullptr;   // the SwiGLU epilogue's Q8 rows
     float* hd2 = gv ? (float*)sc_.get(S_HD, (size_t)rows * (F / QK) * sizeof(float)) : nullptr;
     for (int l = 0; l < h.txt_layers; l++) {
@@ -439,8 +448,13 @@ void Session::decoder_layers(float* x, int rows, const int* d_pos, const int* d_
             linear_q8(xq, xd, rows, L.qkv, nullptr, nullptr, qkv, QD + 2 * KD, EPI_STORE, st_, zq);
         }
         if (fuse_qk) {   // decode rows: q/k norm + RoPE + KV write inside the attention kernel
+            // a verify pass's row i attends the K/V rows 0…i-1 write in this layer: all rows' K/V go to the cache in a
+            // launch of their own first; the fused kernel then rewrites each row's own K/V with the same bits
+            if (rows_share_kv)
+                qk_norm_rope(qkv, rows, nh, nkv, hd, d_pos, d_slot, L.q_norm, L.k_norm, rope_, h.rms_eps, qh, kc, vc,
+                             st_);
             QkFuse fz{qkv, d_pos, d_slot, L.q_norm, L.k_norm, rope_, h.rms_eps, kc, vc};
-            if (rows <= 4 && attn_part_ && attn_split_) {   // long key ranges split over workgroups
+            if ((rows <= 4 || exact) && attn_part_ && attn_split_) {   // long key ranges split over workgroups
                 fz.part = attn_part_;
                 fz.cnt = attn_cnt_;
             }
@@ -484,13 +498,19 @@ void Session::mx_ws(int64_t rows, int64_t kmax) {
     set_mx_workspace(sc_.get(S_MX, bytes), bytes);
 }
 
-void Session::lm_head_rows(const float* x, int rows, int ldx, float* logits) {
+void Session::lm_head_rows(const float* x, int rows, int ldx, float* logits, bool exact) {
     const qasr_hparams& h = m_->hp;
     int8_t* xq = (int8_t*)sc_.get(S_XQ, (size_t)std::max(rows, 1) * std::max(h.txt_h, std::max(h.txt_ffn, h.txt_heads * h.head_dim)));
     float* xd = (float*)sc_.get(S_XD, (size_t)std::max(rows, 1) * (std::max(h.txt_h, std::max(h.txt_ffn, h.txt_heads * h.head_dim)) / QK) * sizeof(float));
     rmsnorm_q8(x, rows, h.txt_h, ldx, m_->out_norm, h.rms_eps, xq, xd, st_);
     mx_ws(rows, h.txt_h);
-    linear_q8(xq, xd, rows, m_->lm_head, nullptr, nullptr, logits, h.vocab, EPI_STORE, st_);
+    // ≤ 4 rows (1-row decode steps) and exact rows (verify passes): the weight-streaming GEMV, one per-row arithmetic
+    // for any row count (k_gemv_wide's row groups); more rows: the MFMA GEMM
+    if ((rows <= kGemvRows || exact) && gemv_fused_ok(GV_NONE, rows, h.txt_h))
+        gemv_fused(GV_NONE, xq, xd, nullptr, 0, nullptr, 0.f, rows, m_->lm_head, nullptr, logits, h.vocab, EPI_STORE,
+                   nullptr, nullptr, st_);
+    else
+        linear_q8(xq, xd, rows, m_->lm_head, nullptr, nullptr, logits, h.vocab, EPI_STORE, st_);
 }
 
 // row bucket of a decode step: 1/2/4 rows (GEMV path), 8, then steps of 16 / 32 / 64 / 128 rows
@@ -536,7 +556,7 @@ void Session::draft_step(int B) {
     embed_rows(tab, B, m_->tok_embd, nullptr, x, st_);
     decoder_layers(x, B, tab + R, tab + 2 * R, tab + 3 * R, tab + 4 * R, 0, /*dense=*/false, /*rows_share_kv=*/B > 1);
     float* logits = (float*)sc_.get(S_LOGITS, (size_t)R * h.vocab * sizeof(float));
-    lm_head_rows(x, B, h.txt_h, logits);
+    lm_head_rows(x, B, h.txt_h, logits, /*exact=*/true);
     int* d_tok = (int*)sc_.get(S_TOK, (size_t)R * sizeof(int));
     argmax_rows(logits, B, h.vocab, d_tok, st_, sc_.get(S_ARGP, argmax_scratch_bytes(R)));
     QASR_HIP(hipMemcpyAsync((int*)pin_cnt_ + 8, d_tok, (size_t)B * sizeof(int), hipMemcpyDeviceToHost, st_));
@@ -589,6 +609,12 @@ void Session::draft_decode(int n_prompt, int base, int budget, int dummy, std::v
                 if (match(j)) best = j;
             if (best >= 0)
                 for (int k = best + order; k < H && (int)draft.size() < cap; k++) draft.push_back(history_[k]);
+        }
+        if (draft_noise_ > 0.f) {   // set_draft_noise: corrupt proposals (splitmix64 stream)
+            for (int32_t& t : draft) {
+                const uint64_t r = smix(noise_state_++);
+                if ((double)(r >> 11) * 0x1.0p-53 < draft_noise_) t = (int32_t)(smix(r) % (uint64_t)h.vocab);
+            }
         }
     };
     std::vector<int32_t> draft;
@@ -930,10 +956,10 @@ void Session::run_host(const std::vector<const float*>& pcm, const std::vector<i
     float* d = (float*)sc_.get(S_PCM, (size_t)std::max<int64_t>(total, 1) * sizeof(float));
     for (size_t i = 0; i < len.size(); i++)
         QASR_HIP(hipMemcpyAsync(d + off[i], pcm[i], (size_t)len[i] * sizeof(float), hipMemcpyHostToDevice, st_));
-    // encoder cache: only a window that GROWS the previous one (the previous samples are its prefix — the app's
-    // interim window before it reaches 12 s) and holds a complete encoder window runs in the fixed order, stores its
-    // windows and may reuse the previous run's; any other run (a new utterance, a sliding window) keeps the faster
-    // row-count-dependent GEMM choices and clears the cache
+    // encoder cache: every single-utterance run encodes in the row-count-independent order (front_end), so each of
+    // its complete windows is a function of the window's samples and the request's mel maximum; the run stores them,
+    // and the next run reuses those its sample prefix shares bitwise (the app's growing interim window before it
+    // reaches 12 s) when its mel maximum is the same bits.  A sliding window shares no prefix and reuses nothing.
     const bool single = enc_cache_ && len.size() == 1;
     ec_run_ = false;
     ec_cand_ = 0;
@@ -946,10 +972,10 @@ void Session::run_host(const std::vector<const float*>& pcm, const std::vector<i
         const int per = m_->hp.n_window_infer / 100;
         const auto frames_in = [&](int w, int64_t n) { return 16000LL * (per * w - 1) + 16040 <= n; };
         // (Q8 precision only: the MXFP8 GEMMs have no row-count-independent order)
-        ec_run_ = !m_->mx() && !ec_pcm_.empty() && L == (int64_t)ec_pcm_.size() && frames_in(1, len[0]);
+        ec_run_ = !m_->mx() && frames_in(1, len[0]);
         // windows whose chunks' frames all lie in the samples this run shares with the previous one (bitwise)
         while (ec_run_ && ec_cand_ < ec_windows_ && frames_in(ec_cand_ + 1, L)) ec_cand_++;
-        ec_windows_ = 0;   // invalid until this run stores its own (an exception or a non-growing run leaves it empty)
+        ec_windows_ = 0;   // invalid until this run stores its own (an exception leaves it empty)
     }
     try {
         run_batch(d, off, len, max_new, force_tps, out, times);
@@ -960,6 +986,7 @@ void Session::run_host(const std::vector<const float*>& pcm, const std::vector<i
         throw;
     }
     if (single) ec_pcm_.assign(pcm[0], pcm[0] + len[0]);
+    if (ec_run_) ec_umax_ = ((volatile const unsigned*)pin_cnt_)[60];   // this run's mel maximum (the stream is idle)
     ec_run_ = false;
 }
 
@@ -1059,7 +1086,7 @@ void Session::prefill_logits_host(const float* embeds, int n, std::vector<float>
 // prompt from the audio, then the forced continuation one token per step (the decode path, M = 1):
 // logits [n_forced + 1][V]
 void Session::forced_logits_host(const float* pcm, int64_t n, const int32_t* forced, int n_forced,
-                                 std::vector<float>& logits) {
+                                 std::vector<float>& logits, bool one_pass) {
     const qasr_hparams& h = m_->hp;
     const int H = h.txt_h, V = h.vocab;
     float* d = (float*)sc_.get(S_PCM, (size_t)n * sizeof(float));
@@ -1088,6 +1115,30 @@ void Session::forced_logits_host(const float* pcm, int64_t n, const int32_t* for
     float* lg = (float*)sc_.get(S_LOGITS, (size_t)V * sizeof(float));
     lm_head_rows(x + (size_t)(P - 1) * H, 1, H, lg);
     QASR_HIP(hipMemcpyAsync(logits.data(), lg, (size_t)V * sizeof(float), hipMemcpyDeviceToHost, st_));
+    if (one_pass && n_forced > 0) {
+        // the whole continuation as one verify pass of the streaming decode (draft_step): row i feeds forced[i] at
+        // position P + i and its logits predict the token after it — the rows a drafted decode accepts from
+        QASR_CHECK(n_forced <= kDraftRows, QASR_E_INVALID, "one-pass forced logits: at most kDraftRows tokens");
+        QASR_HIP(hipStreamSynchronize(st_));
+        constexpr int R = kDraftRows;
+        std::vector<int> hb((size_t)5 * R, 0);
+        for (int i = 0; i < n_forced; i++) {
+            hb[i] = forced[i];
+            hb[R + i] = P + i;
+            hb[2 * R + i] = P + i;
+            hb[3 * R + i] = 0;
+            hb[4 * R + i] = P + i + 1;
+        }
+        int* tab = (int*)sc_.get(S_DTAB, (size_t)6 * R * sizeof(int));
+        QASR_HIP(hipMemcpyAsync(tab, hb.data(), hb.size() * sizeof(int), hipMemcpyHostToDevice, st_));
+        sc_.get(S_X, (size_t)R * H * sizeof(float));
+        sc_.get(S_LOGITS, (size_t)R * V * sizeof(float));
+        draft_step(n_forced);
+        QASR_HIP(hipMemcpyAsync(logits.data() + V, sc_.get(S_LOGITS, 0), (size_t)n_forced * V * sizeof(float),
+                                hipMemcpyDeviceToHost, st_));
+        QASR_HIP(hipStreamSynchronize(st_));
+        return;
+    }
     for (int i = 0; i < n_forced; i++) {
         const int p = P + i;
         std::vector<int> one_id = {forced[i]}, one_pos = {p}, one_slot = {p}, one_kvs = {0}, one_kvl = {p + 1};

@@ -55,8 +55,9 @@ class Session {
     void encode_host(const float* mel, int t_pad, int t_valid, std::vector<float>& emb, std::vector<float>* enc,
                      int& n_tok);
     void prefill_logits_host(const float* embeds, int n, std::vector<float>& logits);
+    // one_pass: the forced continuation in ONE draft verify pass (n_forced ≤ kDraftRows) instead of one step each
     void forced_logits_host(const float* pcm, int64_t n, const int32_t* forced, int n_forced,
-                            std::vector<float>& logits);
+                            std::vector<float>& logits, bool one_pass = false);
 
     Model& model() { return *m_; }
     int n_ctx() const { return n_ctx_; }
@@ -66,6 +67,12 @@ class Session {
     // transcripts (prompt-lookup: the tokens that followed the same bigram last time) and verify a whole draft in one
     // teacher-forced pass; the accepted tokens are exactly greedy's (up to near-ties of f32 summation order)
     void set_draft(bool on) { draft_ = on; }
+    // benchmark / test hook: each proposed draft token is replaced by a random id with probability `rate` (draft
+    // acceptance below the degenerate 100 % of synthetic weights; the output stays greedy's, only the speed changes)
+    void set_draft_noise(float rate, uint64_t seed) {
+        draft_noise_ = rate;
+        noise_state_ = seed;
+    }
     struct DraftStats {
         int64_t passes = 0, proposed = 0, accepted = 0, tokens = 0;
     };
@@ -106,7 +113,8 @@ class Session {
     void draft_step(int B);
     void draft_decode(int n_prompt, int base, int budget, int dummy, std::vector<int32_t>& toks, bool& eos,
                       bool forced);
-    void lm_head_rows(const float* x, int rows, int ldx, float* logits);
+    // exact: every row with the 1-row arithmetic (verify passes; ≤ 4 rows always are)
+    void lm_head_rows(const float* x, int rows, int ldx, float* logits, bool exact = false);
     void mx_ws(int64_t rows, int64_t kmax);
     template <class T>
     T* upload(int slot, const std::vector<T>& v);
@@ -132,6 +140,8 @@ class Session {
     std::map<int, hipGraphExec_t> draft_graphs_;
     uint64_t draft_key_[4] = {~0ull, ~0ull, ~0ull, ~0ull};
     bool draft_ = false;
+    float draft_noise_ = 0.f;
+    uint64_t noise_state_ = 0;
     // 1–4-row decode: norms / SwiGLU fused into the GEMV prologues (QASR_NO_DEC_FUSE=1: the separate launches,
     // for A/B parity and timing; read once per session, so captured step graphs stay consistent)
     bool dec_fuse_ = getenv("QASR_NO_DEC_FUSE") == nullptr;
@@ -150,10 +160,10 @@ class Session {
     DraftStats dstats_;
     // encoder cache: the previous single-utterance run's samples, mel maximum, precision generation and the
     // embedding rows of its ec_windows_ complete windows (ec_emb_, device); ec_cand_ = windows the current run's
-    // sample prefix allows (run_host → front_end), ec_umax_new_ = the current run's mel maximum
+    // sample prefix allows (run_host → front_end)
     bool enc_cache_ = false;
     std::vector<float> ec_pcm_;
-    unsigned ec_umax_ = 0, ec_umax_new_ = 0;
+    unsigned ec_umax_ = 0;
     uint64_t ec_prec_ = 0;
     int ec_windows_ = 0, ec_cand_ = 0;
     bool ec_run_ = false;

@@ -17,7 +17,8 @@ enum Epi : int {
 
 // ---- Q8_0 weights / activations (kernels_q8.hip)
 void repack_q8(const uint8_t* blocks, int64_t nblk, int8_t* qs, __half* sc, hipStream_t s);
-void synth_q8(uint64_t base, int64_t nblk, float dbase, int8_t* qs, __half* sc, hipStream_t s);
+// gain_bpr > 0: blocks per row of a table whose rows get synth_row_gain (token_embd.weight, see common.h)
+void synth_q8(uint64_t base, int64_t nblk, float dbase, int8_t* qs, __half* sc, hipStream_t s, int64_t gain_bpr = 0);
 void synth_f32(uint64_t base, int64_t n, float center, float scale, float* out, hipStream_t s);
 void synth_f16(uint64_t base, int64_t n, float scale, __half* out, hipStream_t s);
 // quantise rows of x (row stride ldx floats) into q [M][K] / d [M][K/32]
@@ -32,6 +33,10 @@ constexpr int kGemvRows = 4;
 // rows up to which the decoder layer runs on the fused weight-streaming GEMVs (gemv_fused: norm prologue, SwiGLU
 // epilogue, 5 launches per layer) instead of the MFMA GEMMs (QASR_GV_ROWS overrides, for A/B timing)
 constexpr int kGemvWideRows = 8;
+// rows up to which gemv_fused runs (groups of 8 against the weights held in registers, each row with the per-row
+// arithmetic of a 1-row launch): the draft verify passes of the streaming decode, whose rows must be the same bits
+// as one-token greedy steps (engine.cpp, exact rows)
+constexpr int kExactRows = 32;
 int gemv_layer_rows();
 void gemv_q8(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const float* bias, const float* res, float* y,
              int ldy, int epi, hipStream_t s, int cols = 0);
@@ -132,7 +137,7 @@ struct QkFuse {
     float eps;
     __half* kc;
     __half* vc;
-    // split-K over the key range (1–4 decode rows, long contexts): partial (m, l, Σp·v) per (row, KV head, split)
+    // split-K over the key range (≤ kExactRows decode rows, long contexts): partial (m, l, Σp·v) per (row, KV head, split)
     // and an arrival counter per (row, KV head), zero between launches (kAttnSplitScratch sizes them); nullptr = one
     // workgroup per (row, KV head)
     float* part = nullptr;
@@ -143,8 +148,8 @@ struct QkFuse {
     int split_keys = 128;
 };
 constexpr int kAttnSplitMax = 16;      // workgroups per (row, KV head) at most
-// scratch floats / counters for rows ≤ 4 decode rows of a model (G query heads per KV head, hd 128)
-inline size_t attn_split_floats(int nkv, int G) { return (size_t)4 * nkv * kAttnSplitMax * G * (2 + 128); }
+// scratch floats / counters for up to `rows` split decode rows of a model (G query heads per KV head, hd 128)
+inline size_t attn_split_floats(int rows, int nkv, int G) { return (size_t)rows * nkv * kAttnSplitMax * G * (2 + 128); }
 void attention_decode_fused(const QkFuse& fz, int ldkv, const int* kv_start, const int* kv_len, int rows, int nh,
                             int nkv, int hd, float scale, int8_t* oq, float* od, hipStream_t s, int64_t total_keys = 0);
 void attention(const __half* Q, int ldq, const __half* K, const __half* V, int ldkv, const int* kv_start,

@@ -141,8 +141,10 @@ __global__ __launch_bounds__(256) void k_attention(const __half* __restrict__ Q,
         const int nslot = nh + 2 * nkv, kvd = nkv * HD;
         const float* src = fz.qkv + (size_t)r * nslot * HD;
         const int p = fz.pos[r], sl = fz.slot[r];
-        // the new K/V row is written (and read back through the barrier) by the piece whose range holds its slot
-        const bool own = S == 1 || (sl >= kb0 && sl < kb0 + Ls);
+        // the new K/V row is written (and read back through the barrier) by the piece whose range holds its slot;
+        // a slot outside the row's key range (never from the engine) is written by piece 0, as the unsplit kernel does
+        const bool own = S == 1 || (sl >= kb0 && sl < kb0 + Ls) ||
+                         (piece == 0 && (sl < kv_start[r] || sl >= kv_start[r] + Lr));
         sl_new = own ? sl : -1;
         const int e0 = (2 * lane) & (HD / 2 - 1);
         const float4 cs = *(const float4*)(fz.rope_cs + ((size_t)p * (HD / 2) + e0) * 2);
@@ -811,7 +813,8 @@ void attention_decode_fused(const QkFuse& fz, int ldkv, const int* kv_start, con
     ProfScope ps(s, "attention", 4.0 * hd * nh * (double)total_keys, 4.0 * hd * nh * (double)total_keys);
     QASR_CHECK(hd == 128 && nkv > 0 && nh % nkv == 0, QASR_E_INVALID, "attention_decode_fused: hd 128 only");
     const int G = nh / nkv;
-    QASR_CHECK(!fz.part || (rows <= 4 && fz.cnt), QASR_E_INVALID, "attention_decode_fused: split-K is for ≤ 4 rows");
+    QASR_CHECK(!fz.part || (rows <= kExactRows && fz.cnt), QASR_E_INVALID,
+               "attention_decode_fused: split-K is for ≤ kExactRows rows");
     const unsigned b4 = (unsigned)(rows * nkv * (fz.part ? kAttnSplitMax : 1));
     // many rows (≥ 192: ≥ 1,536 workgroups) → the 32-key-chunk kernel, 103 VGPRs and 4 waves per SIMD instead of 3
     // (tools/attn_batch.py, profiles/r2_attn_batch_chunk.jsonl: 256 rows 35.9 → 31.2 µs); fewer rows → the 64-key

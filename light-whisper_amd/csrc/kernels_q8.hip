@@ -73,11 +73,13 @@ void repack_q8(const uint8_t* blocks, int64_t nblk, int8_t* qs, __half* sc, hipS
     k_repack_q8<<<(unsigned)cdiv64(nblk, 256), 256, 0, s>>>(blocks, nblk, qs, sc);
 }
 
-__global__ void k_synth_q8(uint64_t base, int64_t nblk, float dbase, int8_t* __restrict__ qs, __half* __restrict__ sc) {
+__global__ void k_synth_q8(uint64_t base, int64_t nblk, float dbase, int64_t gain_bpr, int8_t* __restrict__ qs,
+                           __half* __restrict__ sc) {
     int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= nblk) return;
     uint64_t h = smix(base + (uint64_t)b);
     float d = dbase * (0.5f + unit_from(h));
+    if (gain_bpr > 0) d = d * synth_row_gain(base, b / gain_bpr);   // the vocabulary table's row norms
     sc[b] = f2h(d);
     int32_t w[8];
 #pragma unroll
@@ -100,9 +102,9 @@ __global__ void k_synth_q8(uint64_t base, int64_t nblk, float dbase, int8_t* __r
     o[1] = make_int4(w[4], w[5], w[6], w[7]);
 }
 
-void synth_q8(uint64_t base, int64_t nblk, float dbase, int8_t* qs, __half* sc, hipStream_t s) {
+void synth_q8(uint64_t base, int64_t nblk, float dbase, int8_t* qs, __half* sc, hipStream_t s, int64_t gain_bpr) {
     if (nblk <= 0) return;
-    k_synth_q8<<<(unsigned)cdiv64(nblk, 256), 256, 0, s>>>(base, nblk, dbase, qs, sc);
+    k_synth_q8<<<(unsigned)cdiv64(nblk, 256), 256, 0, s>>>(base, nblk, dbase, gain_bpr, qs, sc);
 }
 
 __global__ void k_synth_f32(uint64_t base, int64_t n, float center, float scale, float* out) {
@@ -264,6 +266,9 @@ void gemv_q8(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const flo
 // (swiglu_q8_block: swiglu_q8's lane arithmetic) is the epilogue, into yq [M][N/2] / yd [M][N/64].
 // The dot products, their order and the store / residual epilogue are k_gemv_q8's, so the outputs are bit-identical
 // to the separate launches (tests/test_ops_gpu.py::test_gemv_fused_*).
+// M > MR (a draft verify pass, up to kExactRows rows): the rows run in groups of MR against the weights held in
+// registers, each group with exactly the per-row code of an MR-row launch — so every row's result is the same bits
+// as when it runs alone (a 1-row decode step): the exact-row contract of the streaming decode (engine.cpp).
 template <int MR, int CPW, int T, int PRO, bool SWI, int NWV>
 __global__ __launch_bounds__(64 * NWV) void k_gemv_wide(const int8_t* __restrict__ W, const __half* __restrict__ Wsc,
                                                         int N, int K, int M, const int8_t* __restrict__ X,
@@ -305,69 +310,82 @@ __global__ __launch_bounds__(64 * NWV) void k_gemv_wide(const int8_t* __restrict
     const int8_t* xq = X;
     const float* xd = Xd;
     if constexpr (PRO == GV_RMS) {
+        // the Q8 rows of all M rows in LDS ([M][K] int8, then [M][K/32] scales)
         int8_t* sq = (int8_t*)gv_smem;
-        float* sd = (float*)(gv_smem + (size_t)MR * K);
+        float* sd = (float*)(gv_smem + (size_t)M * K);
+        for (int g0 = 0; g0 < M; g0 += MR) {   // M is uniform: every thread meets the barriers inside
+            if (g0 > 0 && tid < 256) {
 #pragma unroll
-        for (int m = 0; m < MR; m++)   // M is uniform: every thread meets the barriers inside
-            if (m < M)
-                rms_row_q8_finish<RK>(rv[m], rg, K, eps, sq + (size_t)m * K, sd + (size_t)m * nb, part[m], tid < 256);
+                for (int m = 0; m < MR; m++)
+                    if (g0 + m < M) rms_row_load<RK>(src + (size_t)(g0 + m) * ld_src, K, nw, rv[m], rg);
+            }
+#pragma unroll
+            for (int m = 0; m < MR; m++)
+                if (g0 + m < M)
+                    rms_row_q8_finish<RK>(rv[m], rg, K, eps, sq + (size_t)(g0 + m) * K, sd + (size_t)(g0 + m) * nb,
+                                          part[m], tid < 256);
+        }
         __syncthreads();
         xq = sq;
         xd = sd;
     }
     const bool even = (lane & 1) == 0;
-    float acc[CPW][MR];
-#pragma unroll
-    for (int c = 0; c < CPW; c++)
-#pragma unroll
-        for (int m = 0; m < MR; m++) acc[c][m] = 0.f;
-#pragma unroll
-    for (int t = 0; t < T; t++) {
-        const int k = 16 * (lane + 64 * t);
-        const bool in = k < K;
-        const int kc = min(k, K - 16), blk = kc >> 5;
-        int4 x[MR];
-        float dx[MR];
-#pragma unroll
-        for (int m = 0; m < MR; m++) {
-            const int mm = min(m, M - 1);
-            x[m] = *(const int4*)(xq + (size_t)mm * K + kc);
-            dx[m] = xd[(size_t)mm * nb + blk];
-        }
-#pragma unroll
-        for (int c = 0; c < CPW; c++) {
-#pragma unroll
-            for (int m = 0; m < MR; m++) {
-                int p = __builtin_amdgcn_sdot4(w[c][t].x, x[m].x, 0, false);
-                p = __builtin_amdgcn_sdot4(w[c][t].y, x[m].y, p, false);
-                p = __builtin_amdgcn_sdot4(w[c][t].z, x[m].z, p, false);
-                p = __builtin_amdgcn_sdot4(w[c][t].w, x[m].w, p, false);
-                p += __builtin_amdgcn_update_dpp(0, p, 0xB1, 0xf, 0xf, false);   // + lane ^ 1
-                acc[c][m] += (even && in) ? (float)p * (dw[c][t] * dx[m]) : 0.f;
-            }
-        }
-    }
-    if constexpr (SWI) {
+    for (int g0 = 0; g0 < M; g0 += MR) {
+        float acc[CPW][MR];
 #pragma unroll
         for (int c = 0; c < CPW; c++)
 #pragma unroll
+            for (int m = 0; m < MR; m++) acc[c][m] = 0.f;
+#pragma unroll
+        for (int t = 0; t < T; t++) {
+            const int k = 16 * (lane + 64 * t);
+            const bool in = k < K;
+            const int kc = min(k, K - 16), blk = kc >> 5;
+            int4 x[MR];
+            float dx[MR];
+#pragma unroll
             for (int m = 0; m < MR; m++) {
-                const float v = wave_sum(acc[c][m]);
-                if (lane == 0 && m < M) gub[m][wv * CPW + c] = v;
+                const int mm = min(g0 + m, M - 1);
+                x[m] = *(const int4*)(xq + (size_t)mm * K + kc);
+                dx[m] = xd[(size_t)mm * nb + blk];
             }
-        __syncthreads();
-        const int m = 2 * wv + (lane >> 5), j = lane & 31;   // rows 2w, 2w+1 on wave w's lane halves
-        if (m < M)   // uniform over each 32-lane group
-            swiglu_q8_block(gub[m], j, yq + (size_t)m * (N / 2) + 32 * blockIdx.x + j,
-                            yd + (size_t)m * (N / 64) + blockIdx.x);
-    } else {
 #pragma unroll
-        for (int c = 0; c < CPW; c++) {
+            for (int c = 0; c < CPW; c++) {
 #pragma unroll
-            for (int m = 0; m < MR; m++) {
-                const float v = wave_sum(acc[c][m]);
-                const int n = n0 + c;
-                if (lane == 0 && m < M && n < N) y[(size_t)m * ldy + n] = epi_apply(epi, v, m, n, nullptr, res, ldy);
+                for (int m = 0; m < MR; m++) {
+                    int p = __builtin_amdgcn_sdot4(w[c][t].x, x[m].x, 0, false);
+                    p = __builtin_amdgcn_sdot4(w[c][t].y, x[m].y, p, false);
+                    p = __builtin_amdgcn_sdot4(w[c][t].z, x[m].z, p, false);
+                    p = __builtin_amdgcn_sdot4(w[c][t].w, x[m].w, p, false);
+                    p += __builtin_amdgcn_update_dpp(0, p, 0xB1, 0xf, 0xf, false);   // + lane ^ 1
+                    acc[c][m] += (even && in) ? (float)p * (dw[c][t] * dx[m]) : 0.f;
+                }
+            }
+        }
+        if constexpr (SWI) {
+            if (g0 > 0) __syncthreads();   // the previous group's SwiGLU has read gub
+#pragma unroll
+            for (int c = 0; c < CPW; c++)
+#pragma unroll
+                for (int m = 0; m < MR; m++) {
+                    const float v = wave_sum(acc[c][m]);
+                    if (lane == 0 && g0 + m < M) gub[m][wv * CPW + c] = v;
+                }
+            __syncthreads();
+            const int m = 2 * wv + (lane >> 5), j = lane & 31;   // rows 2w, 2w+1 on wave w's lane halves
+            if (m < MR && g0 + m < M)   // uniform over each 32-lane group
+                swiglu_q8_block(gub[m], j, yq + (size_t)(g0 + m) * (N / 2) + 32 * blockIdx.x + j,
+                                yd + (size_t)(g0 + m) * (N / 64) + blockIdx.x);
+        } else {
+#pragma unroll
+            for (int c = 0; c < CPW; c++) {
+#pragma unroll
+                for (int m = 0; m < MR; m++) {
+                    const float v = wave_sum(acc[c][m]);
+                    const int n = n0 + c, row = g0 + m;
+                    if (lane == 0 && row < M && n < N)
+                        y[(size_t)row * ldy + n] = epi_apply(epi, v, row, n, nullptr, res, ldy);
+                }
             }
         }
     }
@@ -393,7 +411,7 @@ template <int MR, int CPW, int T, int PRO, bool SWI, int NWV>
 static void gv_go(const GvArgs& a, hipStream_t s) {
     const Q8Mat& W = *a.W;
     const dim3 g(cdiv(W.N, NWV * CPW));
-    const size_t lds = PRO == GV_RMS ? (size_t)MR * W.K + (size_t)MR * (W.K / QK) * sizeof(float) : 0;
+    const size_t lds = PRO == GV_RMS ? (size_t)a.M * W.K + (size_t)a.M * (W.K / QK) * sizeof(float) : 0;
     k_gemv_wide<MR, CPW, T, PRO, SWI, NWV><<<g, 64 * NWV, lds, s>>>(W.qs, W.sc, W.N, W.K, a.M, a.xq, a.xd, a.src,
                                                                     a.ld_src, a.nw, a.eps, a.res, a.y, a.ldy, a.epi,
                                                                     a.yq, a.yd);
@@ -439,8 +457,9 @@ int gemv_layer_rows() {
 }
 
 bool gemv_fused_ok(int pro, int M, int K) {
-    if (M < 1 || M > kGemvWideRows || K % QK != 0 || K < QK) return false;
-    return pro == GV_RMS ? K <= 4096 : K <= 6144;
+    if (M < 1 || M > kExactRows || K % QK != 0 || K < QK) return false;
+    // GV_RMS keeps the M quantised rows in LDS (K + K/32·4 bytes each) beside the static arrays
+    return pro == GV_RMS ? K <= 4096 && (size_t)M * K * 9 / 8 <= 144 * 1024 : K <= 6144;
 }
 
 void gemv_fused(int pro, const int8_t* xq, const float* xd, const float* src, int ld_src, const float* nw, float eps,
@@ -466,7 +485,12 @@ void gemv_fused(int pro, const int8_t* xq, const float* xd, const float* src, in
     else gv_mr<8>(pro, swi, cpw, T, a, s);
 }
 
-static std::atomic<int> g_det{0};
+// deterministic by default (a transcript is a function of the weights and the audio); QASR_ATOMICS=1 (or
+// qasr_set_deterministic(0)) lets decode-shape GEMMs split K with f32 atomics instead (throughput A/B runs)
+static std::atomic<int> g_det{[] {
+    const char* e = getenv("QASR_ATOMICS");
+    return e && atoi(e) != 0 ? 0 : 1;
+}()};
 static std::atomic<uint64_t> g_det_gen{0};
 void set_deterministic(bool on) {
     if (g_det.exchange(on ? 1 : 0) != (on ? 1 : 0)) g_det_gen++;
@@ -1922,14 +1946,27 @@ static const DecPick kDecDown[] = {{32, 16, 8}, {64, 15, 8}, {96, 10, 8}, {128, 
 // gate/up with the SwiGLU epilogue: split-K through the fix-up workspace pays off only at ≤ 32 rows
 static const DecPick kDecGu[] = {{16, 15, 2}, {32, 23, 2}};
 
+// Deterministic mode (the default): split-K only through the fix-up of the wave-64 tiles (12, 15, 20, 22, 23), else
+// unsplit (one-K-group, two-K-group or K-over-waves tiles); the winners of tools/dec_gemm_sweep.py run in that mode
+// (profiles/r3a_dec_sweep_det.log, cold weights, every configuration × split).  Used when the fix-up workspace is
+// registered (the session's decode steps), else the heuristic below.
+static const DecPick kDetQkv[] = {{64, 15, 4}, {96, 15, 4}, {128, 15, 2}, {192, 12, 4}, {224, 12, 3}, {256, 14, 1}};
+static const DecPick kDetO[] = {{16, 24, 0}, {32, 22, 6}, {96, 15, 4}, {128, 16, 1}, {192, 12, 6}, {224, 12, 4},
+                                {256, 12, 3}};
+static const DecPick kDetDown[] = {{64, 15, 8}, {128, 15, 4}, {192, 12, 8}, {256, 12, 4}};
+static const DecPick kDetGu[] = {{64, 12, 4}, {128, 12, 2}, {256, 12, 1}};
+
 static bool dec_table_pick(int M, const Q8Mat& W, int epi, int& cfg, int& splits) {
     if (M > 256 || W.K % 128 != 0 || W.N >= 32768) return false;
     const DecPick* t = nullptr;
     int n = 0;
-    if (epi == EPI_STORE && W.K <= 2048) t = kDecQkv, n = sizeof(kDecQkv) / sizeof(DecPick);
-    else if (epi == EPI_RESID && W.K <= 2048) t = kDecO, n = sizeof(kDecO) / sizeof(DecPick);
-    else if (epi == EPI_RESID) t = kDecDown, n = sizeof(kDecDown) / sizeof(DecPick);
-    else if (epi == EPI_SWIGLU && g_fix_part) t = kDecGu, n = sizeof(kDecGu) / sizeof(DecPick);
+    const bool det = deterministic() && g_fix_part;
+#define QASR_TAB(a, b) (det ? (t = a, n = sizeof(a) / sizeof(DecPick)) : (t = b, n = sizeof(b) / sizeof(DecPick)))
+    if (epi == EPI_STORE && W.K <= 2048) QASR_TAB(kDetQkv, kDecQkv);
+    else if (epi == EPI_RESID && W.K <= 2048) QASR_TAB(kDetO, kDecO);
+    else if (epi == EPI_RESID) QASR_TAB(kDetDown, kDecDown);
+    else if (epi == EPI_SWIGLU && g_fix_part) QASR_TAB(kDetGu, kDecGu);
+#undef QASR_TAB
     if (!t) return false;
     for (int i = 0; i < n; i++)
         if (M <= t[i].m_max) {
@@ -1947,6 +1984,22 @@ static int g_ws_rows = [] {
 void set_gemm_ws_rows(int rows, bool all_shapes) {
     g_ws_rows = std::max(0, std::min(64, rows));
     g_ws_all = all_shapes;
+}
+
+// The configurations whose outputs are each one fma chain over the K blocks in order (one K group, no split): the
+// register-staged tiles 0–3 and the LDS-DMA tiles 4–13, 16–18, 21–23.  Stable order picks among them (K % 128 == 0):
+// 128×128 for prefill-sized M, else the largest of 64×64 / 32×64 / 32×32 that fills the chip (≥ 256 tiles) — the
+// smallest otherwise; the SwiGLU epilogue needs 64-column wave tiles (12), GELU+Q8 64-column workgroup tiles.
+static int stable_pick(int M, int N, int epi) {
+    if (epi == EPI_SWIGLU) return M > 256 ? 13 : 12;
+    if (M > 256) return N >= 32768 ? 8 : 4;
+    const int cand[3] = {10, 17, 16};
+    const int n = epi == EPI_GELU_Q8 ? 2 : 3;
+    for (int i = 0; i < n; i++) {
+        const GemmCfg& g = kGemmCfgs[cand[i]];
+        if ((long)cdiv(N, g.bn) * cdiv(M, g.bm) >= 256) return cand[i];
+    }
+    return cand[n - 1];
 }
 
 // force_cfg: -1 auto, else an index into kGemmCfgs (a DMA config on K % 64 != 0 falls back to auto);
@@ -1968,9 +2021,10 @@ void gemm_q8(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const flo
     };
     int pick;
     if (g_stable && W.K % 128 == 0 && force_cfg < 0) {
-        // row-count-independent order: 64×64 tiles, K-128 stages, one K group, no split — every output is its blocks'
-        // fma chain in K order, the same for any M (StableOrderScope)
-        pick = 10;
+        // row-count-independent order (StableOrderScope): a one-K-group configuration without split — every output is
+        // its blocks' fma chain in K order, acc = fma((float)Σq·q, d_x·d_w, acc), the same bits for any tile shape and
+        // any M (tests/test_ops_gpu.py::test_gemm_chain_configs_bit_identical); the tile by the row count
+        pick = stable_pick(M, W.N, epi);
         force_splits = 1;
     } else if (W.K % 64 == 0) {
         // measured on the engine's shapes (tools/gemm_tune.py, profiles/): 128×128 tiles with K-64 stages on prefill
@@ -2015,7 +2069,8 @@ void gemm_q8(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const flo
     // The fix-up's serial tail (store → count → reload) costs more than f32 atomics on the plain-store / residual
     // decode shapes (profiles/r2_dec_gemm_sweep_fixup.log), so those keep the atomics (deterministic mode: no split);
     // the SwiGLU epilogue (no atomic form) splits only through the fix-up, deterministic either way.
-    const bool fix_epi = epi == EPI_SWIGLU || g_fix_all;
+    // deterministic mode: every split epilogue goes through the fix-up (the tiles that have it; the others run unsplit)
+    const bool fix_epi = epi == EPI_SWIGLU || g_fix_all || deterministic();
     if (force_splits > 1 && fix_epi && fixup_ok(std::min(force_splits, steps))) {
         const int sps = cdiv(steps, std::min(force_splits, steps));
         dim3 grid(cdiv(W.N, cf.bn), cdiv(M, cf.bm), cdiv(steps, sps));

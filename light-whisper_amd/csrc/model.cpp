@@ -296,7 +296,7 @@ std::unique_ptr<Model> make_synthetic_model(const qasr_hparams& hp, uint64_t see
     auto q8 = [&](const std::string& name, float sigma) {
         const TensorSlot& t = m.slots.at(name);
         synth_q8(base(name), t.rows * (t.cols / QK), sigma / 73.6f, (int8_t*)t.base + t.row0 * t.ld,
-                 t.sc + t.row0 * (t.ld / QK), s);
+                 t.sc + t.row0 * (t.ld / QK), s, name == "token_embd.weight" ? t.cols / QK : 0);
     };
     auto f32 = [&](const std::string& name, float center, float scale) {
         const TensorSlot& t = m.slots.at(name);

@@ -88,6 +88,7 @@ SIGNATURES = {
     "qasr_result_free": (None, [C.POINTER(Result)]),
     "qasr_session_close": (None, [P]),
     "qasr_session_forced_logits": (C.c_int, [P, P, SZ, P, I32, P]),
+    "qasr_session_forced_logits_verify": (C.c_int, [P, P, SZ, P, I32, P]),
     "qasr_session_mel": (C.c_int, [P, P, SZ, P, C.POINTER(I32), C.POINTER(I32)]),
     "qasr_session_encode": (C.c_int, [P, P, I32, I32, P, P, C.POINTER(I32)]),
     "qasr_session_prefill_logits": (C.c_int, [P, P, I32, P]),
@@ -105,6 +106,7 @@ SIGNATURES = {
     "qasr_resample_linear": (C.c_int, [P, SZ, C.c_double, P, SZ, C.POINTER(SZ)]),
     "qasr_audio_load_path": (C.c_int, [C.c_char_p, P, SZ, C.POINTER(SZ)]),
     "qasr_session_set_draft": (C.c_int, [P, I32]),
+    "qasr_session_set_draft_noise": (C.c_int, [P, F32, C.c_uint64]),
     "qasr_session_draft_stats": (C.c_int, [P, C.POINTER(C.c_int64)]),
     "qasr_session_set_encoder_cache": (C.c_int, [P, I32]),
     "qasr_session_encoder_cache_stats": (C.c_int, [P, C.POINTER(C.c_int64)]),
@@ -145,6 +147,7 @@ SIGNATURES = {
     "qasr_stream_sync": (C.c_int, [P]),
     "qasr_prof_enable": (C.c_int, [C.c_int]),
     "qasr_set_deterministic": (C.c_int, [I32]),
+    "qasr_get_deterministic": (C.c_int, [P]),
     "qasr_prof_reset": (C.c_int, []),
     "qasr_prof_report": (C.c_int, [C.c_char_p, SZ, C.POINTER(SZ)]),
 }

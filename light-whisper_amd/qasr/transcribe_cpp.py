@@ -206,6 +206,10 @@ class Session:
         """streaming decode: draft from this session's earlier transcripts, verify in one pass (greedy's tokens)"""
         check(_lib.load().qasr_session_set_draft(self._h, 1 if on else 0))
 
+    def set_draft_noise(self, rate: float, seed: int = 0):
+        """benchmark / test hook: replace each proposed draft token by a random id with probability `rate`"""
+        check(_lib.load().qasr_session_set_draft_noise(self._h, float(rate), int(seed)))
+
     def draft_stats(self) -> dict:
         st = (C.c_int64 * 4)()
         check(_lib.load().qasr_session_draft_stats(self._h, st))
@@ -228,14 +232,16 @@ class Session:
         check(lib.qasr_session_audio_embeds(self._h, out.ctypes.data_as(C.c_void_p), n.value, C.byref(n)))
         return out
 
-    def forced_logits(self, audio, forced) -> np.ndarray:
+    def forced_logits(self, audio, forced, one_pass: bool = False) -> np.ndarray:
+        """teacher-forced logits [len(forced)+1][vocab]: one decode step per forced token, or (one_pass) the forced
+        tokens as ONE draft verify pass (≤ 32) — bit-identical by the exact-row contract"""
         a = _f32(audio)
         f = np.ascontiguousarray(forced, dtype=np.int32)
         v = self.model.hparams["vocab"]
         out = np.empty((f.size + 1, v), np.float32)
-        check(_lib.load().qasr_session_forced_logits(self._h, a.ctypes.data_as(C.c_void_p), a.size,
-                                                     f.ctypes.data_as(C.c_void_p), f.size,
-                                                     out.ctypes.data_as(C.c_void_p)))
+        fn = _lib.load().qasr_session_forced_logits_verify if one_pass else _lib.load().qasr_session_forced_logits
+        check(fn(self._h, a.ctypes.data_as(C.c_void_p), a.size, f.ctypes.data_as(C.c_void_p), f.size,
+                 out.ctypes.data_as(C.c_void_p)))
         return out
 
     def mel(self, audio):

@@ -42,6 +42,7 @@ ROOT = os.path.abspath(os.path.join(HERE, "..", ".."))
 REF_RES = "/root/reference/src-tauri/resources"
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 sys.path.insert(0, os.path.join(ROOT, "oracle"))
+sys.path.insert(0, ROOT)
 
 
 # ---------------------------------------------------------------------------------------------- VAD post
@@ -306,15 +307,14 @@ def tiny_tensors(cfg=TINY, seed=TINY_SEED):
     return oracle.Model(cfg, seed=seed).export()
 
 
-def make_hf_tiny():
+def hf_model(c, tens, audio_token_id):
+    """transformers' Qwen3ASRForConditionalGeneration (the in-container stand-in for the model math) at
+    config c, loaded with the synthetic GGUF-style tensors `tens` dequantised (Q8_0 → f32, f16 → f32)"""
     import torch
     from transformers import Qwen3ASRConfig, Qwen3ASRForConditionalGeneration
-    from transformers.models.qwen3_asr.feature_extraction_qwen3_asr import Qwen3ASRFeatureExtractor
 
     import oracle
 
-    c = TINY
-    tens = tiny_tensors()
     torch.manual_seed(0)
     cfg = Qwen3ASRConfig(
         audio_config=dict(num_mel_bins=128, encoder_layers=c["enc_layers"], encoder_attention_heads=c["enc_heads"],
@@ -325,7 +325,7 @@ def make_hf_tiny():
                          num_key_value_heads=c["txt_kv_heads"], head_dim=c["head_dim"], vocab_size=c["vocab"],
                          rms_norm_eps=c["rms_eps"], max_position_embeddings=4096, tie_word_embeddings=True,
                          rope_parameters={"rope_type": "default", "rope_theta": c["rope_theta"]}),
-        audio_token_id=4000,
+        audio_token_id=audio_token_id,
     )
     model = Qwen3ASRForConditionalGeneration(cfg).eval()
 
@@ -380,7 +380,14 @@ def make_hf_tiny():
     missing, unexpected = model.load_state_dict(sd, strict=False)
     missing = [m for m in missing if "positional_embedding" not in m]
     assert not missing and not unexpected, (missing, unexpected)
+    return model
 
+
+def make_hf_tiny():
+    import torch
+    from transformers.models.qwen3_asr.feature_extraction_qwen3_asr import Qwen3ASRFeatureExtractor
+
+    model = hf_model(TINY, tiny_tensors(), 4000)
     fe = Qwen3ASRFeatureExtractor()
     rng = np.random.default_rng(5)
     out = {}
@@ -415,6 +422,55 @@ def make_hf_tiny():
     out["dec__logits"] = logits.numpy().astype(np.float32)
     np.savez_compressed(os.path.join(HERE, "hf_tiny.npz"), **out)
     print("hf_tiny.npz", {k: v.shape for k, v in out.items()})
+
+
+# ---------------------------------------------------------------------------------------------- HF at 0.6B dims
+REAL_SEED = 7   # tests/test_model_real_gpu.py's synthetic-weight seed
+
+
+def make_hf_06b():
+    """the oracle pinned at the real qwen3-asr-0.6b dimensions (18 encoder layers, d 896, 14 heads; 28
+    decoder layers, GQA 16/8, head 128, the 151,936-row tied vocabulary).  transformers' qwen3_asr on the oracle's
+    seeded synthetic weights (Q8_0 dequantised), 10 s of speech-like audio: the log-mel, the encoder / projector rows
+    (a row subset + float64 sums) and the decoder logits of the chat prompt's last 8 rows, stored compactly (top-64
+    values and indices per row + float64 checksums).  tests/test_oracle_cpu.py checks the oracle (float mode) against
+    it."""
+    import torch
+    from transformers.models.qwen3_asr.feature_extraction_qwen3_asr import Qwen3ASRFeatureExtractor
+
+    import oracle
+    from bench import speech_like
+
+    c = oracle.arch_config("qwen3-asr-0.6b")
+    sp = oracle.QWEN_SPECIAL
+    model = hf_model(c, oracle.Model(c, seed=REAL_SEED).export(), sp["tok_audio_pad"])
+    audio = speech_like(np.random.default_rng(505), 160000)
+    fe = Qwen3ASRFeatureExtractor()
+    feats = fe(audio, sampling_rate=16000, return_tensors="pt", return_attention_mask=True)
+    x, mask = feats["input_features"], feats["attention_mask"]
+    t_valid = int(mask.sum())
+    t_pad = (t_valid + 99) // 100 * 100
+    with torch.no_grad():
+        a = model.model.get_audio_features(x, mask, return_dict=True)
+    enc = a.last_hidden_state.numpy().astype(np.float32)
+    proj = a.pooler_output.numpy().astype(np.float32)
+    rows = np.array([0, 1, 12, 13, 51, 103, 104, 117, enc.shape[0] - 1], np.int32)
+    ids = oracle.chat_prompt(proj.shape[0])
+    ids_t = torch.tensor([ids])
+    with torch.no_grad():
+        emb = model.model.language_model.embed_tokens(ids_t)
+        emb[0, (ids_t == sp["tok_audio_pad"])[0]] = torch.from_numpy(proj)
+        h = model.model.language_model(inputs_embeds=emb).last_hidden_state
+        logits = model.lm_head(h[:, -8:])[0].numpy().astype(np.float32)
+    top = np.argsort(-logits, axis=1, kind="stable")[:, :64]
+    out = {"audio": audio, "mel": x[0, :, :t_pad].numpy().astype(np.float32), "t_valid": np.array(t_valid),
+           "enc_rows": rows, "enc_sel": enc[rows], "proj_sel": proj[rows],
+           "enc_sum": enc.astype(np.float64).sum(1), "proj_sum": proj.astype(np.float64).sum(1),
+           "ids": np.array(ids, np.int32), "logit_top_idx": top.astype(np.int32),
+           "logit_top_val": np.take_along_axis(logits, top, 1),
+           "logit_sum": logits.astype(np.float64).sum(1), "logit_abs_sum": np.abs(logits.astype(np.float64)).sum(1)}
+    np.savez_compressed(os.path.join(HERE, "hf_06b.npz"), **out)
+    print("hf_06b.npz", {k: v.shape for k, v in out.items()})
 
 
 # ---------------------------------------------------------------------------------------------- transcript parse
@@ -556,6 +612,6 @@ print(json.dumps(out))
 
 
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["vad_post", "audio_io", "protocol", "dfsmn", "hf_tiny", "parse", "wav"]
+    which = sys.argv[1:] or ["vad_post", "audio_io", "protocol", "dfsmn", "hf_tiny", "hf_06b", "parse", "wav"]
     for w in which:
         globals()[f"make_{w}"]()

@@ -172,7 +172,7 @@ def test_real_decode_fusion_bit_identical(pair, monkeypatch):
         b = s2.run(audio, force_tokens_per_s=8).tokens
         assert len(a) == 41 and a == b
     finally:
-        _lib.check(_lib.load().qasr_set_deterministic(0))
+        _lib.check(_lib.load().qasr_set_deterministic(1))   # the default
         s2.close()
 
 
@@ -187,7 +187,7 @@ def test_real_deterministic_mode_repeats(pair):
     try:
         assert np.array_equal(s.forced_logits(audio, forced), s.forced_logits(audio, forced))
     finally:
-        _lib.check(_lib.load().qasr_set_deterministic(0))
+        _lib.check(_lib.load().qasr_set_deterministic(1))   # the default
 
 
 def test_real_batch_equals_single_and_oracle(pair):
@@ -246,3 +246,64 @@ def test_real_mxfp8_against_q8(pair):
     # observed (r2): 3.95e-2 of the logit range (e4m3 element rounding), argmax equal on all 7 rows
     assert e < 8e-2
     assert (got.argmax(1) == ref.argmax(1))[clear].all()
+
+
+def test_real_draft_verify_pass_bit_identical(pair):
+    """exact-row contract at the real shapes: a forced continuation of 1–32 tokens fed as ONE draft
+    verify pass gives the same logits, bit for bit, as one decode step per token — including a 20 s prompt, whose
+    > 256 keys split each row's key range over workgroups exactly as a single row's"""
+    arch, _, s, _ = pair
+    for secs, seed, ns in ((4.0, 31, (2, 9, 32)), (20.0, 32, (1, 17))):
+        audio = clip(secs, seed)
+        for n in ns:
+            forced = np.array([1000 + 37 * i for i in range(n)], np.int32)
+            assert np.array_equal(s.forced_logits(audio, forced), s.forced_logits(audio, forced, one_pass=True)), \
+                (secs, n)
+
+
+def _interim_windows(seconds=17.0, seed=40):
+    """the app's interim loop (interim.rs:135-156): the window grows from the utterance start while it is shorter than
+    12 s, then slides (the last 12 s); ticks every 1.4 s here, plus the final request over the whole recording"""
+    rec = np.concatenate([clip(5.0, seed), clip(4.0, seed + 1), clip(8.0, seed + 2)])[: int(seconds * 16000)]
+    out, t = [], 1.4
+    while t < seconds:
+        n = int(t * 16000)
+        out.append(rec[max(0, n - 12 * 16000): n])
+        t += 1.4
+    return out + [rec, rec]
+
+
+def test_real_streaming_bit_identical(pair):
+    """the product transcript is a pure function of (weights, audio).  An interim replay across the
+    12 s boundary (growing, then sliding windows, then the final request, repeated) through a session with prompt-
+    lookup drafts and the encoder cache on gives the SAME audio-embedding rows and tokens as a plain session, for
+    draft noise 0 / 20 / 50 % (acceptance below the degenerate 100 % of synthetic transcripts), and the plain
+    session repeats itself bit for bit."""
+    arch, m, s, _ = pair
+    windows = _interim_windows()
+    H = m.hparams["txt_h"]
+    plain = [s.run(w, max_new_tokens=40) for w in windows]
+    plain_emb = [None] * len(windows)
+    for i, w in enumerate(windows[-3:]):   # the plain session repeats itself (deterministic by default)
+        r = s.run(w, max_new_tokens=40)
+        assert r.tokens == plain[len(windows) - 3 + i].tokens
+    for noise in (0.0, 0.2, 0.5):
+        st = m.session(kv_type="f16", n_ctx=4096)
+        st.set_draft(True)
+        st.set_encoder_cache(True)
+        st.set_draft_noise(noise, seed=5)
+        for i, w in enumerate(windows):
+            got = st.run(w, max_new_tokens=40)
+            assert got.tokens == plain[i].tokens, (noise, i)
+            if noise == 0.0:
+                if plain_emb[i] is None:
+                    s.run(w, max_new_tokens=1)
+                    plain_emb[i] = s.audio_embeds().reshape(-1, H)
+                assert np.array_equal(st.audio_embeds().reshape(-1, H), plain_emb[i]), i
+        ds, ec = st.draft_stats(), st.encoder_cache_stats()
+        record(f"real_streaming[{arch}]", noise=noise, **{f"draft_{k}": v for k, v in ds.items()},
+               **{f"cache_{k}": v for k, v in ec.items()})
+        assert ds["accepted"] > 0 and ec["windows_reused"] > 0, (ds, ec)
+        if noise > 0:
+            assert ds["proposed"] > ds["accepted"], ds
+        st.close()

@@ -360,11 +360,88 @@ def test_gemv_fused_rejects_bad_shapes(torch_dev):
 
     x = empty((8, 8192), torch.float32, torch_dev)
     y = empty((8, 64), torch.float32, torch_dev)
-    for pro, m, k, epi in ((1, 9, 1024, 0), (1, 1, 8192, 0), (0, 1, 8192, 0), (3, 1, 1024, 0), (1, 1, 100, 0),
-                           (0, 1, 1024, 3)):
+    for pro, m, k, epi in ((1, 33, 1024, 0), (0, 33, 1024, 0), (1, 1, 8192, 0), (0, 1, 8192, 0), (3, 1, 1024, 0),
+                           (1, 1, 100, 0), (0, 1, 1024, 3)):
         with pytest.raises(_lib.QasrError):
             _lib.check(L().qasr_op_gemv_fused(pro, ptr(x), 2 * k, ptr(x), 1e-6, m, ptr(x), ptr(x), ptr(x), ptr(x), 64,
                                               k, None, ptr(y), 64, epi, ptr(x), ptr(x), None))
+
+
+@pytest.mark.parametrize("pro,n,k,epi", [(1, 4096, 2048, 0), (0, 2048, 2048, 1), (0, 2048, 6144, 1),
+                                         (0, 151936, 2048, 0), (1, 12288, 2048, 3), (1, 1024, 1024, 1)])
+def test_gemv_exact_rows(torch_dev, pro, n, k, epi):
+    """exact-row contract of the draft verify passes (engine.cpp): every row of a 2–32-row gemv_fused launch (rows in
+    groups of 8 against the weights held in registers) is the same bits as that row in a 1-row launch; for given Q8
+    rows also the same bits as gemv_q8's single row (the 1-row decode step's vocabulary projection)"""
+    import torch
+
+    rng = np.random.default_rng(21)
+    M = 32
+    x = dev((rng.standard_normal((M, k)) * 3).astype(np.float32), torch_dev)
+    w = dev((1 + 0.1 * rng.standard_normal(k)).astype(np.float32), torch_dev)
+    xq = dev(rng.integers(-127, 128, (M, k), dtype=np.int8), torch_dev)
+    xd = dev((rng.random((M, k // 32)) * 0.02).astype(np.float32), torch_dev)
+    res = dev(rng.standard_normal((M, n)).astype(np.float32), torch_dev)
+    wq, ws = _q8_weights(torch_dev, n, k, 6)
+    f = n // 2
+
+    def launch(rows, r0):
+        y = res[r0:r0 + rows].clone()
+        h = empty((rows, f), torch.int8, torch_dev) if epi == 3 else None
+        hd = empty((rows, f // 32), torch.float32, torch_dev) if epi == 3 else None
+        yp = None if epi == 3 else ptr(y)
+        if pro == 1:
+            _lib.check(L().qasr_op_gemv_fused(1, C.c_void_p(x.data_ptr() + r0 * k * 4), k, ptr(w), 1e-6, rows, None,
+                                              None, ptr(wq), ptr(ws), n, k, yp, yp, n, epi, ptr(h), ptr(hd), None))
+        else:
+            _lib.check(L().qasr_op_gemv_fused(0, None, 0, None, 0.0, rows, C.c_void_p(xq.data_ptr() + r0 * k),
+                                              C.c_void_p(xd.data_ptr() + r0 * (k // 32) * 4), ptr(wq), ptr(ws), n, k,
+                                              yp, yp, n, epi, None, None, None))
+        return (host(h), host(hd)) if epi == 3 else host(y)
+
+    single = [launch(1, r) for r in range(M)]
+    for rows in (2, 5, 8, 9, 16, 23, 32):
+        got = launch(rows, 0)
+        for r in range(rows):
+            if epi == 3:
+                assert np.array_equal(got[0][r], single[r][0][0]) and np.array_equal(got[1][r], single[r][1][0]), (rows, r)
+            else:
+                assert np.array_equal(got[r], single[r][0]), (rows, r)
+    if pro == 0:
+        for r in (0, 17, 31):
+            y = res[r:r + 1].clone()
+            _lib.check(L().qasr_op_linear_q8(C.c_void_p(xq.data_ptr() + r * k),
+                                             C.c_void_p(xd.data_ptr() + r * (k // 32) * 4), 1, ptr(wq), ptr(ws), n, k,
+                                             None, ptr(y), ptr(y), n, epi, 1, None))
+            assert np.array_equal(host(y)[0], single[r][0]), r
+
+
+GEMM_CHAIN_CFGS = [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 16, 17, 18, 21, 22, 23]
+
+
+@pytest.mark.parametrize("m,n,k,epi", [(13, 1024, 1024, 0), (104, 3072, 1024, 0), (160, 1024, 4096, 1),
+                                       (300, 4096, 1024, 0), (7, 2048, 2048, 1)])
+def test_gemm_chain_configs_bit_identical(torch_dev, m, n, k, epi):
+    """the stable GEMM order (StableOrderScope: single-utterance encoder runs, the encoder cache): every one-K-group,
+    unsplit configuration computes each output as the same fma chain over its K blocks, so all of them — any tile
+    shape, any row count — give the same bits; a row subset gives the rows' bits of the full launch"""
+    rng = np.random.default_rng(22)
+    xq = dev(rng.integers(-127, 128, (m, k), dtype=np.int8), torch_dev)
+    xd = dev((rng.random((m, k // 32)) * 0.02).astype(np.float32), torch_dev)
+    res = dev(rng.standard_normal((m, n)).astype(np.float32), torch_dev)
+    wq, ws = _q8_weights(torch_dev, n, k, 7)
+
+    def run(cfg, rows=m):
+        y = res[:rows].clone()
+        _lib.check(L().qasr_op_linear_q8(ptr(xq), ptr(xd), rows, ptr(wq), ptr(ws), n, k, None, ptr(y), ptr(y), n,
+                                         epi, 16 + cfg + 32, None))
+        return host(y)
+
+    want = run(10)
+    for cfg in GEMM_CHAIN_CFGS:
+        assert np.array_equal(run(cfg), want), cfg
+    for cfg in (10, 16, 4):
+        assert np.array_equal(run(cfg, rows=max(1, m // 3)), want[:max(1, m // 3)]), cfg
 
 
 @pytest.mark.parametrize("m", [1, 4, 40])

@@ -133,3 +133,49 @@ def test_q8_roundtrip_and_block_dots():
     y = oracle.dequantize_q8(q, 256)
     assert np.abs(y - x).max() <= np.abs(x).max() / 127 * 0.5 + 1e-6
     assert q.shape == (4, 8 * 34)
+
+
+def test_oracle_matches_transformers_at_06b_dims():
+    """the oracle pinned at the real qwen3-asr-0.6b dimensions (18 encoder layers of d 896 / 14 heads
+    with 104-token windows; 28 decoder layers, GQA 16/8, the 151,936-row tied vocabulary) against transformers'
+    qwen3_asr on the same seeded synthetic weights (tests/golden/hf_06b.npz, make_golden.py make_hf_06b): log-mel,
+    encoder / projector rows and float64 row sums, and the chat prompt's last 8 logit rows (top-64 entries + float64
+    sums).  Oracle in float mode (dequantised weights, f32 activations: HF's own arithmetic, f32 summation order
+    aside)."""
+    import os
+
+    hf = np.load(os.path.join(os.path.dirname(__file__), "golden", "hf_06b.npz"))
+    cfg = oracle.arch_config("qwen3-asr-0.6b")
+    oracle.set_mode(engine=False)
+    try:
+        m = oracle.Model(cfg, seed=7)
+        mel, tv = oracle.mel(hf["audio"])
+        assert tv == int(hf["t_valid"]) == 1000
+        assert np.abs(mel - hf["mel"]).max() < 1e-4
+        proj, enc = m.encode(hf["mel"], tv, want_enc=True)
+        assert proj.shape == (130, 1024) and enc.shape == (130, 896)
+        rows = hf["enc_rows"]
+        e_enc = np.abs(enc[rows] - hf["enc_sel"]).max() / np.abs(hf["enc_sel"]).max()
+        e_proj = np.abs(proj[rows] - hf["proj_sel"]).max() / np.abs(hf["proj_sel"]).max()
+        e_sum = np.abs(proj.astype(np.float64).sum(1) - hf["proj_sum"]).max() / np.abs(proj).max()
+        ids = hf["ids"]
+        kv = oracle.KV(m, 160)
+        x = kv.embed(ids)
+        x[ids == oracle.QWEN_SPECIAL["tok_audio_pad"]] = proj
+        kv.forward(x[:-8])
+        lg = np.concatenate([kv.forward(x[i:i + 1]) for i in range(len(ids) - 8, len(ids))])
+        top_i, top_v = hf["logit_top_idx"], hf["logit_top_val"]
+        span = np.abs(top_v).max()
+        e_lg = np.abs(np.take_along_axis(lg, top_i, 1) - top_v).max() / span
+        e_lsum = np.abs(lg.astype(np.float64).sum(1) - hf["logit_sum"]).max() / np.abs(hf["logit_abs_sum"]).max()
+        print(f"0.6B dims vs HF: enc {e_enc:.2e} proj {e_proj:.2e} proj-sum {e_sum:.2e} logits {e_lg:.2e} "
+              f"logit-sum {e_lsum:.2e}")
+        # observed (r3): enc 6.9e-7, proj 7.8e-7, proj row sums 1.7e-5, logits 2.3e-7 of the span, logit sums 1.2e-8
+        # (f32 summation order through 18 + 28 layers); bounds ≈ 10x
+        assert e_enc < 1e-5 and e_proj < 1e-5 and e_sum < 2e-4
+        assert e_lg < 3e-6 and e_lsum < 2e-7
+        assert (lg.argmax(1) == top_i[:, 0]).all()
+        # the top-64 set agrees wherever the 64th and 65th entries of HF's row are not within the error
+        assert all(len(set(np.argsort(-lg[r])[:16]) ^ set(top_i[r, :16])) <= 2 for r in range(8))
+    finally:
+        oracle.set_mode(engine=True)

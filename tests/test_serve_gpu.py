@@ -6,7 +6,10 @@ decode and the reply are the production code.
 Checked: the init line; a transcribe whose speech FireRedVAD accepts → vad_segments > 0 and the reply's text equal
 to Session.run on the same cropped samples (the in-process C ABI, qwen3_asr_server.py:321,326); hot_words accepted
 and ignored (the reference ignores them); stats; a short interim replay (interim.rs:135-156: the last
-≤12 s re-sent each tick) followed by the final request; exit.
+≤12 s re-sent each tick) followed by the final request; exit.  The interim replay runs at both model sizes — C3 is
+quoted on qwen3-asr-1.7b — with the engine's defaults (prompt-lookup drafts and the encoder cache ON): every reply
+equals the plain in-process Session.run (no drafts, no cache) bit for bit, the final request repeated gives the same
+reply, and its first tokens match the oracle up to a clear-margin rule.
 """
 import base64
 import json
@@ -25,14 +28,14 @@ MAX_NEW = 48
 
 
 class Engine:
-    def __init__(self, tmp_path, extra=None):
+    def __init__(self, tmp_path, extra=None, engine=ENGINE):
         from qasr import _lib
 
         env = {k: v for k, v in os.environ.items() if k not in ("QASR_PROTOCOL_TEST_FAKE",)}
         # synthetic weights rarely emit EOS: cap the natural decode (the reference decodes to EOS or n_ctx)
         env.update(QASR_SYNTHETIC="1", QASR_MAX_NEW_TOKENS=str(MAX_NEW), LIGHT_WHISPER_DATA_DIR=str(tmp_path),
                    HF_HUB_CACHE=str(tmp_path / "hf"), **(extra or {}))
-        self.p = subprocess.Popen([_lib.ENGINE_PATH, "serve", "--engine", ENGINE], stdin=subprocess.PIPE,
+        self.p = subprocess.Popen([_lib.ENGINE_PATH, "serve", "--engine", engine], stdin=subprocess.PIPE,
                                   stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True, env=env)
         self.init = json.loads(self.p.stdout.readline())
 
@@ -59,30 +62,44 @@ def pcm_request(audio_i16, rid, hot_words=None):
     return req
 
 
-@pytest.fixture(scope="module")
-def ref(torch_dev):
-    """in-process engine pieces on the same weights: the synthetic 0.6B model (seed 0, as QASR_SYNTHETIC) + VAD"""
+def _ref(engine):
+    """in-process engine pieces on the same weights: the synthetic model (seed 0, as QASR_SYNTHETIC) + VAD; the
+    session has no drafts and no encoder cache (the plain decode the served transcripts must equal bit for bit)"""
     from qasr.firered_vad import FireRedVad
     from qasr.transcribe_cpp import Model
 
-    m = Model.synthetic(ENGINE, seed=0)
+    m = Model.synthetic(engine, seed=0)
     s = m.session(kv_type="f16", n_ctx=32768)
     v = FireRedVad()
+    return m, s, v
+
+
+@pytest.fixture(scope="module")
+def ref(torch_dev):
+    m, s, v = _ref(ENGINE)
     yield s, v
     v.close()
     s.close()
     m.close()
 
 
-def expected(ref, audio_i16):
-    """what transcribe_audio replies for this PCM: FireRedVAD crop → session.run → .strip()"""
-    s, v = ref
+def crop(ref, audio_i16):
+    """FireRedVAD crop of transcribe_audio (qwen3_asr_server.py:152-173): (samples, segments) or (None, 0)"""
+    _, v = ref
     a = audio_i16.astype(np.float32) / 32768.0
     segs = v.speech_timestamps(a)
     if not segs:
         return None, 0
     st, en = max(0, segs[0]["start"]), min(a.size, segs[-1]["end"])
-    return s.run(a[st:en], max_new_tokens=MAX_NEW).text.strip(), len(segs)
+    return a[st:en], len(segs)
+
+
+def expected(ref, audio_i16):
+    """what transcribe_audio replies for this PCM: FireRedVAD crop → session.run → .strip()"""
+    a, n = crop(ref, audio_i16)
+    if a is None:
+        return None, 0
+    return ref[0].run(a, max_new_tokens=MAX_NEW).text.strip(), n
 
 
 def speech_clip(seconds, seed):
@@ -123,13 +140,28 @@ def test_serve_real_backend(ref, tmp_path):
     assert e.p.returncode == 0
 
 
-def test_serve_interim_replay(ref, tmp_path):
-    """C3 in miniature: a recording growing in 0.7 s steps, each tick re-sends the last ≤12 s (interim.rs:135-146),
-    then the final request; every reply is the in-process result on the same crop."""
-    e = Engine(tmp_path)
+@pytest.fixture(scope="module", params=["qwen3-asr-0.6b", "qwen3-asr-1.7b"])
+def ref_arch(request, torch_dev):
+    m, s, v = _ref(request.param)
+    yield request.param, (s, v)
+    v.close()
+    s.close()
+    m.close()
+
+
+def test_serve_interim_replay(ref_arch, tmp_path):
+    """C3 (interim.rs:135-146): a recording growing in steps, each tick re-sends the last ≤12 s — growing
+    windows, then sliding ones past 12 s — then the final request, sent twice.  The engine runs with its defaults
+    (drafts + encoder cache on); every reply's text equals the plain in-process Session.run on the same crop (bit-
+    identical transcripts: the drafts and the cache change the speed, not the tokens), and the repeated final request
+    gives the same reply.  The final crop's first tokens match the oracle's greedy tokens up to a clear-margin rule."""
+    import oracle
+
+    engine, ref = ref_arch
+    e = Engine(tmp_path, engine=engine)
     try:
-        full = speech_clip(14.0, 4)
-        ticks = [int(t * 16000) for t in (0.7, 1.4, 2.1, 5.6, 9.8, 14.0)]
+        full = speech_clip(15.0, 4)
+        ticks = [int(t * 16000) for t in (0.7, 1.4, 2.1, 5.6, 9.8, 11.2, 11.9, 12.6, 13.3, 14.0, 15.0)]
         for i, end in enumerate(ticks):
             win = full[max(0, end - 12 * 16000):end]
             line, r = e.ask(pcm_request(win, 100 + i, hot_words=["热词"]))
@@ -139,9 +171,29 @@ def test_serve_interim_replay(ref, tmp_path):
                 continue
             want, nseg = expected(ref, win)
             assert r["vad_segments"] == nseg
-            assert r["text"] == (want or "")
-        _, fin = e.ask(pcm_request(full, 200))
+            assert r["text"] == (want or ""), (engine, i)
+        finals = [e.ask(pcm_request(full, 200 + k))[1] for k in range(2)]
         want, nseg = expected(ref, full)
-        assert nseg > 0 and fin["vad_segments"] == nseg and fin["text"] == want
+        assert nseg > 0 and all(f["vad_segments"] == nseg and f["text"] == want for f in finals), engine
+        _, st = e.ask({"action": "stats", "request_id": 300})
+        # (windows the VAD rejects or shorter than 0.5 s do not count: qwen3_asr_server.py:290-315)
+        assert 2 <= st["stats"]["transcription_count"] <= len(ticks) + 2
     finally:
         e.close()
+    # the final crop against the oracle (same seeded weights): first tokens equal up to a near-tie of the oracle logits
+    a, _ = crop(ref, full)
+    got = ref[0].run(a, max_new_tokens=12).tokens
+    oracle.set_mode(engine=True)
+    o = oracle.Model(oracle.arch_config(engine), seed=0)
+    rmel, rtv = oracle.mel(a)
+    remb = o.encode(rmel, rtv)
+    sp = oracle.QWEN_SPECIAL
+    ids = np.array(oracle.chat_prompt(remb.shape[0]), np.int32)
+    toks, lg = oracle.KV(o, len(ids) + 16).generate(ids, sp["tok_audio_pad"], remb, eos=(sp["tok_eos0"], sp["tok_eos1"]),
+                                                    max_new=12, want_logits=True)
+    n = min(len(got), len(toks))
+    div = next((j for j in range(n) if got[j] != toks[j]), n)
+    if div < n:
+        top2 = np.sort(lg[div])[-2:]
+        assert top2[1] - top2[0] < 0.02 * np.abs(lg[div]).max(), (engine, div, got, list(toks))
+    assert div >= min(4, n), (engine, got, list(toks))

@@ -154,3 +154,41 @@ def test_long_form_probability_gather_gloo():
     for rank, got, (f0, f1, h0, h1) in out:
         assert np.array_equal(got, want)
         assert h0 == max(0, f0 - 160) and h1 == min(1001, f1 + 160)
+
+
+def _bench(args, env_extra=None, timeout=120):
+    import subprocess
+
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, env=env, capture_output=True,
+                          text=True, timeout=timeout)
+
+
+def test_bench_gpus_launcher_dry_run():
+    """`bench.py --gpus N` without WORLD_SIZE spawns N ranks through torch.distributed.run on 127.0.0.1; every
+    child sees WORLD_SIZE == N (the launcher logic end to end, minus the GPU work)."""
+    import json
+
+    r = _bench(["--gpus", "2", "--steps", "3", "--dry-run-launch"])
+    assert r.returncode == 0, r.stderr
+    cmd = json.loads(r.stdout.strip().splitlines()[-1])["launch"]
+    assert cmd[1:3] == ["-m", "torch.distributed.run"] and "--nproc-per-node=2" in cmd
+    assert "--master-addr=127.0.0.1" in cmd and cmd[cmd.index(os.path.join(ROOT, "bench.py")) + 1:] == \
+        ["--gpus", "2", "--steps", "3"]
+    import subprocess
+
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    out = subprocess.run(cmd + ["--dry-run-launch"], env=env, capture_output=True, text=True, timeout=180)
+    assert out.returncode == 0, out.stderr
+    lines = [json.loads(x) for x in out.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 2 and all(x == {"launch": None, "world": 2} for x in lines)
+
+
+def test_bench_gpus_fails_loudly_without_devices():
+    """--gpus 2 with fewer visible GPUs (none here) exits non-zero before any rank starts; a rank whose WORLD_SIZE
+    disagrees with --gpus exits non-zero too."""
+    r = _bench(["--gpus", "2", "--no-cpu-baseline"], {"QASR_DIST_BACKEND": "nccl"})
+    assert r.returncode == 2 and "only 0 GPU(s) visible" in r.stderr
+    r = _bench(["--gpus", "1", "--no-cpu-baseline"], {"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode == 2 and "WORLD_SIZE=2 but --gpus 1" in r.stderr

@@ -3,6 +3,7 @@
 larger than the Infinity Cache, as in a decode step that streams 28 layers) and print the best few per (shape, M)
 next to the heuristic.  Tuning aid for gemm_q8's decode table (kernels_q8.hip).  GPU.
 usage: python tools/dec_gemm_sweep.py [out.json]"""
+import ctypes as C
 import json
 import os
 import sys
@@ -29,6 +30,11 @@ def main():
         part = torch.empty(256 * 12288 * 8, dtype=torch.float32, device=dev)
         cnt = torch.zeros(8192, dtype=torch.int32, device=dev)
         _lib.check(lib.qasr_op_set_gemm_fixup(part.data_ptr(), part.numel() * 4, cnt.data_ptr(), cnt.numel()))
+    det = C.c_int32(0)
+    _lib.check(lib.qasr_get_deterministic(C.byref(det)))
+    det = det.value == 1   # the default: split-K only through the fix-up (wave-64 tiles), the rest unsplit
+    wave64 = {12, 15, 20, 22, 23}
+    print(f"deterministic={det} fix-up={fix}", flush=True)
     shapes = [s for s in SHAPES if s[0] in os.environ.get("SHAPES", "qkv,o,down,gu").split(",")]
     cfgs = [int(c) for c in os.environ["CFGS"].split(",")] if "CFGS" in os.environ else CFGS
     for tag, N, K, epi in shapes:
@@ -41,8 +47,14 @@ def main():
             y = torch.zeros(M, N, device=dev)
             hq = torch.empty(M, N // 2, dtype=torch.int8, device=dev)
             hd = torch.empty(M, N // 64, device=dev)
-            combos = [(-1, 0)] + ([(c, s) for c in SWIGLU_CFGS for s in (SPLITS if fix and c < 24 else [0])]
-                                  if epi == 3 else [(c, s) for c in cfgs for s in (SPLITS if c < 24 else [0])])
+            def splits(c):
+                if c >= 24:
+                    return [0]
+                if det and not (fix and c in wave64):
+                    return [1]
+                return SPLITS if (fix or epi != 3) else [0]
+            combos = [(-1, 0)] + ([(c, s) for c in SWIGLU_CFGS for s in splits(c)]
+                                  if epi == 3 else [(c, s) for c in cfgs for s in splits(c)])
             times = []
             for cfg, sp in combos:
                 def run(i):
@@ -72,7 +84,7 @@ def main():
                 times.append((round(e0.elapsed_time(e1) / n * 1e3, 2), cfg, sp))
             heur = next(t for t in times if t[1] < 0)
             best = sorted(times)[:6]
-            result[f"{tag}:{M}"] = {"heuristic_us": heur[0], "best": best}
+            result[f"{tag}:{M}"] = {"heuristic_us": heur[0], "best": best, "all": sorted(times)}
             print(f"{tag:5s} M={M:4d} heuristic {heur[0]:7.1f}us | best " +
                   "  ".join(f"{t:6.1f}us c{c}s{s}" for t, c, s in best), flush=True)
         del wq, ws
