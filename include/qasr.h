@@ -122,9 +122,17 @@ QASR_API int qasr_session_open(qasr_model* m, const char* kv_type, int32_t n_ctx
 QASR_API int qasr_session_run(qasr_session* s, const float* pcm16k, size_t n, int32_t timestamps, qasr_result* out);
 /* Hot-word context (opt-in — the reference ignores hot_words): token ids placed in the system turn
    of the chat prompt (HF Qwen3-ASR `prompt=`, processing_qwen3_asr.py:513-538) for the session's following runs;
-   n = 0 restores the reference's prompt.  qasr_model_tokenize: UTF-8 → ids by greedy longest match over the
-   byte-level vocabulary (decodes back to the same text; not the canonical BPE segmentation). */
+   n = 0 restores the reference's prompt.  qasr_model_tokenize: UTF-8 → ids as Qwen2Tokenizer.encode(text,
+   add_special_tokens=False) (tokenization_qwen2.py: the Qwen2 pre-tokenizer regex, GPT-2 byte-level alphabet, the
+   GGUF's tokenizer.ggml.merges by rank; NFC input assumed), or by greedy longest match when the vocabulary has no
+   merges (synthetic models).  qasr_tokenizer_*: the same encoder on a given vocabulary + merge list. */
 QASR_API int qasr_session_set_context(qasr_session* s, const int32_t* ids, int32_t n);
+typedef struct qasr_tokenizer qasr_tokenizer;
+QASR_API int qasr_tokenizer_open(const char* const* pieces, int32_t n_pieces, const uint8_t* is_special /* or NULL */,
+                                 const char* const* merges, int32_t n_merges, qasr_tokenizer** out);
+QASR_API int qasr_tokenizer_encode(const qasr_tokenizer* t, const char* text, size_t len, int32_t* ids, size_t cap,
+                                   size_t* n_out);
+QASR_API void qasr_tokenizer_close(qasr_tokenizer* t);
 /* Streaming decode (the app's interim loop re-sends the last ≤ 12 s every 140-460 ms, interim.rs:
    135-156): on = 1 makes the session's single-utterance runs draft their continuation from its earlier transcripts
    (prompt lookup: the tokens that followed the same bigram before) and verify each draft in one teacher-forced pass

@@ -2,8 +2,9 @@
 // sf.read(path, dtype="float32", always_2d=True) → audio.mean(axis=1, dtype=float32) → _resample(audio, rate).
 // soundfile / libsndfile are not part of this image; the WAV container and libsndfile's float normalisation of
 // integer PCM (int16 / 2^15, int24 / 2^23, int32 / 2^31, unsigned 8-bit (x − 128) / 2^7) are restated here for PCM
-// 8/16/24/32 and IEEE float32 (WAVE_FORMAT_EXTENSIBLE included).  Other codecs (ADPCM, µ-law …) are refused with
-// an error reply instead of being decoded.
+// 8/16/24/32, IEEE float32 / float64 (doubles narrowed to float) and G.711 µ-law / A-law (libsndfile's 16-bit
+// decode tables — Sun g711.c ulaw2linear / alaw2linear — times 1/0x8000), WAVE_FORMAT_EXTENSIBLE included.  Other
+// codecs (ADPCM, GSM …) and containers (FLAC, OGG …) are refused with an error reply (INTEGRATION.md lists them).
 #include <stdio.h>
 #include <string.h>
 
@@ -24,6 +25,19 @@ std::string slurp(const char* path) {
     while ((n = fread(buf, 1, sizeof buf, f)) > 0) s.append(buf, n);
     fclose(f);
     return s;
+}
+
+// G.711 code → 16-bit linear (libsndfile ulaw_decode / alaw_decode)
+int ulaw_linear(unsigned char c) {
+    const int u = ~c & 0xFF;
+    const int t = (((u & 0x0F) << 3) + 0x84) << ((u & 0x70) >> 4);
+    return (u & 0x80) ? 0x84 - t : t - 0x84;
+}
+int alaw_linear(unsigned char c) {
+    const int a = c ^ 0x55, seg = (a & 0x70) >> 4;
+    int t = (a & 0x0F) << 4;
+    t = seg == 0 ? t + 8 : (t + 0x108) << (seg - 1);
+    return (a & 0x80) ? t : -t;
 }
 
 uint16_t u16(const std::string& d, size_t at) { return (uint16_t)((uint8_t)d[at] | ((uint8_t)d[at + 1] << 8)); }
@@ -53,7 +67,8 @@ void read_wav(const std::string& path, std::vector<float>& mono, int& rate) {
         } else if (id == "data") {
             QASR_CHECK(ch > 0 && rate > 0, QASR_E_FORMAT, open_err + "Format not recognised.");
             const bool pcm = fmt == 1 && (bits == 8 || bits == 16 || bits == 24 || bits == 32);
-            QASR_CHECK(pcm || (fmt == 3 && bits == 32), QASR_E_FORMAT, open_err + "Unsupported WAV sample format");
+            const bool flt = fmt == 3 && (bits == 32 || bits == 64), g711 = (fmt == 6 || fmt == 7) && bits == 8;
+            QASR_CHECK(pcm || flt || g711, QASR_E_FORMAT, open_err + "Unsupported WAV sample format");
             const size_t n = (size_t)std::min<uint64_t>(sz, d.size() - body);
             const size_t bps = (size_t)bits / 8, frames = n / (bps * (size_t)ch);
             mono.assign(frames, 0.f);
@@ -63,7 +78,13 @@ void read_wav(const std::string& path, std::vector<float>& mono, int& rate) {
                 for (int c = 0; c < ch; c++) {
                     const unsigned char* p = base + (i * (size_t)ch + (size_t)c) * bps;
                     float v;
-                    if (fmt == 3) memcpy(&v, p, 4);
+                    if (fmt == 3 && bits == 64) {
+                        double dv;
+                        memcpy(&dv, p, 8);
+                        v = (float)dv;
+                    } else if (fmt == 3) memcpy(&v, p, 4);
+                    else if (fmt == 7) v = (float)ulaw_linear(p[0]) * (1.f / 32768.f);
+                    else if (fmt == 6) v = (float)alaw_linear(p[0]) * (1.f / 32768.f);
                     else if (bits == 16) v = (float)(int16_t)(p[0] | (p[1] << 8)) / 32768.f;
                     else if (bits == 24)
                         v = (float)((int32_t)(((uint32_t)p[0] << 8) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 24)) >> 8) /

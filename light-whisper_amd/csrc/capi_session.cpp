@@ -209,6 +209,38 @@ QASR_API int qasr_model_tokenize(const qasr_model* m, const char* text, size_t l
     });
 }
 
+// a stand-alone byte-level BPE tokenizer (pieces + merges), the model tokenizer's encoder without a model
+struct qasr_tokenizer {
+    qasr::Tokenizer t;
+};
+
+QASR_API int qasr_tokenizer_open(const char* const* pieces, int32_t n_pieces, const uint8_t* is_special,
+                                 const char* const* merges, int32_t n_merges, qasr_tokenizer** out) {
+    return guard([&] {
+        QASR_CHECK(pieces && n_pieces > 0 && n_merges >= 0 && (merges || n_merges == 0) && out, QASR_E_INVALID,
+                   "bad arguments");
+        auto t = std::make_unique<qasr_tokenizer>();
+        t->t.pieces.assign(pieces, pieces + n_pieces);
+        t->t.is_special.assign(n_pieces, 0);
+        if (is_special) t->t.is_special.assign(is_special, is_special + n_pieces);
+        t->t.merges.assign(merges, merges + n_merges);
+        *out = t.release();
+    });
+}
+
+QASR_API int qasr_tokenizer_encode(const qasr_tokenizer* t, const char* text, size_t len, int32_t* ids, size_t cap,
+                                   size_t* n_out) {
+    return guard([&] {
+        QASR_CHECK(t && (text || len == 0) && n_out, QASR_E_INVALID, "null argument");
+        const std::vector<int32_t> v = t->t.encode(std::string(text ? text : "", len));
+        *n_out = v.size();
+        QASR_CHECK(!ids || cap >= v.size(), QASR_E_CAPACITY, "id buffer too small");
+        if (ids && !v.empty()) memcpy(ids, v.data(), v.size() * sizeof(int32_t));
+    });
+}
+
+QASR_API void qasr_tokenizer_close(qasr_tokenizer* t) { delete t; }
+
 QASR_API int qasr_model_detokenize(const qasr_model* m, const int32_t* ids, int32_t n, char* out, size_t cap,
                                   size_t* written) {
     return guard([&] {

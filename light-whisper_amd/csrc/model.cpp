@@ -655,6 +655,9 @@ std::unique_ptr<Model> load_gguf_model(const std::string& path, bool shell) {
     build_tables(m, s);
     m.weights_pending = shell;
     m.tok.pieces = toks->arr_s;
+    // byte-level BPE merges ("a b", by rank) for hot-word context encoding (tokenizer.cpp Tokenizer::encode)
+    if (const GgufValue* mg = f.get("tokenizer.ggml.merges"))
+        if (mg->arr_type == 8) m.tok.merges = mg->arr_s;
     m.tok.is_special.assign(m.tok.pieces.size(), 0);
     if (const GgufValue* tt = f.get("tokenizer.ggml.token_type"))
         for (size_t i = 0; i < tt->arr_i.size() && i < m.tok.is_special.size(); i++)

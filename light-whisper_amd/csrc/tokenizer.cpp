@@ -3,9 +3,12 @@
 #include <string.h>
 
 #include <algorithm>
+#include <climits>
+#include <mutex>
 #include <unordered_map>
 
 #include "common.h"
+#include "unicode_ranges.h"
 
 namespace qasr {
 
@@ -246,7 +249,7 @@ void Tokenizer::parse(const std::string& raw, std::string& language, std::string
     }
 }
 
-std::vector<int32_t> Tokenizer::encode(const std::string& text) const {
+std::vector<int32_t> Tokenizer::encode_greedy(const std::string& text) const {
     const ByteMap& bm = bmap();
     std::unordered_map<std::string, int32_t> index;
     size_t maxlen = 1;
@@ -275,6 +278,158 @@ std::vector<int32_t> Tokenizer::encode(const std::string& text) const {
         QASR_CHECK(best_id >= 0, QASR_E_FORMAT, "tokenizer: byte without a piece");
         out.push_back(best_id);
         i += best;
+    }
+    return out;
+}
+
+struct Tokenizer::Index {
+    std::unordered_map<std::string, int32_t> piece;   // non-special pieces (first id wins)
+    std::unordered_map<std::string, int> rank;        // "a b" → merge rank
+    std::vector<std::pair<std::string, int32_t>> special;   // special pieces, longest first
+};
+
+const Tokenizer::Index& Tokenizer::index() const {
+    static std::mutex mu;   // a model's tokenizer is shared by its sessions' threads
+    std::lock_guard<std::mutex> lock(mu);
+    if (index_) return *index_;
+    auto ix = std::make_shared<Index>();
+    for (int32_t id = 0; id < (int32_t)pieces.size(); id++) {
+        if (pieces[id].empty()) continue;
+        if (!is_special.empty() && is_special[id]) ix->special.emplace_back(pieces[id], id);
+        else ix->piece.emplace(pieces[id], id);
+    }
+    std::stable_sort(ix->special.begin(), ix->special.end(),
+                     [](const auto& a, const auto& b) { return a.first.size() > b.first.size(); });
+    for (int r = 0; r < (int)merges.size(); r++) ix->rank.emplace(merges[r], r);
+    index_ = ix;
+    return *index_;
+}
+
+namespace {
+bool in_ranges(const UniRange* r, size_t n, char32_t c) {
+    size_t lo = 0, hi = n;
+    while (lo < hi) {
+        const size_t mid = (lo + hi) / 2;
+        if (c < r[mid].lo) hi = mid;
+        else if (c > r[mid].hi) lo = mid + 1;
+        else return true;
+    }
+    return false;
+}
+bool uni_L(char32_t c) { return in_ranges(kUniLetter, sizeof kUniLetter / sizeof kUniLetter[0], c); }
+bool uni_N(char32_t c) { return in_ranges(kUniNumber, sizeof kUniNumber / sizeof kUniNumber[0], c); }
+// \s of the regex engines (the Unicode White_Space property)
+bool uni_ws(char32_t c) {
+    return (c >= 0x09 && c <= 0x0D) || c == 0x20 || c == 0x85 || c == 0xA0 || c == 0x1680 || (c >= 0x2000 && c <= 0x200A) ||
+           c == 0x2028 || c == 0x2029 || c == 0x202F || c == 0x205F || c == 0x3000;
+}
+bool uni_nl(char32_t c) { return c == '\r' || c == '\n'; }
+char32_t lower1(char32_t c) { return c >= 'A' && c <= 'Z' ? c + 32 : c; }
+
+// length of the Qwen2 pre-tokenizer match at i (tokenization_qwen2.py PRETOKENIZE_REGEX, alternatives in order):
+//   (?i:'s|'t|'re|'ve|'m|'ll|'d) | [^\r\n\p{L}\p{N}]?\p{L}+ | \p{N} | ?[^\s\p{L}\p{N}]+[\r\n]* | \s*[\r\n]+ |
+//   \s+(?!\S) | \s+
+size_t pretoken(const std::u32string& c, size_t i) {
+    const size_t n = c.size();
+    if (c[i] == '\'' && i + 1 < n) {
+        const char32_t a = lower1(c[i + 1]);
+        if (a == 's' || a == 't' || a == 'm' || a == 'd') return 2;
+        if (i + 2 < n) {
+            const char32_t b = lower1(c[i + 2]);
+            if ((a == 'r' && b == 'e') || (a == 'v' && b == 'e') || (a == 'l' && b == 'l')) return 3;
+        }
+    }
+    auto other = [](char32_t x) { return !uni_ws(x) && !uni_L(x) && !uni_N(x); };
+    {
+        size_t j = i;
+        if (!uni_nl(c[j]) && !uni_L(c[j]) && !uni_N(c[j]) && j + 1 < n && uni_L(c[j + 1])) j++;
+        if (uni_L(c[j])) {
+            while (j < n && uni_L(c[j])) j++;
+            return j - i;
+        }
+    }
+    if (uni_N(c[i])) return 1;
+    {
+        size_t j = i;
+        if (c[j] == ' ' && j + 1 < n && other(c[j + 1])) j++;
+        if (other(c[j])) {
+            while (j < n && other(c[j])) j++;
+            while (j < n && uni_nl(c[j])) j++;
+            return j - i;
+        }
+    }
+    if (uni_ws(c[i])) {
+        size_t j = i;
+        while (j < n && uni_ws(c[j])) j++;
+        for (size_t k = j; k > i; k--)
+            if (uni_nl(c[k - 1])) return k - i;    // \s*[\r\n]+: up to the run's last newline
+        if (j == n) return j - i;                  // \s+(?!\S)
+        if (j - i >= 2) return j - i - 1;          //   (leaving the last space to the next token)
+        return j - i;                              // \s+
+    }
+    return 1;
+}
+}  // namespace
+
+// BPE of one pre-token (byte-level symbols), merges by rank (lowest first, every occurrence left to right)
+void Tokenizer::bpe_word(const std::string& word, const Index& ix, std::vector<int32_t>& out) const {
+    const ByteMap& bm = bmap();
+    std::vector<std::string> sym;
+    for (unsigned char ch : word) {
+        std::string u;
+        append_utf8(u, bm.byte2cp[ch]);
+        sym.push_back(u);
+    }
+    while (sym.size() > 1) {
+        int best = INT32_MAX;
+        size_t at = 0;
+        for (size_t k = 0; k + 1 < sym.size(); k++) {
+            auto it = ix.rank.find(sym[k] + " " + sym[k + 1]);
+            if (it != ix.rank.end() && it->second < best) best = it->second, at = k;
+        }
+        if (best == INT32_MAX) break;
+        const std::string a = sym[at], b = sym[at + 1];
+        std::vector<std::string> nw;
+        for (size_t k = 0; k < sym.size();) {
+            if (k + 1 < sym.size() && sym[k] == a && sym[k + 1] == b) {
+                nw.push_back(a + b);
+                k += 2;
+            } else {
+                nw.push_back(sym[k++]);
+            }
+        }
+        sym.swap(nw);
+    }
+    for (const std::string& x : sym) {
+        auto it = ix.piece.find(x);
+        QASR_CHECK(it != ix.piece.end(), QASR_E_FORMAT, "tokenizer: BPE symbol without a piece");
+        out.push_back(it->second);
+    }
+}
+
+std::vector<int32_t> Tokenizer::encode(const std::string& text) const {
+    if (merges.empty()) return encode_greedy(text);
+    const Index& ix = index();
+    std::vector<int32_t> out;
+    size_t pos = 0;
+    while (pos < text.size()) {
+        // the next special piece (added tokens are matched before the pre-tokenizer)
+        size_t sp_at = std::string::npos;
+        const std::pair<std::string, int32_t>* sp = nullptr;
+        for (const auto& s : ix.special) {
+            const size_t f = text.find(s.first, pos);
+            if (f != std::string::npos && (f < sp_at)) sp_at = f, sp = &s;
+        }
+        const size_t end = sp ? sp_at : text.size();
+        const std::u32string c = to_u32(text.substr(pos, end - pos));
+        for (size_t i = 0; i < c.size();) {
+            const size_t len = pretoken(c, i);
+            bpe_word(to_utf8(c.substr(i, len)), ix, out);
+            i += len;
+        }
+        if (!sp) break;
+        out.push_back(sp->second);
+        pos = sp_at + sp->first.size();
     }
     return out;
 }

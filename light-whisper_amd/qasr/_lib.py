@@ -106,6 +106,9 @@ SIGNATURES = {
     "qasr_resample_linear": (C.c_int, [P, SZ, C.c_double, P, SZ, C.POINTER(SZ)]),
     "qasr_audio_load_path": (C.c_int, [C.c_char_p, P, SZ, C.POINTER(SZ)]),
     "qasr_session_set_draft": (C.c_int, [P, I32]),
+    "qasr_tokenizer_open": (C.c_int, [P, I32, P, P, I32, P]),
+    "qasr_tokenizer_encode": (C.c_int, [P, C.c_char_p, SZ, P, SZ, P]),
+    "qasr_tokenizer_close": (None, [P]),
     "qasr_session_set_draft_noise": (C.c_int, [P, F32, C.c_uint64]),
     "qasr_session_draft_stats": (C.c_int, [P, C.POINTER(C.c_int64)]),
     "qasr_session_set_encoder_cache": (C.c_int, [P, I32]),

@@ -473,6 +473,65 @@ def make_hf_06b():
     print("hf_06b.npz", {k: v.shape for k, v in out.items()})
 
 
+# ---------------------------------------------------------------------------------------------- BPE encode
+BPE_CASES = ["Kubernetes", "张三", "ROCm 7.2", "light-whisper", "I'm here", "don't STOP", "They'LL go", "hello world",
+             "  leading spaces", "trailing spaces   ", "tab\tseparated", "line\nbreak", "crlf\r\nline",
+             "multi\n\n\nblank", "   ", "\n", "", "a", "1234567", "3.14159", "v2.0-rc1", "x86_64", "C++17",
+             "email@example.com", "https://example.com/a?b=c", "深度学习", "语音识别模型", "東京タワー", "カタカナ",
+             "ひらがな", "한국어 음성", "Привет мир", "Ελληνικά", "mixed中文English混合", "数字123和letters",
+             "emoji 😀 test", "(括号)", "「引用」", "full，width。", "€100", "naïve café", "Straße", "ÀÉÎÕÜ",
+             "hot-word, another; third", "Qwen3-ASR", "MI355X", "GPT-4o", "O'Brien", "rock'n'roll", "   x   ",
+             "\u3000全角空格", "a\u00a0b", "end.\r\n", "...!!!???", "#hashtag @mention", "1,000,000",
+             "pi=3.1415926535", "ＡＢＣ１２３", "日本語とEnglishの混在", "word" * 8]
+
+
+def make_bpe():
+    """byte-level BPE encoding of hot-word context (Qwen2 / Qwen3 tokenizer semantics: NFC, the
+    Qwen2 pre-tokenizer regex, GPT-2 byte↔unicode map, BPE merges by rank).  A synthetic vocabulary + merge list is
+    trained here (tokenizers BpeTrainer on a seeded multilingual corpus — no download) and the expected ids of
+    BPE_CASES come from transformers.Qwen2Tokenizer built on it (tests/test_host_cpu.py pins the engine's encoder)."""
+    from tokenizers import Regex, Tokenizer, models, pre_tokenizers, trainers
+    from transformers import Qwen2Tokenizer
+    from transformers.models.qwen2.tokenization_qwen2 import PRETOKENIZE_REGEX
+
+    rng = np.random.default_rng(17)
+    words = ("the quick brown fox jumps over lazy dog speech recognition model audio stream token hot word "
+             "kubernetes cluster deploy gpu kernel memory bandwidth latency throughput english chinese japanese "
+             "don't I'm you're we've they'll she'd it's hello world light whisper").split()
+    han = [chr(c) for c in range(0x4E00, 0x4E00 + 400)] + list("张三深度学习语音识别模型中文混合数字和括号引用全角空格東京")
+    kana = [chr(c) for c in range(0x3041, 0x3097)] + [chr(c) for c in range(0x30A1, 0x30FB)]
+    lines = []
+    for _ in range(4000):
+        k = rng.integers(0, 5)
+        if k == 0:
+            lines.append(" ".join(rng.choice(words, rng.integers(3, 12))))
+        elif k == 1:
+            lines.append("".join(rng.choice(han, rng.integers(2, 20))))
+        elif k == 2:
+            lines.append("".join(rng.choice(kana, rng.integers(2, 12))) + "。")
+        elif k == 3:
+            lines.append(f"{rng.integers(0, 100000)} items, v{rng.integers(0, 9)}.{rng.integers(0, 9)} ok!")
+        else:
+            lines.append(" ".join(rng.choice(words, 3)) + " " + "".join(rng.choice(han, 4)) + "\n\n")
+    tk = Tokenizer(models.BPE())
+    tk.pre_tokenizer = pre_tokenizers.Sequence([pre_tokenizers.Split(Regex(PRETOKENIZE_REGEX), behavior="isolated"),
+                                                pre_tokenizers.ByteLevel(add_prefix_space=False, use_regex=False)])
+    tk.train_from_iterator(lines, trainers.BpeTrainer(vocab_size=1500, initial_alphabet=pre_tokenizers.ByteLevel.alphabet(),
+                                                      show_progress=False))
+    model = json.loads(tk.to_str())["model"]
+    vocab = model["vocab"]
+    merges = [m if isinstance(m, str) else " ".join(m) for m in model["merges"]]
+    vocab = {k: v for k, v in sorted(vocab.items(), key=lambda kv: kv[1])}
+    ref = Qwen2Tokenizer(vocab=dict(vocab), merges=[tuple(m.split(" ")) for m in merges])
+    cases = [{"text": t, "ids": ref.encode(t, add_special_tokens=False)} for t in BPE_CASES]
+    bdir = os.path.join(HERE, "bpe")
+    os.makedirs(bdir, exist_ok=True)
+    json.dump(vocab, open(os.path.join(bdir, "vocab.json"), "w"), ensure_ascii=False)
+    open(os.path.join(bdir, "merges.txt"), "w").write("#version: 0.2\n" + "\n".join(merges) + "\n")
+    json.dump(cases, open(os.path.join(bdir, "cases.json"), "w"), ensure_ascii=False, indent=0)
+    print("bpe:", len(vocab), "pieces,", len(merges), "merges,", len(cases), "cases")
+
+
 # ---------------------------------------------------------------------------------------------- transcript parse
 def make_parse():
     from transformers.models.qwen3_asr.processing_qwen3_asr import _parse_single_output
@@ -514,7 +573,7 @@ def _wav_bytes(frames: np.ndarray, rate: int, fmt: int, bits: int, extensible=Fa
         v = frames.astype("<i4").reshape(-1)
         data = np.stack([(v & 0xFF), (v >> 8) & 0xFF, (v >> 16) & 0xFF], 1).astype(np.uint8).tobytes()
     else:
-        dt = {8: np.uint8, 16: "<i2", 32: "<f4" if fmt == 3 else "<i4"}[bits]
+        dt = {8: np.uint8, 16: "<i2", 32: "<f4" if fmt == 3 else "<i4", 64: "<f8"}[bits]
         data = frames.astype(dt).tobytes()
     ba = ch * bits // 8
     if extensible:
@@ -539,13 +598,19 @@ def make_wav():
         ("pcm8_mono_8k", 8000, 1, 1, 8, 0.8, False),
         ("pcm32_stereo_22k05", 22050, 2, 1, 32, 0.6, False),
         ("pcm16_ext_3ch_16k", 16000, 3, 1, 16, 0.3, True),
+        # float64 and G.711 (fmt 7 µ-law, fmt 6 A-law) — libsndfile decodes them too
+        ("float64_mono_16k", 16000, 1, 3, 64, 0.5, False),
+        ("ulaw_mono_8k", 8000, 1, 7, 8, 0.5, False),
+        ("alaw_stereo_8k", 8000, 2, 6, 8, 0.4, False),
     ]
     for name, rate, ch, fmt, bits, secs, ext in specs:
         n = int(rate * secs)
         x = (0.4 * np.sin(2 * np.pi * 220 * np.arange(n)[:, None] / rate + np.arange(ch)) +
              0.05 * rng.standard_normal((n, ch)))
         if fmt == 3:
-            fr = x.astype(np.float32)
+            fr = x.astype(np.float32 if bits == 32 else np.float64)
+        elif fmt in (6, 7):   # 8-bit G.711 codes of the companded signal (every byte is a valid code)
+            fr = np.clip(np.round(127.5 + 127.5 * np.sign(x) * np.log1p(255 * np.abs(x)) / np.log(256)), 0, 255)
         elif bits == 8:
             fr = np.clip(np.round(x * 127 + 128), 0, 255)
         else:
@@ -576,7 +641,17 @@ def read(path, dtype="float32", always_2d=True):
             if fmt == 0xFFFE: fmt = struct.unpack("<H", d[b + 24:b + 26])[0]
         elif cid == b"data":
             raw = d[b:b + sz]
-            if fmt == 3: x = np.frombuffer(raw, "<f4").astype(np.float32)
+            if fmt == 3 and bits == 64: x = np.frombuffer(raw, "<f8").astype(np.float32)
+            elif fmt == 3: x = np.frombuffer(raw, "<f4").astype(np.float32)
+            elif fmt == 7:   # libsndfile ulaw_decode table (Sun g711.c ulaw2linear), normalised by 1/0x8000
+                u = ~np.frombuffer(raw, np.uint8).astype(np.int32) & 0xFF
+                t = (((u & 0x0F) << 3) + 0x84) << ((u & 0x70) >> 4)
+                x = np.where(u & 0x80, 0x84 - t, t - 0x84).astype(np.float32) * np.float32(1.0 / 32768)
+            elif fmt == 6:   # libsndfile alaw_decode table (Sun g711.c alaw2linear)
+                a = np.frombuffer(raw, np.uint8).astype(np.int32) ^ 0x55
+                t, seg = (a & 0x0F) << 4, (a & 0x70) >> 4
+                t = np.where(seg == 0, t + 8, (t + 0x108) << np.maximum(seg - 1, 0))
+                x = np.where(a & 0x80, t, -t).astype(np.float32) * np.float32(1.0 / 32768)
             elif bits == 16: x = np.frombuffer(raw, "<i2").astype(np.float32) / np.float32(2 ** 15)
             elif bits == 32: x = (np.frombuffer(raw, "<i4").astype(np.float32) / np.float32(2 ** 31)).astype(np.float32)
             elif bits == 8: x = (np.frombuffer(raw, np.uint8).astype(np.float32) - 128) / np.float32(128)
@@ -612,6 +687,6 @@ print(json.dumps(out))
 
 
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["vad_post", "audio_io", "protocol", "dfsmn", "hf_tiny", "hf_06b", "parse", "wav"]
+    which = sys.argv[1:] or ["vad_post", "audio_io", "protocol", "dfsmn", "hf_tiny", "hf_06b", "bpe", "parse", "wav"]
     for w in which:
         globals()[f"make_{w}"]()
