@@ -11,8 +11,9 @@ Workload (BASELINE.json configs[3], "1.7B Q8, VAD-split segments batch-sharded";
 A step = one qasr_run_batch_device call over the rank's resident segments: log-mel → conv stack → encoder →
 projector → prefill → continuous-batching decode → detokenise.
 
-Launch: python bench.py [--gpus N --steps K --warmup W]; N>1 via torch.distributed.run (RCCL only for the
-barrier and the max-over-ranks time).  Prints ONE JSON line (rank 0).
+Launch: python bench.py [--gpus N --steps K --warmup W]; N>1: one rank per GPU under torch.distributed.run (spawned
+by this script when WORLD_SIZE is unset); the weight broadcast and token gather are libqasr's own RCCL communicator,
+torch.distributed carries the barrier and the max-over-ranks time.  Prints ONE JSON line (rank 0).
 """
 from __future__ import annotations
 
@@ -271,14 +272,21 @@ def main():
     torch.cuda.synchronize()
 
     collectives = {}
+    comm = None
     if world > 1:
         # rank 0 builds the weights, every other rank opens a shell of the same device layout and
-        # ONE RCCL broadcast over the whole blob fills it (qasr/dist.py); untimed, like a server's load
+        # ONE RCCL broadcast over the whole blob fills it — libqasr's own communicator (qasr_dist_*; torch only hands
+        # the unique id over); the gloo rehearsal (ranks sharing a card) uses torch.distributed.  Untimed, like a
+        # server's load.
         from qasr import dist as qdist
 
         model = Model.synthetic(args.arch, seed=0) if rank == 0 else Model.shell(args.arch)
-        collectives["weight_broadcast"] = qdist.broadcast_weights(model, rank, torch.device("cuda", local))
-        collectives["backend"] = backend
+        if backend == "gloo":
+            collectives["weight_broadcast"] = qdist.broadcast_weights(model, rank, torch.device("cuda", local))
+        else:
+            comm = qdist.NativeComm(rank, world, local, qdist.torch_exchange)
+            collectives["weight_broadcast"] = comm.broadcast_weights(model)
+        collectives["backend"] = "libqasr-rccl" if comm else backend
     else:
         model = Model.synthetic(args.arch, seed=0)
     if args.precision != "q8":
@@ -346,7 +354,7 @@ def main():
     if world > 1:
         # token streams of every rank to rank 0 (untimed): all-gather of counts, then of the ragged payload
         t_g = time.perf_counter()
-        every = qdist.gather_token_streams(streams, coll_dev)
+        every = comm.gather_tokens(streams) if comm else qdist.gather_token_streams(streams, coll_dev)
         collectives["token_gather"] = {"segments": sum(len(e) for e in every),
                                        "tokens": sum(len(x) for e in every for x in e),
                                        "ms": round((time.perf_counter() - t_g) * 1e3, 3)}
@@ -431,6 +439,8 @@ def main():
         print(json.dumps(line, ensure_ascii=False), flush=True)
     sess.close()
     model.close()
+    if comm:
+        comm.close()
     if world > 1:
         dist.destroy_process_group()
 

@@ -352,6 +352,36 @@ QASR_API int qasr_stream_sync(void* stream);
 QASR_API int qasr_set_deterministic(int32_t on);
 QASR_API int qasr_get_deterministic(int32_t* on);
 
+/* -------------------------------------------------------------------------------------------- multi-GPU */
+/* Native RCCL collectives (north_star: "RCCL over xGMI used only to broadcast Q8 weights and gather
+   token streams"), so a host without PyTorch (the Rust app) drives the N-GPU path over this ABI.
+   One process per GPU.  Rank 0 calls qasr_dist_unique_id and hands the 128 bytes to every rank out of band (a pipe,
+   a file, a TCP store); each rank calls qasr_dist_init with its rank, the world size and its device.
+   qasr_dist_broadcast_weights: ONE broadcast of the model's weight blob from `root` (which loaded or generated it)
+   into the other ranks' shells (qasr_model_open_shell: identical layout), then every rank's wrapping 64-bit blob
+   checksum all-gathered and compared (error if any differs); the shells then accept sessions.
+   qasr_dist_broadcast: the same collective on any device buffer (send NULL = in place).
+   qasr_dist_gather_tokens: every rank's segments' token ids ([n_seg] lengths + the flat ids, host arrays) to every
+   rank, in rank order: rank_segs [world] = segments per rank; with all_lens / all_tokens NULL only the totals are
+   reported (*n_segs_out, *n_tokens_out), then call again with buffers of that size.  Not in the reference (it runs
+   one process, one device, one utterance). */
+typedef struct qasr_comm qasr_comm;
+typedef struct {
+    uint64_t bytes;      /* blob bytes broadcast */
+    double ms;           /* wall time of the broadcast */
+    uint64_t checksum;   /* the root's wrapping 64-bit blob sum */
+    int32_t checksums_agree;
+} qasr_dist_info;
+QASR_API int qasr_dist_unique_id(uint8_t* out /* 128 bytes */, size_t cap);
+QASR_API int qasr_dist_init(const uint8_t* id /* 128 bytes */, int32_t rank, int32_t world, int32_t device,
+                            qasr_comm** out);
+QASR_API void qasr_dist_close(qasr_comm* c);
+QASR_API int qasr_dist_broadcast(qasr_comm* c, const void* send, void* recv, size_t bytes, int32_t root);
+QASR_API int qasr_dist_broadcast_weights(qasr_comm* c, qasr_model* m, int32_t root, qasr_dist_info* info);
+QASR_API int qasr_dist_gather_tokens(qasr_comm* c, const int32_t* lens, int32_t n_seg, const int32_t* tokens,
+                                     int32_t* rank_segs /* [world] */, int32_t* all_lens, size_t lens_cap,
+                                     int32_t* all_tokens, size_t tokens_cap, size_t* n_segs_out, size_t* n_tokens_out);
+
 /* -------------------------------------------------------------------------------------------- profiling */
 /* live per-kernel-class timing (hipEvents on each instrumented launch's stream) + algorithmic FLOPs/bytes;
    report = JSON {"gemm_q8": {"count", "ms", "flops", "bytes"}, ...}.  Used by bench.py for its roofline. */

@@ -1,0 +1,203 @@
+// extern "C": the native multi-GPU collectives (north_star: "RCCL over xGMI used only to broadcast Q8
+// weights and gather token streams").  One process per GPU; the host (Rust via the C ABI, or bench.py / qasr.dist
+// over ctypes) exchanges the 128-byte unique id out of band, then every rank opens a communicator on its device.
+//   * qasr_dist_broadcast_weights: ONE ncclBroadcast over the model's whole weight blob (rank 0 loaded or generated
+//     it, the others hold shells of the identical layout, qasr_model_open_shell) — a single large message, the shape
+//     a per-link-bound ring over xGMI wants — then a wrapping 64-bit checksum per rank, all-gathered and compared;
+//   * qasr_dist_gather_tokens: every rank's per-segment token ids to every rank (two all-gathers: the counts, then
+//     the ragged payload padded to the largest rank).
+// Neither runs inside a timed step.  The reference has no multi-GPU path.
+#include <string.h>
+
+#include <chrono>
+#include <memory>
+#include <vector>
+
+#include <rccl/rccl.h>
+
+#include "../../include/qasr.h"
+#include "capi_handles.h"
+#include "capi_util.h"
+
+using namespace qasr;
+
+struct qasr_comm {
+    ncclComm_t c = nullptr;
+    int rank = 0, world = 1, device = 0;
+    hipStream_t st = nullptr;
+    ~qasr_comm() {
+        if (c) (void)ncclCommDestroy(c);
+        if (st) (void)hipStreamDestroy(st);
+    }
+};
+
+namespace {
+
+#define QASR_NCCL(x)                                                                                              \
+    do {                                                                                                          \
+        const ncclResult_t r_ = (x);                                                                              \
+        if (r_ != ncclSuccess) throw Error(QASR_E_BACKEND, std::string("RCCL: ") + #x + ": " + ncclGetErrorString(r_)); \
+    } while (0)
+
+// wrapping 64-bit sum of a blob (bytes % 8 == 0): order-independent, so every rank's value is the same for the
+// same bytes whatever the reduction order
+__global__ void k_blob_checksum(const unsigned long long* __restrict__ p, size_t n, unsigned long long* out) {
+    __shared__ unsigned long long part[256];
+    unsigned long long s = 0;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) s += p[i];
+    part[threadIdx.x] = s;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if ((int)threadIdx.x < o) part[threadIdx.x] += part[threadIdx.x + o];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) atomicAdd(out, part[0]);
+}
+
+uint64_t blob_checksum(const void* dev, size_t bytes, unsigned long long* scratch, hipStream_t st) {
+    QASR_CHECK(bytes % 8 == 0, QASR_E_INVALID, "checksum: blob size must be a multiple of 8");
+    QASR_HIP(hipMemsetAsync(scratch, 0, sizeof(unsigned long long), st));
+    k_blob_checksum<<<1024, 256, 0, st>>>((const unsigned long long*)dev, bytes / 8, scratch);
+    QASR_HIP(hipGetLastError());
+    unsigned long long h = 0;
+    QASR_HIP(hipMemcpyAsync(&h, scratch, sizeof h, hipMemcpyDeviceToHost, st));
+    QASR_HIP(hipStreamSynchronize(st));
+    return h;
+}
+
+template <class T>
+struct DevBuf {
+    T* p = nullptr;
+    explicit DevBuf(size_t n) { QASR_HIP(hipMalloc(&p, std::max<size_t>(n, 1) * sizeof(T))); }
+    ~DevBuf() {
+        if (p) (void)hipFree(p);
+    }
+};
+
+}  // namespace
+
+extern "C" {
+
+QASR_API int qasr_dist_unique_id(uint8_t* out, size_t cap) {
+    return guard([&] {
+        QASR_CHECK(out && cap >= NCCL_UNIQUE_ID_BYTES, QASR_E_INVALID, "unique id buffer: 128 bytes");
+        ncclUniqueId id;
+        QASR_NCCL(ncclGetUniqueId(&id));
+        memcpy(out, id.internal, NCCL_UNIQUE_ID_BYTES);
+    });
+}
+
+QASR_API int qasr_dist_init(const uint8_t* id, int32_t rank, int32_t world, int32_t device, qasr_comm** out) {
+    return guard([&] {
+        QASR_CHECK(id && out && world >= 1 && rank >= 0 && rank < world, QASR_E_INVALID, "bad arguments");
+        auto c = std::make_unique<qasr_comm>();
+        QASR_HIP(hipSetDevice(device));
+        ncclUniqueId uid;
+        memcpy(uid.internal, id, NCCL_UNIQUE_ID_BYTES);
+        QASR_NCCL(ncclCommInitRank(&c->c, world, uid, rank));
+        QASR_HIP(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
+        c->rank = rank, c->world = world, c->device = device;
+        *out = c.release();
+    });
+}
+
+QASR_API void qasr_dist_close(qasr_comm* c) { delete c; }
+
+QASR_API int qasr_dist_broadcast(qasr_comm* c, const void* send, void* recv, size_t bytes, int32_t root) {
+    return guard([&] {
+        QASR_CHECK(c && recv && root >= 0 && root < c->world, QASR_E_INVALID, "bad arguments");
+        QASR_NCCL(ncclBroadcast(send ? send : recv, recv, bytes, ncclUint8, root, c->c, c->st));
+        QASR_HIP(hipStreamSynchronize(c->st));
+    });
+}
+
+QASR_API int qasr_dist_broadcast_weights(qasr_comm* c, qasr_model* m, int32_t root, qasr_dist_info* info) {
+    return guard([&] {
+        QASR_CHECK(c && m && root >= 0 && root < c->world, QASR_E_INVALID, "bad arguments");
+        Model& md = *m->m;
+        QASR_CHECK(c->rank == root || md.weights_pending, QASR_E_INVALID,
+                   "weight broadcast: non-root ranks receive into a shell (qasr_model_open_shell)");
+        QASR_HIP(hipDeviceSynchronize());   // the root's load / generation has landed
+        const auto t0 = std::chrono::steady_clock::now();
+        QASR_NCCL(ncclBroadcast(md.mem.base, md.mem.base, md.mem.bytes, ncclUint8, root, c->c, c->st));
+        QASR_HIP(hipStreamSynchronize(c->st));
+        const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        // every rank's checksum, all-gathered: the copy is verified before sessions may open
+        DevBuf<unsigned long long> scratch(1);
+        const uint64_t mine = blob_checksum(md.mem.base, md.mem.bytes, scratch.p, c->st);
+        DevBuf<unsigned long long> all((size_t)c->world);
+        QASR_HIP(hipMemcpyAsync(all.p + c->rank, &mine, sizeof mine, hipMemcpyHostToDevice, c->st));
+        QASR_NCCL(ncclAllGather(all.p + c->rank, all.p, 1, ncclUint64, c->c, c->st));
+        std::vector<uint64_t> sums((size_t)c->world);
+        QASR_HIP(hipMemcpyAsync(sums.data(), all.p, sums.size() * 8, hipMemcpyDeviceToHost, c->st));
+        QASR_HIP(hipStreamSynchronize(c->st));
+        bool agree = true;
+        for (uint64_t s : sums) agree = agree && s == sums[(size_t)root];
+        if (info) {
+            info->bytes = (uint64_t)md.mem.bytes;
+            info->ms = ms;
+            info->checksum = sums[(size_t)root];
+            info->checksums_agree = agree ? 1 : 0;
+        }
+        QASR_CHECK(agree, QASR_E_BACKEND, "weight broadcast: checksums differ across ranks");
+        if (c->rank != root) md.weights_pending = false;
+    });
+}
+
+QASR_API int qasr_dist_gather_tokens(qasr_comm* c, const int32_t* lens, int32_t n_seg, const int32_t* tokens,
+                                     int32_t* rank_segs, int32_t* all_lens, size_t lens_cap, int32_t* all_tokens,
+                                     size_t tokens_cap, size_t* n_segs_out, size_t* n_tokens_out) {
+    return guard([&] {
+        QASR_CHECK(c && n_seg >= 0 && (lens || n_seg == 0) && rank_segs && n_segs_out && n_tokens_out,
+                   QASR_E_INVALID, "bad arguments");
+        int64_t ntok = 0;
+        for (int i = 0; i < n_seg; i++) {
+            QASR_CHECK(lens[i] >= 0, QASR_E_INVALID, "negative segment length");
+            ntok += lens[i];
+        }
+        QASR_CHECK(ntok == 0 || tokens, QASR_E_INVALID, "tokens missing");
+        const int W = c->world;
+        // (1) counts
+        DevBuf<int64_t> cnt((size_t)2 * W);
+        const int64_t mine[2] = {n_seg, ntok};
+        QASR_HIP(hipMemcpyAsync(cnt.p + 2 * c->rank, mine, sizeof mine, hipMemcpyHostToDevice, c->st));
+        QASR_NCCL(ncclAllGather(cnt.p + 2 * c->rank, cnt.p, 2, ncclInt64, c->c, c->st));
+        std::vector<int64_t> counts((size_t)2 * W);
+        QASR_HIP(hipMemcpyAsync(counts.data(), cnt.p, counts.size() * 8, hipMemcpyDeviceToHost, c->st));
+        QASR_HIP(hipStreamSynchronize(c->st));
+        int64_t max_seg = 1, max_tok = 1, tot_seg = 0, tot_tok = 0;
+        for (int r = 0; r < W; r++) {
+            max_seg = std::max(max_seg, counts[2 * r]);
+            max_tok = std::max(max_tok, counts[2 * r + 1]);
+            tot_seg += counts[2 * r];
+            tot_tok += counts[2 * r + 1];
+            rank_segs[r] = (int32_t)counts[2 * r];
+        }
+        *n_segs_out = (size_t)tot_seg;
+        *n_tokens_out = (size_t)tot_tok;
+        if (!all_lens && !all_tokens) return;   // size query
+        QASR_CHECK(all_lens && all_tokens && lens_cap >= (size_t)tot_seg && tokens_cap >= (size_t)tot_tok,
+                   QASR_E_CAPACITY, "gather buffers too small");
+        // (2) the ragged payload, padded to the largest rank
+        DevBuf<int32_t> dl((size_t)max_seg * W), dt((size_t)max_tok * W);
+        QASR_HIP(hipMemsetAsync(dl.p + max_seg * c->rank, 0, (size_t)max_seg * 4, c->st));
+        QASR_HIP(hipMemsetAsync(dt.p + max_tok * c->rank, 0, (size_t)max_tok * 4, c->st));
+        if (n_seg) QASR_HIP(hipMemcpyAsync(dl.p + max_seg * c->rank, lens, (size_t)n_seg * 4, hipMemcpyHostToDevice, c->st));
+        if (ntok) QASR_HIP(hipMemcpyAsync(dt.p + max_tok * c->rank, tokens, (size_t)ntok * 4, hipMemcpyHostToDevice, c->st));
+        QASR_NCCL(ncclAllGather(dl.p + max_seg * c->rank, dl.p, (size_t)max_seg, ncclInt32, c->c, c->st));
+        QASR_NCCL(ncclAllGather(dt.p + max_tok * c->rank, dt.p, (size_t)max_tok, ncclInt32, c->c, c->st));
+        std::vector<int32_t> hl((size_t)max_seg * W), ht((size_t)max_tok * W);
+        QASR_HIP(hipMemcpyAsync(hl.data(), dl.p, hl.size() * 4, hipMemcpyDeviceToHost, c->st));
+        QASR_HIP(hipMemcpyAsync(ht.data(), dt.p, ht.size() * 4, hipMemcpyDeviceToHost, c->st));
+        QASR_HIP(hipStreamSynchronize(c->st));
+        size_t os = 0, ot = 0;
+        for (int r = 0; r < W; r++) {
+            memcpy(all_lens + os, hl.data() + (size_t)max_seg * r, (size_t)counts[2 * r] * 4);
+            memcpy(all_tokens + ot, ht.data() + (size_t)max_tok * r, (size_t)counts[2 * r + 1] * 4);
+            os += (size_t)counts[2 * r];
+            ot += (size_t)counts[2 * r + 1];
+        }
+    });
+}
+
+}  // extern "C"

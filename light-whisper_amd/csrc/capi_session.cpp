@@ -18,15 +18,7 @@
 
 using namespace qasr;
 
-struct qasr_model {
-    std::unique_ptr<Model> m;
-};
-struct qasr_session {
-    std::unique_ptr<Session> s;
-};
-struct qasr_vad {
-    std::unique_ptr<Vad> v;
-};
+#include "capi_handles.h"
 
 namespace {
 

@@ -106,6 +106,12 @@ SIGNATURES = {
     "qasr_resample_linear": (C.c_int, [P, SZ, C.c_double, P, SZ, C.POINTER(SZ)]),
     "qasr_audio_load_path": (C.c_int, [C.c_char_p, P, SZ, C.POINTER(SZ)]),
     "qasr_session_set_draft": (C.c_int, [P, I32]),
+    "qasr_dist_unique_id": (C.c_int, [P, SZ]),
+    "qasr_dist_init": (C.c_int, [P, I32, I32, I32, P]),
+    "qasr_dist_close": (None, [P]),
+    "qasr_dist_broadcast": (C.c_int, [P, P, P, SZ, I32]),
+    "qasr_dist_broadcast_weights": (C.c_int, [P, P, I32, P]),
+    "qasr_dist_gather_tokens": (C.c_int, [P, P, I32, P, P, P, SZ, P, SZ, P, P]),
     "qasr_tokenizer_open": (C.c_int, [P, I32, P, P, I32, P]),
     "qasr_tokenizer_encode": (C.c_int, [P, C.c_char_p, SZ, P, SZ, P]),
     "qasr_tokenizer_close": (None, [P]),

@@ -1,6 +1,10 @@
 """The two collectives of the multi-GPU path (north_star: "RCCL over xGMI used only to broadcast Q8
-weights and gather token streams").  One process per GPU, torch.distributed with the "nccl" backend (= RCCL on
-ROCm) on the GPU box, "gloo" in the CPU tests; nothing here runs inside a timed step.
+weights and gather token streams").  One process per GPU; nothing here runs inside a timed step.
+
+On GPUs the collectives are libqasr's own RCCL communicator (`NativeComm`, include/qasr.h qasr_dist_*: the path a
+host without PyTorch — the Rust app — drives); torch.distributed only carries the 128-byte unique id to every rank
+(and the bench's barrier / timing reductions).  The torch.distributed versions below serve the "gloo" rehearsal
+(ranks sharing one card, which RCCL refuses) and the CPU tests.
 
 * `broadcast_weights`: rank 0 holds the loaded (or generated) model, every other rank a shell with the identical
   device layout (`Model.shell`, include/qasr.h qasr_model_open_shell); ONE broadcast over the whole weight blob
@@ -111,3 +115,87 @@ def gather_token_streams(streams: list[list[int]], device) -> list[list[list[int
         offs = np.concatenate([[0], np.cumsum(ln)])
         out.append([tk[offs[i]:offs[i + 1]].tolist() for i in range(nseg)])
     return out
+
+
+class NativeComm:
+    """libqasr's RCCL communicator (qasr_dist_*).  Rank 0 creates the unique id; `exchange` (any callable that
+    returns rank 0's bytes on every rank, e.g. torch.distributed.broadcast_object_list) distributes it."""
+
+    def __init__(self, rank: int, world: int, device: int, exchange):
+        import ctypes as C
+
+        from . import _lib
+
+        self._lib = _lib.load()
+        uid = (C.c_uint8 * 128)()
+        if rank == 0:
+            _lib.check(self._lib.qasr_dist_unique_id(uid, 128))
+        got = exchange(bytes(uid))
+        uid = (C.c_uint8 * 128).from_buffer_copy(got)
+        self._h = C.c_void_p()
+        _lib.check(self._lib.qasr_dist_init(uid, rank, world, device, C.byref(self._h)))
+        self.rank, self.world = rank, world
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.qasr_dist_close(self._h)
+            self._h = None
+
+    def broadcast_weights(self, model, root: int = 0) -> dict:
+        """rank `root`'s model blob into every other rank's shell; checksums compared inside (error if any differs)"""
+        import ctypes as C
+
+        from . import _lib
+
+        class Info(C.Structure):
+            _fields_ = [("bytes", C.c_uint64), ("ms", C.c_double), ("checksum", C.c_uint64),
+                        ("checksums_agree", C.c_int32)]
+
+        info = Info()
+        _lib.check(self._lib.qasr_dist_broadcast_weights(self._h, model._h, root, C.byref(info)))
+        return {"bytes": int(info.bytes), "ms": round(info.ms, 3), "native_rccl": True,
+                "GB_per_s": round(info.bytes / info.ms / 1e6, 1) if info.ms > 0 else None,
+                "checksums_agree": bool(info.checksums_agree)}
+
+    def broadcast(self, send_ptr, recv_ptr: int, nbytes: int, root: int = 0):
+        from . import _lib
+
+        _lib.check(self._lib.qasr_dist_broadcast(self._h, send_ptr, recv_ptr, nbytes, root))
+
+    def gather_tokens(self, streams: list[list[int]]) -> list[list[list[int]]]:
+        """every rank's per-segment token ids → [rank][segment] -> ids, on every rank"""
+        import ctypes as C
+
+        from . import _lib
+
+        lens = np.array([len(x) for x in streams], np.int32)
+        flat = np.concatenate([np.asarray(x, np.int32) for x in streams]) if lens.sum() else np.zeros(1, np.int32)
+        rank_segs = (C.c_int32 * self.world)()
+        ns, nt = C.c_size_t(0), C.c_size_t(0)
+        vp = lambda a: a.ctypes.data_as(C.c_void_p)  # noqa: E731
+        _lib.check(self._lib.qasr_dist_gather_tokens(self._h, vp(lens) if lens.size else None, int(lens.size),
+                                                     vp(flat), rank_segs, None, 0, None, 0, C.byref(ns),
+                                                     C.byref(nt)))
+        al = np.zeros(max(1, ns.value), np.int32)
+        at = np.zeros(max(1, nt.value), np.int32)
+        _lib.check(self._lib.qasr_dist_gather_tokens(self._h, vp(lens) if lens.size else None, int(lens.size),
+                                                     vp(flat), rank_segs, vp(al), al.size, vp(at), at.size,
+                                                     C.byref(ns), C.byref(nt)))
+        out, s0, t0 = [], 0, 0
+        for r in range(self.world):
+            segs = []
+            for ln in al[s0:s0 + rank_segs[r]]:
+                segs.append(at[t0:t0 + int(ln)].tolist())
+                t0 += int(ln)
+            s0 += rank_segs[r]
+            out.append(segs)
+        return out
+
+
+def torch_exchange(payload: bytes) -> bytes:
+    """rank 0's bytes on every rank over the initialised torch.distributed group (the unique-id hand-off)"""
+    import torch.distributed as dist
+
+    box = [payload if dist.get_rank() == 0 else None]
+    dist.broadcast_object_list(box, src=0)
+    return box[0]
