@@ -128,22 +128,68 @@ def traffic_per_launch(kernel):
 
 
 # bench kernel class (ProfScope names) → tools/pmc_classes.py classes it spans
-PMC_CLASSES = {"gemm_q8": ("gemm_q8_prefill", "gemm_q8_decode"), "gemm_mx": ("gemm_mx",),
-               "attention": ("attention_decode", "attention_tile"), "gemv_q8": ("gemv_q8",)}
+PMC_CLASSES = {"gemm_q8_prefill": ("gemm_q8_prefill",), "gemm_q8_decode": ("gemm_q8_decode",), "gemm_mx": ("gemm_mx",),
+               "attention": ("attention_decode", "attention_tile"), "gemv_q8": ("gemv_q8",),
+               "conv3x3_f16": ("conv3x3",)}
+# compute-bound classes (priced against the dense MFMA peak of their dtype, MI355X_MICROARCH.md); the rest stream HBM
+MFMA_PEAK_TF = {"gemm_q8_prefill": 5000.0, "gemm_mx": 5000.0, "conv3x3_f16": 2500.0, "mel_frames": 2500.0}
+
+
+def class_roofline(name, p):
+    """roofline object of one kernel class from the instrumented step: algorithmic flops (MFMA classes) or bytes
+    (the others) per launch ÷ the class's average launch time (HIP events on the engine's stream)"""
+    avg_s = p["ms"] / p["count"] / 1e3
+    base = {"kernel": name, "avg_launch_us": round(avg_s * 1e6, 2), "launches": p["count"],
+            "ms_per_step": round(p["ms"], 3),
+            "algorithmic_bytes_per_launch": round(p["bytes"] / p["count"]),
+            "measured_on": "one instrumented step after the timed region (HIP events per launch)"}
+    if name in MFMA_PEAK_TF:
+        peak = MFMA_PEAK_TF[name]
+        ach = p["flops"] / p["count"] / avg_s / 1e12
+        r = {"bound": "mfma", "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s", "frac": round(ach / peak, 4),
+             "traffic": traffic_per_launch(name)}
+    else:
+        ach = p["bytes"] / p["count"] / avg_s / 1e9
+        r = {"bound": "hbm", "achieved": round(ach, 1), "peak": 8000.0, "unit": "GB/s", "frac": round(ach / 8000.0, 4),
+             "traffic": None}
+    r.update(base)
+    ev = pmc_evidence(name)
+    if ev:
+        r["committed_pmc"] = ev
+        if ev["matches_build"]:   # counters of this very build: they stand for the class's traffic
+            r["mfma_busy"], r["hbm_gbps"] = ev["mfma_busy"], ev["hbm_gbps"]
+            r["traffic"] = ev["hbm_bytes_per_launch"]
+    return r
+
+
+def lib_sha16():
+    import hashlib
+
+    p = os.path.join(ROOT, "light-whisper_amd", "libqasr.so")
+    return hashlib.sha256(open(p, "rb").read()).hexdigest()[:16] if os.path.exists(p) else None
 
 
 def pmc_evidence(kernel):
-    """MFMA-busy and HBM traffic of `kernel`'s class from the newest committed per-class counter passes of this bench
-    command (profiles/*pmc_classes*.json, tools/pmc_round.sh → tools/pmc_classes.py; raw SQ/GRBM/TCC counters
-    summed over the classes it spans): MFMA busy = SQ_VALU_MFMA_BUSY_CYCLES / (1,024 SIMDs × GRBM_GUI_ACTIVE/8),
-    HBM = 2·FETCH_SIZE + WRITE_SIZE (gfx950 FETCH_SIZE counts half of 16-B streaming reads).  None if absent."""
+    """MFMA-busy and HBM traffic of `kernel`'s class from committed per-class counter passes of this bench command
+    (profiles/*pmc_classes*.json, tools/pmc_round.sh → tools/pmc_classes.py; raw SQ/GRBM/TCC counters summed over the
+    classes it spans): MFMA busy = SQ_VALU_MFMA_BUSY_CYCLES / (1,024 SIMDs × GRBM_GUI_ACTIVE/8), HBM = 2·FETCH_SIZE +
+    WRITE_SIZE (gfx950 FETCH_SIZE counts half of 16-B streaming reads).  These are COMMITTED counters, not measured by
+    this run: the file whose recorded library hash equals the loaded libqasr.so is used (matches_build true), else the
+    newest by its recorded timestamp (matches_build false: counters of an earlier build).  None if absent."""
     import glob
 
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_classes*.json")))
+    files = glob.glob(os.path.join(ROOT, "profiles", "*pmc_classes*.json"))
     names = PMC_CLASSES.get(kernel, (kernel,))
     if not files:
         return None
-    with open(files[-1]) as f:
+    sha = lib_sha16()
+    meta = {}
+    for fpath in files:
+        with open(fpath) as f:
+            meta[fpath] = json.load(f).get("_meta", {})
+    same = [fp for fp in files if sha and meta[fp].get("lib_sha256_16") == sha]
+    pick = max(same or files, key=lambda fp: (meta[fp].get("generated_utc", ""), os.path.basename(fp)))
+    with open(pick) as f:
         pmc = json.load(f)
     busy = grbm = fetch = write = time_ns = launches = 0.0
     found = []
@@ -161,7 +207,8 @@ def pmc_evidence(kernel):
     if not found:
         return None
     hbm_bytes = (2 * fetch + write) * 1024
-    return {"source": os.path.relpath(files[-1], ROOT), "classes": found,
+    return {"source": os.path.relpath(pick, ROOT), "matches_build": bool(same), "classes": found,
+            "note": "committed counters from the source file's rocprofv3 --pmc passes, not measured by this run",
             "mfma_busy": round(busy / (1024 * grbm / 8), 4) if grbm else None,
             "hbm_gbps": round(hbm_bytes / time_ns, 1) if time_ns else None,
             "hbm_bytes_per_launch": round(hbm_bytes / launches) if launches else None}
@@ -371,30 +418,13 @@ def main():
         # roofline of the dominant kernel class (most device time inside the timed region)
         roof = None
         if prof:
-            name, p = max(prof.items(), key=lambda kv: kv[1]["ms"])
-            avg_s = p["ms"] / p["count"] / 1e3
-            if name in ("gemm_q8", "gemm_mx", "conv3x3_f16", "mel_frames"):
-                # dense i8 / MX-fp8 / f16 MFMA peaks (MI355X_MICROARCH.md)
-                peak = 5000.0 if name in ("gemm_q8", "gemm_mx") else 2500.0
-                ach = p["flops"] / p["count"] / avg_s / 1e12
-                roof = {"bound": "mfma", "kernel": name, "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
-                        "frac": round(ach / peak, 4), "traffic": traffic_per_launch(name),
-                        "algorithmic_bytes_per_launch": round(p["bytes"] / p["count"]),
-                        "avg_launch_us": round(avg_s * 1e6, 2), "launches": p["count"],
-                        "measured_on": "one instrumented step after the timed region (HIP events per launch)"}
-            else:
-                ach = p["bytes"] / p["count"] / avg_s / 1e9
-                roof = {"bound": "hbm", "kernel": name, "achieved": round(ach, 1), "peak": 8000.0, "unit": "GB/s",
-                        "frac": round(ach / 8000.0, 4), "traffic": None,
-                        "avg_launch_us": round(avg_s * 1e6, 2), "launches": p["count"],
-                        "measured_on": "one instrumented step after the timed region (HIP events per launch)"}
-            # hardware-counter evidence for the same kernel class (north_star: "rocprof HBM GB/s and MFMA-busy")
-            ev = pmc_evidence(name)
-            if ev:
-                roof["mfma_busy"], roof["hbm_gbps"] = ev["mfma_busy"], ev["hbm_gbps"]
-                roof["traffic"] = ev["hbm_bytes_per_launch"]   # the newest counter passes supersede older ones
-                roof["pmc"] = ev
-            roof["breakdown_ms"] = {k: round(v["ms"], 3) for k, v in sorted(prof.items(), key=lambda kv: -kv[1]["ms"])}
+            # the dominant kernel class (most device time in the instrumented step) is the line's roofline; the other
+            # heavy classes follow in by_class, each priced against its own bound (decode GEMMs stream weights, the
+            # prefill GEMMs are MFMA-bound)
+            order = sorted(prof.items(), key=lambda kv: -kv[1]["ms"])
+            roof = class_roofline(*order[0])
+            roof["by_class"] = {k: class_roofline(k, v) for k, v in order[1:5]}
+            roof["breakdown_ms"] = {k: round(v["ms"], 3) for k, v in order}
         cpu = None
         if not args.no_cpu_baseline:
             try:

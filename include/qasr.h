@@ -287,11 +287,6 @@ QASR_API int qasr_op_gemm_mx(const uint8_t* x8, const uint8_t* xs, int32_t M, co
 QASR_API int qasr_op_linear_q8_ex(const int8_t* xq, const float* xd, int32_t M, const int8_t* wqs, const void* wsc,
                                   int32_t N, int32_t K, const float* bias, void* y, int32_t ldy, int32_t epi,
                                   int8_t* yq, float* yd, int32_t cfg, void* stream);
-/* Q8 GEMM on f16-carried operands (each f16 holds a Q8 integer exactly): y = epi(X·Wᵀ), scales as qasr_op_linear_q8;
-   K % 64 == 0; cfg 0..3 = tiles 128x128, 64x128, 64x64, 128x64. */
-QASR_API int qasr_op_linear_q8h(const void* xq16, const float* xd, int32_t M, const void* wq16, const void* wsc,
-                                int32_t N, int32_t K, const float* bias, const float* res, float* y, int32_t ldy,
-                                int32_t epi, int32_t cfg, void* stream);
 QASR_API int qasr_op_swiglu_q8_interleaved(const float* gu, int32_t M, int32_t F, int8_t* q, float* d, void* stream);
 /* The 1–4-row decoder GEMV (about one workgroup per CU) with the row operations around it fused; bit-identical to
    the separate launches.  pro 0: activations = the Q8 rows xq [M][K] / xd [M][K/32], K ≤ 6144; pro 1: activations

@@ -101,17 +101,6 @@ QASR_API int qasr_op_linear_q8_ex(const int8_t* xq, const float* xd, int32_t M, 
     });
 }
 
-QASR_API int qasr_op_linear_q8h(const void* xq16, const float* xd, int32_t M, const void* wq16, const void* wsc,
-                                int32_t N, int32_t K, const float* bias, const float* res, float* y, int32_t ldy,
-                                int32_t epi, int32_t cfg, void* stream) {
-    return guard([&] {
-        QASR_CHECK(K % 64 == 0 && N > 0 && M > 0 && ldy >= N && epi >= 0 && epi <= 2, QASR_E_INVALID,
-                   "linear_q8h: bad shape");
-        gemm_q8h((const __half*)xq16, xd, M, (const __half*)wq16, (const __half*)wsc, N, K, bias, res, y, ldy, epi,
-                 cfg, S(stream));
-        launched();
-    });
-}
 
 QASR_API int qasr_op_rmsnorm_q8(const float* x, int32_t M, int32_t H, const float* w, float eps, int8_t* q, float* d,
                                 void* stream) {

@@ -67,9 +67,6 @@ bool stable_order();
 void gemm_q8(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const float* bias, const float* res, float* y,
              int ldy, int epi, hipStream_t s, int force_cfg = -1, int force_splits = 0, int8_t* yq = nullptr,
              float* yd = nullptr, bool y_zeroed = false);
-// the Q8 GEMM on f16-carried int8 operands (x [M][K], w [N][K] f16 holding the Q8 integers; scales as gemm_q8)
-void gemm_q8h(const __half* xq, const float* xd, int M, const __half* wq, const __half* wsc, int N, int K,
-              const float* bias, const float* res, float* y, int ldy, int epi, int cfg, hipStream_t s);
 // MXFP8 precision mode (C5): Q8 blocks → e4m3 elements + e8m0 block exponents (activations f32 d, weights f16 d);
 // the block-scaled fp8 GEMM (same epilogues as gemm_q8, K % 128 == 0); gemm_q8 routes to it when W.mx is set,
 // converting the Q8 activations into the workspace registered by set_mx_workspace

@@ -329,10 +329,14 @@ __global__ __launch_bounds__(256) void k_conv3x3_gelu_c32(const __half* __restri
 // contributes one contiguous 2·BK-byte run.  Tile 256 positions × 160 channels (C = 480: three column tiles, so
 // each gathered activation panel is re-read 3×, not 5× as with 96-channel tiles — the kernel is bound by these
 // L2/Infinity-Cache re-reads, ≈120 GB per C4 step at 96×128), 8 waves of 64×80, K step 96 (three 32-deep MFMA
-// slices), one LDS buffer (row stride 104 halves: conflict-free b128 fragments; 86 KB) refilled from a register
-// prefetch of the next step between two barriers, and unconditional clamped staging loads (padding taps and tails
-// zeroed by masks at the LDS write).  128×96 → 128×160 → 256×160: 20.6 → 16.1 → 15.0 ms per C4 step.
-constexpr int CV_BM = 256, CV_BN = 160, CV_BK = 96, CV_LD = CV_BK + 8, CV_TJ = CV_BN / 32, CV_NT = 512;
+// slices), one LDS buffer (78 KB) refilled from a register prefetch of the next step between two barriers, and
+// unconditional clamped staging loads (padding taps and tails zeroed by masks at the LDS write).  128×96 → 128×160 →
+// 256×160: 20.6 → 16.1 → 15.0 ms per C4 step.  LDS image: 192-B rows (no pad), 16-B chunk c of row r at chunk
+// c ^ ((r >> 1) & 3): every ds_read_b128 fragment lane group ({0–3,12–15,20–27}, … — MI355X_MICROARCH.md §LDS) and
+// every ds_write_b128 8-lane group hits distinct banks (the previous 208-B padded rows were 2-way on both; r2 PMC:
+// 3.6 conflict cycles per LDS instruction).
+constexpr int CV_BM = 256, CV_BN = 160, CV_BK = 96, CV_LD = CV_BK, CV_TJ = CV_BN / 32, CV_NT = 512;
+__device__ __forceinline__ int cv_swz(int row) { return (row >> 1) & 3; }
 constexpr int CV_ACH = CV_BM * (CV_BK / 8) / CV_NT;                  // 6 A chunks of 16 B per thread
 constexpr int CV_BCH = (CV_BN * (CV_BK / 8) + CV_NT - 1) / CV_NT;            // B chunks per thread (last partial)
 
@@ -400,15 +404,16 @@ __global__ __launch_bounds__(CV_NT) void k_conv3x3_gelu(const __half* __restrict
 #pragma unroll
         for (int c = 0; c < CV_ACH; c++) {
             const int ch = tid + CV_NT * c;
-            *(int4*)(&As[buf][(ch / SEG) * CV_LD + (ch % SEG) * 8]) = masked(ra[c], oka >> c);
+            *(int4*)(&As[buf][(ch / SEG) * CV_LD + ((ch % SEG) ^ cv_swz(ch / SEG)) * 8]) = masked(ra[c], oka >> c);
         }
 #pragma unroll
         for (int c = 0; c < CV_BCH; c++) {
             const int ch = tid + CV_NT * c;
-            if (ch < CV_BN * SEG) *(int4*)(&Bs[buf][(ch / SEG) * CV_LD + (ch % SEG) * 8]) = masked(rb[c], okb >> c);
+            if (ch < CV_BN * SEG)
+                *(int4*)(&Bs[buf][(ch / SEG) * CV_LD + ((ch % SEG) ^ cv_swz(ch / SEG)) * 8]) = masked(rb[c], okb >> c);
         }
     };
-    const int fr = lane & 15, fk = 8 * (lane >> 4);
+    const int fr = lane & 15, kg = lane >> 4;
     gload(0);
     lstore(0);
     __syncthreads();
@@ -419,10 +424,12 @@ __global__ __launch_bounds__(CV_NT) void k_conv3x3_gelu(const __half* __restrict
 #pragma unroll
         for (int ks = 0; ks < CV_BK / 32; ks++) {
             v8h a[4], b[CV_TJ];
+            // fragment rows are fr + multiples of 16, so their swizzle is cv_swz(fr)
+            const int fo = ((ks * 4 + kg) ^ cv_swz(fr)) * 8;
 #pragma unroll
-            for (int i = 0; i < 4; i++) a[i] = *(const v8h*)(as + (wr * 64 + i * 16 + fr) * CV_LD + ks * 32 + fk);
+            for (int i = 0; i < 4; i++) a[i] = *(const v8h*)(as + (wr * 64 + i * 16 + fr) * CV_LD + fo);
 #pragma unroll
-            for (int j = 0; j < CV_TJ; j++) b[j] = *(const v8h*)(bs + (wc * 16 * CV_TJ + j * 16 + fr) * CV_LD + ks * 32 + fk);
+            for (int j = 0; j < CV_TJ; j++) b[j] = *(const v8h*)(bs + (wc * 16 * CV_TJ + j * 16 + fr) * CV_LD + fo);
 #pragma unroll
             for (int i = 0; i < 4; i++)
 #pragma unroll

@@ -1409,182 +1409,6 @@ static bool gemm_q8_ws(const int8_t* xq, const float* xd, int M, const Q8Mat& W,
     return true;
 }
 
-// ------------------------------------------------------------------------------------------------ GEMM (f16 operands)
-// Same contract as k_gemm_q8d, with the int8 operands carried as f16 (every Q8 value is exact in f16):
-// v_mfma_f32_16x16x32_f16 returns each block's exact integer sum already in f32, so the per-block rescale is
-// d_x·d_w and one fma (no int→float conversion).  A stage is one Q8 block (K = 32 → 64-B rows of f16), chunk c of
-// row r at c ^ (3·((r >> 3) & 1)) so the ds_read_b128 fragment reads are conflict-free; NBUF stages in flight.
-template <int WM, int WN, int TI, int TJ, int NBUF>
-__global__ __launch_bounds__(256, 2) void k_gemm_q8h(const __half* __restrict__ X, const float* __restrict__ Xd, int M,
-                                                     const __half* __restrict__ W, const __half* __restrict__ Wsc,
-                                                     int N, int K, const float* __restrict__ bias, const float* res,
-                                                     float* y, int ldy, int epi, int steps_per_split,
-                                                     int8_t* __restrict__ yq, float* __restrict__ yd) {
-    typedef _Float16 v8h __attribute__((ext_vector_type(8)));
-    typedef float v4f __attribute__((ext_vector_type(4)));
-    static_assert(WM * WN == 4, "4 waves");
-    constexpr int BM = WM * 16 * TI, BN = WN * 16 * TJ, BK = 32, NF = TI * TJ;
-    static_assert(BM % 64 == 0 && BN % 64 == 0 && BM <= 256 && BN <= 256, "tile sides: multiples of 64, <= 256");
-    constexpr int OB = BM * 64, OSA = OB + BN * 64, OSB = OSA + BM * 4, STAGE = OSB + BN * 4;
-    constexpr int AI = BM / 64, BI = BN / 64;
-    constexpr int NPW = AI + BI + 2;
-    constexpr int D = NBUF - 1;
-    __shared__ __attribute__((aligned(1024))) char smem[NBUF * STAGE];
-
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int wr = wave / WN, wc = wave % WN;
-    const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM;
-    const int nb = K / QK;
-    const int k_begin = blockIdx.z * steps_per_split * BK;
-    const int k_end = min(K, k_begin + steps_per_split * BK);
-    const int nsteps = max(0, (k_end - k_begin) / BK);
-
-    auto sw = [](int r) { return ((r >> 3) & 1) * 3; };
-    const __half* a_src[AI];
-    const __half* b_src[BI];
-#pragma unroll
-    for (int u = 0; u < AI; u++) {
-        const int row = 16 * (wave * AI + u) + (lane >> 2), c = (lane & 3) ^ sw(row);
-        a_src[u] = X + (size_t)min(m0 + row, M - 1) * K + 8 * c;
-    }
-#pragma unroll
-    for (int u = 0; u < BI; u++) {
-        const int row = 16 * (wave * BI + u) + (lane >> 2), c = (lane & 3) ^ sw(row);
-        b_src[u] = W + (size_t)min(n0 + row, N - 1) * K + 8 * c;
-    }
-    const bool sa_on = lane < BM / 4, sb_on = lane < BN / 4;
-    const float* sa_src = Xd + (size_t)min(m0 + wave * (BM / 4) + min(lane, BM / 4 - 1), M - 1) * nb;
-    const uint32_t* sb_src =
-        (const uint32_t*)Wsc + (size_t)min(n0 + wave * (BN / 4) + min(lane, BN / 4 - 1), N - 1) * (nb / 2);
-
-    const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
-    const uint32_t wa = __builtin_amdgcn_readfirstlane(lds0 + 1024 * (wave * AI));
-    const uint32_t wb = __builtin_amdgcn_readfirstlane(lds0 + OB + 1024 * (wave * BI));
-    const uint32_t wsa = __builtin_amdgcn_readfirstlane(lds0 + OSA + wave * (BM / 4) * 4);
-    const uint32_t wsb = __builtin_amdgcn_readfirstlane(lds0 + OSB + wave * (BN / 4) * 4);
-    auto issue = [&](int s, int buf) {
-        const int k0 = k_begin + s * BK;
-        const uint32_t so = buf * STAGE;
-#pragma unroll
-        for (int u = 0; u < AI; u++) dma_lds16(a_src[u] + k0, wa + so + 1024 * u);
-#pragma unroll
-        for (int u = 0; u < BI; u++) dma_lds16(b_src[u] + k0, wb + so + 1024 * u);
-        if (sa_on) dma_lds4(sa_src + k0 / QK, wsa + so);
-        if (sb_on) dma_lds4(sb_src + k0 / 64, wsb + so);
-    };
-
-    const int fr = lane & 15, kh = lane >> 4, fq = 4 * kh;
-    const int arow = wr * 16 * TI, bcol = wc * 16 * TJ;
-    const bool active = m0 + arow < M;
-    const int foff = 16 * (kh ^ (((fr >> 3) & 1) * 3));
-
-    float acc[TI][TJ][4];
-#pragma unroll
-    for (int i = 0; i < TI; i++)
-#pragma unroll
-        for (int j = 0; j < TJ; j++)
-#pragma unroll
-            for (int r = 0; r < 4; r++) acc[i][j][r] = 0.f;
-
-#pragma unroll
-    for (int t = 0; t < D; t++)
-        if (t < nsteps) issue(t, t);
-    for (int s = 0; s < nsteps; s++) {
-        wait_stages<NPW, D>(min(D - 1, nsteps - 1 - s));
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-        if (s + D < nsteps) issue(s + D, (s + D) % NBUF);
-        if (!active) continue;
-        const char* st = smem + (s % NBUF) * STAGE;
-        const int hsel = ((k_begin + s * BK) / QK) & 1;
-        // OP (outer-product scales, as in k_gemm_q8d): d_x(row)·d_w(col) of one i-fragment's 16×16·TJ outputs from
-        // one v_mfma_f32_16x16x1_4b_f32 (exact: a product of two f16 values), so the rescale is ONE fma per output
-        // and block — the f16 MFMA already returns the exact integer block sum as f32 (no cvt): same values as
-        // k_gemm_q8d's cvt + fma, hence bit-identical outputs
-        constexpr bool OP = TJ <= 4;
-        float sb[TJ], sa[TI][4], sal[TI], sbl = 0.f;
-        v8h a[TI], b[TJ];
-        if constexpr (OP) {
-            const int cl = min(lane, 16 * TJ - 1);
-            const uint32_t v = *(const uint32_t*)(st + OSB + 4 * (bcol + cl));
-            sbl = __half2float(__ushort_as_half((unsigned short)(hsel ? v >> 16 : v & 0xffff)));
-        } else {
-#pragma unroll
-            for (int j = 0; j < TJ; j++) {
-                const uint32_t v = *(const uint32_t*)(st + OSB + 4 * (bcol + 16 * j + fr));
-                sb[j] = __half2float(__ushort_as_half((unsigned short)(hsel ? v >> 16 : v & 0xffff)));
-            }
-        }
-#pragma unroll
-        for (int i = 0; i < TI; i++) {
-            int off = (arow + 16 * i + fr) * 64 + foff;
-            asm volatile("" : "+v"(off));
-            a[i] = *(const v8h*)(st + off);
-            if constexpr (OP) {
-                sal[i] = *(const float*)(st + OSA + 4 * (arow + 16 * i + fr));
-            } else {
-                const float4 v = *(const float4*)(st + OSA + 4 * (arow + 16 * i + fq));
-                sa[i][0] = v.x, sa[i][1] = v.y, sa[i][2] = v.z, sa[i][3] = v.w;
-            }
-        }
-#pragma unroll
-        for (int j = 0; j < TJ; j++) {
-            int off = OB + (bcol + 16 * j + fr) * 64 + foff;
-            asm volatile("" : "+v"(off));
-            b[j] = *(const v8h*)(st + off);
-        }
-        constexpr int LAG = 3;
-        constexpr int NPR = LAG / TJ + 2;   // outer-product results live at once (ring)
-        v4f c[LAG + 1];
-        v16f prod[NPR];
-#pragma unroll
-        for (int q = 0; q < NF + LAG; q++) {
-            if (q < NF) {
-                if constexpr (OP) {
-                    if (q % TJ == 0) {
-                        const v16f z = {};
-                        prod[(q / TJ) % NPR] = __builtin_amdgcn_mfma_f32_16x16x1f32(sal[q / TJ], sbl, z, 0, 0, 0);
-                    }
-                }
-                c[q % (LAG + 1)] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[q / TJ], b[q % TJ], v4f{0.f, 0.f, 0.f, 0.f},
-                                                                          0, 0, 0);
-            }
-            if (q >= LAG) {
-                const int p = q - LAG, i = p / TJ, j = p % TJ;
-#pragma unroll
-                for (int r = 0; r < 4; r++) {
-                    if constexpr (OP)
-                        acc[i][j][r] = fmaf(c[p % (LAG + 1)][r], prod[(p / TJ) % NPR][4 * j + r], acc[i][j][r]);
-                    else
-                        acc[i][j][r] = fmaf(c[p % (LAG + 1)][r], sa[i][r] * sb[j], acc[i][j][r]);
-                }
-            }
-        }
-#pragma unroll
-        for (int t = 0; t < NF; t++) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-            __builtin_amdgcn_sched_group_barrier(0x002, OP ? 4 : 8, 0);
-        }
-    }
-    if (!active) return;
-    gemm_epilogue<TI, TJ>(acc, M, N, m0, n0, arow, bcol, fr, fq, bias, res, y, ldy, epi, yq, yd);
-}
-
-void gemm_q8h(const __half* xq, const float* xd, int M, const __half* wq, const __half* wsc, int N, int K,
-              const float* bias, const float* res, float* y, int ldy, int epi, int cfg, hipStream_t s) {
-    QASR_CHECK(K % 64 == 0, QASR_E_INVALID, "gemm_q8h: K % 64");
-    ProfScope ps(s, "gemm_q8", 2.0 * M * N * K, 0.0);
-    static const int bm[] = {128, 64, 64, 128}, bn[] = {128, 128, 64, 64};
-    cfg = cfg < 0 || cfg > 3 ? 1 : cfg;
-    dim3 grid(cdiv(N, bn[cfg]), cdiv(M, bm[cfg]), 1);
-    const int sps = K / 32;
-    switch (cfg) {
-        case 0: k_gemm_q8h<2, 2, 4, 4, 4><<<grid, 256, 0, s>>>(xq, xd, M, wq, wsc, N, K, bias, res, y, ldy, epi, sps, nullptr, nullptr); break;
-        case 1: k_gemm_q8h<2, 2, 2, 4, 4><<<grid, 256, 0, s>>>(xq, xd, M, wq, wsc, N, K, bias, res, y, ldy, epi, sps, nullptr, nullptr); break;
-        case 2: k_gemm_q8h<2, 2, 2, 2, 4><<<grid, 256, 0, s>>>(xq, xd, M, wq, wsc, N, K, bias, res, y, ldy, epi, sps, nullptr, nullptr); break;
-        default: k_gemm_q8h<2, 2, 4, 2, 4><<<grid, 256, 0, s>>>(xq, xd, M, wq, wsc, N, K, bias, res, y, ldy, epi, sps, nullptr, nullptr); break;
-    }
-}
 
 template <int TI, int TJ>
 static void launch_gemm(dim3 grid, hipStream_t s, const int8_t* xq, const float* xd, int M, const Q8Mat& W,
@@ -2010,7 +1834,9 @@ void gemm_q8(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const flo
         gemm_mx_q8in(xq, xd, M, W, bias, res, y, ldy, epi, s, yq, yd, y_zeroed);
         return;
     }
-    ProfScope ps(s, "gemm_q8", 2.0 * M * W.N * W.K, q8_bytes(M, W, epi));
+    // two classes for the bench's roofline: prefill / encoder shapes (M > 256 rows, MFMA-bound) and decode-step
+    // shapes (≤ 256 rows, bound by the weight stream and the per-block rescale)
+    ProfScope ps(s, M > 256 ? "gemm_q8_prefill" : "gemm_q8_decode", 2.0 * M * W.N * W.K, q8_bytes(M, W, epi));
     if (force_cfg < 0 && force_splits <= 0 && !g_stable && M <= g_ws_rows &&
         gemm_q8_ws(xq, xd, M, W, bias, res, y, ldy, epi, s, yq, yd, 0))
         return;

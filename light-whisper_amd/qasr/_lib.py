@@ -139,7 +139,6 @@ SIGNATURES = {
     "qasr_op_q8_to_mx": (C.c_int, [P, P, I32, C.c_int64, P, P, P]),
     "qasr_op_gemm_mx": (C.c_int, [P, P, I32, P, P, I32, I32, P, P, P, I32, I32, P, P, I32, P]),
     "qasr_op_linear_q8_ex": (C.c_int, [P, P, I32, P, P, I32, I32, P, P, I32, I32, P, P, I32, P]),
-    "qasr_op_linear_q8h": (C.c_int, [P, P, I32, P, P, I32, I32, P, P, P, I32, I32, I32, P]),
     "qasr_op_attention_decode_fused": (C.c_int, [P, I32, I32, I32, I32, P, P, P, P, P, F32, P, P, P, P, F32, P, P,
                                                  P]),
     "qasr_op_attention_decode_split": (C.c_int, [P, I32, I32, I32, I32, P, P, P, P, P, F32, P, P, P, P, F32, P, P,

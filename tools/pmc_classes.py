@@ -84,9 +84,18 @@ def main():
             r["wait_inst_frac"] = round(s.get("SQ_WAIT_INST_ANY", 0) / s["SQ_WAVE_CYCLES"], 3)
             r["active_inst_frac"] = round(s.get("SQ_ACTIVE_INST_ANY", 0) / s["SQ_WAVE_CYCLES"], 3)
         res[k] = r
+    # provenance: the library build the passes profiled (bench.py uses the counters only for the same build)
+    import datetime
+    import hashlib
+    import os
+
+    lib = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "light-whisper_amd", "libqasr.so")
+    res["_meta"] = {"lib_sha256_16": hashlib.sha256(open(lib, "rb").read()).hexdigest()[:16] if os.path.exists(lib)
+                    else None, "generated_utc": datetime.datetime.now(datetime.timezone.utc).isoformat(timespec="seconds")}
     json.dump(res, open(out, "w"), indent=1)
     for k, r in res.items():
-        print(k, {x: y for x, y in r.items() if x != "raw"})
+        if k != "_meta":
+            print(k, {x: y for x, y in r.items() if x != "raw"})
 
 
 if __name__ == "__main__":
