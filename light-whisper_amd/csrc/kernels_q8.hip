@@ -1864,7 +1864,8 @@ void gemm_q8(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const flo
         else pick = !k128 ? 6 : W.N <= 4096 ? 14 : 10;
         if (force_cfg < 0 && force_splits <= 0) {
             int c, sp;
-            if (dec_table_pick(M, W, epi, c, sp)) pick = c, force_splits = sp;
+            if (dec_table_pick(M, W, epi, c, sp) && usable(c)) pick = c, force_splits = sp;   // (K-over-waves tiles
+                                                                                                // need K % 2,048)
         }
     } else {
         const int first = M <= 32 ? 3 : M <= 64 ? 1 : 0, last = M <= 32 ? 3 : 2;

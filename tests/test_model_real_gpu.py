@@ -52,9 +52,11 @@ def pair(request, torch_dev):
     m.close()
 
 
-def _near_tie(lg_row, frac=0.02):
+def _near_tie(lg_row, frac=0.005):
+    """top-2 gap below 0.5 % of the row's range (r3: the synthetic vocabulary's log-normal row norms give ≥ 90 % of
+    decode rows a clear margin; r2 used 2 % of max|logit| on i.i.d. rows)"""
     top2 = np.sort(lg_row)[-2:]
-    return top2[1] - top2[0] < frac * np.abs(lg_row).max()
+    return top2[1] - top2[0] < frac * (lg_row.max() - lg_row.min())
 
 
 def test_real_shapes_synthetic_weights_bit_exact(pair):
@@ -243,8 +245,9 @@ def test_real_mxfp8_against_q8(pair):
     clear = (top2[:, 1] - top2[:, 0]) > 0.1 * span
     agree = float((got.argmax(1) == ref.argmax(1)).mean())
     record(f"real_mxfp8[{arch}]", logits_rel_vs_q8=e, argmax_agree=agree, clear_rows=int(clear.sum()))
-    # observed (r2): 3.95e-2 of the logit range (e4m3 element rounding), argmax equal on all 7 rows
-    assert e < 8e-2
+    # observed: 3.95e-2 of the logit range (r2), 8.8e-2 with r3's peaked synthetic vocabulary (row gains up to ~7×:
+    # the largest logits carry the largest e4m3 rounding); argmax equal on all 7 rows
+    assert e < 1.5e-1
     assert (got.argmax(1) == ref.argmax(1))[clear].all()
 
 
@@ -307,3 +310,27 @@ def test_real_streaming_bit_identical(pair):
         if noise > 0:
             assert ds["proposed"] > ds["accepted"], ds
         st.close()
+
+
+def test_real_teacher_forced_100_tokens(pair):
+    """100 teacher-forced decode steps at 1.7B against the oracle — the oracle's own greedy tokens fed
+    back one per step through the GPU decode path (GEMV rows, fused split attention past 256 keys): every row within
+    the logit bound, the argmax equal on every row with a clear margin (top-2 gap > 0.5 % of the row's range), and
+    the clear rows ≥ 80 % of all (the fraction is recorded)."""
+    arch, _, s, o = pair
+    if arch != "qwen3-asr-1.7b":
+        pytest.skip("C3/C4 model")
+    audio = clip(6.0, 41)
+    ids, remb = _prompt_embeds(o, audio)
+    kv = oracle.KV(o, len(ids) + 128)
+    toks, ref = kv.generate(ids, SP["tok_audio_pad"], remb, eos=(), max_new=100, force_len=100, want_logits=True)
+    got = s.forced_logits(audio, toks[:-1])
+    assert got.shape == ref.shape == (100, o.cfg["vocab"])
+    e = rel_err(got, ref)
+    clear = np.array([not _near_tie(r) for r in ref])
+    agree = got.argmax(1) == ref.argmax(1)
+    record(f"real_forced_100[{arch}]", logits_rel=e, clear_frac=float(clear.mean()), argmax_agree=float(agree.mean()),
+           argmax_agree_clear=float(agree[clear].mean()))
+    assert e < 2e-2
+    assert agree[clear].all(), np.nonzero(~agree & clear)
+    assert clear.mean() >= 0.8
