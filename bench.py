@@ -129,10 +129,11 @@ def traffic_per_launch(kernel):
 
 # bench kernel class (ProfScope names) → tools/pmc_classes.py classes it spans
 PMC_CLASSES = {"gemm_q8_prefill": ("gemm_q8_prefill",), "gemm_q8_decode": ("gemm_q8_decode",), "gemm_mx": ("gemm_mx",),
-               "attention": ("attention_decode", "attention_tile"), "gemv_q8": ("gemv_q8",),
+               "attention_decode": ("attention_decode",), "attention_tile": ("attention_tile",), "gemv_q8": ("gemv_q8",),
                "conv3x3_f16": ("conv3x3",)}
 # compute-bound classes (priced against the dense MFMA peak of their dtype, MI355X_MICROARCH.md); the rest stream HBM
-MFMA_PEAK_TF = {"gemm_q8_prefill": 5000.0, "gemm_mx": 5000.0, "conv3x3_f16": 2500.0, "mel_frames": 2500.0}
+MFMA_PEAK_TF = {"gemm_q8_prefill": 5000.0, "gemm_mx": 5000.0, "conv3x3_f16": 2500.0, "mel_frames": 2500.0,
+                "attention_tile": 2500.0}
 
 
 def class_roofline(name, p):

@@ -293,6 +293,9 @@ struct Server {
             // turns it off)
             const char* ec = getenv("QASR_STREAM_ENC_CACHE");
             qasr_session_set_encoder_cache(session, !(ec && std::string(ec) == "0"));
+            // benchmark hook (tools/stream_bench.py --draft-noise): corrupt proposed draft tokens at this rate — the
+            // transcripts stay greedy's, only the acceptance (and the speed) changes
+            if (const char* dn = getenv("QASR_DRAFT_NOISE")) qasr_session_set_draft_noise(session, (float)atof(dn), 1);
             if (qasr_vad_open(nullptr, &vad) != QASR_OK) return fail(qasr_last_error());
             backend = "hip";
             device = "hip";

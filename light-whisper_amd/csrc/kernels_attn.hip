@@ -574,9 +574,12 @@ __global__ __launch_bounds__(256) void k_attn_tile(const __half* __restrict__ Q,
     const int fr = lane & 15, kh = lane >> 4;
     const int r0 = SINGLE ? tile : tile * 16;
     _Float16* vs = vs_all[w];
-    // V image: 16-byte chunk ch of key row kr at kr·HD·2 + 16·(ch ^ swz(kr)) (conflict-free transposed reads)
+    // V image: 16-byte chunk ch of key row kr at kr·HD·2 + 16·(ch ^ swz(kr)), swz(kr) = ((kr >> 1) & 3) << 1 |
+    // (kr & 1) << 3 (mod the row's chunks): each ds_read_b64_tr_b16 32-lane group (8 key rows × 2 chunks) and each
+    // ds_write_b128 8-lane group hits distinct banks for hd 64 and 128 (MI355X_MICROARCH.md §LDS; the r2 swizzle was
+    // 4-way / 2-way on the reads: 0.82 conflict cycles per LDS instruction)
     auto voff = [&](int kr, int ch) -> int {
-        return kr * HD * 2 + 16 * (ch ^ (((kr & 3) << 2 | ((kr >> 2) & 3)) & (CPR - 1)));
+        return kr * HD * 2 + 16 * (ch ^ (((((kr >> 1) & 3) << 1) | ((kr & 1) << 3)) & (CPR - 1)));
     };
 
     // this lane's query row (fr) and its key range
@@ -810,7 +813,9 @@ static void launch_attention(int G, int rows, hipStream_t s, const __half* Q, in
 void attention_decode_fused(const QkFuse& fz, int ldkv, const int* kv_start, const int* kv_len, int rows, int nh,
                             int nkv, int hd, float scale, int8_t* oq, float* od, hipStream_t s, int64_t total_keys) {
     if (rows <= 0) return;
-    ProfScope ps(s, "attention", 4.0 * hd * nh * (double)total_keys, 4.0 * hd * nh * (double)total_keys);
+    // QKᵀ + PV: 4·hd flops per (query head, key); bytes: the f16 K and V rows once per (KV head, key) — the G query
+    // heads of a group share every load
+    ProfScope ps(s, "attention_decode", 4.0 * hd * nh * (double)total_keys, 4.0 * hd * nkv * (double)total_keys);
     QASR_CHECK(hd == 128 && nkv > 0 && nh % nkv == 0, QASR_E_INVALID, "attention_decode_fused: hd 128 only");
     const int G = nh / nkv;
     QASR_CHECK(!fz.part || (rows <= kExactRows && fz.cnt), QASR_E_INVALID,
@@ -842,8 +847,10 @@ void attention(const __half* Q, int ldq, const __half* K, const __half* V, int l
                const int* kv_len, int rows, int nh, int nkv, int hd, float scale, float* o, int8_t* oq, float* od,
                hipStream_t s, int64_t total_keys, bool dense) {
     if (rows <= 0) return;
-    // QKᵀ + PV: 4·hd flops per (query head, key); f16 K/V bytes read per (query head, key)
-    ProfScope ps(s, "attention", 4.0 * hd * nh * (double)total_keys, 4.0 * hd * nh * (double)total_keys);
+    // QKᵀ + PV: 4·hd flops per (query head, key); bytes: K and V once per (KV head, key) for per-row decode rows, once
+    // per (16-row tile, KV head, key) for the dense tile kernel (prefill / encoder: MFMA-priced in bench.py)
+    ProfScope ps(s, dense ? "attention_tile" : "attention_decode", 4.0 * hd * nh * (double)total_keys,
+                 4.0 * hd * nkv * (double)total_keys / (dense ? 16.0 : 1.0));
     QASR_CHECK(nkv > 0 && nh % nkv == 0, QASR_E_INVALID, "attention: bad head counts");
     const int G = nh / nkv;
     // QASR_ATTN_SINGLE=1 (A/B only): decode rows as single-row MFMA tiles instead of the f32 per-row kernel, which

@@ -314,6 +314,7 @@ __global__ __launch_bounds__(64 * NWV) void k_gemv_wide(const int8_t* __restrict
         int8_t* sq = (int8_t*)gv_smem;
         float* sd = (float*)(gv_smem + (size_t)M * K);
         for (int g0 = 0; g0 < M; g0 += MR) {   // M is uniform: every thread meets the barriers inside
+            if (g0 > 0) __syncthreads();   // the previous group's part[] reads are done (MR = 1 reuses part[0])
             if (g0 > 0 && tid < 256) {
 #pragma unroll
                 for (int m = 0; m < MR; m++)
@@ -479,9 +480,11 @@ void gemv_fused(int pro, const int8_t* xq, const float* xd, const float* src, in
     // columns per wave: about one workgroup of four waves per CU on the decoder shapes (N 1,024–4,096)
     const int cpw = W.N >= 4096 ? 4 : W.N >= 2048 ? 2 : 1;
     const GvArgs a{&W, M, xq, xd, src, ld_src, nw, eps, res, y, ldy, epi, yq, yd};
-    if (M <= 1) gv_mr<1>(pro, swi, cpw, T, a, s);
-    else if (M <= 2) gv_mr<2>(pro, swi, cpw, T, a, s);
-    else if (M <= 4) gv_mr<4>(pro, swi, cpw, T, a, s);
+    // QASR_EXACT_MR (diagnosis): the row-group size of launches with more rows (1, 2, 4 or 8)
+    static const int mr = getenv("QASR_EXACT_MR") ? atoi(getenv("QASR_EXACT_MR")) : 8;
+    if (M <= 1 || mr == 1) gv_mr<1>(pro, swi, cpw, T, a, s);
+    else if (M <= 2 || mr == 2) gv_mr<2>(pro, swi, cpw, T, a, s);
+    else if (M <= 4 || mr == 4) gv_mr<4>(pro, swi, cpw, T, a, s);
     else gv_mr<8>(pro, swi, cpw, T, a, s);
 }
 

@@ -31,6 +31,10 @@ def main():
 
     s = m.session(kv_type="f16", n_ctx=4096)
     ref = s.forced_logits(audio, forced)
+    if "--mr-child" in sys.argv:
+        show(f"QASR_EXACT_MR={os.environ.get('QASR_EXACT_MR')}: verify vs steps", ref,
+             s.forced_logits(audio, forced, one_pass=True))
+        return
     v1 = s.forced_logits(audio, forced, one_pass=True)
     v2 = s.forced_logits(audio, forced, one_pass=True)
     show("verify vs steps", ref, v1)
@@ -43,10 +47,18 @@ def main():
     os.environ["QASR_NO_QK_FUSE"] = "1"
     show("no qk fuse: verify vs steps", s.forced_logits(audio, forced), s.forced_logits(audio, forced, one_pass=True))
     del os.environ["QASR_NO_QK_FUSE"]
+    for mr in ("4", "2", "1"):
+        os.environ["QASR_EXACT_MR"] = mr   # read once per process: a child process per setting
+        import subprocess
+
+        code = (f"import sys; sys.argv=['x','{arch}','{secs}','{n}','--mr-child']; "
+                f"exec(open('{os.path.abspath(__file__)}').read())")
+        subprocess.run([sys.executable, "-c", code], env=dict(os.environ), check=False)
+        del os.environ["QASR_EXACT_MR"]
     for k in (2, 4, 8, 9, 16):
         f = forced[:k]
         show(f"k={k} verify vs steps", s.forced_logits(audio, f), s.forced_logits(audio, f, one_pass=True))
 
 
-if __name__ == "__main__":
+if __name__ == "__main__" or "--mr-child" in sys.argv:
     main()

@@ -95,6 +95,9 @@ def main():
     ap.add_argument("--draft", type=int, default=1, help="QASR_STREAM_DRAFT (prompt-lookup drafts, 1 = default on)")
     ap.add_argument("--enc-cache", type=int, default=1,
                     help="QASR_STREAM_ENC_CACHE (encoder windows of growing interim windows reused, 1 = default on)")
+    ap.add_argument("--draft-noise", type=float, default=0.0,
+                    help="QASR_DRAFT_NOISE: replace each proposed draft token by a random id with this probability "
+                         "(acceptance below the degenerate 100 %% of synthetic transcripts; the output is unchanged)")
     a = ap.parse_args()
     audio = (speech_like(np.random.default_rng(3), int(a.seconds * SR)) if a.speech_only else
              recording(a.seconds, seed=3))
@@ -102,7 +105,7 @@ def main():
     with tempfile.TemporaryDirectory() as tmp:
         eng = Engine(a.engine, {"QASR_SYNTHETIC": "1", "QASR_FORCE_TOKENS_PER_S": "8", "HF_HUB_CACHE": tmp,
                                 "LIGHT_WHISPER_DATA_DIR": tmp, "QASR_STREAM_DRAFT": str(a.draft),
-                                "QASR_STREAM_ENC_CACHE": str(a.enc_cache)})
+                                "QASR_STREAM_ENC_CACHE": str(a.enc_cache), "QASR_DRAFT_NOISE": str(a.draft_noise)})
         assert eng.init.get("success"), eng.init
         eng.request(transcribe_req(audio[: 2 * SR], hot))   # first-request warm-up (graphs, buffers)
         clock, interval, last, lat, inf, vad, sizes, speech = 0.0, I_BASE, 0, [], [], [], [], []
@@ -133,7 +136,7 @@ def main():
     out = {"workload": f"C3 streaming: {a.seconds:g} s " + ("continuous speech-like audio" if a.speech_only else
                                                                "recording (seed 3)")
                        + ", interim ticks (interim.rs policy), ≤12 s windows, 100 hot words, + final request",
-           "draft": bool(a.draft), "encoder_cache": bool(a.enc_cache),
+           "draft": bool(a.draft), "draft_noise": a.draft_noise, "encoder_cache": bool(a.enc_cache),
            "engine": a.engine, "weights": "synthetic (QASR_SYNTHETIC=1), 8 forced tokens/audio-s",
            "requests": int(lat.size), "mean_window_s": round(float(np.mean(sizes)), 2),
            "p50_ms": round(float(np.median(lat)), 2), "p95_ms": round(float(np.percentile(lat, 95)), 2),
