@@ -848,3 +848,61 @@ def test_linear_q8_weight_stream_vs_gemm(torch_dev):
     finally:
         _lib.check(L().qasr_op_set_gemm_ws_rows(16, 0))
     assert np.abs(y1 - y0).max() <= 1e-5 * np.abs(y0).max()
+
+
+@pytest.mark.parametrize("split,P,R", [(True, 275, 17), (False, 275, 17), (True, 40, 9), (False, 600, 8)])
+def test_attention_verify_rows_exact(torch_dev, split, P, R):
+    """exact-row contract of the draft verify pass (engine.cpp decoder_layers, rows_share_kv): R consecutive positions
+    of ONE utterance — qk_norm_rope writes every row's K/V first, then one fused decode attention launch (row i
+    attends the rows 0…i-1 of the same pass) — gives, row by row, the same Q8 output bits and the same caches as R
+    one-row decode steps (each step's fused kernel writes its own K/V), with and without the key-range split"""
+    import torch
+
+    hd, nh, nkv = 128, 16, 8
+    nslot = nh + 2 * nkv
+    rng = np.random.default_rng(31)
+    qkv = rng.standard_normal((R, nslot * hd)).astype(np.float32)
+    qnw = (1 + 0.1 * rng.standard_normal(hd)).astype(np.float32)
+    knw = (1 + 0.1 * rng.standard_normal(hd)).astype(np.float32)
+    tab = np.empty((1024, hd // 2, 2), np.float32)
+    _lib.check(L().qasr_op_rope_table(1024, hd, 1e6, tab.ctypes.data_as(C.c_void_p)))
+    slots = P + R + 1
+    kc0 = (0.5 * rng.standard_normal((slots, nkv * hd))).astype(np.float16)
+    vc0 = (0.5 * rng.standard_normal((slots, nkv * hd))).astype(np.float16)
+    pos = np.arange(P, P + R, dtype=np.int32)
+    start = np.zeros(R, np.int32)
+    klen = (pos + 1).astype(np.int32)
+    scale = 1.0 / np.sqrt(hd)
+    keep = [dev(a, torch_dev) for a in (qkv, pos, qnw, knw, tab, start, klen)]
+    part = torch.empty(32 * nkv * 16 * 2 * (2 + hd), dtype=torch.float32, device=torch_dev)
+    cnt = torch.zeros(32 * nkv, dtype=torch.int32, device=torch_dev)
+
+    def attn(qkv_p, rows, pos_p, kc, vc, st_p, len_p, oq, od):
+        args = (qkv_p, rows, nh, nkv, hd, pos_p, pos_p, ptr(keep[2]), ptr(keep[3]), ptr(keep[4]), 1e-6, ptr(kc),
+                ptr(vc), st_p, len_p, scale, ptr(oq), ptr(od))
+        if split:
+            _lib.check(L().qasr_op_attention_decode_split(*args, ptr(part), ptr(cnt), None))
+        else:
+            _lib.check(L().qasr_op_attention_decode_fused(*args, None))
+
+    # steps: one row per launch, in position order
+    kc_s, vc_s = dev(kc0, torch_dev), dev(vc0, torch_dev)
+    oq_s = torch.zeros((R, nh * hd), dtype=torch.int8, device=torch_dev)
+    od_s = torch.zeros((R, nh * hd // 32), dtype=torch.float32, device=torch_dev)
+    for i in range(R):
+        attn(C.c_void_p(keep[0].data_ptr() + i * nslot * hd * 4), 1, C.c_void_p(keep[1].data_ptr() + 4 * i), kc_s,
+             vc_s, C.c_void_p(keep[5].data_ptr() + 4 * i), C.c_void_p(keep[6].data_ptr() + 4 * i),
+             oq_s[i:i + 1], od_s[i:i + 1])
+    # verify pass: K/V of all rows first, then one launch over the R rows
+    kc_v, vc_v = dev(kc0, torch_dev), dev(vc0, torch_dev)
+    qo = torch.empty((R, nh * hd), dtype=torch.float16, device=torch_dev)
+    _lib.check(L().qasr_op_qk_norm_rope(ptr(keep[0]), R, nh, nkv, hd, ptr(keep[1]), ptr(keep[1]), ptr(keep[2]),
+                                        ptr(keep[3]), ptr(keep[4]), 1e-6, ptr(qo), ptr(kc_v), ptr(vc_v), None))
+    oq_v = torch.zeros_like(oq_s)
+    od_v = torch.zeros_like(od_s)
+    attn(ptr(keep[0]), R, ptr(keep[1]), kc_v, vc_v, ptr(keep[5]), ptr(keep[6]), oq_v, od_v)
+    assert np.array_equal(host(kc_s), host(kc_v)) and np.array_equal(host(vc_s), host(vc_v))
+    a, b = host(oq_s), host(oq_v)
+    bad = [i for i in range(R) if not np.array_equal(a[i], b[i])]
+    assert not bad, bad
+    assert np.array_equal(host(od_s), host(od_v))

@@ -47,18 +47,15 @@ def main():
     os.environ["QASR_NO_QK_FUSE"] = "1"
     show("no qk fuse: verify vs steps", s.forced_logits(audio, forced), s.forced_logits(audio, forced, one_pass=True))
     del os.environ["QASR_NO_QK_FUSE"]
-    for mr in ("4", "2", "1"):
-        os.environ["QASR_EXACT_MR"] = mr   # read once per process: a child process per setting
-        import subprocess
+    import subprocess
 
-        code = (f"import sys; sys.argv=['x','{arch}','{secs}','{n}','--mr-child']; "
-                f"exec(open('{os.path.abspath(__file__)}').read())")
-        subprocess.run([sys.executable, "-c", code], env=dict(os.environ), check=False)
-        del os.environ["QASR_EXACT_MR"]
+    for mr in ("4", "2", "1"):   # QASR_EXACT_MR is read once per process: a child process per setting
+        subprocess.run([sys.executable, os.path.abspath(__file__), arch, str(secs), str(n), "--mr-child"],
+                       env=dict(os.environ, QASR_EXACT_MR=mr), check=False)
     for k in (2, 4, 8, 9, 16):
         f = forced[:k]
         show(f"k={k} verify vs steps", s.forced_logits(audio, f), s.forced_logits(audio, f, one_pass=True))
 
 
-if __name__ == "__main__" or "--mr-child" in sys.argv:
+if __name__ == "__main__":
     main()
