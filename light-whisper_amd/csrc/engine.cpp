@@ -527,7 +527,7 @@ int row_bucket(int m) {
 
 // one decode step over B rows, fully on the device: plan → embed → 28 layers → lm_head → argmax → accept →
 // active count to the pinned host word.  Capturable (no allocation once the scratch is sized, no sync).
-void Session::decode_step(const DecState& ds, int B, bool sizing) {
+void Session::decode_step(const DecState& ds, int B, bool sizing, int64_t keys) {
     (void)sizing;
     const qasr_hparams& h = m_->hp;
     const int H = h.txt_h, V = h.vocab;
@@ -535,7 +535,7 @@ void Session::decode_step(const DecState& ds, int B, bool sizing) {
     dec_plan(ds, B, tab, tab + B, tab + 2 * B, tab + 3 * B, tab + 4 * B, tab + 5 * B, st_);
     float* x = (float*)sc_.get(S_X, (size_t)B * H * sizeof(float));
     embed_rows(tab, B, m_->tok_embd, nullptr, x, st_);
-    decoder_layers(x, B, tab + B, tab + 2 * B, tab + 3 * B, tab + 4 * B, 0);
+    decoder_layers(x, B, tab + B, tab + 2 * B, tab + 3 * B, tab + 4 * B, keys);
     float* logits = (float*)sc_.get(S_LOGITS, (size_t)B * V * sizeof(float));
     lm_head_rows(x, B, H, logits);
     int* d_tok = (int*)sc_.get(S_TOK, (size_t)B * sizeof(int));
@@ -912,7 +912,13 @@ void Session::run_batch(const float* dpcm, const std::vector<int64_t>& off, cons
             }
             QASR_HIP(hipGraphLaunch(it->second, st_));
         } else {
-            decode_step(ds, B, false);
+            // eager steps (profiling runs): the keys the step's rows attend, for the attention's algorithmic bytes —
+            // known on the host only with a forced token count (utterance u is active while step < budget[u])
+            int64_t keys = 0;
+            if (force_tps > 0)
+                for (int u = 0; u < count; u++)
+                    if (budget[u] > step) keys += n_prompt[u] + step;
+            decode_step(ds, B, false, keys);
         }
         QASR_HIP(hipEventRecord(step_ev_[step & 1], st_));
         QASR_HIP(hipEventSynchronize(step_ev_[(step - 1) & 1]));

@@ -108,7 +108,8 @@ class Session {
                         int64_t total_keys, bool dense = false, bool rows_share_kv = false);
     void ensure_kv(int64_t slots);
     void enc_cache_store(int64_t n, int total_tokens);
-    void decode_step(const DecState& ds, int B, bool sizing);
+    // keys: Σ key-range lengths of the step's rows when known on the host (profiling's algorithmic bytes), else 0
+    void decode_step(const DecState& ds, int B, bool sizing, int64_t keys = 0);
     // one verify pass of B rows (last accepted token + draft, padded): tables in S_DTAB, argmax → pinned host
     void draft_step(int B);
     void draft_decode(int n_prompt, int base, int budget, int dummy, std::vector<int32_t>& toks, bool& eos,
