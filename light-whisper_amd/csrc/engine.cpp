@@ -401,6 +401,23 @@ std::vector<float> Session::last_audio_embeds() {
 }
 
 // ------------------------------------------------------------------------------------------ decoder
+static const bool g_dump = getenv("QASR_DUMP_DIR") != nullptr;
+
+void Session::dump_rows(const char* what, int l, int rows, const void* p, size_t bytes) {
+    static int seq = 0;
+    std::vector<char> h(bytes);
+    QASR_HIP(hipStreamSynchronize(st_));
+    QASR_HIP(hipMemcpy(h.data(), p, bytes, hipMemcpyDeviceToHost));
+    const char* dir = getenv("QASR_DUMP_DIR");
+    if (!dir) return;
+    char fn[1024];
+    snprintf(fn, sizeof fn, "%s/%06d_%s_L%02d_r%d.bin", dir, seq++, what, l, rows);
+    if (FILE* f = fopen(fn, "wb")) {
+        fwrite(h.data(), 1, bytes, f);
+        fclose(f);
+    }
+}
+
 void Session::decoder_layers(float* x, int rows, const int* d_pos, const int* d_slot, const int* d_kvs,
                              const int* d_kvl, int64_t total_keys, bool dense, bool rows_share_kv) {
     const qasr_hparams& h = m_->hp;
@@ -439,6 +456,8 @@ void Session::decoder_layers(float* x, int rows, const int* d_pos, const int* d_
         __half* vc = vc_ + (size_t)l * layer_kv;
         // decode-sized steps: the norm launch also clears the QKV output, so the split-K QKV GEMM needs no memset
         const bool zq = rows <= 256;
+        const bool dmp = g_dump && rows <= kExactRows;
+        if (dmp) dump_rows("x_in", l, rows, x, (size_t)rows * H * sizeof(float));
         if (gv) {
             gemv_fused(GV_RMS, nullptr, nullptr, x, H, L.attn_norm, h.rms_eps, rows, L.qkv, nullptr, qkv, QD + 2 * KD,
                        EPI_STORE, nullptr, nullptr, st_);
@@ -447,6 +466,7 @@ void Session::decoder_layers(float* x, int rows, const int* d_pos, const int* d_
                        zq ? (int64_t)rows * (QD + 2 * KD) : 0);
             linear_q8(xq, xd, rows, L.qkv, nullptr, nullptr, qkv, QD + 2 * KD, EPI_STORE, st_, zq);
         }
+        if (dmp) dump_rows("qkv", l, rows, qkv, (size_t)rows * (QD + 2 * KD) * sizeof(float));
         if (fuse_qk) {   // decode rows: q/k norm + RoPE + KV write inside the attention kernel
             // a verify pass's row i attends the K/V rows 0…i-1 write in this layer: all rows' K/V go to the cache in a
             // launch of their own first; the fused kernel then rewrites each row's own K/V with the same bits
@@ -464,10 +484,19 @@ void Session::decoder_layers(float* x, int rows, const int* d_pos, const int* d_
             attention(qh, QD, kc, vc, KD, d_kvs, d_kvl, rows, nh, nkv, hd, scale, nullptr, xq, xd, st_, total_keys,
                       dense);
         }
+        if (dmp) {
+            dump_rows("att_q", l, rows, xq, (size_t)rows * QD);
+            dump_rows("att_d", l, rows, xd, (size_t)rows * (QD / QK) * sizeof(float));
+        }
         if (gv) {   // O-projection + residual; norm + gate/up + SwiGLU + Q8; down-projection + residual
             gemv_fused(GV_NONE, xq, xd, nullptr, 0, nullptr, 0.f, rows, L.o, x, x, H, EPI_RESID, nullptr, nullptr, st_);
+            if (dmp) dump_rows("x_mid", l, rows, x, (size_t)rows * H * sizeof(float));
             gemv_fused(GV_RMS, nullptr, nullptr, x, H, L.ffn_norm, h.rms_eps, rows, L.gu, nullptr, nullptr, 0,
                        EPI_SWIGLU, hq2, hd2, st_);
+            if (dmp) {
+                dump_rows("h_q", l, rows, hq2, (size_t)rows * F);
+                dump_rows("h_d", l, rows, hd2, (size_t)rows * (F / QK) * sizeof(float));
+            }
             gemv_fused(GV_NONE, hq2, hd2, nullptr, 0, nullptr, 0.f, rows, L.down, x, x, H, EPI_RESID, nullptr, nullptr,
                        st_);
             continue;

@@ -116,6 +116,8 @@ class Session {
                       bool forced);
     // exact: every row with the 1-row arithmetic (verify passes; ≤ 4 rows always are)
     void lm_head_rows(const float* x, int rows, int ldx, float* logits, bool exact = false);
+    // diagnosis (QASR_DUMP_DIR set): a decode-sized stage's output rows to $QASR_DUMP_DIR/<seq>_<what>_L<l>_r<rows>.bin
+    void dump_rows(const char* what, int l, int rows, const void* p, size_t bytes);
     void mx_ws(int64_t rows, int64_t kmax);
     template <class T>
     T* upload(int slot, const std::vector<T>& v);

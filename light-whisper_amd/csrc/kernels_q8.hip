@@ -209,7 +209,7 @@ __global__ __launch_bounds__(256) void k_gemv_q8(const int8_t* __restrict__ W, c
                     p = __builtin_amdgcn_sdot4(w[c][t].z, x[m][t].z, p, false);
                     p = __builtin_amdgcn_sdot4(w[c][t].w, x[m][t].w, p, false);
                     p += __builtin_amdgcn_update_dpp(0, p, 0xB1, 0xf, 0xf, false);   // + lane ^ 1
-                    acc[c][m] += (even && in[t]) ? (float)p * (dw[c][t] * dx[m][t]) : 0.f;
+                    if (even && in[t]) acc[c][m] = fmaf((float)p, dw[c][t] * dx[m][t], acc[c][m]);
                 }
             }
         }
@@ -359,7 +359,8 @@ __global__ __launch_bounds__(64 * NWV) void k_gemv_wide(const int8_t* __restrict
                     p = __builtin_amdgcn_sdot4(w[c][t].z, x[m].z, p, false);
                     p = __builtin_amdgcn_sdot4(w[c][t].w, x[m].w, p, false);
                     p += __builtin_amdgcn_update_dpp(0, p, 0xB1, 0xf, 0xf, false);   // + lane ^ 1
-                    acc[c][m] += (even && in) ? (float)p * (dw[c][t] * dx[m]) : 0.f;
+                    // an explicit fma: the same rounding in every row-group instantiation (see rms_row_q8_finish)
+                    if (even && in) acc[c][m] = fmaf((float)p, dw[c][t] * dx[m], acc[c][m]);
                 }
             }
         }

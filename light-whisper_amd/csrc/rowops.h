@@ -48,20 +48,25 @@ __device__ __forceinline__ void rms_row_q8_finish(const float4 (&v)[KC], const f
         __syncthreads();
         return;
     }
+    // non-contractible operations: a caller that runs several rows (k_gemv_wide's row groups) may have them packed
+    // or fused differently by the compiler, and a one-ulp change of the sum can flip a Q8 rounding of the row
     float ss = 0.f;
 #pragma unroll
-    for (int k = 0; k < KC; k++) ss += v[k].x * v[k].x + v[k].y * v[k].y + v[k].z * v[k].z + v[k].w * v[k].w;
+    for (int k = 0; k < KC; k++)
+        ss = __fadd_rn(ss, __fadd_rn(__fadd_rn(__fmul_rn(v[k].x, v[k].x), __fmul_rn(v[k].y, v[k].y)),
+                                     __fadd_rn(__fmul_rn(v[k].z, v[k].z), __fmul_rn(v[k].w, v[k].w))));
     ss = wave_sum(ss);
     if (lane == 0) part[tid >> 6] = ss;
     __syncthreads();
-    ss = (part[0] + part[1]) + (part[2] + part[3]);
-    const float inv = 1.0f / sqrtf(ss / (float)H + eps);
+    ss = __fadd_rn(__fadd_rn(part[0], part[1]), __fadd_rn(part[2], part[3]));
+    const float inv = __fdiv_rn(1.0f, __fsqrt_rn(__fadd_rn(__fdiv_rn(ss, (float)H), eps)));
 #pragma unroll
     for (int k = 0; k < KC; k++) {
         const int c = tid + 256 * k;
         if (256 * k + (tid & ~7) < nc) {   // 8-thread blocks are all in or all out (nc % 8 == 0)
             const float4 g = gw[k];
-            const float4 y = make_float4(v[k].x * inv * g.x, v[k].y * inv * g.y, v[k].z * inv * g.z, v[k].w * inv * g.w);
+            const float4 y = make_float4(__fmul_rn(__fmul_rn(v[k].x, inv), g.x), __fmul_rn(__fmul_rn(v[k].y, inv), g.y),
+                                         __fmul_rn(__fmul_rn(v[k].z, inv), g.z), __fmul_rn(__fmul_rn(v[k].w, inv), g.w));
             quant4_store(y, c, lane, q, d);
         }
     }
