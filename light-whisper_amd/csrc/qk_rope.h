@@ -1,6 +1,7 @@
 // q/k RMS-norm + RoPE of one head (hd 128) held two dims per lane (2·lane, 2·lane+1) by one wave, shared by
 // k_qk_norm_rope_row (kernels_nn.hip) and the fused decode attention (kernels_attn.hip).  Written with
-// non-contractible operations so that both kernels round identically (the fused path is tested bit for bit).
+// separately rounded operations (the build's -ffp-contract=off keeps them unfused) so that both kernels round identically
+// (the fused path is tested bit for bit).
 #pragma once
 #include <hip/hip_fp16.h>
 #include <hip/hip_runtime.h>

@@ -48,8 +48,9 @@ __device__ __forceinline__ void rms_row_q8_finish(const float4 (&v)[KC], const f
         __syncthreads();
         return;
     }
-    // non-contractible operations: a caller that runs several rows (k_gemv_wide's row groups) may have them packed
-    // or fused differently by the compiler, and a one-ulp change of the sum can flip a Q8 rounding of the row
+    // separately rounded operations: a caller that runs several rows (k_gemv_wide's row groups) may have them packed
+    // or fused differently by the compiler, and a one-ulp change of the sum can flip a Q8 rounding of the row.  (HIP's
+    // __fmul_rn / __fadd_rn are the plain operators: the build's -ffp-contract=off is what keeps them unfused.)
     float ss = 0.f;
 #pragma unroll
     for (int k = 0; k < KC; k++)

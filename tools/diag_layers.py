@@ -2,7 +2,7 @@
 """Diagnosis (GPU): where a draft verify pass first departs from one decode step per token.  Runs a forced
 continuation both ways with QASR_DUMP_DIR set (engine.cpp dump_rows: every decode-sized stage's output rows per
 layer) and prints, per layer and stage, the rows whose bytes differ and the largest difference.
-usage: python tools/diag_layers.py [arch] [seconds] [n]"""
+usage: python tools/diag_layers.py [arch] [seconds] [n] [audio seed] [prior runs: n1,n2,…]"""
 import os
 import re
 import sys
@@ -37,9 +37,15 @@ def main():
     arch = sys.argv[1] if len(sys.argv) > 1 else "qwen3-asr-1.7b"
     secs = float(sys.argv[2]) if len(sys.argv) > 2 else 20.0
     n = int(sys.argv[3]) if len(sys.argv) > 3 else 17
+    aseed = int(sys.argv[4]) if len(sys.argv) > 4 else 32
+    prior = [int(v) for v in sys.argv[5].split(",")] if len(sys.argv) > 5 else []
     m = Model.synthetic(arch, seed=7)
     s = m.session(kv_type="f16", n_ctx=4096)
-    audio = speech_like(np.random.default_rng(32), int(secs * 16000))
+    audio = speech_like(np.random.default_rng(aseed), int(secs * 16000))
+    for p in prior:   # earlier forced runs in the same session (the test's order)
+        f = np.array([1000 + 37 * i for i in range(p)], np.int32)
+        same = np.array_equal(s.forced_logits(audio, f), s.forced_logits(audio, f, one_pass=True))
+        print(f"prior n={p}: {'identical' if same else 'DIFFER'}", flush=True)
     forced = np.array([1000 + 37 * i for i in range(n)], np.int32)
     da, db = os.path.join(TMP, "steps"), os.path.join(TMP, "verify")
     os.makedirs(da)
