@@ -240,8 +240,7 @@ QASR_API int qasr_op_quant_rows(const float* x, int32_t M, int32_t K, int32_t ld
 QASR_API int qasr_op_repack_q8(const uint8_t* blocks, int64_t nblk, int8_t* qs, void* sc, void* stream);
 /* path: 0 auto, 1 GEMV (M <= 8), 2 MFMA GEMM, 3 / 4 / 5 GEMV with 1 / 2 / 4 columns per wave;
  * 16 + cfg + 32*splits: MFMA GEMM with a forced configuration (kernels_q8.hip kGemmCfgs, 0..15; 31 = heuristic)
- * and split-K count (0 heuristic); 1024 + cfg: any configuration index (31.. = the A-stationary decode kernel) —
- * tuning only.  epi: 0 store, 1 residual, 2 gelu */
+ * and split-K count (0 heuristic) — tuning only.  epi: 0 store, 1 residual, 2 gelu */
 QASR_API int qasr_op_linear_q8(const int8_t* xq, const float* xd, int32_t M, const int8_t* wqs, const void* wsc,
                                int32_t N, int32_t K, const float* bias, const float* res, float* y, int32_t ldy,
                                int32_t epi, int32_t path, void* stream);
@@ -268,17 +267,6 @@ QASR_API int qasr_op_gemm_swiglu_q8_cfg(const int8_t* xq, const float* xd, int32
    register their own for the decode steps (used there for the SwiGLU epilogue).  Not in
    the reference (an engine-internal tuning / test hook). */
 QASR_API int qasr_op_set_gemm_fixup(void* part, int64_t part_bytes, void* cnt, int32_t ncnt);
-/* The batched decode step's residual projection with the next RMSNorm folded in (engine.cpp decoder layer; replaces
-   linear_q8(epi 1) + rmsnorm_q8, i.e. ggml's mul_mat + add + rms_norm + mul + the Q8_0 quantisation of the next
-   mul_mat's input inside transcribe_cpp's session.run, qwen3_asr_server.py:321): y = y + X·Wᵀ in place, and the
-   next input rows Q8(RMSNorm(y)·nw) → yq [M][N] int8 / yd [M][N/32] f32 — q = round(y·nw / d'), d' = amax/127 of
-   the block, block scale f16(d'·inv_rms(row)).  ssp: M·N/64 floats of scratch; cnt: 64 zeroed uint32 counters
-   (left zero).  Needs deterministic mode and a registered fix-up workspace (qasr_op_set_gemm_fixup), M ≤ 256,
-   K % 128 == 0, N % 64 == 0, N ≤ 4096; QASR_E_INVALID (nothing launched) otherwise.  The engine uses it only with
-   QASR_NORM_FUSE=1 (measured slower than the two launches on the C4 bench). */
-QASR_API int qasr_op_linear_resid_rmsq8(const int8_t* xq, const float* xd, int32_t M, const int8_t* wqs,
-                                        const void* wsc, int32_t N, int32_t K, float* y, const float* nw, float eps,
-                                        int8_t* yq, float* yd, float* ssp, void* cnt, void* stream);
 /* Rows (0..64) up to which the Q8 GEMM's automatic choice streams the weights straight into the matrix core's operand
    registers (k_gemm_q8_ws: decode rows, every weight byte read once, no LDS staging); 0 = never.  all_shapes = 0: only
    on the wide decoder matrices where it is faster (QKV, gate/up); 1: every shape it supports (tests).  Process-wide;

@@ -49,8 +49,6 @@ QASR_API int qasr_op_linear_q8(const int8_t* xq, const float* xd, int32_t M, con
             gemv_q8(xq, xd, M, W, bias, res, y, ldy, epi, S(stream), path == 1 ? 0 : 1 << (path - 3));
         } else if (path == 2) {
             gemm_q8(xq, xd, M, W, bias, res, y, ldy, epi, S(stream));
-        } else if (path >= 1024) {   // 1024 + cfg: any configuration index, heuristic split
-            gemm_q8(xq, xd, M, W, bias, res, y, ldy, epi, S(stream), path - 1024, 0);
         } else if (path >= 16) {
             const int cfg = (path - 16) % 32, splits = (path - 16) / 32;
             gemm_q8(xq, xd, M, W, bias, res, y, ldy, epi, S(stream), cfg == 31 ? -1 : cfg, splits);
@@ -167,24 +165,8 @@ QASR_API int qasr_op_gemm_swiglu_q8_cfg(const int8_t* xq, const float* xd, int32
         W.sc = (__half*)wsc;
         W.N = N;
         W.K = K;
-        gemm_q8(xq, xd, M, W, nullptr, nullptr, nullptr, N, EPI_SWIGLU, S(stream),
-                cfg < 0 ? -1 : cfg >= 1024 ? cfg - 1024 : cfg % 32, cfg < 0 || cfg >= 1024 ? 0 : cfg / 32, hq, hd);
-        launched();
-    });
-}
-
-QASR_API int qasr_op_linear_resid_rmsq8(const int8_t* xq, const float* xd, int32_t M, const int8_t* wqs,
-                                        const void* wsc, int32_t N, int32_t K, float* y, const float* nw, float eps,
-                                        int8_t* yq, float* yd, float* ssp, void* cnt, void* stream) {
-    return guard([&] {
-        Q8Mat W;
-        W.qs = (int8_t*)wqs;
-        W.sc = (__half*)wsc;
-        W.N = N;
-        W.K = K;
-        const bool ok = M > 0 && gemm_q8_resid_rmsq8(xq, xd, M, W, y, NormFuse{nw, eps, ssp, (unsigned*)cnt}, yq, yd,
-                                                      S(stream), /*force=*/true);
-        QASR_CHECK(ok, QASR_E_INVALID, "linear_resid_rmsq8: shape / mode without the fused form");
+        gemm_q8(xq, xd, M, W, nullptr, nullptr, nullptr, N, EPI_SWIGLU, S(stream), cfg < 0 ? -1 : cfg % 32,
+                cfg < 0 ? 0 : cfg / 32, hq, hd);
         launched();
     });
 }

@@ -138,9 +138,6 @@ Session::Session(Model* m, int n_ctx) : m_(m), n_ctx_(n_ctx) {
         QASR_HIP(hipMalloc(&fix_part_, fix_floats_ * sizeof(float)));
         QASR_HIP(hipMalloc(&fix_cnt_, (size_t)kFixCounters * sizeof(unsigned)));
         QASR_HIP(hipMemset(fix_cnt_, 0, (size_t)kFixCounters * sizeof(unsigned)));
-        QASR_HIP(hipMalloc(&nf_ssp_, (size_t)256 * (kNormFuseMaxN / 64) * sizeof(float)));
-        QASR_HIP(hipMalloc(&nf_cnt_, (size_t)kNormFuseCounters * sizeof(unsigned)));
-        QASR_HIP(hipMemset(nf_cnt_, 0, (size_t)kNormFuseCounters * sizeof(unsigned)));
     }
 }
 
@@ -153,8 +150,6 @@ Session::~Session() {
     if (fix_part_) (void)hipFree(fix_part_);
     if (ec_emb_) (void)hipFree(ec_emb_);
     if (fix_cnt_) (void)hipFree(fix_cnt_);
-    if (nf_ssp_) (void)hipFree(nf_ssp_);
-    if (nf_cnt_) (void)hipFree(nf_cnt_);
     if (pin_) (void)hipHostFree(pin_);
     for (auto& g : graphs_) (void)hipGraphExecDestroy(g.second);
     for (auto& g : draft_graphs_) (void)hipGraphExecDestroy(g.second);
@@ -455,12 +450,6 @@ void Session::decoder_layers(float* x, int rows, const int* d_pos, const int* d_
                "decoder: a verify pass needs the exact-row path (≤ kExactRows rows, GEMV shapes)");
     int8_t* hq2 = gv ? (int8_t*)sc_.get(S_HQ, (size_t)rows * F) : nullptr;   // the SwiGLU epilogue's Q8 rows
     float* hd2 = gv ? (float*)sc_.get(S_HD, (size_t)rows * (F / QK) * sizeof(float)) : nullptr;
-    // batched decode steps (deterministic mode, the fix-up workspace registered): the O- and down-projection epilogues
-    // also write the next RMSNorm's Q8 rows (gemm_q8_resid_rmsq8), so no norm launch runs between the GEMMs.  Two Q8
-    // buffers alternate: P holds the QKV input and then the attention output, Q the post-attention norm's rows, P the
-    // SwiGLU rows, Q the next layer's QKV input — a GEMM never writes the buffer it reads.
-    const bool nq = !gv && fused && !dense && rows <= 256 && nf_ssp_ && H <= kNormFuseMaxN;
-    bool pre = false;   // xq / xd already hold this layer's QKV input (the previous down-projection wrote it)
     for (int l = 0; l < h.txt_layers; l++) {
         const DecLayer& L = m_->dec[l];
         __half* kc = kc_ + (size_t)l * layer_kv;
@@ -473,10 +462,9 @@ void Session::decoder_layers(float* x, int rows, const int* d_pos, const int* d_
             gemv_fused(GV_RMS, nullptr, nullptr, x, H, L.attn_norm, h.rms_eps, rows, L.qkv, nullptr, qkv, QD + 2 * KD,
                        EPI_STORE, nullptr, nullptr, st_);
         } else {
-            if (!pre)
-                rmsnorm_q8(x, rows, H, H, L.attn_norm, h.rms_eps, xq, xd, st_, zq ? qkv : nullptr,
-                           zq ? (int64_t)rows * (QD + 2 * KD) : 0);
-            linear_q8(xq, xd, rows, L.qkv, nullptr, nullptr, qkv, QD + 2 * KD, EPI_STORE, st_, zq && !pre);
+            rmsnorm_q8(x, rows, H, H, L.attn_norm, h.rms_eps, xq, xd, st_, zq ? qkv : nullptr,
+                       zq ? (int64_t)rows * (QD + 2 * KD) : 0);
+            linear_q8(xq, xd, rows, L.qkv, nullptr, nullptr, qkv, QD + 2 * KD, EPI_STORE, st_, zq);
         }
         if (dmp) dump_rows("qkv", l, rows, qkv, (size_t)rows * (QD + 2 * KD) * sizeof(float));
         if (fuse_qk) {   // decode rows: q/k norm + RoPE + KV write inside the attention kernel
@@ -511,21 +499,6 @@ void Session::decoder_layers(float* x, int rows, const int* d_pos, const int* d_
             }
             gemv_fused(GV_NONE, hq2, hd2, nullptr, 0, nullptr, 0.f, rows, L.down, x, x, H, EPI_RESID, nullptr, nullptr,
                        st_);
-            continue;
-        }
-        if (nq) {   // P = xq / xd (attention output), Q = hq / hd_
-            if (!gemm_q8_resid_rmsq8(xq, xd, rows, L.o, x, NormFuse{L.ffn_norm, h.rms_eps, nf_ssp_, nf_cnt_}, hq, hd_,
-                                     st_)) {
-                linear_q8(xq, xd, rows, L.o, nullptr, x, x, H, EPI_RESID, st_);
-                rmsnorm_q8(x, rows, H, H, L.ffn_norm, h.rms_eps, hq, hd_, st_);
-            }
-            gemm_q8(hq, hd_, rows, L.gu, nullptr, nullptr, nullptr, 2 * F, EPI_SWIGLU, st_, -1, 0, xq, xd);
-            pre = l + 1 < h.txt_layers &&
-                  gemm_q8_resid_rmsq8(xq, xd, rows, L.down, x,
-                                      NormFuse{m_->dec[l + 1].attn_norm, h.rms_eps, nf_ssp_, nf_cnt_}, hq, hd_, st_);
-            if (!pre) linear_q8(xq, xd, rows, L.down, nullptr, x, x, H, EPI_RESID, st_);
-            std::swap(xq, hq);   // the next layer's P is this layer's Q
-            std::swap(xd, hd_);
             continue;
         }
         linear_q8(xq, xd, rows, L.o, nullptr, x, x, H, EPI_RESID, st_);

@@ -158,10 +158,6 @@ class Session {
     float* fix_part_ = nullptr;
     size_t fix_floats_ = 0;
     unsigned* fix_cnt_ = nullptr;
-    // decode-step residual GEMMs with the next RMSNorm folded in (gemm_q8_resid_rmsq8): per-64-column partial sums of
-    // squares [256][kNormFuseMaxN / 64] + per-row-tile arrival counters (zeroed once, kept zero by the kernels)
-    float* nf_ssp_ = nullptr;
-    unsigned* nf_cnt_ = nullptr;
     std::vector<int32_t> history_;   // previous transcripts (the lookup corpus), oldest first
     int hist_last_ = 0;              // where the latest transcript starts in history_
     DraftStats dstats_;

@@ -13,19 +13,7 @@ enum Epi : int {
     EPI_SWIGLU = 3, // W rows gate/up interleaved by 16 (interleave_gate_up): h = silu(g)·u → Q8 rows (yq, yd)
     EPI_GELU_Q8 = 4,   // h = gelu_erf(acc + bias) → Q8 rows (yq [M][N], yd [M][N/32]); y unused
     EPI_STORE_F16 = 5, // y (as __half, row stride ldy) = f16(acc + bias)
-    EPI_RESID_NQ8 = 6, // y = res + acc in place, + the next RMSNorm's Q8 rows (gemm_q8_resid_rmsq8 only)
 };
-
-// The residual GEMM of a decode step with the following RMSNorm + Q8 folded in (gemm_q8_resid_rmsq8): the norm weight,
-// eps, a [M][N/64] float slab of per-64-column partial sums of squares and one arrival counter per 64-row tile (zero
-// between launches; the kernel keeps them so)
-struct NormFuse {
-    const float* w = nullptr;
-    float eps = 0.f;
-    float* ssp = nullptr;
-    unsigned* cnt = nullptr;
-};
-constexpr int kNormFuseCounters = 64, kNormFuseMaxN = 4096;
 
 // ---- Q8_0 weights / activations (kernels_q8.hip)
 void repack_q8(const uint8_t* blocks, int64_t nblk, int8_t* qs, __half* sc, hipStream_t s);
@@ -102,16 +90,6 @@ struct FixupScope {   // registers a fix-up workspace for the calls in its scope
     FixupScope(const FixupScope&) = delete;
     FixupScope& operator=(const FixupScope&) = delete;
 };
-// y = y + xq·Wᵀ (the residual stream, in place, ldy = N) and, in the same launch, the next layer input Q8(RMSNorm(y)·nw)
-// → yq [M][N] / yd [M][N/32] (what rmsnorm_q8 would write, up to f32 rounding: q = round(y·nw / d'), d' = amax/127 of
-// the block, and the block scale f16(d'·inv_rms(row)) once the row's last 64-column tile has counted in).  Decode steps
-// in deterministic mode with the fix-up workspace registered (≤ 256 rows, K % 128 == 0, N % 64 == 0, N ≤
-// kNormFuseMaxN); returns false without launching anything otherwise — the caller then runs the residual GEMM and
-// rmsnorm_q8 as two launches.
-// Opt-in for the engine (QASR_NORM_FUSE=1: measured slower than the two launches on the C4 bench); force: regardless
-// of the switch (the op-level entry point).
-bool gemm_q8_resid_rmsq8(const int8_t* xq, const float* xd, int M, const Q8Mat& W, float* y, const NormFuse& nf,
-                         int8_t* yq, float* yd, hipStream_t s, bool force = false);
 size_t mx_workspace_bytes(int64_t M, int64_t K);
 // rows of a [2F][K] gate|up matrix → interleaved by 16 (32j+t: t<16 gate 16j+t, else up 16j+t-16)
 int64_t gate_up_interleaved_row(int64_t r, int64_t F);

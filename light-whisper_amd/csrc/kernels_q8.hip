@@ -483,9 +483,12 @@ void gemv_fused(int pro, const int8_t* xq, const float* xd, const float* src, in
     const GvArgs a{&W, M, xq, xd, src, ld_src, nw, eps, res, y, ldy, epi, yq, yd};
     // QASR_EXACT_MR (diagnosis): the row-group size of launches with more rows (1, 2, 4 or 8)
     static const int mr = getenv("QASR_EXACT_MR") ? atoi(getenv("QASR_EXACT_MR")) : 8;
+    // the SwiGLU launch (8 columns per wave) runs its rows in groups of 4 from K 2,048 up: 8-row groups spill 108 VGPRs
+    // there (a row's arithmetic is the same in every group size — test_gemv_exact_rows)
+    const bool mr4 = swi && T >= 2;
     if (M <= 1 || mr == 1) gv_mr<1>(pro, swi, cpw, T, a, s);
     else if (M <= 2 || mr == 2) gv_mr<2>(pro, swi, cpw, T, a, s);
-    else if (M <= 4 || mr == 4) gv_mr<4>(pro, swi, cpw, T, a, s);
+    else if (M <= 4 || mr == 4 || mr4) gv_mr<4>(pro, swi, cpw, T, a, s);
     else gv_mr<8>(pro, swi, cpw, T, a, s);
 }
 
@@ -701,101 +704,6 @@ __device__ __forceinline__ bool splitk_fixup(float (&acc)[TI][TJ][4], bool has, 
     return true;
 }
 
-// ---- residual GEMM + the next RMSNorm's Q8 rows (EPI_RESID_NQ8, 64-column wave tiles: TJ = 4)
-// Per row and 32-column block of the wave's 64 columns: x = res + acc (stored in place), then the block of x·nw is
-// quantised with d' = amax/127 — RMSNorm multiplies the whole row by one inv > 0, so round(x·nw / d') is the Q8 of
-// x·inv·nw up to f32 rounding, and only the block scale waits for inv.  d' goes to yd and the row's Σx² over these 64
-// columns (one fixed-order tree: the same bits in every launch) to ssp[row][col/64], both write-through (agent-scope
-// stores), for the row tile's last workgroup (norm_rowtile_finish).
-__device__ __forceinline__ float sum16(float v) {
-    v = sum8(v);
-    return v + dpp<0x140>(v);
-}
-template <int TI>
-__device__ __forceinline__ void epi_resid_nq8(const float (&acc)[TI][4][4], int M, int N, int m0, int n0, int arow,
-                                              int bcol, int fr, int fq, float* y, const NormFuse& nf,
-                                              int8_t* __restrict__ yq, float* yd) {
-    const int nct = N >> 6, ct = (n0 + bcol) >> 6, nb = N / QK;
-    float wv[4];
-#pragma unroll
-    for (int j = 0; j < 4; j++) wv[j] = nf.w[n0 + bcol + 16 * j + fr];
-#pragma unroll
-    for (int i = 0; i < TI; i++) {
-#pragma unroll
-        for (int r = 0; r < 4; r++) {
-            const int row = m0 + arow + 16 * i + fq + r;
-            const bool ok = row < M;   // uniform over the 16 lanes of a DPP row (same fq)
-            float x[4];
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                float* p = y + (size_t)row * N + n0 + bcol + 16 * j + fr;
-                x[j] = ok ? __fadd_rn(acc[i][j][r], *p) : 0.f;
-                if (ok) *p = x[j];
-            }
-            const float ss = sum16(__fadd_rn(__fadd_rn(__fmul_rn(x[0], x[0]), __fmul_rn(x[1], x[1])),
-                                             __fadd_rn(__fmul_rn(x[2], x[2]), __fmul_rn(x[3], x[3]))));
-#pragma unroll
-            for (int b = 0; b < 2; b++) {
-                const float h0 = __fmul_rn(x[2 * b], wv[2 * b]), h1 = __fmul_rn(x[2 * b + 1], wv[2 * b + 1]);
-                const float am = max16(fmaxf(fabsf(h0), fabsf(h1)));
-                const float dd = am / 127.f;
-                const int c0 = n0 + bcol + 32 * b;
-                if (ok) {
-                    int8_t* qr = yq + (size_t)row * N + c0;
-                    qr[fr] = (int8_t)(am == 0.f ? 0 : (int)roundf(h0 / dd));
-                    qr[16 + fr] = (int8_t)(am == 0.f ? 0 : (int)roundf(h1 / dd));
-                    if (fr == 0)
-                        __hip_atomic_store(yd + (size_t)row * nb + c0 / QK, dd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                }
-            }
-            if (ok && fr == 0)
-                __hip_atomic_store(nf.ssp + (size_t)row * nct + ct, ss, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
-}
-
-// Every thread of the workgroup calls this after its epilogue: the workgroup's write-through stores drained, one lane
-// counts it in on the row tile's counter (agent scope, the split-K fix-up's hand-off); the last of the gridDim.x column
-// tiles resets the counter and, per row of the tile, sums the row's ssp partials (4 threads per row: k ≡ q mod 4 in
-// order, then (s0 + s1) + (s2 + s3)), forms inv exactly as rms_row_q8_finish does and rewrites the row's block scales
-// d' → f16(d'·inv).
-template <int BM>
-__device__ __forceinline__ void norm_rowtile_finish(int M, int N, int m0, const NormFuse& nf, float* yd, int* flag) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const unsigned prev = __hip_atomic_fetch_add(nf.cnt + blockIdx.y, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const int last = prev == gridDim.x - 1;
-        if (last) __hip_atomic_store(nf.cnt + blockIdx.y, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        *flag = last;
-    }
-    __syncthreads();
-    if (!*flag) return;
-    static_assert(4 * BM <= 256, "norm_rowtile_finish: 4 threads per row");
-    const int t = threadIdx.x;
-    if (t >= 4 * BM) return;   // whole waves (4·BM is a multiple of 64)
-    const int row = m0 + (t >> 2), q = t & 3, nct = N >> 6, nb = N / QK;
-    const bool ok = row < M;
-    float s = 0.f;
-    if (ok)
-        for (int k = q; k < nct; k += 4)
-            s = __fadd_rn(s, __hip_atomic_load(nf.ssp + (size_t)row * nct + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    s = __fadd_rn(s, __shfl_xor(s, 1));
-    s = __fadd_rn(s, __shfl_xor(s, 2));
-    if (!ok) return;
-    const float inv = __fdiv_rn(1.0f, __fsqrt_rn(__fadd_rn(__fdiv_rn(s, (float)N), nf.eps)));
-    float* dr = yd + (size_t)row * nb;
-    for (int b0 = q; b0 < nb; b0 += 32) {   // 8 scales per thread in flight
-        float dv[8];
-#pragma unroll
-        for (int u = 0; u < 8; u++)
-            if (b0 + 4 * u < nb) dv[u] = __hip_atomic_load(dr + b0 + 4 * u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#pragma unroll
-        for (int u = 0; u < 8; u++)
-            if (b0 + 4 * u < nb) dr[b0 + 4 * u] = __half2float(f2h(__fmul_rn(dv[u], inv)));
-    }
-}
-
 constexpr int GBK = 128;     // K per step
 constexpr int GLD = 144;     // LDS row stride (bytes)
 
@@ -979,16 +887,13 @@ __global__ __launch_bounds__(256) void k_gemm_q8(const int8_t* __restrict__ X, c
 //  * Compute: MFMA q is issued LAG MFMAs before its int32 result is rescaled into the f32 accumulator
 //    (cvt, d_x·d_w, fma: 3 VALU per output and block); sched_group_barrier pins the MFMA/VALU interleave.  Waves
 //    whose rows all lie past M (padded decode buckets) skip the math but still stage their share.
-//  * NORMQ (64-column wave tiles only): the EPI_RESID_NQ8 epilogue — residual + the next RMSNorm's Q8 rows, the row
-//    tile's last workgroup applying the rms scale (norm_rowtile_finish); every wave reaches its barriers.
-template <int WM, int WN, int TI, int TJ, int NBUF, int BK = 64, int KG = 1, bool NORMQ = false>
+template <int WM, int WN, int TI, int TJ, int NBUF, int BK = 64, int KG = 1>
 __global__ __launch_bounds__(256 * KG, 2 / KG) void k_gemm_q8d(const int8_t* __restrict__ X, const float* __restrict__ Xd, int M,
                                                      const int8_t* __restrict__ W, const __half* __restrict__ Wsc,
                                                      int N, int K, const float* __restrict__ bias, const float* res,
                                                      float* y, int ldy, int epi, int steps_per_split,
                                                      int8_t* __restrict__ yq, float* __restrict__ yd,
-                                                     float* fix_part, unsigned* fix_cnt, NormFuse nf) {
-    static_assert(!NORMQ || (TJ == 4 && TI * TJ <= 4 && WN == 1), "k_gemm_q8d: the norm epilogue needs 64-column wave tiles");
+                                                     float* fix_part, unsigned* fix_cnt) {
     static_assert(WM * WN == 4, "k_gemm_q8d: 4 waves per K group");
     static_assert(BK == 64 || BK == 128, "k_gemm_q8d: a stage is 2 or 4 Q8 blocks");
     // KG K groups of 4 waves share the tile: group g takes blocks [g·KB/KG, (g+1)·KB/KG) of every stage and the
@@ -1186,7 +1091,7 @@ __global__ __launch_bounds__(256 * KG, 2 / KG) void k_gemm_q8d(const int8_t* __r
                     red[(i * TJ + j) * 64] = make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
         }
         __syncthreads();
-        if (!NORMQ && kg == 1 && (TI * TJ > 4 || TJ != 4 || !fix_part)) return;
+        if (kg == 1 && (TI * TJ > 4 || TJ != 4 || !fix_part)) return;
         if (kg == 0 && active) {
 #pragma unroll
             for (int i = 0; i < TI; i++)
@@ -1196,14 +1101,6 @@ __global__ __launch_bounds__(256 * KG, 2 / KG) void k_gemm_q8d(const int8_t* __r
                     acc[i][j][0] += v.x, acc[i][j][1] += v.y, acc[i][j][2] += v.z, acc[i][j][3] += v.w;
                 }
         }
-    }
-    if constexpr (NORMQ) {
-        // the split's last workgroup (or the only one) runs the epilogue; the workgroups that run it count in per row tile
-        if (fix_part && gridDim.z > 1 && !splitk_fixup<TI, TJ>(acc, kg == 0 && active, lw, 4, fix_part, fix_cnt, (int*)smem))
-            return;
-        if (kg == 0 && active) epi_resid_nq8<TI>(acc, M, N, m0, n0, arow, bcol, fr, fq, y, nf, yq, yd);
-        norm_rowtile_finish<BM>(M, N, m0, nf, yd, (int*)smem);
-        return;
     }
     // split-K fix-up (the 64-column wave tiles of ≤ 64×64 workgroup tiles — the SwiGLU-capable decode tiles; the
     // others keep their register budget): the last workgroup of the tile adds the partials
@@ -1464,168 +1361,6 @@ __global__ __launch_bounds__(64 * CG * KS) void k_gemm_q8_ws(const int8_t* __res
         }
 }
 
-// ------------------------------------------------------------------------------------------------ GEMM (A-stationary)
-// Batched decode steps (17–256 rows, K ≤ 2048: the QKV, O and gate/up projections).  The 64-row activation panel is
-// the small operand: it is staged ONCE into LDS (64·K int8 + 64·K/32 f32 scales ≤ 144 KB, one workgroup per CU) and
-// stays there while the weights stream from HBM straight into the MFMA operand registers, each weight byte read once
-// per row group — no LDS ring, no per-stage barrier, no A-panel re-reads per column tile (the LDS-DMA tiles' decode
-// configurations re-read A and B per 64×64 tile and run at 20–30 % of their VALU floor on these shapes,
-// profiles/r3a_dec_sweep_det.log).  Workgroup = NCW column groups of 64 × KW K slices (one wave each).
-//  * B (weights): lane (fr, g) loads the 16 bytes [16g, 16g+16) of column fr's 64-byte span (two Q8 blocks) of each of
-//    the wave's 4 column fragments, U spans per load group, two groups in flight (the k_gemm_q8_ws stream).
-//    v_mfma_i32_16x16x64_i8 pairs byte j of lane group g in both operands, so the weight span masked to lane groups
-//    0–1 (block 2s) or 2–3 (block 2s+1) gives each block's exact int32 sum — masked once per span and column
-//    fragment, reused by the 4 row fragments.
-//  * A (activations): row r's 16-byte chunk c stored at chunk c ^ (r & 15) (source-address swizzle of the lane-linear
-//    DMA) → conflict-free ds_read_b128 of lane (fr, g) = row 16i+fr, chunk 4s+g.  Scales block-major [K/32][64].
-//  * Rescale: the outer-product MFMA (v_mfma_f32_16x16x1f32: lane l supplies d_x of row l&15 and d_w of column l; register
-//    4j+r of lane (fr, g) = d_x[4g+r]·d_w[16j+fr]) + cvt + fma per output and block, as k_gemm_q8d's OP tiles.
-//  * The KW partial tiles are summed through LDS in K-slice order (deterministic), and the slice-0 wave of each column
-//    group runs the shared 16·4 × 64 epilogue (store / residual / SwiGLU + Q8 / residual + next-norm Q8).
-// Every output is one fixed-order sum (per K slice: blocks in order by fma; slices in order): the same bits in every
-// launch of the configuration.
-template <int NCW, int KW, bool NORMQ = false>
-__global__ __launch_bounds__(64 * NCW * KW) void k_gemm_q8_as(const int8_t* __restrict__ X, const float* __restrict__ Xd,
-                                                             int M, const int8_t* __restrict__ W,
-                                                             const __half* __restrict__ Wsc, int N, int K,
-                                                             const float* __restrict__ bias, const float* res, float* y,
-                                                             int ldy, int epi, int8_t* __restrict__ yq,
-                                                             float* __restrict__ yd, NormFuse nf) {
-    constexpr int NW = NCW * KW, U = 2, BM = 64;
-    extern __shared__ __attribute__((aligned(16))) char smem_as[];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int cg = wave % NCW, ks = wave / NCW;
-    const int m0 = blockIdx.y * BM, nb = K / QK, ns = nb / 2;
-    const int per = ns / KW, s0 = ks * per;   // host: ns % (KW·U) == 0
-    const int n0 = (blockIdx.x * NCW + cg) * 64;
-    const int fr = lane & 15, g = lane >> 4;
-    int8_t* sA = (int8_t*)smem_as;                      // [64][K] swizzled
-    float* sX = (float*)(smem_as + (size_t)BM * K);     // [nb][64]
-    const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem_as;
-
-    // ---- weight stream: column n0 + 16j + fr, span s → 16 bytes per lane; scales of the lane's own column n0 + lane
-    const int8_t* wp[4];
-#pragma unroll
-    for (int j = 0; j < 4; j++) wp[j] = W + (size_t)min(n0 + 16 * j + fr, N - 1) * K + 16 * g;
-    const uint32_t* sp = (const uint32_t*)(Wsc + (size_t)min(n0 + lane, N - 1) * nb);
-    v4i wv[2][U][4];
-    uint32_t sw[2][U];
-    auto load = [&](auto bufc, int s) {
-        constexpr int buf = decltype(bufc)::value;
-#pragma unroll
-        for (int u = 0; u < U; u++) {
-#pragma unroll
-            for (int j = 0; j < 4; j++) wv[buf][u][j] = __builtin_nontemporal_load((const v4i*)(wp[j] + 64 * (size_t)(s + u)));
-            sw[buf][u] = sp[s + u];
-        }
-    };
-    using B0 = std::integral_constant<int, 0>;
-    using B1 = std::integral_constant<int, 1>;
-    load(B0{}, s0);   // the first weight group flies while the activation panel is staged
-
-    // ---- activation panel → LDS (lane-linear DMA; the swizzle goes on the source address)
-    {
-        const int cpr = K / 16;                 // 16-byte chunks per row
-        const int pieces = BM * cpr / 64;       // 1-KB DMA pieces
-        for (int p = wave; p < pieces; p += NW) {
-            const int c = p * 64 + lane, row = c / cpr, ch = c % cpr;
-            const int src = (ch & ~15) | ((ch ^ row) & 15);
-            dma_lds16(X + (size_t)min(m0 + row, M - 1) * K + 16 * src, __builtin_amdgcn_readfirstlane(lds0 + 1024 * p));
-        }
-        for (int b = wave; b < nb; b += NW)     // scales [b][row]
-            dma_lds4(Xd + (size_t)min(m0 + lane, M - 1) * nb + b,
-                     __builtin_amdgcn_readfirstlane(lds0 + BM * K + 256 * b));
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-
-    float acc[4][4][4];
-#pragma unroll
-    for (int i = 0; i < 4; i++)
-#pragma unroll
-        for (int j = 0; j < 4; j++)
-#pragma unroll
-            for (int r = 0; r < 4; r++) acc[i][j][r] = 0.f;
-    const bool lo = g < 2;
-    const v4i zero = {0, 0, 0, 0};
-    auto compute = [&](auto bufc, int s) {
-        constexpr int buf = decltype(bufc)::value;
-#pragma unroll
-        for (int u = 0; u < U; u++) {
-            const int sp_ = s + u;
-            v4i a[4];
-#pragma unroll
-            for (int i = 0; i < 4; i++) {
-                const int row = 16 * i + fr;
-                int off = row * K + 16 * ((4 * sp_ + g) ^ fr);
-                asm volatile("" : "+v"(off));
-                a[i] = *(const v4i*)(sA + off);
-            }
-#pragma unroll
-            for (int h = 0; h < 2; h++) {   // block 2·sp_ + h
-                const int blk = 2 * sp_ + h;
-                const uint32_t h2 = sw[buf][u];
-                const float dwl = __half2float(__ushort_as_half((unsigned short)(h ? h2 >> 16 : h2 & 0xffff)));
-                v4i bm[4];
-#pragma unroll
-                for (int j = 0; j < 4; j++) bm[j] = (lo == (h == 0)) ? wv[buf][u][j] : zero;
-#pragma unroll
-                for (int i = 0; i < 4; i++) {
-                    const float dxl = sX[blk * BM + 16 * i + fr];
-                    const v16f prod = __builtin_amdgcn_mfma_f32_16x16x1f32(dxl, dwl, v16f{}, 0, 0, 0);
-#pragma unroll
-                    for (int j = 0; j < 4; j++) {
-                        const v4i c = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[i], bm[j], zero, 0, 0, 0);
-#pragma unroll
-                        for (int r = 0; r < 4; r++) acc[i][j][r] = fmaf((float)c[r], prod[4 * j + r], acc[i][j][r]);
-                    }
-                }
-            }
-        }
-    };
-    const int end = s0 + per;
-    for (int s = s0; s < end; s += 2 * U) {
-        if (s + U < end) load(B1{}, s + U);
-        compute(B0{}, s);
-        if (s + U >= end) break;
-        if (s + 2 * U < end) load(B0{}, s + 2 * U);
-        compute(B1{}, s + U);
-    }
-    // ---- K slices summed in order through LDS (the activation panel is dead once every wave left the loop)
-    if constexpr (KW > 1) {
-        __syncthreads();
-        float4* red = (float4*)smem_as;   // [KW-1][NCW][16 (i·4+j)][64]
-        if (ks > 0) {
-#pragma unroll
-            for (int i = 0; i < 4; i++)
-#pragma unroll
-                for (int j = 0; j < 4; j++)
-                    red[(((ks - 1) * NCW + cg) * 16 + i * 4 + j) * 64 + lane] =
-                        make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
-        }
-        __syncthreads();
-        if (ks == 0) {
-#pragma unroll
-            for (int w = 1; w < KW; w++)
-#pragma unroll
-                for (int i = 0; i < 4; i++)
-#pragma unroll
-                    for (int j = 0; j < 4; j++) {
-                        const float4 v = red[(((w - 1) * NCW + cg) * 16 + i * 4 + j) * 64 + lane];
-                        acc[i][j][0] += v.x, acc[i][j][1] += v.y, acc[i][j][2] += v.z, acc[i][j][3] += v.w;
-                    }
-        }
-    }
-    const bool mine = ks == 0 && n0 < N;   // wave-uniform
-    if constexpr (NORMQ) {
-        __syncthreads();   // the reduction buffer is read; its LDS takes the finish flag
-        if (mine) epi_resid_nq8<4>(acc, M, N, m0, n0, 0, 0, fr, 4 * g, y, nf, yq, yd);
-        norm_rowtile_finish<BM>(M, N, m0, nf, yd, (int*)smem_as);
-        return;
-    }
-    if (mine) gemm_epilogue<4, 4>(acc, M, N, m0, n0, 0, 0, fr, 4 * g, bias, res, y, ldy, epi, yq, yd);
-}
-
 template <int TI, int CG, int KS>
 static void launch_ws(hipStream_t s, const int8_t* xq, const float* xd, int M, const Q8Mat& W, const float* bias,
                       const float* res, float* y, int ldy, int epi, int8_t* yq, float* yd) {
@@ -1693,13 +1428,12 @@ static void launch_gemm_dma(dim3 grid, hipStream_t s, const int8_t* xq, const fl
                             const float* bias, const float* res, float* y, int ldy, int epi, int sps, int8_t* yq,
                             float* yd, float* fix_part, unsigned* fix_cnt) {
     k_gemm_q8d<WM, WN, TI, TJ, NBUF, BK, KG><<<grid, 256 * KG, 0, s>>>(xq, xd, M, W.qs, W.sc, W.N, W.K, bias, res, y, ldy, epi, sps, yq,
-                                                    yd, fix_part, fix_cnt, NormFuse{});
+                                                    yd, fix_part, fix_cnt);
 }
 
 // GEMM configurations: 0..3 register-staged kernel (any K % 32 == 0), 4..11 LDS-DMA kernel, 2×2 waves, stages of
 // 64 (4..7) or 128 (8..11) K (K % bk == 0); 12..13 LDS-DMA, 4×1 waves (64-column wave tiles), K-128 stages.
-// ks: waves of the K-over-waves decode kernel (bk unused); kw: K slices of the A-stationary kernel (bn = 64·NCW)
-struct GemmCfg { int bm, bn, bk; bool dma; int ks = 0; int kw = 0; };
+struct GemmCfg { int bm, bn, bk; bool dma; int ks = 0; };   // ks: waves of the K-over-waves decode kernel (bk unused)
 static const GemmCfg kGemmCfgs[] = {
     {128, 128, 128, false}, {64, 128, 128, false}, {64, 64, 128, false}, {32, 64, 128, false},   // 0..3
     {128, 128, 64, true}, {64, 128, 64, true}, {64, 64, 64, true}, {128, 64, 64, true},          // 4..7
@@ -1713,9 +1447,6 @@ static const GemmCfg kGemmCfgs[] = {
     // 24..30 decode kernel k_gemm_q8_ks<TI, TJ, NW>: full K per workgroup, K split over NW waves
     {32, 16, 0, false, 16}, {32, 32, 0, false, 16}, {64, 16, 0, false, 16}, {64, 32, 0, false, 8},
     {16, 64, 0, false, 16}, {32, 64, 0, false, 8}, {64, 64, 0, false, 8},
-    // 31..37 A-stationary decode kernel k_gemm_q8_as<NCW, KW> (K ≤ 2048): 64 rows × 64·NCW columns, KW K slices
-    {64, 64, 0, false, 0, 4}, {64, 64, 0, false, 0, 8}, {64, 128, 0, false, 0, 2}, {64, 128, 0, false, 0, 4},
-    {64, 192, 0, false, 0, 2}, {64, 256, 0, false, 0, 2}, {64, 64, 0, false, 0, 2},
 };
 constexpr int kNumGemmCfgs = sizeof(kGemmCfgs) / sizeof(kGemmCfgs[0]);
 
@@ -1726,39 +1457,6 @@ static void launch_ks(hipStream_t s, const int8_t* xq, const float* xd, int M, c
     const size_t lds = std::max<size_t>((size_t)(W.K / QK) * 16 * TI * 4, (size_t)NW * TI * TJ * 64 * 16);
     QASR_CHECK(lds <= 160 * 1024, QASR_E_INVALID, "gemm_q8: decode tile's LDS exceeds 160 KB");
     k_gemm_q8_ks<TI, TJ, NW><<<grid, 64 * NW, lds, s>>>(xq, xd, M, W.qs, W.sc, W.N, W.K, bias, res, y, ldy, epi, yq, yd);
-}
-
-template <int NCW, int KW, bool NORMQ = false>
-static void launch_as(hipStream_t s, const int8_t* xq, const float* xd, int M, const Q8Mat& W, const float* bias,
-                      const float* res, float* y, int ldy, int epi, int8_t* yq, float* yd, const NormFuse& nf) {
-    const dim3 grid(cdiv(W.N, 64 * NCW), cdiv(M, 64));
-    const size_t lds = std::max<size_t>((size_t)64 * W.K + (size_t)(W.K / QK) * 64 * 4,
-                                        (size_t)(KW - 1) * NCW * 16 * 64 * 16);
-    QASR_CHECK(lds <= 160 * 1024, QASR_E_INVALID, "gemm_q8_as: LDS");
-    k_gemm_q8_as<NCW, KW, NORMQ><<<grid, 64 * NCW * KW, lds, s>>>(xq, xd, M, W.qs, W.sc, W.N, W.K, bias, res, y, ldy,
-                                                                 epi, yq, yd, nf);
-}
-
-// the A-stationary kernel's shape rules: K ≤ 2048 (the 64-row panel in LDS), the K slices a whole number of
-// two-span load groups, epilogues on 64-column wave tiles
-static bool as_usable(int cfg, int K) {
-    const GemmCfg& g = kGemmCfgs[cfg];
-    return g.kw > 0 && K <= 2048 && K % 1024 == 0 && (K / 64) % (g.kw * 2) == 0;
-}
-
-template <bool NORMQ>
-static void launch_as_cfg(int cfg, hipStream_t s, const int8_t* xq, const float* xd, int M, const Q8Mat& W,
-                          const float* bias, const float* res, float* y, int ldy, int epi, int8_t* yq, float* yd,
-                          const NormFuse& nf = NormFuse{}) {
-    switch (cfg) {
-        case 31: launch_as<1, 4, NORMQ>(s, xq, xd, M, W, bias, res, y, ldy, epi, yq, yd, nf); break;
-        case 32: launch_as<1, 8, NORMQ>(s, xq, xd, M, W, bias, res, y, ldy, epi, yq, yd, nf); break;
-        case 33: launch_as<2, 2, NORMQ>(s, xq, xd, M, W, bias, res, y, ldy, epi, yq, yd, nf); break;
-        case 34: launch_as<2, 4, NORMQ>(s, xq, xd, M, W, bias, res, y, ldy, epi, yq, yd, nf); break;
-        case 35: launch_as<3, 2, NORMQ>(s, xq, xd, M, W, bias, res, y, ldy, epi, yq, yd, nf); break;
-        case 36: launch_as<4, 2, NORMQ>(s, xq, xd, M, W, bias, res, y, ldy, epi, yq, yd, nf); break;
-        default: launch_as<1, 2, NORMQ>(s, xq, xd, M, W, bias, res, y, ldy, epi, yq, yd, nf); break;
-    }
 }
 
 static void launch_ks_cfg(int cfg, hipStream_t s, const int8_t* xq, const float* xd, int M, const Q8Mat& W,
@@ -2151,7 +1849,6 @@ void gemm_q8(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const flo
         return;
     auto usable = [&](int c) {
         const GemmCfg& g = kGemmCfgs[c];
-        if (g.kw) return as_usable(c, W.K) && M <= 256 && epi != EPI_STORE_F16;
         if (g.ks) return W.K % (QK * 4 * g.ks) == 0 && (epi != EPI_GELU_Q8 || g.bn % 32 == 0);
         return !g.dma || W.K % g.bk == 0;
     };
@@ -2188,12 +1885,6 @@ void gemm_q8(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const flo
     }
     if (force_cfg >= 0 && force_cfg < kNumGemmCfgs && usable(force_cfg)) pick = force_cfg;
     const GemmCfg& cf = kGemmCfgs[pick];
-    if (cf.kw) {   // A-stationary decode kernel: one launch over the whole K, no split-K, no memset
-        QASR_CHECK(epi != EPI_SWIGLU || (W.N % 64 == 0 && yq && yd), QASR_E_INVALID, "gemm_q8: SwiGLU epilogue shape");
-        QASR_CHECK(epi != EPI_GELU_Q8 || (W.N % 32 == 0 && yq && yd), QASR_E_INVALID, "gemm_q8: GELU+Q8 epilogue shape");
-        launch_as_cfg<false>(pick, s, xq, xd, M, W, bias, res, y, ldy, epi, yq, yd);
-        return;
-    }
     if (cf.ks) {   // decode kernel: one launch over the whole K, no split-K, no memset
         QASR_CHECK(epi != EPI_SWIGLU || (cf.bn == 64 && W.N % 64 == 0 && yq && yd), QASR_E_INVALID,
                    "gemm_q8: SwiGLU epilogue needs a 64-column wave tile");
@@ -2245,48 +1936,6 @@ void gemm_q8(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const flo
         QASR_HIP(hipMemsetAsync(y, 0, (size_t)M * ldy * sizeof(float), s));
     dim3 grid(cdiv(W.N, cf.bn), cdiv(M, cf.bm), splits);
     launch_cfg(pick, grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd);
-}
-
-// Residual GEMM + next RMSNorm's Q8 (EPI_RESID_NQ8): the 64-column wave tiles 12 / 15 / 22 and their fix-up splits,
-// picked per row bucket from the deterministic-mode sweep of the residual shapes (profiles/r3a_dec_sweep_det.log: the
-// fastest 64-column-wave entry per bucket; O-projection K ≤ 2048, down-projection K > 2048)
-static const DecPick kNqO[] = {{16, 15, 4}, {32, 22, 6}, {128, 15, 4}, {192, 12, 6}, {224, 12, 4}, {256, 12, 3}};
-static const DecPick kNqDown[] = {{64, 15, 8}, {128, 15, 4}, {192, 12, 8}, {256, 12, 4}};
-
-template <int KG, int NBUF>
-static void launch_nq(dim3 grid, hipStream_t s, const int8_t* xq, const float* xd, int M, const Q8Mat& W, float* y,
-                      int sps, int8_t* yq, float* yd, const NormFuse& nf) {
-    k_gemm_q8d<4, 1, 1, 4, NBUF, 128, KG, true><<<grid, 256 * KG, 0, s>>>(
-        xq, xd, M, W.qs, W.sc, W.N, W.K, nullptr, y, y, W.N, EPI_RESID_NQ8, sps, yq, yd, g_fix_part, g_fix_cnt, nf);
-}
-
-bool gemm_q8_resid_rmsq8(const int8_t* xq, const float* xd, int M, const Q8Mat& W, float* y, const NormFuse& nf,
-                         int8_t* yq, float* yd, hipStream_t s, bool force) {
-    // opt-in (QASR_NORM_FUSE=1): measured slower than the separate rmsnorm_q8 launch on the C4 bench (528.5 against
-    // 521 ms per step, profiles/r3i_bench_*: the row tile's last-arriver tail costs more than the launch it saves)
-    static const bool on = getenv("QASR_NORM_FUSE") && atoi(getenv("QASR_NORM_FUSE")) != 0;
-    if (!(on || force) || M < 1 || M > 256 || W.mx || g_stable || !deterministic() || !g_fix_part || W.K % 128 != 0 ||
-        W.N % 64 != 0 || W.N > kNormFuseMaxN || !nf.w || !nf.ssp || !nf.cnt || !yq || !yd)
-        return false;
-    const DecPick* t = W.K <= 2048 ? kNqO : kNqDown;
-    const int n = W.K <= 2048 ? (int)(sizeof(kNqO) / sizeof(DecPick)) : (int)(sizeof(kNqDown) / sizeof(DecPick));
-    int cfg = 12, splits = 1;
-    for (int i = 0; i < n; i++)
-        if (M <= t[i].m_max) {
-            cfg = t[i].cfg, splits = t[i].splits;
-            break;
-        }
-    const int steps = W.K / 128, tiles_y = cdiv(M, 64), tiles = cdiv(W.N, 64) * tiles_y;
-    QASR_CHECK(tiles_y <= kNormFuseCounters, QASR_E_INVALID, "gemm_q8_resid_rmsq8: row tiles");
-    splits = std::max(1, std::min(splits, steps));
-    if (splits > 1 && (tiles > g_fix_ncnt || (size_t)tiles * splits * 64 * 64 > g_fix_floats)) splits = 1;
-    const int sps = cdiv(steps, splits);
-    const dim3 grid(cdiv(W.N, 64), tiles_y, cdiv(steps, sps));
-    ProfScope ps(s, "gemm_q8_decode", 2.0 * M * W.N * W.K, q8_bytes(M, W, EPI_RESID) + (double)M * W.N * 1.125);
-    if (cfg == 15) launch_nq<2, 3>(grid, s, xq, xd, M, W, y, sps, yq, yd, nf);
-    else if (cfg == 22) launch_nq<1, 6>(grid, s, xq, xd, M, W, y, sps, yq, yd, nf);
-    else launch_nq<1, 3>(grid, s, xq, xd, M, W, y, sps, yq, yd, nf);
-    return true;
 }
 
 int64_t gate_up_interleaved_row(int64_t r, int64_t F) {

@@ -810,87 +810,6 @@ def test_gemm_swiglu_q8_fixup(torch_dev, fixup, m, f, k, cfg):
     assert not host(fixup).any()
 
 
-# the A-stationary decode kernel k_gemm_q8_as (kGemmCfgs 31..37: 64-row activation panel in LDS, weights straight into
-# the MFMA operands, K split over waves): path 1024 + cfg
-AS_CFGS = list(range(31, 38))
-
-
-@pytest.mark.parametrize("cfg", AS_CFGS)
-@pytest.mark.parametrize("m,n,k", [(64, 128, 1024), (100, 320, 2048), (256, 1024, 2048), (17, 4096, 2048)])
-def test_linear_q8_as_exact_integer(torch_dev, cfg, m, n, k):
-    """integer-exact inputs: every block dot, its masked 16x16x64 MFMA pair and the K-slice sums are exact"""
-    y, ref = _linear_case(torch_dev, m, n, k, 1024 + cfg, 0, seed=m + n + cfg, exact=True)
-    assert np.array_equal(y, ref)
-
-
-@pytest.mark.parametrize("cfg", AS_CFGS)
-@pytest.mark.parametrize("epi", [0, 1, 2])
-@pytest.mark.parametrize("m,n,k", [(37, 320, 2048), (130, 1024, 1024), (200, 2048, 2048)])
-def test_linear_q8_as_vs_oracle(torch_dev, cfg, epi, m, n, k):
-    """store / residual / GELU epilogues on the A-stationary tiles (rows past M clamped and dropped), repeats
-    bit-identical"""
-    y, ref = _linear_case(torch_dev, m, n, k, 1024 + cfg, epi, seed=k + epi + cfg)
-    scale = np.abs(ref).max() + 1e-6
-    assert np.abs(y - ref).max() <= 2e-5 * scale * np.sqrt(k / 256)
-    y2, _ = _linear_case(torch_dev, m, n, k, 1024 + cfg, epi, seed=k + epi + cfg)
-    assert np.array_equal(y, y2)
-
-
-@pytest.mark.parametrize("cfg", [1024 + c for c in AS_CFGS])
-@pytest.mark.parametrize("m,f,k", [(40, 512, 1024), (256, 1024, 2048), (150, 768, 2048)])
-def test_gemm_swiglu_q8_as(torch_dev, m, f, k, cfg):
-    """the A-stationary tiles with the SwiGLU + Q8 epilogue"""
-    test_gemm_swiglu_q8(torch_dev, m, f, k, cfg)
-
-
-@pytest.mark.parametrize("m", [9, 16, 33, 100, 130, 200, 256])
-@pytest.mark.parametrize("n,k", [(2048, 2048), (2048, 6144), (1024, 3072)])
-def test_linear_resid_rmsq8(torch_dev, fixup, m, n, k):
-    """the residual GEMM with the next RMSNorm + Q8 in its epilogue (batched decode steps): y = res + X·Wᵀ against
-    the oracle, and the Q8 rows against rmsnorm_q8 run on that same y — q within one step of the int8 grid at < 0.1 %
-    of elements (f32 rounding of x·nw / d' vs x·inv·nw / d), block scales within one f16 ulp; repeats bit-identical,
-    the row-tile and fix-up counters left at zero"""
-    import torch
-
-    rng = np.random.default_rng(m + n + k)
-    x = rng.standard_normal((m, k)).astype(np.float32)
-    res = (rng.standard_normal((m, n)) * 2.0).astype(np.float32)
-    nw = (1.0 + 0.3 * rng.standard_normal(n)).astype(np.float32)
-    blocks = oracle.synth_q8(m + k, "w", n, k, 0.05)
-    qs, sc = q8_split(blocks, n, k)
-    xq = empty((m, k), torch.int8, torch_dev)
-    xdd = empty((m, k // 32), torch.float32, torch_dev)
-    xt = dev(x, torch_dev)
-    _lib.check(L().qasr_op_quant_rows(ptr(xt), m, k, k, ptr(xq), ptr(xdd), None))
-    wq, ws, nwd = dev(qs, torch_dev), dev(sc, torch_dev), dev(nw, torch_dev)
-    ssp = empty((m * n // 64,), torch.float32, torch_dev)
-    cnt = torch.zeros(64, dtype=torch.int32, device=torch_dev)
-    outs = []
-    for _ in range(3):
-        y = dev(res, torch_dev)
-        yq = empty((m, n), torch.int8, torch_dev)
-        yd = empty((m, n // 32), torch.float32, torch_dev)
-        _lib.check(L().qasr_op_linear_resid_rmsq8(ptr(xq), ptr(xdd), m, ptr(wq), ptr(ws), n, k, ptr(y), ptr(nwd), 1e-6,
-                                                  ptr(yq), ptr(yd), ptr(ssp), ptr(cnt), None))
-        outs.append((host(y), host(yq), host(yd)))
-    for o in outs[1:]:
-        assert all(np.array_equal(a, b) for a, b in zip(outs[0], o))
-    assert not host(cnt).any() and not host(fixup).any()
-    yv, qv, dv = outs[0]
-    ref = oracle.linear_q8(x, blocks, n, None) + res
-    scale = np.abs(ref).max() + 1e-6
-    assert np.abs(yv - ref).max() <= 2e-5 * scale * np.sqrt(k / 256)
-    # rmsnorm_q8 of the kernel's own y
-    q2 = empty((m, n), torch.int8, torch_dev)
-    d2 = empty((m, n // 32), torch.float32, torch_dev)
-    _lib.check(L().qasr_op_rmsnorm_q8(ptr(dev(yv, torch_dev)), m, n, ptr(nwd), 1e-6, ptr(q2), ptr(d2), None))
-    qr, dr = host(q2).astype(np.int32), host(d2)
-    dq = np.abs(qv.astype(np.int32) - qr)
-    assert dq.max() <= 1 and (dq > 0).mean() < 1e-3, ((dq > 0).mean(), dq.max())
-    assert np.all(np.abs(dv - dr) <= dr * 2.0 ** -10), np.abs(dv - dr).max()
-    assert (dv != dr).mean() < 0.02
-
-
 @pytest.fixture
 def ws_all():
     """the weight-streaming kernel on every shape it supports up to 64 rows (restored to the default afterwards)"""

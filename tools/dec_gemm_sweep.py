@@ -16,9 +16,9 @@ from qasr import _lib  # noqa: E402
 
 SHAPES = [("qkv", 4096, 2048, 0), ("o", 2048, 2048, 1), ("down", 2048, 6144, 1), ("gu", 12288, 2048, 3)]
 MS = [int(x) for x in os.environ.get("MS", "16,32,64,96,128,160,192,224,256").split(",")]
-CFGS = list(range(4, 38))
+CFGS = list(range(4, 31))
 SPLITS = [1, 2, 3, 4, 6, 8]
-SWIGLU_CFGS = [4, 5, 8, 9, 12, 13, 15, 20, 22, 23, 28, 29, 30] + list(range(31, 38))
+SWIGLU_CFGS = [4, 5, 8, 9, 12, 13, 15, 20, 22, 23, 28, 29, 30]
 
 
 def main():
@@ -48,7 +48,7 @@ def main():
             hq = torch.empty(M, N // 2, dtype=torch.int8, device=dev)
             hd = torch.empty(M, N // 64, device=dev)
             def splits(c):
-                if c >= 24:   # K over waves / A-stationary: no split-K
+                if c >= 24:
                     return [0]
                 if det and not (fix and c in wave64):
                     return [1]
@@ -61,10 +61,9 @@ def main():
                     if epi == 3:
                         _lib.check(lib.qasr_op_gemm_swiglu_q8_cfg(xq.data_ptr(), xd.data_ptr(), M, wq[i].data_ptr(),
                                                                   ws[i].data_ptr(), N, K, hq.data_ptr(), hd.data_ptr(),
-                                                                  (1024 + cfg if cfg >= 31 else cfg + 32 * sp)
-                                                                  if cfg >= 0 else cfg, None))
+                                                                  cfg + 32 * sp if cfg >= 0 else cfg, None))
                         return
-                    path = 2 if cfg < 0 else 1024 + cfg if cfg >= 31 else 16 + cfg + 32 * sp
+                    path = 2 if cfg < 0 else 16 + cfg + 32 * sp
                     # a store GEMM with split-K clears y inside gemm_q8 (hipMemsetAsync): timed as part of it
                     _lib.check(lib.qasr_op_linear_q8(xq.data_ptr(), xd.data_ptr(), M, wq[i].data_ptr(),
                                                      ws[i].data_ptr(), N, K, None,
