@@ -80,7 +80,7 @@ __global__ __launch_bounds__(256) void k_attention(const __half* __restrict__ Q,
     constexpr int VU = 8;         // keys per PV iteration
     __shared__ float sp[4][G][CH];
     __shared__ float cm_s[4][G], cl_s[4][G];
-    __shared__ float ca_s[4][G][HD];
+    __shared__ __align__(16) float ca_s[4][G][HD];
     __shared__ __align__(16) __half2 kn[FUSED ? HD / 2 : 1];   // FUSED: the new K row (f16), see the K preload
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     // NW = 4: one workgroup per (row, KV head), its 4 waves take contiguous quarters of the key range and merge
@@ -137,7 +137,9 @@ __global__ __launch_bounds__(256) void k_attention(const __half* __restrict__ Q,
         // rounding: bit-identical).  q stays in LDS; K/V go to the cache and the barrier makes the new row
         // visible to the waves that read it below (workgroup-scope ordering of global memory).
         static_assert(HD == 128 && NW == 4, "fused q/k prologue: hd 128 decode kernel");
-        __shared__ float qs[G][HD];
+        // q rows in LDS with 4 floats of padding per 16 (element e at e + 4·(e/16)): the 8 lanes groups' ds_read_b128 of
+        // dims 16·sub … 16·sub + 15 then fall in distinct banks (unpadded, sub and sub + 4 collided)
+        __shared__ __align__(16) float qs[G][HD + HD / 4];
         const int nslot = nh + 2 * nkv, kvd = nkv * HD;
         const float* src = fz.qkv + (size_t)r * nslot * HD;
         const int p = fz.pos[r], sl = fz.slot[r];
@@ -161,8 +163,7 @@ __global__ __launch_bounds__(256) void k_attention(const __half* __restrict__ Q,
             const __half2 hv = norm_rope_hd128(v, g, cs, lo, fz.eps);
             if (t < G) {
                 const float2 back = __half22float2(hv);
-                qs[t][2 * lane] = back.x;
-                qs[t][2 * lane + 1] = back.y;
+                *(float2*)&qs[t][2 * lane + 4 * (lane >> 3)] = make_float2(back.x, back.y);
             } else {
                 *(__half2*)(fz.kc + (size_t)sl * kvd + kvh * HD + 2 * lane) = hv;
                 kn[lane] = hv;
@@ -173,7 +174,7 @@ __global__ __launch_bounds__(256) void k_attention(const __half* __restrict__ Q,
         for (int g = 0; g < G; g++)
 #pragma unroll
             for (int j = 0; j < QD / 2; j++)
-                qv[g][j] = (h2v){(_Float16)qs[g][sub * QD + 2 * j], (_Float16)qs[g][sub * QD + 2 * j + 1]};
+                qv[g][j] = (h2v){(_Float16)qs[g][sub * (QD + 4) + 2 * j], (_Float16)qs[g][sub * (QD + 4) + 2 * j + 1]};
     } else {
 #pragma unroll
         for (int g = 0; g < G; g++) {
@@ -413,7 +414,8 @@ __global__ __launch_bounds__(256) void k_attention(const __half* __restrict__ Q,
             if constexpr (DEC) {
                 if (vg == 0) {
 #pragma unroll
-                    for (int j = 0; j < 8; j++) ca_s[w][g][vd + j] = av[g][j];
+                    for (int j = 0; j < 8; j += 4)   // two ds_write_b128 per lane (8 scalar writes were 2-way conflicted)
+                        *(float4*)&ca_s[w][g][vd + j] = make_float4(av[g][j], av[g][j + 1], av[g][j + 2], av[g][j + 3]);
                 }
             } else {
 #pragma unroll
