@@ -297,6 +297,13 @@ QASR_API int qasr_op_gemv_fused(int32_t pro, const float* src, int32_t ld_src, c
                                 const int8_t* xq, const float* xd, const int8_t* wqs, const void* wsc, int32_t N,
                                 int32_t K, const float* res, float* y, int32_t ldy, int32_t epi, int8_t* hq,
                                 float* hd, void* stream);
+/* The draft verify passes' exact-row linear on the matrix core (engine.cpp, ≥ 5 rows): y = X·Wᵀ (epi 0) or y = res +
+   X·Wᵀ (epi 1, y may alias res) with bit for bit the arithmetic of qasr_op_gemv_fused(pro 0) on each row alone — the
+   exact-row contract that makes drafted decoding emit greedy's tokens (qwen3_asr_server.py:321's session.run is one
+   greedy decode).  M 1..32, K a multiple of 1,024 (K/1024 ∈ {1,2,3,4,6}). */
+QASR_API int qasr_op_gemm_exact_rows(const int8_t* xq, const float* xd, int32_t M, const int8_t* wqs, const void* wsc,
+                                     int32_t N, int32_t K, const float* res, float* y, int32_t ldy, int32_t epi,
+                                     void* stream);
 QASR_API int qasr_op_qk_norm_rope(const float* qkv, int32_t rows, int32_t nh, int32_t nkv, int32_t hd,
                                   const int32_t* pos, const int32_t* slot, const float* qnw, const float* knw,
                                   const float* rope_cs, float eps, void* qout, void* kc, void* vc, void* stream);

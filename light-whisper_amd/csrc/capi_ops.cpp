@@ -171,6 +171,22 @@ QASR_API int qasr_op_gemm_swiglu_q8_cfg(const int8_t* xq, const float* xd, int32
     });
 }
 
+QASR_API int qasr_op_gemm_exact_rows(const int8_t* xq, const float* xd, int32_t M, const int8_t* wqs, const void* wsc,
+                                     int32_t N, int32_t K, const float* res, float* y, int32_t ldy, int32_t epi,
+                                     void* stream) {
+    return guard([&] {
+        QASR_CHECK(N > 0 && ldy >= N && (epi == EPI_STORE || (epi == EPI_RESID && res)), QASR_E_INVALID,
+                   "gemm_exact_rows: bad shape / epilogue");
+        Q8Mat W;
+        W.qs = (int8_t*)wqs;
+        W.sc = (__half*)wsc;
+        W.N = N;
+        W.K = K;
+        gemm_exact_rows(xq, xd, M, W, res, y, ldy, epi, S(stream));
+        launched();
+    });
+}
+
 QASR_API int qasr_op_set_gemm_ws_rows(int32_t rows, int32_t all_shapes) {
     return guard([&] {
         QASR_CHECK(rows >= 0 && rows <= 64, QASR_E_INVALID, "set_gemm_ws_rows: 0..64");

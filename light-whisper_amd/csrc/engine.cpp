@@ -445,11 +445,18 @@ void Session::decoder_layers(float* x, int rows, const int* d_pos, const int* d_
     const bool gv_shapes = gemv_fused_ok(GV_RMS, rows, H) && gemv_fused_ok(GV_NONE, rows, F) &&
                            gemv_fused_ok(GV_NONE, rows, QD);
     // GEMV row counts: the norms and the SwiGLU run inside the GEMVs' prologues (5 launches per layer, not 8)
-    const bool gv = gv_shapes && (exact || (rows <= gemv_layer_rows() && dec_fuse_));
-    QASR_CHECK(!rows_share_kv || (exact && gv), QASR_E_INTERNAL,
+    // exact rows from exact_mfma_rows() up: the same arithmetic on the matrix core (gemm_exact_rows: the block dots by
+    // MFMA, the GEMV's fma chains and wave-sum tree in-lane), with the norms and the SwiGLU as their own launches
+    // (rmsnorm_q8 / swiglu_q8 are the fused prologue's / epilogue's arithmetic) — 8 launches per layer, each near a
+    // 1-row launch's time, where the GEMV's v_dot4 rows cost ~10× a 1-row step at 32 rows
+    const bool xm = exact && rows >= exact_mfma_rows() && gemm_exact_rows_ok(rows, m_->dec[0].qkv) &&
+                    gemm_exact_rows_ok(rows, m_->dec[0].down) && gemm_exact_rows_ok(rows, m_->dec[0].gu);
+    const bool gv = !xm && gv_shapes && (exact || (rows <= gemv_layer_rows() && dec_fuse_));
+    QASR_CHECK(!rows_share_kv || (exact && (gv || xm)), QASR_E_INTERNAL,
                "decoder: a verify pass needs the exact-row path (≤ kExactRows rows, GEMV shapes)");
-    int8_t* hq2 = gv ? (int8_t*)sc_.get(S_HQ, (size_t)rows * F) : nullptr;   // the SwiGLU epilogue's Q8 rows
-    float* hd2 = gv ? (float*)sc_.get(S_HD, (size_t)rows * (F / QK) * sizeof(float)) : nullptr;
+    int8_t* hq2 = gv || xm ? (int8_t*)sc_.get(S_HQ, (size_t)rows * F) : nullptr;   // the SwiGLU Q8 rows
+    float* hd2 = gv || xm ? (float*)sc_.get(S_HD, (size_t)rows * (F / QK) * sizeof(float)) : nullptr;
+    float* gux = xm ? (float*)sc_.get(S_GU, (size_t)rows * 2 * F * sizeof(float)) : nullptr;
     for (int l = 0; l < h.txt_layers; l++) {
         const DecLayer& L = m_->dec[l];
         __half* kc = kc_ + (size_t)l * layer_kv;
@@ -458,7 +465,10 @@ void Session::decoder_layers(float* x, int rows, const int* d_pos, const int* d_
         const bool zq = rows <= 256;
         const bool dmp = g_dump && rows <= kExactRows;
         if (dmp) dump_rows("x_in", l, rows, x, (size_t)rows * H * sizeof(float));
-        if (gv) {
+        if (xm) {
+            rmsnorm_q8(x, rows, H, H, L.attn_norm, h.rms_eps, xq, xd, st_);
+            gemm_exact_rows(xq, xd, rows, L.qkv, nullptr, qkv, QD + 2 * KD, EPI_STORE, st_);
+        } else if (gv) {
             gemv_fused(GV_RMS, nullptr, nullptr, x, H, L.attn_norm, h.rms_eps, rows, L.qkv, nullptr, qkv, QD + 2 * KD,
                        EPI_STORE, nullptr, nullptr, st_);
         } else {
@@ -487,6 +497,19 @@ void Session::decoder_layers(float* x, int rows, const int* d_pos, const int* d_
         if (dmp) {
             dump_rows("att_q", l, rows, xq, (size_t)rows * QD);
             dump_rows("att_d", l, rows, xd, (size_t)rows * (QD / QK) * sizeof(float));
+        }
+        if (xm) {   // the same four steps as separate launches with the exact-row MFMA linears
+            gemm_exact_rows(xq, xd, rows, L.o, x, x, H, EPI_RESID, st_);
+            if (dmp) dump_rows("x_mid", l, rows, x, (size_t)rows * H * sizeof(float));
+            rmsnorm_q8(x, rows, H, H, L.ffn_norm, h.rms_eps, xq, xd, st_);
+            gemm_exact_rows(xq, xd, rows, L.gu, nullptr, gux, 2 * F, EPI_STORE, st_);
+            swiglu_q8(gux, rows, F, hq2, hd2, st_, /*interleaved=*/true);
+            if (dmp) {
+                dump_rows("h_q", l, rows, hq2, (size_t)rows * F);
+                dump_rows("h_d", l, rows, hd2, (size_t)rows * (F / QK) * sizeof(float));
+            }
+            gemm_exact_rows(hq2, hd2, rows, L.down, x, x, H, EPI_RESID, st_);
+            continue;
         }
         if (gv) {   // O-projection + residual; norm + gate/up + SwiGLU + Q8; down-projection + residual
             gemv_fused(GV_NONE, xq, xd, nullptr, 0, nullptr, 0.f, rows, L.o, x, x, H, EPI_RESID, nullptr, nullptr, st_);
@@ -535,7 +558,9 @@ void Session::lm_head_rows(const float* x, int rows, int ldx, float* logits, boo
     mx_ws(rows, h.txt_h);
     // ≤ 4 rows (1-row decode steps) and exact rows (verify passes): the weight-streaming GEMV, one per-row arithmetic
     // for any row count (k_gemv_wide's row groups); more rows: the MFMA GEMM
-    if ((rows <= kGemvRows || exact) && gemv_fused_ok(GV_NONE, rows, h.txt_h))
+    if (exact && rows >= exact_mfma_rows() && gemm_exact_rows_ok(rows, m_->lm_head))
+        gemm_exact_rows(xq, xd, rows, m_->lm_head, nullptr, logits, h.vocab, EPI_STORE, st_);
+    else if ((rows <= kGemvRows || exact) && gemv_fused_ok(GV_NONE, rows, h.txt_h))
         gemv_fused(GV_NONE, xq, xd, nullptr, 0, nullptr, 0.f, rows, m_->lm_head, nullptr, logits, h.vocab, EPI_STORE,
                    nullptr, nullptr, st_);
     else
@@ -591,6 +616,47 @@ void Session::draft_step(int B) {
     QASR_HIP(hipMemcpyAsync((int*)pin_cnt_ + 8, d_tok, (size_t)B * sizeof(int), hipMemcpyDeviceToHost, st_));
 }
 
+// bucket graphs hold scratch / KV / weight pointers: retire them whenever any of those moved
+void Session::draft_graphs_refresh() {
+    const uint64_t key[4] = {sc_.epoch, kv_epoch_, m_->precision_gen, deterministic_gen()};
+    if (memcmp(key, draft_key_, sizeof key) != 0) {
+        for (auto& g : draft_graphs_) (void)hipGraphExecDestroy(g.second);
+        draft_graphs_.clear();
+        memcpy(draft_key_, key, sizeof key);
+    }
+}
+
+// one verify pass of bucket B (the tables already in S_DTAB): the bucket's captured graph, or an eager pass that also
+// sizes the scratch, then captured for the next time
+void Session::draft_pass(int B) {
+    const bool graphs = !prof_enabled() && !getenv("QASR_NO_GRAPH");
+    auto it = draft_graphs_.find(B);
+    if (graphs && it != draft_graphs_.end()) {
+        QASR_HIP(hipGraphLaunch(it->second, st_));
+        return;
+    }
+    draft_step(B);            // eager: also sizes the scratch this bucket needs before its graph is captured
+    draft_graphs_refresh();   // (a growth retires the other buckets' graphs)
+    if (!graphs) return;
+    QASR_HIP(hipStreamSynchronize(st_));
+    hipGraph_t g;
+    QASR_HIP(hipStreamBeginCapture(st_, hipStreamCaptureModeRelaxed));
+    sc_.capturing = true;
+    try {
+        draft_step(B);
+    } catch (...) {
+        sc_.capturing = false;
+        (void)hipStreamEndCapture(st_, &g);
+        throw;
+    }
+    sc_.capturing = false;
+    QASR_HIP(hipStreamEndCapture(st_, &g));
+    hipGraphExec_t ex;
+    QASR_HIP(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
+    (void)hipGraphDestroy(g);
+    draft_graphs_.emplace(B, ex);
+}
+
 // Prompt-lookup decoding of one utterance (toks holds the first, prefill-chosen token).  Each pass feeds the last
 // accepted token and a draft — the tokens that followed the most recent earlier occurrence of the last two (else one)
 // accepted tokens in the session's history — and accepts greedy's tokens up to and including the first that departs
@@ -602,19 +668,31 @@ void Session::draft_decode(int n_prompt, int base, int budget, int dummy, std::v
                            bool forced) {
     const qasr_hparams& h = m_->hp;
     constexpr int RMAX = kDraftRows;
-    int max_draft = RMAX - 1;
+    // Draft length: with per-token acceptance a, a pass of k drafted tokens yields 1 + a + … + a^k tokens and costs
+    // kPassCost[bucket] (one verify pass of 1/2/4/8/16/32 rows relative to a 1-row step; profiles/r3q_verify_cost.log,
+    // exact-row MFMA linears from 5 rows); k fills a row bucket (1, 3, 7, 15, 31) and is the one with the most tokens
+    // per unit cost at the current estimate of a — never worse than plain greedy steps in expectation, long drafts
+    // only while they keep being accepted (the noise sweep in DESIGN §7)
+    static constexpr double kPassCost[6] = {1.0, 1.05, 1.12, 1.45, 1.6, 2.0};
+    auto draft_len = [&](int cap) {
+        const double a = draft_s_ / (draft_s_ + draft_f_);
+        int best = 0;
+        double best_rate = 1.0 / kPassCost[0];
+        double y = 1.0, p = 1.0;
+        for (int k = 1, b = 1; k <= std::min(cap, RMAX - 1); k++) {
+            p *= a;
+            y += p;
+            if (k + 1 == 1 << b) {   // k + 1 rows fill bucket b
+                const double rate = y / kPassCost[b];
+                if (rate > best_rate) best_rate = rate, best = k;
+                b++;
+            }
+        }
+        return best;
+    };
     int* tab = (int*)sc_.get(S_DTAB, (size_t)6 * RMAX * sizeof(int));
     int* hb = (int*)pinned((size_t)6 * RMAX * sizeof(int));
-    // bucket graphs hold scratch / KV / weight pointers: retire them whenever any of those moved
-    auto refresh = [&] {
-        const uint64_t key[4] = {sc_.epoch, kv_epoch_, m_->precision_gen, deterministic_gen()};
-        if (memcmp(key, draft_key_, sizeof key) != 0) {
-            for (auto& g : draft_graphs_) (void)hipGraphExecDestroy(g.second);
-            draft_graphs_.clear();
-            memcpy(draft_key_, key, sizeof key);
-        }
-    };
-    refresh();
+    draft_graphs_refresh();
     // the continuation of the last bigram (else unigram) in the previous transcripts.  Within the latest transcript —
     // the previous window of the same speech, in step with this decode (a few tokens ahead where the window's start
     // moved) — the occurrence nearest the current position, so a repeated n-gram does not cut the draft short at its
@@ -648,10 +726,9 @@ void Session::draft_decode(int n_prompt, int base, int budget, int dummy, std::v
     };
     std::vector<int32_t> draft;
     eos = false;
-    const bool graphs = !prof_enabled() && !getenv("QASR_NO_GRAPH");
     while ((int)toks.size() < budget) {
         const int pos = n_prompt + (int)toks.size() - 1;   // position of the last accepted token
-        lookup(draft, std::min(max_draft, budget - (int)toks.size() - 1));
+        lookup(draft, draft_len(budget - (int)toks.size() - 1));
         const int R = 1 + (int)draft.size();
         const int B = R <= 1 ? 1 : R <= 2 ? 2 : R <= 4 ? 4 : R <= 8 ? 8 : R <= 16 ? 16 : 32;
         for (int i = 0; i < B; i++) {
@@ -663,32 +740,7 @@ void Session::draft_decode(int n_prompt, int base, int budget, int dummy, std::v
             hb[4 * RMAX + i] = real ? pos + i + 1 : 1;
         }
         QASR_HIP(hipMemcpyAsync(tab, hb, (size_t)5 * RMAX * sizeof(int), hipMemcpyHostToDevice, st_));
-        auto it = draft_graphs_.find(B);
-        if (graphs && it != draft_graphs_.end()) {
-            QASR_HIP(hipGraphLaunch(it->second, st_));
-        } else {
-            draft_step(B);   // eager: also sizes the scratch this bucket needs before its graph is captured
-            refresh();       // (a growth retires the other buckets' graphs)
-            if (graphs) {
-                QASR_HIP(hipStreamSynchronize(st_));
-                hipGraph_t g;
-                QASR_HIP(hipStreamBeginCapture(st_, hipStreamCaptureModeRelaxed));
-                sc_.capturing = true;
-                try {
-                    draft_step(B);
-                } catch (...) {
-                    sc_.capturing = false;
-                    (void)hipStreamEndCapture(st_, &g);
-                    throw;
-                }
-                sc_.capturing = false;
-                QASR_HIP(hipStreamEndCapture(st_, &g));
-                hipGraphExec_t ex;
-                QASR_HIP(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
-                (void)hipGraphDestroy(g);
-                draft_graphs_.emplace(B, ex);
-            }
-        }
+        draft_pass(B);
         QASR_HIP(hipStreamSynchronize(st_));
         const int* got = (const int*)pin_cnt_ + 8;
         dstats_.passes++;
@@ -706,7 +758,13 @@ void Session::draft_decode(int n_prompt, int base, int budget, int dummy, std::v
             if (i < R - 1) acc++;
         }
         dstats_.accepted += acc;
-        max_draft = acc == 0 && R > 1 ? max_draft / 2 : std::min(RMAX - 1, std::max(max_draft * 2, 1));
+        if (R > 1) {   // acc successes, then one rejection unless every drafted token was accepted
+            draft_s_ = 0.8 * draft_s_ + acc;
+            draft_f_ = 0.8 * draft_f_ + (acc < R - 1 ? 1.0 : 0.0);
+        } else {       // a plain step: the estimate relaxes toward the prior, so drafting is tried again later
+            draft_s_ = 0.95 * draft_s_ + 0.05 * 4.0;
+            draft_f_ = 0.95 * draft_f_ + 0.05 * 0.5;
+        }
         if (eos) break;
     }
 }
@@ -1132,8 +1190,8 @@ void Session::forced_logits_host(const float* pcm, int64_t n, const int32_t* for
     encoder(fe, nullptr);
     std::vector<int32_t> ids = build_prompt(h, fe.n_tok[0], 0, context_);
     const int P = (int)ids.size();
-    QASR_CHECK(P + n_forced <= n_ctx_, QASR_E_CAPACITY, "forced sequence exceeds n_ctx");
-    ensure_kv(P + n_forced + 1);
+    QASR_CHECK(P + n_forced + 1 <= n_ctx_, QASR_E_CAPACITY, "forced sequence exceeds n_ctx");
+    ensure_kv(P + n_forced + 2);   // + a dummy slot for a verify pass's bucket padding rows
     logits.assign((size_t)(n_forced + 1) * V, 0.f);
     std::vector<int> pos(P), slot(P), kvs(P, 0), kvl(P);
     for (int i = 0; i < P; i++) {
@@ -1155,20 +1213,25 @@ void Session::forced_logits_host(const float* pcm, int64_t n, const int32_t* for
         // position P + i and its logits predict the token after it — the rows a drafted decode accepts from
         QASR_CHECK(n_forced <= kDraftRows, QASR_E_INVALID, "one-pass forced logits: at most kDraftRows tokens");
         QASR_HIP(hipStreamSynchronize(st_));
+        // (the row bucket of the streaming decode, padded with dummy rows, through the same captured graphs)
         constexpr int R = kDraftRows;
+        const int B = n_forced <= 1 ? 1 : n_forced <= 2 ? 2 : n_forced <= 4 ? 4 : n_forced <= 8 ? 8 : n_forced <= 16 ? 16 : 32;
+        const int dummy = P + n_forced + 1;
         std::vector<int> hb((size_t)5 * R, 0);
-        for (int i = 0; i < n_forced; i++) {
-            hb[i] = forced[i];
-            hb[R + i] = P + i;
-            hb[2 * R + i] = P + i;
-            hb[3 * R + i] = 0;
-            hb[4 * R + i] = P + i + 1;
+        for (int i = 0; i < B; i++) {
+            const bool real = i < n_forced;
+            hb[i] = real ? forced[i] : 0;
+            hb[R + i] = real ? P + i : 0;
+            hb[2 * R + i] = real ? P + i : dummy;
+            hb[3 * R + i] = real ? 0 : dummy;
+            hb[4 * R + i] = real ? P + i + 1 : 1;
         }
         int* tab = (int*)sc_.get(S_DTAB, (size_t)6 * R * sizeof(int));
         QASR_HIP(hipMemcpyAsync(tab, hb.data(), hb.size() * sizeof(int), hipMemcpyHostToDevice, st_));
         sc_.get(S_X, (size_t)R * H * sizeof(float));
         sc_.get(S_LOGITS, (size_t)R * V * sizeof(float));
-        draft_step(n_forced);
+        draft_graphs_refresh();
+        draft_pass(B);
         QASR_HIP(hipMemcpyAsync(logits.data() + V, sc_.get(S_LOGITS, 0), (size_t)n_forced * V * sizeof(float),
                                 hipMemcpyDeviceToHost, st_));
         QASR_HIP(hipStreamSynchronize(st_));

@@ -112,6 +112,8 @@ class Session {
     void decode_step(const DecState& ds, int B, bool sizing, int64_t keys = 0);
     // one verify pass of B rows (last accepted token + draft, padded): tables in S_DTAB, argmax → pinned host
     void draft_step(int B);
+    void draft_pass(int B);
+    void draft_graphs_refresh();
     void draft_decode(int n_prompt, int base, int budget, int dummy, std::vector<int32_t>& toks, bool& eos,
                       bool forced);
     // exact: every row with the 1-row arithmetic (verify passes; ≤ 4 rows always are)
@@ -158,6 +160,9 @@ class Session {
     float* fix_part_ = nullptr;
     size_t fix_floats_ = 0;
     unsigned* fix_cnt_ = nullptr;
+    // draft length control: decayed counts of accepted draft tokens and of rejections (the per-token acceptance
+    // estimate a = S / (S + F)), kept across requests; the prior a ≈ 0.89
+    double draft_s_ = 4.0, draft_f_ = 0.5;
     std::vector<int32_t> history_;   // previous transcripts (the lookup corpus), oldest first
     int hist_last_ = 0;              // where the latest transcript starts in history_
     DraftStats dstats_;

@@ -45,6 +45,15 @@ void gemv_q8(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const flo
 // ld_src floats)·nw), K ≤ 4096; GV_NONE: the Q8 rows xq / xd, K ≤ 6144.  epi EPI_STORE / EPI_RESID into y, or
 // EPI_SWIGLU (GV_RMS only; W = interleaved gate/up, N % 64 == 0): h = Q8(silu(g)·u) into yq [M][N/2] / yd [M][N/64].
 enum GvPro : int { GV_NONE = 0, GV_RMS = 1 };
+// The draft verify passes' linears on the matrix core with EXACTLY k_gemv_wide's 1-row arithmetic (the same block fma
+// chains and wave-sum tree, run in-lane): rows 1..kExactRows, K a multiple of 1,024 (K/1024 ∈ {1,2,3,4,6}), epi store
+// or residual — bit-identical to gemv_fused(GV_NONE) on the same Q8 rows, and to the fused norm / SwiGLU launches when
+// preceded by rmsnorm_q8 / followed by swiglu_q8(interleaved)
+bool gemm_exact_rows_ok(int M, const Q8Mat& W);
+// verify-pass rows from which the engine takes gemm_exact_rows (default 5; QASR_EXACT_MFMA_ROWS, 0 = never)
+int exact_mfma_rows();
+void gemm_exact_rows(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const float* res, float* y, int ldy,
+                     int epi, hipStream_t s);
 bool gemv_fused_ok(int pro, int M, int K);
 void gemv_fused(int pro, const int8_t* xq, const float* xd, const float* src, int ld_src, const float* nw, float eps,
                 int M, const Q8Mat& W, const float* res, float* y, int ldy, int epi, int8_t* yq, float* yd,

@@ -90,8 +90,11 @@ __global__ __launch_bounds__(256) void k_attention(const __half* __restrict__ Q,
     // cut into S ≤ kAttnSplitMax contiguous pieces (≥ fz.split_keys each), the rest exit at once.  Each piece's
     // merged (m, l, Σp·v) goes to fz.part; the last piece to arrive (fz.cnt) combines them in piece order.
     const bool spl = FUSED && fz.part != nullptr;   // uniform
-    const int gw = spl ? blockIdx.x / kAttnSplitMax : NW == 4 ? blockIdx.x : blockIdx.x * 4 + w;
-    const int piece = spl ? blockIdx.x % kAttnSplitMax : 0;
+    // split grid piece-major: every (row, KV head)'s piece 0 is dispatched first, the pieces a short range does not
+    // need (they exit at once) after them, so they never queue ahead of real work
+    const int nitems = rows * nkv;
+    const int gw = spl ? (int)(blockIdx.x % nitems) : NW == 4 ? blockIdx.x : blockIdx.x * 4 + w;
+    const int piece = spl ? (int)(blockIdx.x / nitems) : 0;
     if (NW == 1 && gw >= rows * nkv) return;
     const int part = NW == 4 ? w : 0;
     const int r = gw / nkv, kvh = gw % nkv;

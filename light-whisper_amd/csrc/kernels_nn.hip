@@ -222,7 +222,7 @@ __global__ __launch_bounds__(256) void k_swiglu_q8_lane(const float* __restrict_
 void swiglu_q8(const float* gu, int M, int F, int8_t* q, float* d, hipStream_t s, bool interleaved) {
     int64_t n = (int64_t)M * (F / 32);
     if (n <= 0) return;
-    if (M <= 16)
+    if (M <= 64)   // (the verify passes' ≤ 32 rows included: one lane per element, no 32-deep serial chain)
         k_swiglu_q8_lane<<<(unsigned)cdiv64(n * 32, 256), 256, 0, s>>>(gu, M, F, q, d, interleaved ? 1 : 0);
     else
         k_swiglu_q8<<<(unsigned)cdiv64(n, 256), 256, 0, s>>>(gu, M, F, q, d, interleaved ? 1 : 0);

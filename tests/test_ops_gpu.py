@@ -810,6 +810,31 @@ def test_gemm_swiglu_q8_fixup(torch_dev, fixup, m, f, k, cfg):
     assert not host(fixup).any()
 
 
+@pytest.mark.parametrize("m", [1, 5, 16, 17, 32])
+@pytest.mark.parametrize("n,k,epi", [(4096, 2048, 0), (2048, 2048, 1), (2048, 6144, 1), (12288, 2048, 0),
+                                     (1024, 1024, 0), (1024, 3072, 1), (300, 4096, 0)])
+def test_gemm_exact_rows_match_gemv(torch_dev, m, n, k, epi):
+    """the verify passes' MFMA linear (gemm_exact_rows) == gemv_fused (pro 0) on each row ALONE, bit for bit: the same
+    block fma chains and wave-sum tree (the exact-row contract of the drafted decode)"""
+    import torch
+
+    rng = np.random.default_rng(m + n + k)
+    xq = dev(rng.integers(-127, 128, (m, k), dtype=np.int8), torch_dev)
+    xd = dev((rng.random((m, k // 32)) * 0.02).astype(np.float32), torch_dev)
+    xd[0, 3] = 0.0   # a zero block scale (all-zero block)
+    res = dev((rng.standard_normal((m, n)) * 3).astype(np.float32), torch_dev)
+    wq, ws = _q8_weights(torch_dev, n, k, 9)
+    y = res.clone()
+    _lib.check(L().qasr_op_gemm_exact_rows(ptr(xq), ptr(xd), m, ptr(wq), ptr(ws), n, k, ptr(y) if epi else None, ptr(y),
+                                           n, epi, None))
+    for r in range(m):
+        y1 = res[r:r + 1].clone()
+        _lib.check(L().qasr_op_gemv_fused(0, None, 0, None, 0.0, 1, C.c_void_p(xq.data_ptr() + r * k),
+                                          C.c_void_p(xd.data_ptr() + r * (k // 32) * 4), ptr(wq), ptr(ws), n, k,
+                                          ptr(y1) if epi else None, ptr(y1), n, epi, None, None, None))
+        assert np.array_equal(host(y)[r], host(y1)[0]), r
+
+
 @pytest.fixture
 def ws_all():
     """the weight-streaming kernel on every shape it supports up to 64 rows (restored to the default afterwards)"""
