@@ -669,11 +669,11 @@ void Session::draft_decode(int n_prompt, int base, int budget, int dummy, std::v
     const qasr_hparams& h = m_->hp;
     constexpr int RMAX = kDraftRows;
     // Draft length: with per-token acceptance a, a pass of k drafted tokens yields 1 + a + … + a^k tokens and costs
-    // kPassCost[bucket] (one verify pass of 1/2/4/8/16/32 rows relative to a 1-row step; profiles/r3q_verify_cost.log,
-    // exact-row MFMA linears from 5 rows); k fills a row bucket (1, 3, 7, 15, 31) and is the one with the most tokens
-    // per unit cost at the current estimate of a — never worse than plain greedy steps in expectation, long drafts
-    // only while they keep being accepted (the noise sweep in DESIGN §7)
-    static constexpr double kPassCost[6] = {1.0, 1.05, 1.12, 1.45, 1.6, 2.0};
+    // kPassCost[bucket] (kernel time of one verify pass of 1/2/4/8/16/32 rows relative to a 1-row pass, 1.7B:
+    // profiles/r3u_pass_cost.log — the GEMV rows up to 4, the exact-row MFMA linears from 5); k fills a row bucket
+    // (1, 3, 7, 15, 31) and is the one with the most tokens per unit cost at the current estimate of a — never worse
+    // than plain greedy steps in expectation, long drafts only while they keep being accepted
+    static constexpr double kPassCost[6] = {1.0, 1.24, 1.71, 1.93, 2.04, 2.66};
     auto draft_len = [&](int cap) {
         const double a = draft_s_ / (draft_s_ + draft_f_);
         int best = 0;

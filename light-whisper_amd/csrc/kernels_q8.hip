@@ -475,42 +475,48 @@ bool gemv_fused_ok(int pro, int M, int K) {
 // lane groups 0–1 / 2–3 gives blocks 2s / 2s+1), each lane keeps the 32 leaves of its 4 outputs in registers, and the
 // same fma chains and the same tree run in-lane — the same bits, whatever the row count (test_gemm_exact_rows_match
 // _gemv).  Rows past M are computed on clamped inputs and not stored.
-template <int T>
-__global__ __launch_bounds__(256) void k_gemm_q8_exact(const int8_t* __restrict__ X, const float* __restrict__ Xd, int M,
+template <int T, int RF>
+__global__ __launch_bounds__(256, 2) void k_gemm_q8_exact(const int8_t* __restrict__ X, const float* __restrict__ Xd, int M,
                                                        const int8_t* __restrict__ W, const __half* __restrict__ Wsc,
-                                                       int N, int K, const float* res, float* y, int ldy, int epi,
-                                                       int rfrags) {
-    // a workgroup per 16 × 16 fragment; wave w owns leaves 8w … 8w+7 (blocks 8w + 2j + {0,1} + 32t: spans 4w + j + 16t)
-    __shared__ float hx[4][4][64];   // [wave][r][lane]: H_w = O_2w + O_2w+1 of each output
+                                                       int N, int K, const float* res, float* y, int ldy, int epi) {
+    // a workgroup per 16-column fragment and all RF 16-row fragments (the weight span loaded once for them); wave w
+    // owns leaves 8w … 8w+7 (blocks 8w + 2j + {0,1} + 32t: spans 4w + j + 16t)
+    __shared__ float hx[4][RF][4][64];   // [wave][row fragment][r][lane]: H_w = O_2w + O_2w+1 of each output
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int fr = lane & 15, g = lane >> 4;
-    const int cf = blockIdx.x / rfrags, rf = blockIdx.x % rfrags;
-    const int n0 = cf * 16, m0 = rf * 16;
+    const int n0 = blockIdx.x * 16;
     const int nb = K / QK;
     const int8_t* wp = W + (size_t)min(n0 + fr, N - 1) * K + 16 * g;
-    const int8_t* ap = X + (size_t)min(m0 + fr, M - 1) * K + 16 * g;
     const uint32_t* sp = (const uint32_t*)(Wsc + (size_t)min(n0 + fr, N - 1) * nb);
-    const float* dxp[4];
+    const int8_t* ap[RF];
+    const float* dxp[RF][4];
 #pragma unroll
-    for (int r = 0; r < 4; r++) dxp[r] = Xd + (size_t)min(m0 + 4 * g + r, M - 1) * nb;
-    constexpr int NS = 4 * T;          // spans of this wave
-    constexpr int G8 = NS % 8 == 0 ? 8 : 4;   // spans loaded per group (all of them up to K 2,048; NS = 4T)
-    float leaf[8][4];
+    for (int f = 0; f < RF; f++) {
+        ap[f] = X + (size_t)min(16 * f + fr, M - 1) * K + 16 * g;
+#pragma unroll
+        for (int r = 0; r < 4; r++) dxp[f][r] = Xd + (size_t)min(16 * f + 4 * g + r, M - 1) * nb;
+    }
+    constexpr int NS = 4 * T;                  // spans of this wave
+    constexpr int G8 = RF == 1 && NS % 8 == 0 ? 8 : 4;   // spans loaded per group
+    float leaf[RF][8][4];
     const bool lo = g < 2;
     const v4i zero = {0, 0, 0, 0};
 #pragma unroll
     for (int q0 = 0; q0 < NS; q0 += G8) {
-        v4i wq[G8], aq[G8];
+        v4i wq[G8], aq[G8][RF];
         uint32_t ws[G8];
-        float2 dx[G8][4];
+        float2 dx[G8][RF][4];
 #pragma unroll
         for (int u = 0; u < G8; u++) {
             const int i = q0 + u, s = 4 * wv + (i & 3) + 16 * (i >> 2);
             wq[u] = __builtin_nontemporal_load((const v4i*)(wp + 64 * (size_t)s));
-            aq[u] = *(const v4i*)(ap + 64 * (size_t)s);
             ws[u] = sp[s];
 #pragma unroll
-            for (int r = 0; r < 4; r++) dx[u][r] = *(const float2*)(dxp[r] + 2 * s);
+            for (int f = 0; f < RF; f++) {
+                aq[u][f] = *(const v4i*)(ap[f] + 64 * (size_t)s);
+#pragma unroll
+                for (int r = 0; r < 4; r++) dx[u][f][r] = *(const float2*)(dxp[f][r] + 2 * s);
+            }
         }
 #pragma unroll
         for (int u = 0; u < G8; u++) {
@@ -518,35 +524,41 @@ __global__ __launch_bounds__(256) void k_gemm_q8_exact(const int8_t* __restrict_
 #pragma unroll
             for (int h = 0; h < 2; h++) {
                 const v4i bm = (lo == (h == 0)) ? wq[u] : zero;
-                const v4i c = __builtin_amdgcn_mfma_i32_16x16x64_i8(aq[u], bm, zero, 0, 0, 0);
                 const float dw = __half2float(__ushort_as_half((unsigned short)(h ? ws[u] >> 16 : ws[u] & 0xffff)));
                 const int l = 2 * j + h;
 #pragma unroll
-                for (int r = 0; r < 4; r++) {
-                    const float dxr = h ? dx[u][r].y : dx[u][r].x;
-                    leaf[l][r] = fmaf((float)c[r], dw * dxr, t == 0 ? 0.f : leaf[l][r]);
+                for (int f = 0; f < RF; f++) {
+                    const v4i c = __builtin_amdgcn_mfma_i32_16x16x64_i8(aq[u][f], bm, zero, 0, 0, 0);
+#pragma unroll
+                    for (int r = 0; r < 4; r++) {
+                        const float dxr = h ? dx[u][f][r].y : dx[u][f][r].x;
+                        leaf[f][l][r] = fmaf((float)c[r], dw * dxr, t == 0 ? 0.f : leaf[f][l][r]);
+                    }
                 }
             }
         }
     }
     // this wave's leaves l' = leaf + 0 (the GEMV's xor-1 add of an odd lane's 0), O_2w, O_2w+1, H_w
 #pragma unroll
-    for (int r = 0; r < 4; r++) {
-        float o[2];
+    for (int f = 0; f < RF; f++)
 #pragma unroll
-        for (int gq = 0; gq < 2; gq++) {
-            const float a0 = leaf[4 * gq][r] + 0.f, a1 = leaf[4 * gq + 1][r] + 0.f;
-            const float a2 = leaf[4 * gq + 2][r] + 0.f, a3 = leaf[4 * gq + 3][r] + 0.f;
-            o[gq] = (a0 + a1) + (a2 + a3);
+        for (int r = 0; r < 4; r++) {
+            float o[2];
+#pragma unroll
+            for (int gq = 0; gq < 2; gq++) {
+                const float a0 = leaf[f][4 * gq][r] + 0.f, a1 = leaf[f][4 * gq + 1][r] + 0.f;
+                const float a2 = leaf[f][4 * gq + 2][r] + 0.f, a3 = leaf[f][4 * gq + 3][r] + 0.f;
+                o[gq] = (a0 + a1) + (a2 + a3);
+            }
+            hx[wv][f][r][lane] = o[0] + o[1];
         }
-        hx[wv][r][lane] = o[0] + o[1];
-    }
     __syncthreads();
-    if (wv != 0) return;
+    if (wv >= RF) return;
+    const int f = wv;   // wave f stores row fragment f
 #pragma unroll
     for (int r = 0; r < 4; r++) {
-        const float v = (hx[0][r][lane] + hx[1][r][lane]) + (hx[2][r][lane] + hx[3][r][lane]);
-        const int row = m0 + 4 * g + r, col = n0 + fr;
+        const float v = (hx[0][f][r][lane] + hx[1][f][r][lane]) + (hx[2][f][r][lane] + hx[3][f][r][lane]);
+        const int row = 16 * f + 4 * g + r, col = n0 + fr;
         if (row < M && col < N) y[(size_t)row * ldy + col] = epi_apply(epi, v, row, col, nullptr, res, ldy);
     }
 }
@@ -566,15 +578,22 @@ void gemm_exact_rows(const int8_t* xq, const float* xd, int M, const Q8Mat& W, c
     ProfScope ps(s, "gemm_q8_exact", 2.0 * M * W.N * W.K, q8_bytes(M, W, epi));
     QASR_CHECK(gemm_exact_rows_ok(M, W), QASR_E_INVALID, "gemm_exact_rows: rows 1..32, K a multiple of 1024 (T 1-4, 6)");
     QASR_CHECK(epi == EPI_STORE || (epi == EPI_RESID && res), QASR_E_INVALID, "gemm_exact_rows: store or residual");
-    const int rfrags = cdiv(M, 16);
-    const dim3 grid(cdiv(W.N, 16) * rfrags);
+    const dim3 grid(cdiv(W.N, 16));
+#define EXACT_GO(TT)                                                                                                   \
+    do {                                                                                                               \
+        if (M <= 16)                                                                                                   \
+            k_gemm_q8_exact<TT, 1><<<grid, 256, 0, s>>>(xq, xd, M, W.qs, W.sc, W.N, W.K, res, y, ldy, epi);            \
+        else                                                                                                           \
+            k_gemm_q8_exact<TT, 2><<<grid, 256, 0, s>>>(xq, xd, M, W.qs, W.sc, W.N, W.K, res, y, ldy, epi);            \
+    } while (0)
     switch (W.K / 1024) {
-        case 1: k_gemm_q8_exact<1><<<grid, 256, 0, s>>>(xq, xd, M, W.qs, W.sc, W.N, W.K, res, y, ldy, epi, rfrags); break;
-        case 2: k_gemm_q8_exact<2><<<grid, 256, 0, s>>>(xq, xd, M, W.qs, W.sc, W.N, W.K, res, y, ldy, epi, rfrags); break;
-        case 3: k_gemm_q8_exact<3><<<grid, 256, 0, s>>>(xq, xd, M, W.qs, W.sc, W.N, W.K, res, y, ldy, epi, rfrags); break;
-        case 4: k_gemm_q8_exact<4><<<grid, 256, 0, s>>>(xq, xd, M, W.qs, W.sc, W.N, W.K, res, y, ldy, epi, rfrags); break;
-        default: k_gemm_q8_exact<6><<<grid, 256, 0, s>>>(xq, xd, M, W.qs, W.sc, W.N, W.K, res, y, ldy, epi, rfrags); break;
+        case 1: EXACT_GO(1); break;
+        case 2: EXACT_GO(2); break;
+        case 3: EXACT_GO(3); break;
+        case 4: EXACT_GO(4); break;
+        default: EXACT_GO(6); break;
     }
+#undef EXACT_GO
 }
 
 void gemv_fused(int pro, const int8_t* xq, const float* xd, const float* src, int ld_src, const float* nw, float eps,
