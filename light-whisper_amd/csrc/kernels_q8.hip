@@ -1121,10 +1121,37 @@ __global__ __launch_bounds__(256 * KG, 2 / KG) void k_gemm_q8d(const int8_t* __r
 #pragma unroll
             for (int r = 0; r < 4; r++) acc[i][j][r] = 0.f;
 
+    // decode tiles (≤ 64×64): the fragment offsets are computed once, opaque (so no two reads are ever paired into
+    // ds_read2st64, whose 16-lane groups would conflict on this image), and the K loop is unrolled by the ring depth,
+    // so each stage's LDS base is an immediate of its ds_reads — no per-read address VALU in the K loop (round 3:
+    // 180 VALU per 16 MFMAs in the cfg-12 loop, 52 of them moves and adds for addresses)
+    constexpr bool PREOFF = TI * TJ <= 4;
+    int offa[PREOFF ? KB : 1][PREOFF ? TI : 1], offb[PREOFF ? KB : 1][PREOFF ? TJ : 1];
+    if constexpr (PREOFF) {
+#pragma unroll
+        for (int kb = 0; kb < KB; kb++) {
+#pragma unroll
+            for (int i = 0; i < TI; i++) {
+                offa[kb][i] = (arow + 16 * i + fr) * BK + foff[kb];
+                asm volatile("" : "+v"(offa[kb][i]));
+            }
+#pragma unroll
+            for (int j = 0; j < TJ; j++) {
+                offb[kb][j] = OB + (bcol + 16 * j + fr) * BK + foff[kb];
+                asm volatile("" : "+v"(offb[kb][j]));
+            }
+        }
+    }
+
 #pragma unroll
     for (int t = 0; t < D; t++)
         if (t < nsteps) issue(t, t);
-    for (int s = 0; s < nsteps; s++) {
+    constexpr int UNR = PREOFF ? NBUF : 1;   // stages per trip of the outer loop (one per ring buffer)
+    for (int s0 = 0; s0 < nsteps; s0 += UNR)
+#pragma unroll
+    for (int ub = 0; ub < UNR; ub++) {
+        const int s = s0 + ub;
+        if (UNR > 1 && s >= nsteps) break;
         // this wave's DMAs of stage s have landed and its LDS reads of stage s-1 are done; the barrier then makes
         // that true for every wave, so stage s is readable and buffer (s+D)%NBUF (= stage s-1's) is free
         wait_stages<NPW, D>(min(D - 1, nsteps - 1 - s));
@@ -1132,7 +1159,7 @@ __global__ __launch_bounds__(256 * KG, 2 / KG) void k_gemm_q8d(const int8_t* __r
         asm volatile("" ::: "memory");
         if (s + D < nsteps) issue(s + D, (s + D) % NBUF);
         if (!active) continue;
-        const char* st = smem + (s % NBUF) * STAGE;
+        const char* st = smem + (UNR > 1 ? ub : s % NBUF) * STAGE;
         // fragments and scales of block kb, read just before its MFMAs (the compiler hoists what registers allow)
         constexpr int KBG = KB / KG;   // blocks of this K group per stage
         // OP (outer-product scales): the 16×16·TJ products d_x(row)·d_w(col) of one i-fragment come from one
@@ -1161,15 +1188,23 @@ __global__ __launch_bounds__(256 * KG, 2 / KG) void k_gemm_q8d(const int8_t* __r
                     const float4 v = *(const float4*)(st + OSA + 4 * (kb * BM + arow + 16 * i + fq));
                     sa[sl][i][0] = v.x, sa[sl][i][1] = v.y, sa[sl][i][2] = v.z, sa[sl][i][3] = v.w;
                 }
-                int off = (arow + 16 * i + fr) * BK + foff[kb];
-                asm volatile("" : "+v"(off));
-                a[sl][i] = *(const long*)(st + off);
+                if constexpr (PREOFF) {
+                    a[sl][i] = *(const long*)(st + offa[kb][i]);
+                } else {
+                    int off = (arow + 16 * i + fr) * BK + foff[kb];
+                    asm volatile("" : "+v"(off));
+                    a[sl][i] = *(const long*)(st + off);
+                }
             }
 #pragma unroll
             for (int j = 0; j < TJ; j++) {
-                int off = OB + (bcol + 16 * j + fr) * BK + foff[kb];
-                asm volatile("" : "+v"(off));
-                b[sl][j] = *(const long*)(st + off);
+                if constexpr (PREOFF) {
+                    b[sl][j] = *(const long*)(st + offb[kb][j]);
+                } else {
+                    int off = OB + (bcol + 16 * j + fr) * BK + foff[kb];
+                    asm volatile("" : "+v"(off));
+                    b[sl][j] = *(const long*)(st + off);
+                }
             }
         };
         // MFMA q (block q / NF, fragment q % NF) is issued LAG MFMAs before its rescale, so the int32 result has
