@@ -2,9 +2,10 @@
 """Throughput bench: audio-seconds per wall-second (RTF⁻¹) of Qwen3-ASR-1.7B Q8 on MI355X.
 
 Workload (BASELINE.json configs[3], "1.7B Q8, VAD-split segments batch-sharded"):
-  * 256 segments per rank, lengths U[2,12] s, seeded synthetic speech-like 16 kHz audio (f0 90-250 Hz with
-    jitter, 8 harmonics, 4 Hz syllabic AM, pink noise at -25 dB, peak -12 dBFS), VAD bypassed for ASR timing;
-    the global list of 256·N segments is LPT-sharded over the N ranks (weak scaling, no data-path collective);
+  * 256 segments, lengths U[2,12] s, seeded synthetic speech-like 16 kHz audio (f0 90-250 Hz with jitter, 8
+    harmonics, 4 Hz syllabic AM, pink noise at -25 dB, peak -12 dBFS), VAD bypassed for ASR timing; the global list
+    is LPT-sharded over the N ranks with no data-path collective.  --scaling strong (default): 256 segments IN TOTAL
+    (the config as BASELINE states it: 32 per GPU at N=8); --scaling weak: 256 segments per rank (256·N in all);
   * Qwen3-ASR-1.7B shapes with Q8_0 weights generated on the device from a seed (no checkpoint in the
     container — DESIGN.md §synthetic), f16 KV cache;
   * throughput mode: exactly round(8·seconds)+1 greedy tokens per segment (EOS ignored) so the work is fixed.
@@ -12,8 +13,11 @@ A step = one qasr_run_batch_device call over the rank's resident segments: log-m
 projector → prefill → continuous-batching decode → detokenise.
 
 Launch: python bench.py [--gpus N --steps K --warmup W]; N>1: one rank per GPU under torch.distributed.run (spawned
-by this script when WORLD_SIZE is unset); the weight broadcast and token gather are libqasr's own RCCL communicator,
-torch.distributed carries the barrier and the max-over-ranks time.  Prints ONE JSON line (rank 0).
+by this script when WORLD_SIZE is unset); the weight broadcast and token gather are libqasr's own RCCL communicator
+(unique id handed over through a file, qasr/dist.py file_exchange — no torch on the data path), and a CPU (gloo)
+torch.distributed group carries the barrier and the max-over-ranks time, so each rank opens ONE RCCL communicator.
+QASR_DIST_BACKEND=torch-nccl runs both collectives over torch's NCCL group instead (fallback); =gloo rehearses the
+N>1 flow with ranks sharing a card.  Prints ONE JSON line (rank 0).
 """
 from __future__ import annotations
 
@@ -75,9 +79,10 @@ def lpt_shard(lengths, world):
     return shards
 
 
-def make_workload(world, rank, seed=1):
+def make_workload(world, rank, seed=1, total=None):
+    """this rank's LPT share of `total` segments (default SEG_PER_RANK·world, the weak-scaling list)"""
     rng = np.random.default_rng(seed)
-    total = SEG_PER_RANK * world
+    total = SEG_PER_RANK * world if total is None else total
     secs = rng.uniform(2.0, 12.0, size=total)
     lengths = [int(s * 16000) for s in secs]
     mine = sorted(lpt_shard(lengths, world)[rank])
@@ -223,7 +228,7 @@ def launch_ranks(argv, n, dry_run=False):
     import socket
     import subprocess
 
-    backend = os.environ.get("QASR_DIST_BACKEND", "nccl")
+    backend = os.environ.get("QASR_DIST_BACKEND", "native")
     if not dry_run and backend != "gloo":
         import torch
 
@@ -250,7 +255,11 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--arch", default="qwen3-asr-1.7b")
-    ap.add_argument("--segments", type=int, default=SEG_PER_RANK)
+    ap.add_argument("--segments", type=int, default=SEG_PER_RANK,
+                    help="C4 segments: in total (--scaling strong) or per rank (--scaling weak)")
+    ap.add_argument("--scaling", default="strong", choices=["strong", "weak"],
+                    help="C4: strong = --segments in total, LPT-sharded over the ranks (BASELINE configs[3] as "
+                         "stated); weak = --segments per rank")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-prof", action="store_true")
     ap.add_argument("--precision", default=None, choices=["q8", "mxfp8"],
@@ -287,26 +296,33 @@ def main():
     import torch
     import torch.distributed as dist
 
-    # QASR_DIST_BACKEND=gloo: rehearsal of the N>1 flow on a box with fewer GPUs than ranks (ranks share cards,
-    # collectives staged through host memory); the driver's multi-GPU runs use the default, RCCL
-    backend = os.environ.get("QASR_DIST_BACKEND", "nccl")
+    # QASR_DIST_BACKEND: native (default) — libqasr's RCCL communicator for the two collectives, a gloo (CPU) group
+    # for the barrier and the timing reductions; torch-nccl — torch's NCCL group for everything (fallback); gloo —
+    # rehearsal of the N>1 flow on a box with fewer GPUs than ranks (ranks share cards, collectives via host memory)
+    backend = os.environ.get("QASR_DIST_BACKEND", "native")
+    if backend == "nccl":
+        backend = "native"
+    if backend not in ("native", "torch-nccl", "gloo"):
+        print(f"bench.py: unknown QASR_DIST_BACKEND={backend}", file=sys.stderr, flush=True)
+        sys.exit(2)
     if backend == "gloo":
         local = local % torch.cuda.device_count()
     torch.cuda.set_device(local)
-    coll_dev = torch.device("cpu") if backend == "gloo" else torch.device("cuda", local)
+    coll_dev = torch.device("cuda", local) if backend == "torch-nccl" else torch.device("cpu")
     if world > 1:
-        if backend == "gloo":
-            dist.init_process_group("gloo")
-        else:
+        if backend == "torch-nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
 
     from qasr import _lib
     from qasr.transcribe_cpp import Model
 
     lib = _lib.load()
     _lib.check(lib.qasr_set_device(local))
+    total_segments = args.segments if args.scaling == "strong" else args.segments * world
     if args.workload == "c4":
-        audio = make_workload(world, rank)
+        audio = make_workload(world, rank, total=total_segments)
         lens = [a.size for a in audio]
         offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int64)
         dev = torch.from_numpy(np.concatenate(audio)).to(f"cuda:{local}")   # inputs resident in HBM
@@ -323,18 +339,21 @@ def main():
     comm = None
     if world > 1:
         # rank 0 builds the weights, every other rank opens a shell of the same device layout and
-        # ONE RCCL broadcast over the whole blob fills it — libqasr's own communicator (qasr_dist_*; torch only hands
-        # the unique id over); the gloo rehearsal (ranks sharing a card) uses torch.distributed.  Untimed, like a
-        # server's load.
+        # ONE RCCL broadcast over the whole blob fills it — libqasr's own communicator (qasr_dist_*; the unique id
+        # travels through a file, as a Rust host would hand it over); the fallback and the gloo rehearsal use
+        # torch.distributed.  Untimed, like a server's load.
         from qasr import dist as qdist
 
         model = Model.synthetic(args.arch, seed=0) if rank == 0 else Model.shell(args.arch)
-        if backend == "gloo":
-            collectives["weight_broadcast"] = qdist.broadcast_weights(model, rank, torch.device("cuda", local))
-        else:
-            comm = qdist.NativeComm(rank, world, local, qdist.torch_exchange)
+        if backend == "native":
+            xchg = qdist.file_exchange(rank, world)
+            comm = qdist.NativeComm(rank, world, local, xchg)
+            xchg.cleanup()
             collectives["weight_broadcast"] = comm.broadcast_weights(model)
-        collectives["backend"] = "libqasr-rccl" if comm else backend
+        else:
+            collectives["weight_broadcast"] = qdist.broadcast_weights(model, rank, torch.device("cuda", local))
+        collectives["backend"] = {"native": "libqasr-rccl (file unique-id hand-off) + gloo barrier",
+                                  "torch-nccl": "torch nccl", "gloo": "gloo rehearsal"}[backend]
     else:
         model = Model.synthetic(args.arch, seed=0)
     if args.precision != "q8":
@@ -403,9 +422,13 @@ def main():
         # token streams of every rank to rank 0 (untimed): all-gather of counts, then of the ragged payload
         t_g = time.perf_counter()
         every = comm.gather_tokens(streams) if comm else qdist.gather_token_streams(streams, coll_dev)
-        collectives["token_gather"] = {"segments": sum(len(e) for e in every),
-                                       "tokens": sum(len(x) for e in every for x in e),
+        n_seg = sum(len(e) for e in every)
+        collectives["token_gather"] = {"segments": n_seg, "tokens": sum(len(x) for e in every for x in e),
                                        "ms": round((time.perf_counter() - t_g) * 1e3, 3)}
+        # this run validates its own N>1 collectives: every rank's weight checksum equal to rank 0's and every
+        # segment's stream gathered (C4: the whole segment list)
+        collectives["validated"] = bool(collectives["weight_broadcast"].get("checksums_agree")) and (
+            args.workload != "c4" or n_seg == total_segments)
     else:
         collectives["token_gather"] = {"segments": len(streams), "tokens": sum(len(x) for x in streams), "ms": 0.0}
     t = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
@@ -444,18 +467,21 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 2),
             "higher_is_better": True,
-            "scaling": "weak" if args.workload == "c4" else "strong",
+            "scaling": args.scaling if args.workload == "c4" else "strong",
             "vs_baseline": None,
             "dtype": "i8" if args.precision == "q8" else "fp8e4m3+e8m0",
             "data": "synthetic (seeded speech-like 16 kHz audio; seeded synthetic Q8_0 weights with 1.7B shapes)",
-            "config": {"workload": (f"C4: {SEG_PER_RANK} VAD-split segments/rank, U[2,12] s, LPT-sharded, "
-                                    f"{FORCE_TPS} forced tokens/audio-s") if args.workload == "c4" else
+            "config": {"workload": (f"C4: {total_segments} VAD-split segments"
+                                    f"{' in total' if args.scaling == 'strong' else f' ({SEG_PER_RANK}/rank)'}, "
+                                    f"U[2,12] s, LPT-sharded over {world} rank(s), {FORCE_TPS} forced tokens/audio-s")
+                                   if args.workload == "c4" else
                                    (f"C5: {args.c5_seconds:g} s recording (seed 2), FireRedVAD halo-sharded over "
                                     f"{world} rank(s) + probability all-gather, {c5_info.get('segments')} speech "
                                     f"segments ({c5_info.get('speech_s')} s) LPT-sharded, {FORCE_TPS} forced "
                                     f"tokens/audio-s"),
                        "model": args.arch, "parallelism": f"dp{world}",
-                       **({"segments_per_rank": SEG_PER_RANK, "audio_s_per_rank": round(audio_s, 1)}
+                       **({"segments_total": total_segments, "segments_rank0": len(lens),
+                           "audio_s_rank0": round(audio_s, 1)}
                           if args.workload == "c4" else
                           # C5: value counts the whole recording; ASR runs only on the VAD-kept speech
                           {"recording_s": args.c5_seconds, "segments": c5_info.get("segments"),

@@ -9,6 +9,7 @@
 // Neither runs inside a timed step.  The reference has no multi-GPU path.
 #include <string.h>
 
+#include <algorithm>
 #include <chrono>
 #include <memory>
 #include <vector>
@@ -175,9 +176,23 @@ QASR_API int qasr_dist_gather_tokens(qasr_comm* c, const int32_t* lens, int32_t 
         }
         *n_segs_out = (size_t)tot_seg;
         *n_tokens_out = (size_t)tot_tok;
-        if (!all_lens && !all_tokens) return;   // size query
-        QASR_CHECK(all_lens && all_tokens && lens_cap >= (size_t)tot_seg && tokens_cap >= (size_t)tot_tok,
-                   QASR_E_CAPACITY, "gather buffers too small");
+        // every rank states what it does next — 0 size query, 1 payload, -1 its buffers are too small — and all ranks
+        // decide together, so a caller error on one rank is an error on every rank instead of the others blocking in
+        // the payload all-gather
+        const bool query = !all_lens && !all_tokens;
+        const int32_t st = query ? 0 : (all_lens && all_tokens && lens_cap >= (size_t)tot_seg &&
+                                        tokens_cap >= (size_t)tot_tok) ? 1 : -1;
+        DevBuf<int32_t> sts((size_t)W);
+        QASR_HIP(hipMemcpyAsync(sts.p + c->rank, &st, sizeof st, hipMemcpyHostToDevice, c->st));
+        QASR_NCCL(ncclAllGather(sts.p + c->rank, sts.p, 1, ncclInt32, c->c, c->st));
+        std::vector<int32_t> every((size_t)W);
+        QASR_HIP(hipMemcpyAsync(every.data(), sts.p, every.size() * 4, hipMemcpyDeviceToHost, c->st));
+        QASR_HIP(hipStreamSynchronize(c->st));
+        const int32_t lo = *std::min_element(every.begin(), every.end());
+        const int32_t hi = *std::max_element(every.begin(), every.end());
+        QASR_CHECK(lo >= 0, QASR_E_CAPACITY, "gather buffers too small (on this or another rank)");
+        QASR_CHECK(lo == hi, QASR_E_INVALID, "ranks disagree on size query vs payload gather");
+        if (query) return;
         // (2) the ragged payload, padded to the largest rank
         DevBuf<int32_t> dl((size_t)max_seg * W), dt((size_t)max_tok * W);
         QASR_HIP(hipMemsetAsync(dl.p + max_seg * c->rank, 0, (size_t)max_seg * 4, c->st));

@@ -405,6 +405,9 @@ static const bool g_dump = getenv("QASR_DUMP_DIR") != nullptr;
 
 void Session::dump_rows(const char* what, int l, int rows, const void* p, size_t bytes) {
     static int seq = 0;
+    // a pass being captured into a step graph cannot synchronise its stream (the capture would fail): dumps come
+    // from eager passes only (the diagnosis tools set QASR_NO_GRAPH)
+    if (sc_.capturing) return;
     std::vector<char> h(bytes);
     QASR_HIP(hipStreamSynchronize(st_));
     QASR_HIP(hipMemcpy(h.data(), p, bytes, hipMemcpyDeviceToHost));
@@ -746,6 +749,7 @@ void Session::draft_decode(int n_prompt, int base, int budget, int dummy, std::v
         dstats_.passes++;
         dstats_.proposed += R - 1;
         int acc = 0;
+        bool rejected = false;   // the pass ended on a drafted token greedy did not choose (not on EOS / the budget)
         for (int i = 0; i < R; i++) {
             const int t = got[i];
             if (!forced && (t == h.tok_eos0 || t == h.tok_eos1)) {
@@ -754,13 +758,17 @@ void Session::draft_decode(int n_prompt, int base, int budget, int dummy, std::v
             }
             toks.push_back(t);
             if ((int)toks.size() >= budget) break;
-            if (i < R - 1 && t != draft[i]) break;   // row i + 1 was fed a token greedy did not choose
+            if (i < R - 1 && t != draft[i]) {   // row i + 1 was fed a token greedy did not choose
+                rejected = true;
+                break;
+            }
             if (i < R - 1) acc++;
         }
         dstats_.accepted += acc;
-        if (R > 1) {   // acc successes, then one rejection unless every drafted token was accepted
+        if (R > 1) {   // acc successes, then one rejection if a drafted token was refused — a pass cut short by EOS
+                       // or the token budget rejected nothing, so it leaves the failure count alone
             draft_s_ = 0.8 * draft_s_ + acc;
-            draft_f_ = 0.8 * draft_f_ + (acc < R - 1 ? 1.0 : 0.0);
+            draft_f_ = 0.8 * draft_f_ + (rejected ? 1.0 : 0.0);
         } else {       // a plain step: the estimate relaxes toward the prior, so drafting is tried again later
             draft_s_ = 0.95 * draft_s_ + 0.05 * 4.0;
             draft_f_ = 0.95 * draft_f_ + 0.05 * 0.5;
@@ -1190,8 +1198,11 @@ void Session::forced_logits_host(const float* pcm, int64_t n, const int32_t* for
     encoder(fe, nullptr);
     std::vector<int32_t> ids = build_prompt(h, fe.n_tok[0], 0, context_);
     const int P = (int)ids.size();
-    QASR_CHECK(P + n_forced + 1 <= n_ctx_, QASR_E_CAPACITY, "forced sequence exceeds n_ctx");
-    ensure_kv(P + n_forced + 2);   // + a dummy slot for a verify pass's bucket padding rows
+    // the one-pass verify needs one more KV slot (the dummy slot of its bucket's padding rows); the step-by-step
+    // path accepts a sequence that exactly fills n_ctx
+    const int extra = one_pass ? 1 : 0;
+    QASR_CHECK(P + n_forced + extra <= n_ctx_, QASR_E_CAPACITY, "forced sequence exceeds n_ctx");
+    ensure_kv(P + n_forced + 1 + extra);
     logits.assign((size_t)(n_forced + 1) * V, 0.f);
     std::vector<int> pos(P), slot(P), kvs(P, 0), kvl(P);
     for (int i = 0; i < P; i++) {

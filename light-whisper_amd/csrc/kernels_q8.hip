@@ -13,6 +13,10 @@
 #include "rowops.h"
 #include "xlane.h"
 
+#ifndef QASR_DIAG
+#define QASR_DIAG 0
+#endif
+
 namespace qasr {
 
 // ------------------------------------------------------------------------------------------------ helpers
@@ -1043,7 +1047,8 @@ __global__ __launch_bounds__(256 * KG, 2 / KG) void k_gemm_q8d(const int8_t* __r
     // each), BN·KB/(2·NW) per wave.
     constexpr int SAW = KB * BM / NW, ASI = (SAW + 63) / 64;
     constexpr int SBW = BN * KB / (2 * NW), BSI = (SBW + 63) / 64;
-    constexpr int NPW = AI + BI + ASI + BSI;            // DMA instructions per wave per stage
+    // QASR_DIAG (diagnostic builds only, wrong results): bit 0 skips the scale DMAs, bit 1 the math, bit 2 all DMA
+    constexpr int NPW = (QASR_DIAG & 4) ? 0 : AI + BI + ((QASR_DIAG & 1) ? 0 : ASI + BSI);   // DMAs per wave per stage
     constexpr int D = NBUF - 1;                         // prefetch distance (stages in flight)
     __shared__ __attribute__((aligned(1024))) char smem[NBUF * STAGE];
 
@@ -1091,12 +1096,14 @@ __global__ __launch_bounds__(256 * KG, 2 / KG) void k_gemm_q8d(const int8_t* __r
     const uint32_t wsa = __builtin_amdgcn_readfirstlane(lds0 + OSA + wave * SAW * 4);
     const uint32_t wsb = __builtin_amdgcn_readfirstlane(lds0 + OSB + wave * SBW * 4);
     auto issue = [&](int s, int buf) {
+        if constexpr ((QASR_DIAG & 4) != 0) return;
         const int k0 = k_begin + s * BK;
         const uint32_t so = buf * STAGE;
 #pragma unroll
         for (int u = 0; u < AI; u++) dma_lds16(a_src[u] + k0, wa + so + 1024 * u);
 #pragma unroll
         for (int u = 0; u < BI; u++) dma_lds16(b_src[u] + k0, wb + so + 1024 * u);
+        if constexpr ((QASR_DIAG & 1) != 0) return;
 #pragma unroll
         for (int u = 0; u < ASI; u++) {
             if (64 * u + lane < SAW) dma_lds4(sa_src[u] + k0 / QK, wsa + so + 256 * u);
@@ -1108,7 +1115,7 @@ __global__ __launch_bounds__(256 * KG, 2 / KG) void k_gemm_q8d(const int8_t* __r
 
     const int fr = lane & 15, kh = lane >> 4, fq = 4 * kh;
     const int arow = wr * 16 * TI, bcol = wc * 16 * TJ;
-    const bool active = m0 + arow < M;   // wave-uniform
+    const bool active = (QASR_DIAG & 2) == 0 && m0 + arow < M;   // wave-uniform
     int foff[KB];
 #pragma unroll
     for (int kb = 0; kb < KB; kb++) foff[kb] = 16 * ((2 * kb + (kh >> 1)) ^ swz(fr)) + 8 * (kh & 1);
@@ -1792,6 +1799,7 @@ __global__ __launch_bounds__(256, NBUF <= 2 ? 2 : 1) void k_gemm_mx(const uint8_
     const uint32_t wsa = __builtin_amdgcn_readfirstlane(lds0 + OSA + wave * SAW * 4);
     const uint32_t wsb = __builtin_amdgcn_readfirstlane(lds0 + OSB + wave * SBW * 4);
     auto issue = [&](int s, int buf) {
+        if constexpr ((QASR_DIAG & 4) != 0) return;
         const int k0 = k_begin + s * BK;
         const uint32_t so = buf * STAGE;
 #pragma unroll

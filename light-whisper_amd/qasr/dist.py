@@ -2,9 +2,10 @@
 weights and gather token streams").  One process per GPU; nothing here runs inside a timed step.
 
 On GPUs the collectives are libqasr's own RCCL communicator (`NativeComm`, include/qasr.h qasr_dist_*: the path a
-host without PyTorch — the Rust app — drives); torch.distributed only carries the 128-byte unique id to every rank
-(and the bench's barrier / timing reductions).  The torch.distributed versions below serve the "gloo" rehearsal
-(ranks sharing one card, which RCCL refuses) and the CPU tests.
+host without PyTorch — the Rust app — drives); the 128-byte unique id reaches the other ranks through a file
+(`file_exchange`), as a Rust host would hand it over, and bench.py's barrier / timing reductions run over a CPU (gloo)
+group, so each rank holds exactly one RCCL communicator.  The torch.distributed versions below serve the "gloo"
+rehearsal (ranks sharing one card, which RCCL refuses), the `torch-nccl` fallback and the CPU tests.
 
 * `broadcast_weights`: rank 0 holds the loaded (or generated) model, every other rank a shell with the identical
   device layout (`Model.shell`, include/qasr.h qasr_model_open_shell); ONE broadcast over the whole weight blob
@@ -190,6 +191,59 @@ class NativeComm:
             s0 += rank_segs[r]
             out.append(segs)
         return out
+
+
+def file_exchange(rank: int, world: int, key: str | None = None, directory: str | None = None,
+                  timeout_s: float = 600.0):
+    """The unique-id hand-off without PyTorch (one node): returns `exchange(payload) -> bytes` for NativeComm.  Rank 0
+    publishes its bytes in `<directory>/qasr_uid_<key>.bin` — written under a temporary name and renamed, so a reader
+    never sees a partial file — and every other rank polls for the file.  This is what a host without torch (the Rust
+    app) does with a file or a pipe of its own.  `key` defaults to the launcher's rendezvous
+    (TORCHELASTIC_RUN_ID + MASTER_PORT, fresh for every launch), `directory` to $QASR_RDV_DIR or the temp dir.
+    Rank 0 removes the file once its communicator exists (ncclCommInitRank returns only when every rank joined, i.e.
+    after every rank has read it): call `exchange.cleanup()` then."""
+    import os
+    import tempfile
+
+    if key is None:
+        key = f"{os.environ.get('TORCHELASTIC_RUN_ID', 'run')}_{os.environ.get('MASTER_PORT', '0')}"
+    directory = directory or os.environ.get("QASR_RDV_DIR") or tempfile.gettempdir()
+    path = os.path.join(directory, f"qasr_uid_{key}.bin")
+
+    def exchange(payload: bytes) -> bytes:
+        if world == 1:
+            return payload
+        if rank == 0:
+            tmp = f"{path}.{os.getpid()}.tmp"
+            with open(tmp, "wb") as f:
+                f.write(payload)
+                f.flush()
+                os.fsync(f.fileno())
+            os.replace(tmp, path)
+            return payload
+        t0 = time.monotonic()
+        while True:
+            try:
+                with open(path, "rb") as f:
+                    got = f.read()
+                if len(got) == len(payload):
+                    return got
+            except FileNotFoundError:
+                pass
+            if time.monotonic() - t0 > timeout_s:
+                raise TimeoutError(f"rank {rank}: no unique id at {path} after {timeout_s:.0f} s")
+            time.sleep(0.01)
+
+    def cleanup():
+        if rank == 0:
+            try:
+                os.remove(path)
+            except FileNotFoundError:
+                pass
+
+    exchange.cleanup = cleanup
+    exchange.path = path
+    return exchange
 
 
 def torch_exchange(payload: bytes) -> bytes:

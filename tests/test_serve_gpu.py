@@ -195,5 +195,6 @@ def test_serve_interim_replay(ref_arch, tmp_path):
     div = next((j for j in range(n) if got[j] != toks[j]), n)
     if div < n:
         top2 = np.sort(lg[div])[-2:]
-        assert top2[1] - top2[0] < 0.02 * np.abs(lg[div]).max(), (engine, div, got, list(toks))
+        # the near-tie rule of every parity test: top-2 gap below 0.5 % of the row's range
+        assert top2[1] - top2[0] < 0.005 * (lg[div].max() - lg[div].min()), (engine, div, got, list(toks))
     assert div >= min(4, n), (engine, got, list(toks))

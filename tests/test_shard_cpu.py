@@ -70,6 +70,63 @@ def test_lpt_balance():
         assert max(loads) / min(loads) < 1.01
 
 
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
+def test_strong_sharding_256_total(world):
+    """--scaling strong (the default; BASELINE configs[3] as stated): 256 segments IN TOTAL, LPT over N ranks —
+    every segment on exactly one rank and the audio-seconds balanced (32 segments per GPU at N = 8)"""
+    rng = np.random.default_rng(1)
+    secs = rng.uniform(2.0, 12.0, size=256)
+    lengths = [int(x * 16000) for x in secs]
+    shards = bench.lpt_shard(lengths, world)
+    flat = sorted(i for sh in shards for i in sh)
+    assert flat == list(range(256))                             # disjoint cover of the 256
+    loads = [sum(lengths[i] for i in sh) for sh in shards]
+    assert max(loads) / min(loads) < (1.001 if world == 1 else 1.03)
+    assert max(len(sh) for sh in shards) - min(len(sh) for sh in shards) <= max(2, 256 // world // 4)
+    # make_workload(total=256) hands each rank exactly its shard's audio, and N = 1 is the weak-scaling list
+    got = sum(len(bench.make_workload(world, r, total=256)) for r in range(world)) if world <= 2 else None
+    if got is not None:
+        assert got == 256
+    if world == 1:
+        a, b = bench.make_workload(1, 0, total=256), bench.make_workload(1, 0)
+        assert len(a) == len(b) and all(np.array_equal(x, y) for x, y in zip(a, b))
+
+
+def _xchg_rank(rank, world, key, d, q):
+    sys.path.insert(0, os.path.join(ROOT, "light-whisper_amd"))
+    from qasr import dist as qdist
+
+    x = qdist.file_exchange(rank, world, key=key, directory=d, timeout_s=60)
+    payload = bytes(range(128)) if rank == 0 else bytes(128)
+    got = x(payload)
+    q.put((rank, got))
+
+
+def test_file_unique_id_exchange(tmp_path):
+    """the torch-free unique-id hand-off (qasr/dist.py file_exchange, what a Rust host does with a file of its own):
+    rank 0's 128 bytes reach every rank, readers never see a partial file, rank 0 removes the file afterwards"""
+    import multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    world = 3
+    procs = [ctx.Process(target=_xchg_rank, args=(r, world, "t1", str(tmp_path), q)) for r in (1, 2, 0)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=60) for _ in range(world))
+    for p in procs:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    assert all(v == bytes(range(128)) for v in out.values())
+    sys.path.insert(0, os.path.join(ROOT, "light-whisper_amd"))
+    from qasr import dist as qdist
+
+    x = qdist.file_exchange(0, world, key="t1", directory=str(tmp_path))
+    assert os.path.exists(x.path)
+    x.cleanup()
+    assert not os.path.exists(x.path) and not [f for f in os.listdir(tmp_path) if f.endswith(".tmp")]
+
+
 def test_workload_deterministic():
     a = bench.make_workload(2, 1)
     b = bench.make_workload(2, 1)

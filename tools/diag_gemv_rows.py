@@ -18,6 +18,7 @@ sys.path.insert(0, os.path.join(ROOT, "light-whisper_amd"))
 sys.path.insert(0, os.path.join(ROOT, "oracle"))
 TMP = tempfile.mkdtemp(prefix="qasr_dump_")
 os.environ["QASR_DUMP_DIR"] = TMP
+os.environ["QASR_NO_GRAPH"] = "1"   # dumps synchronise the stream: eager passes only (engine.cpp dump_rows)
 from bench import speech_like  # noqa: E402
 
 

@@ -15,6 +15,7 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "light-whisper_amd"))
 TMP = tempfile.mkdtemp(prefix="qasr_dump_")
 os.environ["QASR_DUMP_DIR"] = TMP   # read when the library loads
+os.environ["QASR_NO_GRAPH"] = "1"   # dumps synchronise the stream: eager passes only (engine.cpp dump_rows)
 from bench import speech_like  # noqa: E402
 
 STAGES = {"x_in": np.float32, "qkv": np.float32, "att_q": np.int8, "att_d": np.float32, "x_mid": np.float32,
