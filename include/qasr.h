@@ -277,6 +277,12 @@ QASR_API int qasr_op_set_gemm_ws_rows(int32_t rows, int32_t all_shapes);
    ldy).  cfg: GEMM configuration (-1 = heuristic). */
 /* MXFP8 precision mode: Q8 blocks (q int8, d f32 or f16) → OCP MXFP8 (e4m3 elements q·d·2^-E
    rounded to nearest even, e8m0 byte E+127 with E the smallest exponent putting the block maximum ≤ 448). */
+/* Regrouped stage scales of a Q8 matrix (sc [N][K/32] f16 → out [K/128][N][4] f16, K % 128 == 0): a K-128 GEMM
+   stage's column scales as one contiguous run (the decode GEMMs' 16-byte scale DMA; a model's decoder matrices
+   carry theirs).  qasr_op_register_stage_scales(wsc, out) makes the qasr_op_* GEMM entry points use `out` for the
+   matrix whose scale pointer is `wsc` (NULL unregisters) — tests and tuning tools. */
+QASR_API int qasr_op_stage_scales(const void* wsc, int32_t N, int32_t K, void* out, void* stream);
+QASR_API int qasr_op_register_stage_scales(const void* wsc, const void* sc4);
 QASR_API int qasr_op_q8_to_mx(const int8_t* q, const void* d, int32_t d_is_f16, int64_t nblk, uint8_t* q8,
                              uint8_t* s8, void* stream);
 /* y = epi(X·Wᵀ) on MXFP8 operands (v_mfma_scale_f32_16x16x128_f8f6f4); epi as qasr_op_linear_q8 (0-2), 3 SwiGLU

@@ -2,7 +2,10 @@
 #include <math.h>
 #include <string.h>
 
+#include <mutex>
 #include <string>
+#include <utility>
+#include <vector>
 
 #include "../../include/qasr.h"
 #include "capi_util.h"
@@ -25,6 +28,37 @@ QASR_API int qasr_op_quant_rows(const float* x, int32_t M, int32_t K, int32_t ld
     });
 }
 
+// Tests and tuning tools: the regrouped stage scales (Q8Mat::sc4, [K/128][N][4]) of a raw weight matrix given to the
+// qasr_op_* GEMM entry points, registered by its scale pointer (a model's matrices carry theirs, model.cpp)
+static std::mutex g_s4_mu;
+static std::vector<std::pair<const void*, const __half*>> g_s4;
+static const __half* stage_scales_of(const void* wsc) {
+    std::lock_guard<std::mutex> lk(g_s4_mu);
+    for (auto& e : g_s4)
+        if (e.first == wsc) return e.second;
+    return nullptr;
+}
+
+QASR_API int qasr_op_stage_scales(const void* wsc, int32_t N, int32_t K, void* out, void* stream) {
+    return guard([&] {
+        q8_stage_scales((const __half*)wsc, N, K, (__half*)out, S(stream));
+        launched();
+    });
+}
+
+QASR_API int qasr_op_register_stage_scales(const void* wsc, const void* sc4) {
+    return guard([&] {
+        QASR_CHECK(wsc, QASR_E_INVALID, "null scale pointer");
+        std::lock_guard<std::mutex> lk(g_s4_mu);
+        for (size_t i = 0; i < g_s4.size(); i++)
+            if (g_s4[i].first == wsc) {
+                g_s4.erase(g_s4.begin() + (long)i);
+                break;
+            }
+        if (sc4) g_s4.emplace_back(wsc, (const __half*)sc4);
+    });
+}
+
 QASR_API int qasr_op_repack_q8(const uint8_t* blocks, int64_t nblk, int8_t* qs, void* sc, void* stream) {
     return guard([&] {
         repack_q8(blocks, nblk, qs, (__half*)sc, S(stream));
@@ -42,6 +76,7 @@ QASR_API int qasr_op_linear_q8(const int8_t* xq, const float* xd, int32_t M, con
         Q8Mat W;
         W.qs = (int8_t*)wqs;
         W.sc = (__half*)wsc;
+        W.sc4 = stage_scales_of(wsc);
         W.N = N;
         W.K = K;
         if (path == 1 || (path >= 3 && path <= 5)) {   // GEMV: auto, or 1 / 2 / 4 columns per wave
@@ -49,6 +84,9 @@ QASR_API int qasr_op_linear_q8(const int8_t* xq, const float* xd, int32_t M, con
             gemv_q8(xq, xd, M, W, bias, res, y, ldy, epi, S(stream), path == 1 ? 0 : 1 << (path - 3));
         } else if (path == 2) {
             gemm_q8(xq, xd, M, W, bias, res, y, ldy, epi, S(stream));
+        } else if (path >= 4096) {   // any configuration index: 4096 + cfg + 256·splits
+            const int cfg = (path - 4096) % 256, splits = (path - 4096) / 256;
+            gemm_q8(xq, xd, M, W, bias, res, y, ldy, epi, S(stream), cfg, splits);
         } else if (path >= 16) {
             const int cfg = (path - 16) % 32, splits = (path - 16) / 32;
             gemm_q8(xq, xd, M, W, bias, res, y, ldy, epi, S(stream), cfg == 31 ? -1 : cfg, splits);
@@ -94,6 +132,7 @@ QASR_API int qasr_op_linear_q8_ex(const int8_t* xq, const float* xd, int32_t M, 
         Q8Mat W;
         W.qs = (int8_t*)wqs;
         W.sc = (__half*)wsc;
+        W.sc4 = stage_scales_of(wsc);
         W.N = N;
         W.K = K;
         gemm_q8(xq, xd, M, W, bias, nullptr, (float*)y, ldy, epi, S(stream), cfg, 0, yq, yd);
@@ -148,6 +187,7 @@ QASR_API int qasr_op_gemm_swiglu_q8(const int8_t* xq, const float* xd, int32_t M
         Q8Mat W;
         W.qs = (int8_t*)wqs;
         W.sc = (__half*)wsc;
+        W.sc4 = stage_scales_of(wsc);
         W.N = N;
         W.K = K;
         gemm_q8(xq, xd, M, W, nullptr, nullptr, nullptr, N, EPI_SWIGLU, S(stream), -1, 0, hq, hd);
@@ -163,10 +203,13 @@ QASR_API int qasr_op_gemm_swiglu_q8_cfg(const int8_t* xq, const float* xd, int32
         Q8Mat W;
         W.qs = (int8_t*)wqs;
         W.sc = (__half*)wsc;
+        W.sc4 = stage_scales_of(wsc);
         W.N = N;
         W.K = K;
-        gemm_q8(xq, xd, M, W, nullptr, nullptr, nullptr, N, EPI_SWIGLU, S(stream), cfg < 0 ? -1 : cfg % 32,
-                cfg < 0 ? 0 : cfg / 32, hq, hd);
+        // cfg + 32·splits (cfg < 31), or 4096 + cfg + 256·splits (any configuration index)
+        const int c = cfg < 0 ? -1 : cfg >= 4096 ? (cfg - 4096) % 256 : cfg % 32;
+        const int sp = cfg < 0 ? 0 : cfg >= 4096 ? (cfg - 4096) / 256 : cfg / 32;
+        gemm_q8(xq, xd, M, W, nullptr, nullptr, nullptr, N, EPI_SWIGLU, S(stream), c, sp, hq, hd);
         launched();
     });
 }
@@ -180,6 +223,7 @@ QASR_API int qasr_op_gemm_exact_rows(const int8_t* xq, const float* xd, int32_t 
         Q8Mat W;
         W.qs = (int8_t*)wqs;
         W.sc = (__half*)wsc;
+        W.sc4 = stage_scales_of(wsc);
         W.N = N;
         W.K = K;
         gemm_exact_rows(xq, xd, M, W, res, y, ldy, epi, S(stream));
@@ -218,6 +262,7 @@ QASR_API int qasr_op_gemv_fused(int32_t pro, const float* src, int32_t ld_src, c
         Q8Mat W;
         W.qs = (int8_t*)wqs;
         W.sc = (__half*)wsc;
+        W.sc4 = stage_scales_of(wsc);
         W.N = N;
         W.K = K;
         gemv_fused(pro, xq, xd, src, ld_src, nw, eps, M, W, res, y, ldy, epi, hq, hd, S(stream));
@@ -302,6 +347,7 @@ QASR_API int qasr_op_embed_rows(const int32_t* ids, int32_t n, const int8_t* wqs
         Q8Mat W;
         W.qs = (int8_t*)wqs;
         W.sc = (__half*)wsc;
+        W.sc4 = stage_scales_of(wsc);
         W.K = K;
         embed_rows(ids, n, W, alt, out, S(stream));
         launched();

@@ -184,6 +184,7 @@ QASR_API int qasr_session_open(qasr_model* m, const char* kv_type, int32_t n_ctx
         QASR_CHECK(!kv_type || std::string(kv_type) == "f16", QASR_E_INVALID, "kv_type must be \"f16\"");
         QASR_CHECK(!m->m->weights_pending, QASR_E_INVALID,
                    "model is a shell whose weights have not arrived (qasr_model_weights_received)");
+        ensure_stage_scales(*m->m);
         auto s = std::make_unique<qasr_session>();
         s->s = std::make_unique<Session>(m->m.get(), n_ctx > 0 ? n_ctx : 32768);
         *out = s.release();

@@ -45,6 +45,10 @@ struct Q8Mat {
     // MXFP8 image of the same rows (precision mode "mxfp8"): e4m3 [N][K] + e8m0 [N][K/32]
     uint8_t* mx = nullptr;
     uint8_t* mxs = nullptr;
+    // the same scales regrouped [K/128][N][4] (derived, K % 128 == 0; decoder matrices): a K-128 GEMM stage's
+    // column scales are ONE contiguous run of 8 bytes per column, staged by 16-byte DMA (model.cpp
+    // ensure_stage_scales, kernels_q8.hip k_gemm_q8d WS4)
+    const __half* sc4 = nullptr;
 };
 
 // Quantised activations X[M][K]: int8 values + per-32-block f16-rounded scale stored as f32.

@@ -103,6 +103,8 @@ size_t mx_workspace_bytes(int64_t M, int64_t K);
 // rows of a [2F][K] gate|up matrix → interleaved by 16 (32j+t: t<16 gate 16j+t, else up 16j+t-16)
 int64_t gate_up_interleaved_row(int64_t r, int64_t F);
 void interleave_gate_up(Q8Mat& W, hipStream_t s);
+// sc [N][K/32] → out [K/128][N][4] (Q8Mat::sc4), K % 128 == 0
+void q8_stage_scales(const __half* sc, int N, int K, __half* out, hipStream_t s);
 // rows of a Q8 table (token embeddings), dequantised; ids < 0 take row -(id+1) of `alt` [*][K] f32 instead
 void embed_rows(const int* ids, int n, const Q8Mat& W, const float* alt, float* out, hipStream_t s);
 

@@ -16,6 +16,9 @@
 #ifndef QASR_DIAG
 #define QASR_DIAG 0
 #endif
+#ifndef QASR_PIN
+#define QASR_PIN 1
+#endif
 
 namespace qasr {
 
@@ -1023,9 +1026,10 @@ __global__ __launch_bounds__(256) void k_gemm_q8(const int8_t* __restrict__ X, c
 //  * Compute: MFMA q is issued LAG MFMAs before its int32 result is rescaled into the f32 accumulator
 //    (cvt, d_x·d_w, fma: 3 VALU per output and block); sched_group_barrier pins the MFMA/VALU interleave.  Waves
 //    whose rows all lie past M (padded decode buckets) skip the math but still stage their share.
-template <int WM, int WN, int TI, int TJ, int NBUF, int BK = 64, int KG = 1>
-__global__ __launch_bounds__(256 * KG, 2 / KG) void k_gemm_q8d(const int8_t* __restrict__ X, const float* __restrict__ Xd, int M,
+template <int WM, int WN, int TI, int TJ, int NBUF, int BK = 64, int KG = 1, bool WS4 = false>
+__global__ __launch_bounds__(256 * KG, KG == 1 ? 2 : 1) void k_gemm_q8d(const int8_t* __restrict__ X, const float* __restrict__ Xd, int M,
                                                      const int8_t* __restrict__ W, const __half* __restrict__ Wsc,
+                                                     const __half* __restrict__ Wsc4,
                                                      int N, int K, const float* __restrict__ bias, const float* res,
                                                      float* y, int ldy, int epi, int steps_per_split,
                                                      int8_t* __restrict__ yq, float* __restrict__ yd,
@@ -1033,22 +1037,36 @@ __global__ __launch_bounds__(256 * KG, 2 / KG) void k_gemm_q8d(const int8_t* __r
     static_assert(WM * WN == 4, "k_gemm_q8d: 4 waves per K group");
     static_assert(BK == 64 || BK == 128, "k_gemm_q8d: a stage is 2 or 4 Q8 blocks");
     // KG K groups of 4 waves share the tile: group g takes blocks [g·KB/KG, (g+1)·KB/KG) of every stage and the
-    // groups' accumulators are summed through LDS at the end (more waves per tile without split-K atomics)
-    static_assert(KG == 1 || (KG == 2 && BK == 128), "k_gemm_q8d: K groups");
+    // groups' accumulators are summed through LDS at the end, in group order (more waves per tile — 8 or 16 — without
+    // split-K; deterministic)
+    static_assert(KG == 1 || ((KG == 2 || KG == 4) && BK == 128), "k_gemm_q8d: K groups");
+    // WS4: the stage's scales by 16-byte DMA — A: one lane per row, its 4 block scales ([M][K/32] f32 rows: 16
+    // contiguous bytes), LDS [BM][4]; B: the regrouped copy Wsc4 [K/128][N][4] f16 (Q8Mat::sc4), the tile's 8·BN
+    // bytes contiguous, LDS [BN][4].  (Otherwise 4-byte gathers, one cache line per lane: 6 instructions and ~384
+    // line touches per 64×64 stage against ~70.)
+    static_assert(!WS4 || BK == 128, "k_gemm_q8d: WS4 stages are K = 128");
     constexpr int NW = 4 * KG;
     constexpr int KB = BK / 32, NF = TI * TJ;
     constexpr int BM = WM * 16 * TI, BN = WN * 16 * TJ;
     constexpr int RP = 1024 / BK;                       // rows per 1-KB DMA piece
     static_assert(BM % (4 * RP) == 0 && BN % (4 * RP) == 0 && BN <= 256 && BM <= 256, "k_gemm_q8d: tile sides");
     constexpr int OB = BM * BK, OSA = OB + BN * BK, OSB = OSA + KB * BM * 4, STAGE = OSB + (KB / 2) * BN * 4;
-    constexpr int AI = BM / RP / NW, BI = BN / RP / NW;   // A / B pieces per wave per stage
-    static_assert(AI * RP * NW == BM && BI * RP * NW == BN, "k_gemm_q8d: pieces per wave");
+    // A / B pieces per wave per stage; with 16 waves (KG 4) a 64×64 stage has fewer A (B) pieces than waves: then
+    // the A and B pieces form one list, PP per wave (UNI)
+    constexpr int PA = BM / RP, PB = BN / RP;
+    constexpr bool UNI = PA % NW != 0 || PB % NW != 0;
+    constexpr int AI = UNI ? 0 : PA / NW, BI = UNI ? 0 : PB / NW, PP = UNI ? (PA + PB) / NW : 0;
+    static_assert(UNI ? (PP * NW == PA + PB && PP >= 1) : (AI * RP * NW == BM && BI * RP * NW == BN),
+                  "k_gemm_q8d: pieces per wave");
     // A scales: [KB][BM] floats gathered by 4-byte DMA (KB·BM/NW per wave); B scales: [KB/2][BN] dwords (two f16
     // each), BN·KB/(2·NW) per wave.
     constexpr int SAW = KB * BM / NW, ASI = (SAW + 63) / 64;
     constexpr int SBW = BN * KB / (2 * NW), BSI = (SBW + 63) / 64;
+    constexpr int AR4 = BM / NW, BL4 = BN / (2 * NW);   // WS4: A-scale rows / B-scale 16-byte lanes per wave
+    static_assert(!WS4 || (AR4 * NW == BM && AR4 <= 64 && BL4 * 2 * NW == BN && BL4 >= 1), "k_gemm_q8d: WS4 tile");
+    constexpr int SCI = WS4 ? 2 : ASI + BSI;            // scale DMA instructions per wave per stage
     // QASR_DIAG (diagnostic builds only, wrong results): bit 0 skips the scale DMAs, bit 1 the math, bit 2 all DMA
-    constexpr int NPW = (QASR_DIAG & 4) ? 0 : AI + BI + ((QASR_DIAG & 1) ? 0 : ASI + BSI);   // DMAs per wave per stage
+    constexpr int NPW = (QASR_DIAG & 4) ? 0 : AI + BI + PP + ((QASR_DIAG & 1) ? 0 : SCI);   // DMAs per wave per stage
     constexpr int D = NBUF - 1;                         // prefetch distance (stages in flight)
     __shared__ __attribute__((aligned(1024))) char smem[NBUF * STAGE];
 
@@ -1064,8 +1082,18 @@ __global__ __launch_bounds__(256 * KG, 2 / KG) void k_gemm_q8d(const int8_t* __r
     auto swz = [](int r) { return BK == 64 ? (r >> 2) & 3 : (r >> 1) & 7; };
 
     // ---- per-lane DMA sources (k-independent parts)
-    const int8_t* a_src[AI];
-    const int8_t* b_src[BI];
+    const int8_t* a_src[AI ? AI : 1];
+    const int8_t* b_src[BI ? BI : 1];
+    const int8_t* u_src[PP ? PP : 1];
+    uint32_t u_dst[PP ? PP : 1];   // LDS byte offsets of the unified pieces (wave-uniform)
+#pragma unroll
+    for (int u = 0; u < PP; u++) {
+        const int p = wave * PP + u;   // wave-uniform
+        const bool isa = p < PA;
+        const int row = RP * (isa ? p : p - PA) + lane / (BK / 16), c = (lane % (BK / 16)) ^ swz(row);
+        u_src[u] = isa ? X + (size_t)min(m0 + row, M - 1) * K + 16 * c : W + (size_t)min(n0 + row, N - 1) * K + 16 * c;
+        u_dst[u] = isa ? 1024 * p : OB + 1024 * (p - PA);
+    }
 #pragma unroll
     for (int u = 0; u < AI; u++) {
         const int row = RP * (wave * AI + u) + lane / (BK / 16), c = (lane % (BK / 16)) ^ swz(row);
@@ -1088,13 +1116,16 @@ __global__ __launch_bounds__(256 * KG, 2 / KG) void k_gemm_q8d(const int8_t* __r
         const int p = wave * SBW + min(64 * u + lane, SBW - 1);
         sb_src[u] = (const uint32_t*)Wsc + (size_t)min(n0 + p % BN, N - 1) * (nb / 2) + p / BN;
     }
+    // WS4 sources: row m0 + wave·AR4 + lane's 16-byte scale group; columns n0 + 2(wave·BL4 + lane) (+1) in Wsc4
+    const float* sa4_src = Xd + (size_t)min(m0 + wave * AR4 + min(lane, AR4 - 1), M - 1) * nb;
+    const __half* sb4_src = Wsc4 + (size_t)4 * min(n0 + 2 * (wave * BL4 + min(lane, BL4 - 1)), N - 2);
 
     // LDS byte address of this wave's pieces (wave-uniform → SGPR for M0)
     const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
     const uint32_t wa = __builtin_amdgcn_readfirstlane(lds0 + 1024 * (wave * AI));
     const uint32_t wb = __builtin_amdgcn_readfirstlane(lds0 + OB + 1024 * (wave * BI));
-    const uint32_t wsa = __builtin_amdgcn_readfirstlane(lds0 + OSA + wave * SAW * 4);
-    const uint32_t wsb = __builtin_amdgcn_readfirstlane(lds0 + OSB + wave * SBW * 4);
+    const uint32_t wsa = __builtin_amdgcn_readfirstlane(lds0 + OSA + (WS4 ? wave * AR4 * 16 : wave * SAW * 4));
+    const uint32_t wsb = __builtin_amdgcn_readfirstlane(lds0 + OSB + (WS4 ? wave * BL4 * 16 : wave * SBW * 4));
     auto issue = [&](int s, int buf) {
         if constexpr ((QASR_DIAG & 4) != 0) return;
         const int k0 = k_begin + s * BK;
@@ -1103,7 +1134,15 @@ __global__ __launch_bounds__(256 * KG, 2 / KG) void k_gemm_q8d(const int8_t* __r
         for (int u = 0; u < AI; u++) dma_lds16(a_src[u] + k0, wa + so + 1024 * u);
 #pragma unroll
         for (int u = 0; u < BI; u++) dma_lds16(b_src[u] + k0, wb + so + 1024 * u);
+#pragma unroll
+        for (int u = 0; u < PP; u++)
+            dma_lds16(u_src[u] + k0, __builtin_amdgcn_readfirstlane(lds0 + u_dst[u]) + so);
         if constexpr ((QASR_DIAG & 1) != 0) return;
+        if constexpr (WS4) {
+            if (lane < AR4) dma_lds16(sa4_src + k0 / QK, wsa + so);
+            if (lane < BL4) dma_lds16(sb4_src + (size_t)(k0 / 128) * N * 4, wsb + so);
+            return;
+        }
 #pragma unroll
         for (int u = 0; u < ASI; u++) {
             if (64 * u + lane < SAW) dma_lds4(sa_src[u] + k0 / QK, wsa + so + 256 * u);
@@ -1175,8 +1214,19 @@ __global__ __launch_bounds__(256 * KG, 2 / KG) void k_gemm_q8d(const int8_t* __r
         constexpr bool OP = TJ <= 4 && KG == 1 && (BK == 64 || TI == 1);
         float sb[KBG][TJ], sa[KBG][TI][4], sal[KBG][TI], sbl[KBG];
         long a[KBG][TI], b[KBG][TJ];
-        auto load_block = [&](int sl, int kb) {
-            if constexpr (OP) {
+        // per-fragment LDS reads of block kb into slot sl: the B scale(s), row fragment i (A bytes + scales), column
+        // fragment j (B bytes) — QASR_PIN issues each one right after the previous block's last use of its registers
+        auto load_bscale = [&](int sl, int kb) {
+            if constexpr (WS4) {   // LDS [BN][4] f16 and [BM][4] f32
+                if constexpr (OP) {
+                    const int cl = min(lane, 16 * TJ - 1);
+                    sbl[sl] = __half2float(*(const __half*)(st + OSB + 8 * (bcol + cl) + 2 * kb));
+                } else {
+#pragma unroll
+                    for (int j = 0; j < TJ; j++)
+                        sb[sl][j] = __half2float(*(const __half*)(st + OSB + 8 * (bcol + 16 * j + fr) + 2 * kb));
+                }
+            } else if constexpr (OP) {
                 const int cl = min(lane, 16 * TJ - 1);
                 const uint32_t v = *(const uint32_t*)(st + OSB + 4 * ((kb >> 1) * BN + bcol + cl));
                 sbl[sl] = __half2float(__ushort_as_half((unsigned short)((kb & 1) ? v >> 16 : v & 0xffff)));
@@ -1187,45 +1237,64 @@ __global__ __launch_bounds__(256 * KG, 2 / KG) void k_gemm_q8d(const int8_t* __r
                     sb[sl][j] = __half2float(__ushort_as_half((unsigned short)((kb & 1) ? v >> 16 : v & 0xffff)));
                 }
             }
-#pragma unroll
-            for (int i = 0; i < TI; i++) {
+        };
+        auto load_afrag = [&](int sl, int kb, int i) {
+            if constexpr (WS4) {
                 if constexpr (OP) {
-                    sal[sl][i] = *(const float*)(st + OSA + 4 * (kb * BM + arow + 16 * i + fr));
+                    sal[sl][i] = *(const float*)(st + OSA + 16 * (arow + 16 * i + fr) + 4 * kb);
                 } else {
-                    const float4 v = *(const float4*)(st + OSA + 4 * (kb * BM + arow + 16 * i + fq));
-                    sa[sl][i][0] = v.x, sa[sl][i][1] = v.y, sa[sl][i][2] = v.z, sa[sl][i][3] = v.w;
-                }
-                if constexpr (PREOFF) {
-                    a[sl][i] = *(const long*)(st + offa[kb][i]);
-                } else {
-                    int off = (arow + 16 * i + fr) * BK + foff[kb];
-                    asm volatile("" : "+v"(off));
-                    a[sl][i] = *(const long*)(st + off);
-                }
-            }
 #pragma unroll
-            for (int j = 0; j < TJ; j++) {
-                if constexpr (PREOFF) {
-                    b[sl][j] = *(const long*)(st + offb[kb][j]);
-                } else {
-                    int off = OB + (bcol + 16 * j + fr) * BK + foff[kb];
-                    asm volatile("" : "+v"(off));
-                    b[sl][j] = *(const long*)(st + off);
+                    for (int r = 0; r < 4; r++)
+                        sa[sl][i][r] = *(const float*)(st + OSA + 16 * (arow + 16 * i + fq + r) + 4 * kb);
                 }
+            } else if constexpr (OP) {
+                sal[sl][i] = *(const float*)(st + OSA + 4 * (kb * BM + arow + 16 * i + fr));
+            } else {
+                const float4 v = *(const float4*)(st + OSA + 4 * (kb * BM + arow + 16 * i + fq));
+                sa[sl][i][0] = v.x, sa[sl][i][1] = v.y, sa[sl][i][2] = v.z, sa[sl][i][3] = v.w;
             }
+            if constexpr (PREOFF) {
+                a[sl][i] = *(const long*)(st + offa[kb][i]);
+            } else {
+                int off = (arow + 16 * i + fr) * BK + foff[kb];
+                asm volatile("" : "+v"(off));
+                a[sl][i] = *(const long*)(st + off);
+            }
+        };
+        auto load_bfrag = [&](int sl, int kb, int j) {
+            if constexpr (PREOFF) {
+                b[sl][j] = *(const long*)(st + offb[kb][j]);
+            } else {
+                int off = OB + (bcol + 16 * j + fr) * BK + foff[kb];
+                asm volatile("" : "+v"(off));
+                b[sl][j] = *(const long*)(st + off);
+            }
+        };
+        auto load_block = [&](int sl, int kb) {
+            load_bscale(sl, kb);
+#pragma unroll
+            for (int i = 0; i < TI; i++) load_afrag(sl, kb, i);
+#pragma unroll
+            for (int j = 0; j < TJ; j++) load_bfrag(sl, kb, j);
         };
         // MFMA q (block q / NF, fragment q % NF) is issued LAG MFMAs before its rescale, so the int32 result has
         // landed by the time the cvt/fma reach it and at most LAG+1 results are live
-        constexpr int LAG = 3, NQ = (KB / KG) * NF;
+        // (the 128×128 prefill tile runs LAG 2: one result ring slot fewer keeps it at ≤ 168 VGPRs, 3 waves per SIMD)
+        constexpr int LAG = (QASR_PIN != 0 && NF >= 16) ? 2 : 3, NQ = (KB / KG) * NF;
         constexpr int NPR = LAG / TJ + 2;   // outer-product results live at once (ring)
         const int kb0 = kg * (KB / KG);
         v4i c[LAG + 1];
         v16f prod[NPR];
+        // QASR_PIN (default): the instruction order is pinned per MFMA slot — [OP MFMA] MFMA q, the next block's
+        // fragment reads (at a block's first MFMA), then the 4 cvt + 4 fma of MFMA q − LAG — with sched_barrier(0)
+        // after each slot.  Left to itself the scheduler consumed every MFMA's result right behind it (an s_nop 7
+        // stall per MFMA, no MFMA ∥ VALU overlap inside a wave: profiles/r4_*), whatever the sched_group_barrier mix.
+        if constexpr (QASR_PIN != 0) load_block(0, kb0);
 #pragma unroll
         for (int q = 0; q < NQ + LAG; q++) {
             if (q < NQ) {
                 const int kb = q / NF, f = q % NF;
-                if (f == 0) load_block(kb, kb0 + kb);
+                if (QASR_PIN == 0 && f == 0) load_block(kb, kb0 + kb);
                 if constexpr (OP) {
                     if (f % TJ == 0) {
                         const v16f z = {};
@@ -1234,6 +1303,14 @@ __global__ __launch_bounds__(256 * KG, 2 / KG) void k_gemm_q8d(const int8_t* __r
                 }
                 c[q % (LAG + 1)] =
                     __builtin_amdgcn_mfma_i32_16x16x32_i8(a[kb][f / TJ], b[kb][f % TJ], v4i{0, 0, 0, 0}, 0, 0, 0);
+                if (QASR_PIN != 0 && kb + 1 < KB / KG) {
+                    // block kb+1's fragments replace block kb's as soon as their last MFMA has issued: row fragment i
+                    // after (i, TJ-1), column fragment j after (TI-1, j), the B scale after the block's last OP MFMA
+                    const int i = f / TJ, j = f % TJ;
+                    if (j == TJ - 1) load_afrag(kb + 1, kb0 + kb + 1, i);
+                    if (i == TI - 1) load_bfrag(kb + 1, kb0 + kb + 1, j);
+                    if (i == TI - 1 && j == 0) load_bscale(kb + 1, kb0 + kb + 1);
+                }
             }
             if (q >= LAG) {
                 const int p = q - LAG, kb = p / NF, f = p % NF, i = f / TJ, j = f % TJ;
@@ -1245,35 +1322,43 @@ __global__ __launch_bounds__(256 * KG, 2 / KG) void k_gemm_q8d(const int8_t* __r
                         acc[i][j][r] = fmaf((float)c[p % (LAG + 1)][r], sa[kb][i][r] * sb[kb][j], acc[i][j][r]);
                 }
             }
+            if constexpr (QASR_PIN != 0) __builtin_amdgcn_sched_barrier(0);
         }
+        if constexpr (QASR_PIN == 0) {
 #pragma unroll
-        for (int t = 0; t < NQ; t++) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-            __builtin_amdgcn_sched_group_barrier(0x002, OP ? 8 : 12, 0);
+            for (int t = 0; t < NQ; t++) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x002, OP ? 8 : 12, 0);
+            }
         }
     }
-    if constexpr (KG == 2) {
-        // group 1 hands its partial sums to group 0 through the (now idle) staging LDS
-        static_assert(4 * 64 * TI * TJ * 4 * 4 <= NBUF * STAGE, "k_gemm_q8d: reduction buffer");
+    if constexpr (KG > 1) {
+        // groups 1 … KG-1 hand their partial sums to group 0 through the (now idle) staging LDS; group 0 adds them in
+        // group order ((acc0 + acc1) + acc2) + acc3 — the same order in every launch
+        static_assert((KG - 1) * 4 * 64 * TI * TJ * 4 * 4 <= NBUF * STAGE, "k_gemm_q8d: reduction buffer");
         __syncthreads();
         float4* red = (float4*)smem + (size_t)lw * 64 * TI * TJ + lane;
-        if (kg == 1 && active) {
+        constexpr int GS = 4 * 64 * TI * TJ;   // float4s per group
+        if (kg > 0 && active) {
 #pragma unroll
             for (int i = 0; i < TI; i++)
 #pragma unroll
                 for (int j = 0; j < TJ; j++)
-                    red[(i * TJ + j) * 64] = make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+                    red[(size_t)(kg - 1) * GS + (i * TJ + j) * 64] =
+                        make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
         }
         __syncthreads();
-        if (kg == 1 && (TI * TJ > 4 || TJ != 4 || !fix_part)) return;
+        if (kg > 0 && (TI * TJ > 4 || TJ != 4 || !fix_part)) return;
         if (kg == 0 && active) {
 #pragma unroll
-            for (int i = 0; i < TI; i++)
+            for (int g = 1; g < KG; g++)
 #pragma unroll
-                for (int j = 0; j < TJ; j++) {
-                    const float4 v = red[(i * TJ + j) * 64];
-                    acc[i][j][0] += v.x, acc[i][j][1] += v.y, acc[i][j][2] += v.z, acc[i][j][3] += v.w;
-                }
+                for (int i = 0; i < TI; i++)
+#pragma unroll
+                    for (int j = 0; j < TJ; j++) {
+                        const float4 v = red[(size_t)(g - 1) * GS + (i * TJ + j) * 64];
+                        acc[i][j][0] += v.x, acc[i][j][1] += v.y, acc[i][j][2] += v.z, acc[i][j][3] += v.w;
+                    }
         }
     }
     // split-K fix-up (the 64-column wave tiles of ≤ 64×64 workgroup tiles — the SwiGLU-capable decode tiles; the
@@ -1281,12 +1366,12 @@ __global__ __launch_bounds__(256 * KG, 2 / KG) void k_gemm_q8d(const int8_t* __r
     if constexpr (TI * TJ <= 4 && TJ == 4) {
         if (fix_part && gridDim.z > 1) {
             if (!splitk_fixup<TI, TJ>(acc, kg == 0 && active, lw, 4, fix_part, fix_cnt, (int*)smem)) return;
-            if ((KG == 2 && kg != 0) || !active) return;
+            if ((KG > 1 && kg != 0) || !active) return;
             gemm_epilogue<TI, TJ, true>(acc, M, N, m0, n0, arow, bcol, fr, fq, bias, res, y, ldy, epi, yq, yd);
             return;
         }
     }
-    if ((KG == 2 && kg != 0) || !active) return;
+    if ((KG > 1 && kg != 0) || !active) return;
     gemm_epilogue<TI, TJ>(acc, M, N, m0, n0, arow, bcol, fr, fq, bias, res, y, ldy, epi, yq, yd);
 }
 
@@ -1597,12 +1682,25 @@ static void launch_gemm(dim3 grid, hipStream_t s, const int8_t* xq, const float*
                         float* yd) {
     k_gemm_q8<TI, TJ><<<grid, 256, 0, s>>>(xq, xd, M, W.qs, W.sc, W.N, W.K, bias, res, y, ldy, epi, sps, yq, yd);
 }
+// K-128 stages take their scales by 16-byte DMA (WS4) when the matrix carries the regrouped copy (Q8Mat::sc4)
+static bool g_ws4 = [] {
+    const char* e = getenv("QASR_STAGE_SCALES");
+    return !(e && atoi(e) == 0);
+}();
+void set_stage_scales(bool on) { g_ws4 = on; }
 template <int WM, int WN, int TI, int TJ, int NBUF = 3, int BK = 64, int KG = 1>
 static void launch_gemm_dma(dim3 grid, hipStream_t s, const int8_t* xq, const float* xd, int M, const Q8Mat& W,
                             const float* bias, const float* res, float* y, int ldy, int epi, int sps, int8_t* yq,
                             float* yd, float* fix_part, unsigned* fix_cnt) {
-    k_gemm_q8d<WM, WN, TI, TJ, NBUF, BK, KG><<<grid, 256 * KG, 0, s>>>(xq, xd, M, W.qs, W.sc, W.N, W.K, bias, res, y, ldy, epi, sps, yq,
-                                                    yd, fix_part, fix_cnt);
+    if constexpr (BK == 128) {
+        if (W.sc4 && g_ws4 && W.N % 2 == 0) {
+            k_gemm_q8d<WM, WN, TI, TJ, NBUF, BK, KG, true><<<grid, 256 * KG, 0, s>>>(
+                xq, xd, M, W.qs, W.sc, W.sc4, W.N, W.K, bias, res, y, ldy, epi, sps, yq, yd, fix_part, fix_cnt);
+            return;
+        }
+    }
+    k_gemm_q8d<WM, WN, TI, TJ, NBUF, BK, KG><<<grid, 256 * KG, 0, s>>>(xq, xd, M, W.qs, W.sc, nullptr, W.N, W.K, bias,
+                                                                      res, y, ldy, epi, sps, yq, yd, fix_part, fix_cnt);
 }
 
 // GEMM configurations: 0..3 register-staged kernel (any K % 32 == 0), 4..11 LDS-DMA kernel, 2×2 waves, stages of
@@ -1621,6 +1719,12 @@ static const GemmCfg kGemmCfgs[] = {
     // 24..30 decode kernel k_gemm_q8_ks<TI, TJ, NW>: full K per workgroup, K split over NW waves
     {32, 16, 0, false, 16}, {32, 32, 0, false, 16}, {64, 16, 0, false, 16}, {64, 32, 0, false, 8},
     {16, 64, 0, false, 16}, {32, 64, 0, false, 8}, {64, 64, 0, false, 8},
+    {0, 0, 0, false},   // 31: reserved (the ops' "auto" code)
+    // round 4, K-128 stages: 32..35 four K groups (16 waves: 4 per SIMD) — 64×64 2×2 / 4×1 (64-column wave tiles:
+    // SwiGLU, fix-up) with rings of 3 / 6; 36..37 one K group, ring 6 — 64×32, 32×64 (256 tiles of N 2,048 at 256
+    // rows); 38..39 two K groups — 128×64 4×1, 128×128 2×2
+    {64, 64, 128, true}, {64, 64, 128, true}, {64, 64, 128, true}, {64, 64, 128, true},      // 32..35
+    {64, 32, 128, true}, {32, 64, 128, true}, {128, 64, 128, true}, {128, 128, 128, true},   // 36..39
 };
 constexpr int kNumGemmCfgs = sizeof(kGemmCfgs) / sizeof(kGemmCfgs[0]);
 
@@ -1674,7 +1778,15 @@ static void launch_cfg(int cfg, dim3 grid, hipStream_t s, const int8_t* xq, cons
         case 20: launch_gemm_dma<4, 1, 1, 4, 6, 128, 2>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd, fp, fc); break;
         case 21: launch_gemm_dma<2, 2, 2, 2, 6, 128>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd, fp, fc); break;
         case 22: launch_gemm_dma<4, 1, 1, 4, 6, 128>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd, fp, fc); break;
-        default: launch_gemm_dma<2, 2, 1, 4, 4, 128>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd, fp, fc); break;
+        case 23: launch_gemm_dma<2, 2, 1, 4, 4, 128>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd, fp, fc); break;
+        case 32: launch_gemm_dma<2, 2, 2, 2, 3, 128, 4>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd, fp, fc); break;
+        case 33: launch_gemm_dma<4, 1, 1, 4, 3, 128, 4>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd, fp, fc); break;
+        case 34: launch_gemm_dma<2, 2, 2, 2, 6, 128, 4>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd, fp, fc); break;
+        case 35: launch_gemm_dma<4, 1, 1, 4, 6, 128, 4>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd, fp, fc); break;
+        case 36: launch_gemm_dma<2, 2, 2, 1, 6, 128>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd, fp, fc); break;
+        case 37: launch_gemm_dma<2, 2, 1, 2, 6, 128>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd, fp, fc); break;
+        case 38: launch_gemm_dma<4, 1, 2, 4, 3, 128, 2>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd, fp, fc); break;
+        default: launch_gemm_dma<2, 2, 4, 4, 2, 128, 2>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd, fp, fc); break;
     }
 }
 
@@ -2024,6 +2136,7 @@ void gemm_q8(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const flo
         return;
     auto usable = [&](int c) {
         const GemmCfg& g = kGemmCfgs[c];
+        if (g.bm == 0) return false;   // reserved slot
         if (g.ks) return W.K % (QK * 4 * g.ks) == 0 && (epi != EPI_GELU_Q8 || g.bn % 32 == 0);
         return !g.dma || W.K % g.bk == 0;
     };
@@ -2071,7 +2184,8 @@ void gemm_q8(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const flo
     const int tiles = cdiv(W.N, cf.bn) * cdiv(M, cf.bm);
     // split-K through the fix-up workspace (any epilogue, deterministic): a forced / table split count of a DMA tile
     auto fixup_ok = [&](int sp) {
-        const bool wave64 = pick == 12 || pick == 15 || pick == 20 || pick == 22 || pick == 23;   // TJ = 4 tiles
+        const bool wave64 = pick == 12 || pick == 15 || pick == 20 || pick == 22 || pick == 23 || pick == 33 ||
+                            pick == 35;   // TJ = 4 tiles
         return cf.dma && wave64 && sp > 1 && g_fix_part && tiles <= g_fix_ncnt &&
                (size_t)tiles * sp * cf.bm * cf.bn <= g_fix_floats;
     };
@@ -2085,14 +2199,16 @@ void gemm_q8(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const flo
         dim3 grid(cdiv(W.N, cf.bn), cdiv(M, cf.bm), cdiv(steps, sps));
         if (epi == EPI_SWIGLU)
             QASR_CHECK(W.N % 64 == 0 && yq && yd && (cf.bn == 128 || pick == 12 || pick == 13 || pick == 15 ||
-                                                     pick == 20 || pick == 22),
+                                                     pick == 20 || pick == 22 || pick == 33 || pick == 35 ||
+                                                     pick == 38),
                        QASR_E_INVALID, "gemm_q8: SwiGLU epilogue needs a 64-column wave tile");
         launch_cfg(pick, grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd, g_fix_part, g_fix_cnt);
         return;
     }
     if (epi == EPI_SWIGLU) {
         QASR_CHECK(W.N % 64 == 0 && yq && yd, QASR_E_INVALID, "gemm_q8: SwiGLU epilogue needs N % 64 == 0");
-        QASR_CHECK(cf.bn == 128 || pick == 12 || pick == 13 || pick == 15 || pick == 20 || pick == 22, QASR_E_INVALID,
+        QASR_CHECK(cf.bn == 128 || pick == 12 || pick == 13 || pick == 15 || pick == 20 || pick == 22 || pick == 33 ||
+                       pick == 35 || pick == 38, QASR_E_INVALID,
                    "gemm_q8: SwiGLU epilogue needs a 64-column wave tile");
         dim3 grid(cdiv(W.N, cf.bn), cdiv(M, cf.bm), 1);
         launch_cfg(pick, grid, s, xq, xd, M, W, bias, res, y, ldy, epi, steps, yq, yd);
@@ -2137,6 +2253,22 @@ void interleave_gate_up(Q8Mat& W, hipStream_t s) {
     QASR_HIP(hipStreamSynchronize(s));
     QASR_HIP(hipFree(q2));
     QASR_HIP(hipFree(s2));
+}
+
+// out[(b/4)·N·4 + 4n + b%4] = sc[n·nb + b]: a K-128 stage's 4 block scales of column n are 8 contiguous bytes and
+// the stage's columns n0… one contiguous run (the 16-byte DMA of k_gemm_q8d<…, WS4>)
+__global__ void k_stage_scales(const __half* __restrict__ sc, int N, int nb, __half* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;   // output index
+    if (i >= (int64_t)N * nb) return;
+    const int64_t g = i / ((int64_t)N * 4), r = i % ((int64_t)N * 4);
+    const int64_t n = r / 4, b = 4 * g + r % 4;
+    out[i] = sc[n * nb + b];
+}
+
+void q8_stage_scales(const __half* sc, int N, int K, __half* out, hipStream_t s) {
+    QASR_CHECK(K % 128 == 0 && N > 0, QASR_E_INVALID, "q8_stage_scales: K % 128 != 0");
+    const int64_t n = (int64_t)N * (K / QK);
+    k_stage_scales<<<(unsigned)cdiv(n, 256), 256, 0, s>>>(sc, N, K / QK, out);
 }
 
 void linear_q8(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const float* bias, const float* res,

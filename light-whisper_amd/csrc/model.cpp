@@ -709,6 +709,32 @@ void set_precision(Model& m, const std::string& mode) {
     m.precision_gen++;
 }
 
+void ensure_stage_scales(Model& m) {
+    std::lock_guard<std::mutex> lk(m.s4_mu);
+    if (m.s4_mem) return;
+    auto each = [&](auto f) {
+        for (auto& L : m.dec) f(L.qkv), f(L.o), f(L.gu), f(L.down);
+        f(m.lm_head);
+    };
+    auto ok = [](const Q8Mat& w) { return w.qs && w.K % 128 == 0 && w.N % 2 == 0; };
+    DevAlloc probe;
+    probe.counting = true;
+    each([&](Q8Mat& w) {
+        if (ok(w)) probe.alloc((size_t)w.N * (w.K / QK) * sizeof(__half));
+    });
+    auto mem = std::make_unique<DevAlloc>();
+    mem->reserve(std::max<size_t>(probe.bytes, 256));
+    hipStream_t s = nullptr;
+    each([&](Q8Mat& w) {
+        if (!ok(w)) return;
+        __half* o = (__half*)mem->alloc((size_t)w.N * (w.K / QK) * sizeof(__half));
+        q8_stage_scales(w.sc, w.N, w.K, o, s);
+        w.sc4 = o;
+    });
+    QASR_HIP(hipStreamSynchronize(s));
+    m.s4_mem = std::move(mem);
+}
+
 // ----------------------------------------------------------------------------------------------- export
 void export_tensor(const Model& m, const std::string& name, void* dst, size_t cap, size_t* written) {
     auto it = m.slots.find(name);

@@ -7,6 +7,7 @@
 #pragma once
 #include <map>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -82,6 +83,9 @@ struct Model {
     // bumped by every precision change: sessions' captured decode graphs hold the GEMM weight pointers of the
     // precision they were captured in, so a change invalidates them (engine.cpp run_batch)
     uint64_t precision_gen = 0;
+    // the decoder matrices' regrouped stage scales (Q8Mat::sc4), derived once the weights are in place
+    std::unique_ptr<DevAlloc> s4_mem;
+    std::mutex s4_mu;
 
     int audio_F3() const { return (((hp.n_mels + 1) / 2 + 1) / 2 + 1) / 2; }
     int64_t weight_bytes() const { return (int64_t)mem.bytes; }
@@ -97,5 +101,8 @@ void export_tensor(const Model& m, const std::string& name, void* dst, size_t ca
 // "q8" (default: the reference's W8A8 arithmetic) or "mxfp8" (block-scaled fp8 GEMMs; tolerance parity only).
 // Open sessions re-capture their decode graphs on their next run (precision_gen).
 void set_precision(Model& m, const std::string& mode);
+// derive Q8Mat::sc4 for the decoder layers' matrices and the vocabulary projection (K % 128 == 0), once; called
+// when a session opens (the weights are final then: loaded, generated or received by broadcast, gate|up interleaved)
+void ensure_stage_scales(Model& m);
 
 }  // namespace qasr

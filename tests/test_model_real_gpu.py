@@ -244,6 +244,49 @@ def test_real_batch_equals_single_and_oracle(pair):
     assert div >= min(6, n)
 
 
+def test_real_batch_c4_scale(pair):
+    """C4 at scale (1.7B, 64 segments of U[2,12] s like bench.py, 8 forced tokens per audio-second: up to 97 tokens,
+    EOS ignored): the batch's token streams against the 64 single runs, and the two shortest segments against the
+    oracle.  The mismatch count and every first divergence are recorded ($QASR_PARITY_LOG); a divergence is allowed
+    only at a near-tie (0.5 % of the row's range) of the single run's teacher-forced logits (batch vs single) or of
+    the oracle's logits (batch vs oracle)."""
+    arch, _, s, o = pair
+    if arch != "qwen3-asr-1.7b":
+        pytest.skip("C4 is quoted on the 1.7B model")
+    rng = np.random.default_rng(11)
+    secs = rng.uniform(2.0, 12.0, size=64)
+    clips = [clip(float(x), 500 + i) for i, x in enumerate(secs)]
+    batch = [r.tokens for r in s.run_batch(clips, force_tokens_per_s=8)]
+    singles = [s.run(c, force_tokens_per_s=8).tokens for c in clips]
+    for i, c in enumerate(clips):
+        n_want = int(round(8 * c.size / 16000.0)) + 1
+        assert len(batch[i]) == n_want and len(singles[i]) == n_want, (i, len(batch[i]), len(singles[i]), n_want)
+    divs = {}
+    for i in range(64):
+        a, b = batch[i], singles[i]
+        d = next((j for j in range(len(a)) if a[j] != b[j]), None)
+        if d is None:
+            continue
+        divs[i] = d
+        lg = s.forced_logits(clips[i], np.asarray(b[:d], np.int32))   # row d: the single path's logits at the split
+        assert _near_tie(lg[d]), f"segment {i}: batch/single diverge at token {d} of {len(a)} without a near-tie"
+    # the oracle on the two shortest segments (forced length, EOS ignored, as the batch)
+    oracle_divs = []
+    for i in np.argsort(secs)[:2]:
+        ids, remb = _prompt_embeds(o, clips[i])
+        n_new = len(batch[i])
+        ref, lg = oracle.KV(o, len(ids) + n_new + 8).generate(ids, SP["tok_audio_pad"], remb, eos=(), max_new=n_new,
+                                                              force_len=n_new, want_logits=True)
+        d = next((j for j in range(n_new) if batch[i][j] != ref[j]), n_new)
+        oracle_divs.append((int(i), d, n_new))
+        if d < n_new:
+            assert _near_tie(lg[d]), f"segment {i}: batch/oracle diverge at token {d} without a near-tie"
+        assert d >= min(8, n_new), (i, d)
+    record(f"real_batch_c4[{arch}]", segments=64, tokens=int(sum(len(b) for b in batch)),
+           batch_vs_single_mismatched_segments=len(divs), first_divergences=sorted(divs.items()),
+           oracle_first_divergence=oracle_divs)
+
+
 def test_real_mxfp8_against_q8(pair):
     """1.7B MXFP8 precision mode (C5; tolerance parity only) against the Q8 path on teacher-forced logits"""
     from qasr.transcribe_cpp import Model

@@ -101,7 +101,9 @@ def test_repack_q8(torch_dev):
     assert np.array_equal(host(sc).view(np.uint16), rs)
 
 
-def _linear_case(torch_dev, m, n, k, path, epi, seed=0, exact=False):
+def _linear_case(torch_dev, m, n, k, path, epi, seed=0, exact=False, s4=False):
+    """s4: register the regrouped stage scales (Q8Mat::sc4) of the weight matrix for this call, so the K-128 tiles
+    stage their scales by 16-byte DMA (kernels_q8.hip k_gemm_q8d WS4)"""
     import torch
 
     rng = np.random.default_rng(seed)
@@ -133,9 +135,19 @@ def _linear_case(torch_dev, m, n, k, path, epi, seed=0, exact=False):
     wq, ws = dev(qs, torch_dev), dev(sc, torch_dev)
     bt = dev(bias, torch_dev) if bias is not None else None
     y = dev(res, torch_dev) if epi == 1 else empty((m, n), torch.float32, torch_dev)
-    _lib.check(L().qasr_op_linear_q8(ptr(xq), ptr(xdd), m, ptr(wq), ptr(ws), n, k, ptr(bt),
-                                     ptr(y) if epi == 1 else None, ptr(y), n, epi, path, None))
-    return host(y), ref.astype(np.float32)
+    s4t = None
+    if s4:
+        s4t = empty((n, k // 32), torch.float16, torch_dev)
+        _lib.check(L().qasr_op_stage_scales(ptr(ws), n, k, ptr(s4t), None))
+        _lib.check(L().qasr_op_register_stage_scales(ptr(ws), ptr(s4t)))
+    try:
+        _lib.check(L().qasr_op_linear_q8(ptr(xq), ptr(xdd), m, ptr(wq), ptr(ws), n, k, ptr(bt),
+                                         ptr(y) if epi == 1 else None, ptr(y), n, epi, path, None))
+        out = host(y)
+    finally:
+        if s4:
+            _lib.check(L().qasr_op_register_stage_scales(ptr(ws), None))
+    return out, ref.astype(np.float32)
 
 
 # path: 1 GEMV, 2 auto, 16 + cfg (+ 32·splits) forces a GEMM configuration (kernels_q8.hip kGemmCfgs: 0..3 register-
@@ -245,10 +257,12 @@ def _il16(f):
     return np.where(r < f, 32 * (r // 16) + r % 16, 32 * ((r - f) // 16) + 16 + (r - f) % 16)
 
 
-@pytest.mark.parametrize("cfg", [-1, 1, 4, 5, 8, 9, 12, 13, 15, 20, 22, 23, 28, 29, 30])
+@pytest.mark.parametrize("cfg,s4", [(c, False) for c in (-1, 1, 4, 5, 8, 9, 12, 13, 15, 20, 22, 23, 28, 29, 30)] +
+                         [(4096 + c, True) for c in (8, 12, 15, 23, 33, 35, 38, 39)])
 @pytest.mark.parametrize("m,f,k", [(3, 256, 512), (40, 512, 1024), (300, 1024, 512), (70, 512, 2048)])
-def test_gemm_swiglu_q8(torch_dev, m, f, k, cfg):
-    """fused gate-up GEMM + SwiGLU + Q8 epilogue vs the oracle's linear_q8 of gate and up"""
+def test_gemm_swiglu_q8(torch_dev, m, f, k, cfg, s4=False):
+    """fused gate-up GEMM + SwiGLU + Q8 epilogue vs the oracle's linear_q8 of gate and up (s4: the K-128 tiles with
+    the regrouped stage scales, including the 16-wave and 128-row decode tiles of round 4)"""
     import torch
 
     rng = np.random.default_rng(m + f)
@@ -269,8 +283,18 @@ def test_gemm_swiglu_q8(torch_dev, m, f, k, cfg):
     _lib.check(L().qasr_op_quant_rows(ptr(xt), m, k, k, ptr(xq), ptr(xdd), None))
     hq = empty((m, f), torch.int8, torch_dev)
     hd = empty((m, f // 32), torch.float32, torch_dev)
-    _lib.check(L().qasr_op_gemm_swiglu_q8_cfg(ptr(xq), ptr(xdd), m, ptr(wq), ptr(ws), 2 * f, k, ptr(hq), ptr(hd), cfg,
-                                              None))
+    s4t = None
+    if s4:
+        s4t = empty((2 * f, k // 32), torch.float16, torch_dev)
+        _lib.check(L().qasr_op_stage_scales(ptr(ws), 2 * f, k, ptr(s4t), None))
+        _lib.check(L().qasr_op_register_stage_scales(ptr(ws), ptr(s4t)))
+    try:
+        _lib.check(L().qasr_op_gemm_swiglu_q8_cfg(ptr(xq), ptr(xdd), m, ptr(wq), ptr(ws), 2 * f, k, ptr(hq), ptr(hd),
+                                                  cfg, None))
+        torch.cuda.synchronize()
+    finally:
+        if s4:
+            _lib.check(L().qasr_op_register_stage_scales(ptr(ws), None))
     assert np.allclose(host(hd), dr, rtol=2e-3)
     assert (np.abs(host(hq).astype(int) - qr) <= 1).all()
     # the unfused path (GEMV rows) on the interleaved layout
@@ -768,6 +792,30 @@ def test_linear_q8_fixup_vs_oracle(torch_dev, fixup, path, epi, m, n, k):
     for _ in range(2):
         y2, _ = _linear_case(torch_dev, m, n, k, path, epi, seed=k + epi)
         assert np.array_equal(y, y2)
+    assert not host(fixup).any()
+
+
+# round 4: K-128 tiles with the stage scales by 16-byte DMA (WS4), the 16-wave tiles (four K groups; their A and B
+# DMA pieces as one list) and the one-group deep-ring 64×32 / 32×64 tiles; 4096 + cfg + 256·splits
+S4_PATHS = [4096 + c + 256 * sp for c, sp in [(8, 1), (10, 1), (12, 1), (14, 1), (15, 1), (16, 1), (17, 1), (18, 1),
+                                              (23, 1), (32, 1), (33, 1), (34, 1), (35, 1), (36, 1), (37, 1), (38, 1),
+                                              (39, 1), (12, 3), (15, 4), (33, 2), (35, 4)]]
+
+
+@pytest.mark.parametrize("path", S4_PATHS)
+@pytest.mark.parametrize("m,n,k", [(64, 128, 1024), (100, 192, 512), (37, 320, 2048), (256, 256, 6144),
+                                   (130, 1024, 1024), (256, 4096, 2048)])
+def test_linear_q8_stage_scales(torch_dev, fixup, path, m, n, k):
+    """exact integers through every new staging path, then real scales: the 16-byte scale DMA gives the bits of the
+    4-byte gathers (same configuration), within the oracle bound; split counts through the fix-up"""
+    y, ref = _linear_case(torch_dev, m, n, k, path, 0, seed=m + n, exact=True, s4=True)
+    assert np.array_equal(y, ref)
+    for epi in (0, 1):
+        y4, ref = _linear_case(torch_dev, m, n, k, path, epi, seed=k + epi + 3, s4=True)
+        y0, _ = _linear_case(torch_dev, m, n, k, path, epi, seed=k + epi + 3, s4=False)
+        assert np.array_equal(y4, y0)
+        scale = np.abs(ref).max() + 1e-6
+        assert np.abs(y4 - ref).max() <= 2e-5 * scale * np.sqrt(k / 256)
     assert not host(fixup).any()
 
 
