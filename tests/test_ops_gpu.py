@@ -258,9 +258,10 @@ def _il16(f):
 
 
 @pytest.mark.parametrize("cfg,s4", [(c, False) for c in (-1, 1, 4, 5, 8, 9, 12, 13, 15, 20, 22, 23, 28, 29, 30)] +
-                         [(4096 + c, True) for c in (8, 12, 15, 23, 33, 35, 38, 39)])
+                         [(4096 + c, True) for c in (8, 12, 15, 23, 33, 35, 38, 39, 40, 41, 42, 43, 44, 45, 46, 47,
+                                                     48)])
 @pytest.mark.parametrize("m,f,k", [(3, 256, 512), (40, 512, 1024), (300, 1024, 512), (70, 512, 2048)])
-def test_gemm_swiglu_q8(torch_dev, m, f, k, cfg, s4=False):
+def test_gemm_swiglu_q8(torch_dev, m, f, k, cfg, s4):
     """fused gate-up GEMM + SwiGLU + Q8 epilogue vs the oracle's linear_q8 of gate and up (s4: the K-128 tiles with
     the regrouped stage scales, including the 16-wave and 128-row decode tiles of round 4)"""
     import torch
@@ -440,7 +441,8 @@ def test_gemv_exact_rows(torch_dev, pro, n, k, epi):
             assert np.array_equal(host(y)[0], single[r][0]), r
 
 
-GEMM_CHAIN_CFGS = [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 16, 17, 18, 21, 22, 23]
+GEMM_CHAIN_CFGS = [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 16, 17, 18, 21, 22, 23,
+                   40, 41, 42, 46, 47]   # 40..: the 32×32×32 kernel (k_q8mm), one K group: the same chain
 
 
 @pytest.mark.parametrize("m,n,k,epi", [(13, 1024, 1024, 0), (104, 3072, 1024, 0), (160, 1024, 4096, 1),
@@ -457,8 +459,9 @@ def test_gemm_chain_configs_bit_identical(torch_dev, m, n, k, epi):
 
     def run(cfg, rows=m):
         y = res[:rows].clone()
+        path = 16 + cfg + 32 if cfg < 31 else 4096 + cfg + 256
         _lib.check(L().qasr_op_linear_q8(ptr(xq), ptr(xd), rows, ptr(wq), ptr(ws), n, k, None, ptr(y), ptr(y), n,
-                                         epi, 16 + cfg + 32, None))
+                                         epi, path, None))
         return host(y)
 
     want = run(10)
@@ -799,7 +802,8 @@ def test_linear_q8_fixup_vs_oracle(torch_dev, fixup, path, epi, m, n, k):
 # DMA pieces as one list) and the one-group deep-ring 64×32 / 32×64 tiles; 4096 + cfg + 256·splits
 S4_PATHS = [4096 + c + 256 * sp for c, sp in [(8, 1), (10, 1), (12, 1), (14, 1), (15, 1), (16, 1), (17, 1), (18, 1),
                                               (23, 1), (32, 1), (33, 1), (34, 1), (35, 1), (36, 1), (37, 1), (38, 1),
-                                              (39, 1), (12, 3), (15, 4), (33, 2), (35, 4)]]
+                                              (39, 1), (12, 3), (15, 4), (33, 2), (35, 4)] +
+            [(c, 1) for c in range(40, 49)]]   # the 32×32×32 kernel
 
 
 @pytest.mark.parametrize("path", S4_PATHS)
@@ -854,7 +858,7 @@ def test_linear_q8_fixup_repeat_stress(torch_dev, fixup, path, m, n, k):
 @pytest.mark.parametrize("m,f,k", [(40, 512, 1024), (70, 512, 2048), (256, 1024, 2048)])
 def test_gemm_swiglu_q8_fixup(torch_dev, fixup, m, f, k, cfg):
     """split-K gate-up GEMM: the SwiGLU + Q8 epilogue runs once per tile on the summed partials"""
-    test_gemm_swiglu_q8(torch_dev, m, f, k, cfg)
+    test_gemm_swiglu_q8(torch_dev, m, f, k, cfg, False)
     assert not host(fixup).any()
 
 
@@ -908,7 +912,7 @@ def test_linear_q8_weight_stream(torch_dev, ws_all, m, n, k, epi):
 @pytest.mark.parametrize("f,k", [(6144, 2048), (3072, 1024), (512, 1024)])
 def test_gemm_swiglu_q8_weight_stream(torch_dev, ws_all, m, f, k):
     """the weight-streaming kernel's SwiGLU + Q8 epilogue (four 16-column groups = one 32-wide h block)"""
-    test_gemm_swiglu_q8(torch_dev, m, f, k, -1)
+    test_gemm_swiglu_q8(torch_dev, m, f, k, -1, False)
 
 
 def test_linear_q8_weight_stream_vs_gemm(torch_dev):

@@ -23,7 +23,7 @@ SHAPES = [  # (tag, M, N, K, epi)
 ]
 
 
-# 2 = auto; 16 + cfg (+ 32·splits): kernels_q8.hip kGemmCfgs — 0..3 register-staged {128², 64×128, 64², 32×64},
+# 2 = auto; 16 + cfg (+ 32·splits), or 4096 + cfg (+ 256·splits) for any index: kernels_q8.hip kGemmCfgs — 0..3 register-staged {128², 64×128, 64², 32×64},
 # 4..7 LDS-DMA K-64 stages {128², 64×128, 64², 128×64}, 8..11 LDS-DMA K-128 stages (same tiles)
 PATHS = [int(p) for p in os.environ.get("PATHS", "2,20,21,22,24,25,26,27").split(",")]
 
@@ -40,6 +40,11 @@ def main():
         xd = torch.rand(M, K // 32, device=dev) * 0.01
         wq = torch.randint(-127, 128, (N, K), dtype=torch.int8, device=dev)
         ws = (torch.rand(N, K // 32, device=dev) * 0.01).half()
+        s4 = None
+        if os.environ.get("S4", "0") == "1" and K % 128 == 0:   # the regrouped stage scales (Q8Mat::sc4)
+            s4 = torch.empty_like(ws)
+            _lib.check(lib.qasr_op_stage_scales(ws.data_ptr(), N, K, s4.data_ptr(), None))
+            _lib.check(lib.qasr_op_register_stage_scales(ws.data_ptr(), s4.data_ptr()))
         y = torch.zeros(M, N, device=dev)
         res = y if epi == 1 else None
         hq = torch.empty(M, N // 2, dtype=torch.int8, device=dev)
@@ -51,7 +56,8 @@ def main():
                 if epi == 3:   # fused SwiGLU + Q8 epilogue; path → forced config
                     _lib.check(lib.qasr_op_gemm_swiglu_q8_cfg(xq.data_ptr(), xd.data_ptr(), M, wq.data_ptr(),
                                                               ws.data_ptr(), N, K, hq.data_ptr(), hd.data_ptr(),
-                                                              -1 if path == 2 else (path - 16) % 32, None))
+                                                              -1 if path == 2 else path if path >= 4096 else
+                                                              (path - 16) % 32, None))
                     return
                 _lib.check(lib.qasr_op_linear_q8(xq.data_ptr(), xd.data_ptr(), M, wq.data_ptr(), ws.data_ptr(), N,
                                                  K, None, res.data_ptr() if res is not None else None,
@@ -72,6 +78,8 @@ def main():
             us = e0.elapsed_time(e1) / iters * 1e3
             out.append(f"{path}:{us:8.1f}us {flops / us / 1e6:6.0f}TF")
         print(f"{tag:14s} M={M:6d} N={N:6d} K={K:5d} | " + " ".join(out), flush=True)
+        if s4 is not None:
+            _lib.check(lib.qasr_op_register_stage_scales(ws.data_ptr(), None))
 
 
 if __name__ == "__main__":
