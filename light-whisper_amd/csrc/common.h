@@ -10,6 +10,14 @@
 
 #include "../../include/qasr.h"
 
+// QASR_FORMAL_HANDOFF=1 (A/B builds): the split-K fix-up and the split decode attention publish their partials with a
+// release on the arrival add and read them after an agent-scope acquire fence (the formal C++ memory-model form),
+// instead of the measured write-through form (sc1 stores, vmcnt(0), relaxed add, sc1 loads: MI355X_MICROARCH.md,
+// inter-workgroup visibility, valid forms table row 1)
+#ifndef QASR_FORMAL_HANDOFF
+#define QASR_FORMAL_HANDOFF 0
+#endif
+
 namespace qasr {
 
 // ------------------------------------------------------------------------------------------------ errors

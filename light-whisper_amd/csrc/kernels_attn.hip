@@ -462,9 +462,12 @@ __global__ __launch_bounds__(256) void k_attention(const __half* __restrict__ Q,
         // with an agent-scope add; the piece whose add comes last reads every state with sc1 loads
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         int prev = 0;
-        if (lane == 0) prev = __hip_atomic_fetch_add(fz.cnt + gw, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (lane == 0)
+            prev = __hip_atomic_fetch_add(fz.cnt + gw, 1, QASR_FORMAL_HANDOFF ? __ATOMIC_RELEASE : __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT);
         prev = __builtin_amdgcn_readfirstlane(prev);
         if (prev != S - 1) return;
+        if constexpr (QASR_FORMAL_HANDOFF) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         if (lane == 0) __hip_atomic_store(fz.cnt + gw, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // next launch
     }
 #pragma unroll

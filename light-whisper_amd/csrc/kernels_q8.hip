@@ -798,8 +798,10 @@ __device__ __forceinline__ bool splitk_fixup(float (&acc)[TI][TJ][4], bool has, 
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
-        const unsigned prev = __hip_atomic_fetch_add(cnt + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned prev = __hip_atomic_fetch_add(cnt + tile, 1u, QASR_FORMAL_HANDOFF ? __ATOMIC_RELEASE : __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT);
         const int last = prev == (unsigned)(S - 1);
+        if (QASR_FORMAL_HANDOFF && last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         if (last) __hip_atomic_store(cnt + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // next launch
         *flag = last;
     }
