@@ -1592,6 +1592,9 @@ __global__ __launch_bounds__(64 * WM * WN * KG) void k_q8mm(const int8_t* __rest
             }
             const v16i z16 = {};
             c[q & 1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[bb & 1], b[bb & 1][j], z16, 0, 0, 0);
+            // the MFMA issues first: left free inside the slot the scheduler put it behind the slot's VALU, so the
+            // next slot's rescale consumed it right away (s_nop 9 per MFMA)
+            __builtin_amdgcn_sched_barrier(0);
             if (j == TN - 1 && bb + 1 < KBG) load((bb + 1) & 1, bb + 1);
             if (q > 0) rescale(q - 1);
             __builtin_amdgcn_sched_barrier(0);
@@ -1927,6 +1930,9 @@ static bool gemm_q8_ws(const int8_t* xq, const float* xd, int M, const Q8Mat& W,
     // straight from L2, so the kernel wins only while they are few — at ≤ 16 rows on the wide decoder matrices (QKV
     // 9.2 → 5.6 µs at 8 rows, gate/up 16.2 → 12.3 µs), not on the 2,048-wide projections or the vocabulary
     if (ks_force <= 0 && !g_ws_all && !(epi == EPI_SWIGLU || (W.N >= 4096 && W.N < 32768))) return false;
+    // round 4: with the pinned LDS-DMA tile the SwiGLU shape at 9–16 rows is faster on the table's cfg 12 / 4 splits
+    // (11.8 against 14.3 µs at 16 rows, profiles/r4b_sweep.log)
+    if (ks_force <= 0 && !g_ws_all && epi == EPI_SWIGLU && M > 8) return false;
     const int TI = (M + 15) / 16, U = TI >= 3 ? 2 : 4;
     const bool swi = epi == EPI_SWIGLU;
     // K split over waves: fill ≈ 1,024 waves (4 per CU) — 16-column groups × KS (SwiGLU: 4 groups, ≤ 8 waves: 16
@@ -2369,10 +2375,10 @@ static const DecPick kDecGu[] = {{16, 15, 2}, {32, 23, 2}};
 // unsplit (one-K-group, two-K-group or K-over-waves tiles); the winners of tools/dec_gemm_sweep.py run in that mode
 // (profiles/r3a_dec_sweep_det.log, cold weights, every configuration × split).  Used when the fix-up workspace is
 // registered (the session's decode steps), else the heuristic below.
-static const DecPick kDetQkv[] = {{64, 15, 4}, {96, 15, 4}, {128, 15, 2}, {192, 12, 4}, {224, 12, 3}, {256, 14, 1}};
-static const DecPick kDetO[] = {{16, 24, 0}, {32, 22, 6}, {96, 15, 4}, {128, 16, 1}, {192, 12, 6}, {224, 12, 4},
-                                {256, 12, 3}};
-static const DecPick kDetDown[] = {{64, 15, 8}, {128, 15, 4}, {192, 12, 8}, {256, 12, 4}};
+// round 4 (pinned slot schedule + 16-byte stage scales): profiles/r4b_sweep*, r4c_sweep* (cold weights)
+static const DecPick kDetQkv[] = {{192, 12, 4}, {256, 12, 3}};
+static const DecPick kDetO[] = {{16, 24, 0}, {64, 12, 4}, {128, 16, 1}, {192, 12, 4}, {256, 12, 3}};
+static const DecPick kDetDown[] = {{192, 12, 8}, {256, 12, 4}};
 static const DecPick kDetGu[] = {{64, 12, 4}, {128, 12, 2}, {256, 12, 1}};
 
 static bool dec_table_pick(int M, const Q8Mat& W, int epi, int& cfg, int& splits) {
