@@ -324,13 +324,31 @@ struct Server {
         return r;
     }
 
-    void warmup() {  // qwen3_asr_server.py:135-150 (1 s of quiet noise through VAD and ASR)
-        std::vector<float> z(16000, 0.f), noise(16000);
+    // the reference's warm-up signal, default_rng(0).standard_normal(16000)·0.002 as f32 (qwen3_asr_server.py:139-140),
+    // precomputed by tools/gen_warmup_noise.py into assets/ beside the VAD weights; an LCG stand-in if it is absent
+    // (the warm-up's output is discarded either way)
+    static std::vector<float> warmup_noise() {
+        std::vector<float> noise(16000);
+        char exe[4096] = {0};
+        const ssize_t n = readlink("/proc/self/exe", exe, sizeof exe - 1);
+        std::string dir = n > 0 ? std::string(exe, (size_t)n) : std::string();
+        dir = dir.substr(0, dir.find_last_of('/') + 1);
+        if (FILE* f = fopen((dir + "../assets/warmup_noise.f32").c_str(), "rb")) {
+            const size_t got = fread(noise.data(), sizeof(float), noise.size(), f);
+            fclose(f);
+            if (got == noise.size()) return noise;
+        }
         uint64_t s = 0x9E3779B97F4A7C15ull;
         for (auto& v : noise) {
             s = s * 6364136223846793005ull + 1442695040888963407ull;
             v = 0.002f * ((float)(s >> 40) / 16777216.0f * 2.f - 1.f);
         }
+        return noise;
+    }
+
+    void warmup() {  // qwen3_asr_server.py:135-150 (1 s of quiet noise through VAD and ASR)
+        std::vector<float> z(16000, 0.f);
+        const std::vector<float> noise = warmup_noise();
         size_t nf = 0;
         std::vector<float> probs(200);
         qasr_vad_probabilities(vad, z.data(), z.size(), probs.data(), probs.size(), &nf);

@@ -213,3 +213,12 @@ def test_bpe_encode_matches_qwen2_tokenizer():
         assert _encode(lib, h, "张三<|im_start|>hello") == a + [nv + 1] + b
     finally:
         lib.qasr_tokenizer_close(h)
+
+
+def test_warmup_noise_asset_matches_reference_signal():
+    """assets/warmup_noise.f32 (engine warm-up) == the reference's default_rng(0).standard_normal(16000)·0.002 as f32
+    (qwen3_asr_server.py:139-140)"""
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "assets", "warmup_noise.f32")
+    got = np.fromfile(path, dtype="<f4")
+    want = np.random.default_rng(0).standard_normal(16_000).astype(np.float32) * 0.002
+    assert got.size == 16_000 and np.array_equal(got, want)

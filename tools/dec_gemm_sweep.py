@@ -19,9 +19,9 @@ from qasr import _lib  # noqa: E402
 
 SHAPES = [("qkv", 4096, 2048, 0), ("o", 2048, 2048, 1), ("down", 2048, 6144, 1), ("gu", 12288, 2048, 3)]
 MS = [int(x) for x in os.environ.get("MS", "16,32,64,96,128,160,192,224,256").split(",")]
-CFGS = list(range(4, 31)) + list(range(32, 40))
+CFGS = list(range(4, 31)) + list(range(32, 49))
 SPLITS = [1, 2, 3, 4, 6, 8]
-SWIGLU_CFGS = [4, 5, 8, 9, 12, 13, 15, 20, 22, 23, 28, 29, 30, 33, 35, 38, 39]
+SWIGLU_CFGS = [4, 5, 8, 9, 12, 13, 15, 20, 22, 23, 28, 29, 30, 33, 35, 38, 39] + list(range(40, 49))
 
 
 def main():
