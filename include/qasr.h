@@ -255,34 +255,11 @@ QASR_API int qasr_op_interleave_gate_up(int8_t* qs, void* sc, int32_t N, int32_t
 /* h = silu(x·Wgᵀ)·(x·Wuᵀ) quantised to Q8 rows (hq [M][N/2], hd [M][N/64]) in the GEMM epilogue; W interleaved */
 QASR_API int qasr_op_gemm_swiglu_q8(const int8_t* xq, const float* xd, int32_t M, const int8_t* wqs, const void* wsc,
                                     int32_t N, int32_t K, int8_t* hq, float* hd, void* stream);
-/* Same, with the GEMM configuration forced (kernels_q8.hip kGemmCfgs index + 32 × split-K count; -1 = heuristic)
-   — tuning and tests.  Split-K needs a fix-up workspace (qasr_op_set_gemm_fixup). */
-QASR_API int qasr_op_gemm_swiglu_q8_cfg(const int8_t* xq, const float* xd, int32_t M, const int8_t* wqs,
-                                        const void* wsc, int32_t N, int32_t K, int8_t* hq, float* hd, int32_t cfg,
-                                        void* stream);
-/* Register (this thread) the split-K fix-up workspace the op-level Q8 GEMMs use: part_bytes of device memory for
-   partial tiles and ncnt device uint32 arrival counters, ZEROED by the caller (the kernels leave them zero).  With
-   it, every split-K GEMM stores partial tiles and the tile's last workgroup adds them in split order and runs the
-   full epilogue (deterministic, any epilogue); without it (part = NULL) split-K adds with f32 atomics.  Sessions
-   register their own for the decode steps (used there for the SwiGLU epilogue).  Not in
-   the reference (an engine-internal tuning / test hook). */
-QASR_API int qasr_op_set_gemm_fixup(void* part, int64_t part_bytes, void* cnt, int32_t ncnt);
-/* Rows (0..64) up to which the Q8 GEMM's automatic choice streams the weights straight into the matrix core's operand
-   registers (k_gemm_q8_ws: decode rows, every weight byte read once, no LDS staging); 0 = never.  all_shapes = 0: only
-   on the wide decoder matrices where it is faster (QKV, gate/up); 1: every shape it supports (tests).  Process-wide;
-   default 16 rows (QASR_WS_ROWS).  Tuning / A/B hook, not in the reference. */
-QASR_API int qasr_op_set_gemm_ws_rows(int32_t rows, int32_t all_shapes);
 /* Q8 GEMM with a fused output epilogue (M > 8, the MFMA path): epi 4 = erf-GELU(acc + bias) quantised to Q8 rows
    (yq [M][N] int8, yd [M][N/32] f32 block scales; y unused), epi 5 = f16(acc + bias) into y (__half, row stride
    ldy).  cfg: GEMM configuration (-1 = heuristic). */
 /* MXFP8 precision mode: Q8 blocks (q int8, d f32 or f16) → OCP MXFP8 (e4m3 elements q·d·2^-E
    rounded to nearest even, e8m0 byte E+127 with E the smallest exponent putting the block maximum ≤ 448). */
-/* Regrouped stage scales of a Q8 matrix (sc [N][K/32] f16 → out [K/128][N][4] f16, K % 128 == 0): a K-128 GEMM
-   stage's column scales as one contiguous run (the decode GEMMs' 16-byte scale DMA; a model's decoder matrices
-   carry theirs).  qasr_op_register_stage_scales(wsc, out) makes the qasr_op_* GEMM entry points use `out` for the
-   matrix whose scale pointer is `wsc` (NULL unregisters) — tests and tuning tools. */
-QASR_API int qasr_op_stage_scales(const void* wsc, int32_t N, int32_t K, void* out, void* stream);
-QASR_API int qasr_op_register_stage_scales(const void* wsc, const void* sc4);
 QASR_API int qasr_op_q8_to_mx(const int8_t* q, const void* d, int32_t d_is_f16, int64_t nblk, uint8_t* q8,
                              uint8_t* s8, void* stream);
 /* y = epi(X·Wᵀ) on MXFP8 operands (v_mfma_scale_f32_16x16x128_f8f6f4); epi as qasr_op_linear_q8 (0-2), 3 SwiGLU
@@ -400,4 +377,7 @@ QASR_API int qasr_prof_report(char* buf, size_t cap, size_t* needed);
 #ifdef __cplusplus
 }
 #endif
+
+/* Engine-internal tuning and A/B hooks (forced GEMM configurations, split-K fix-up workspace, weight-streaming row
+   limit, stage-scale registration) live in qasr_tune.h: they are not part of the drop-in boundary. */
 #endif /* QASR_H */

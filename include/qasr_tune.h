@@ -1,0 +1,44 @@
+/*
+ * qasr_tune.h — engine-internal tuning, A/B and test hooks of libqasr (NOT part of the drop-in boundary in qasr.h:
+ * no reference interface corresponds to them).  The GEMM tuning tools (tools/gemm_tune.py, tools/dec_gemm_sweep.py)
+ * and the kernel parity tests force configurations through them; a host binding the reference's interface never
+ * needs them.  Pointer arguments are DEVICE pointers, `stream` a hipStream_t (NULL = default stream).
+ */
+#ifndef QASR_TUNE_H
+#define QASR_TUNE_H
+
+#include "qasr.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* qasr_op_gemm_swiglu_q8 with the GEMM configuration forced (kernels_q8.hip kGemmCfgs index + 32 × split-K count, or
+   4096 + cfg + 256 × split-K count for configurations ≥ 32; -1 = heuristic).  Split-K needs a fix-up workspace
+   (qasr_op_set_gemm_fixup). */
+QASR_API int qasr_op_gemm_swiglu_q8_cfg(const int8_t* xq, const float* xd, int32_t M, const int8_t* wqs,
+                                        const void* wsc, int32_t N, int32_t K, int8_t* hq, float* hd, int32_t cfg,
+                                        void* stream);
+/* Register (this thread) the split-K fix-up workspace the op-level Q8 GEMMs use: part_bytes of device memory for
+   partial tiles and ncnt device uint32 arrival counters, ZEROED by the caller (the kernels leave them zero).  With
+   it, every split-K GEMM stores partial tiles and the tile's last workgroup adds them in split order and runs the
+   full epilogue (deterministic, any epilogue); without it (part = NULL) split-K adds with f32 atomics.  Sessions
+   register their own for the decode steps (used there for the SwiGLU epilogue).  Not in
+   the reference (an engine-internal tuning / test hook). */
+QASR_API int qasr_op_set_gemm_fixup(void* part, int64_t part_bytes, void* cnt, int32_t ncnt);
+/* Rows (0..64) up to which the Q8 GEMM's automatic choice streams the weights straight into the matrix core's operand
+   registers (k_gemm_q8_ws: decode rows, every weight byte read once, no LDS staging); 0 = never.  all_shapes = 0: only
+   on the wide decoder matrices where it is faster (QKV, gate/up); 1: every shape it supports (tests).  Process-wide;
+   default 16 rows (QASR_WS_ROWS).  Tuning / A/B hook, not in the reference. */
+QASR_API int qasr_op_set_gemm_ws_rows(int32_t rows, int32_t all_shapes);
+/* Regrouped stage scales of a Q8 matrix (sc [N][K/32] f16 → out [K/128][N][4] f16, K % 128 == 0): a K-128 GEMM
+   stage's column scales as one contiguous run (the decode GEMMs' 16-byte scale DMA; a model's decoder matrices
+   carry theirs).  qasr_op_register_stage_scales(wsc, out) makes the qasr_op_* GEMM entry points use `out` for the
+   matrix whose scale pointer is `wsc` (NULL unregisters) — tests and tuning tools. */
+QASR_API int qasr_op_stage_scales(const void* wsc, int32_t N, int32_t K, void* out, void* stream);
+QASR_API int qasr_op_register_stage_scales(const void* wsc, const void* sc4);
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* QASR_TUNE_H */

@@ -8,7 +8,7 @@
 #include <stdexcept>
 #include <string>
 
-#include "../../include/qasr.h"
+#include "../../include/qasr_tune.h"
 
 // QASR_FORMAL_HANDOFF=1 (A/B builds): the split-K fix-up and the split decode attention publish their partials with a
 // release on the arrival add and read them after an agent-scope acquire fence (the formal C++ memory-model form),

@@ -1,6 +1,6 @@
 """Host-side logic of libqasr (no GPU needed) against the reference's own behaviour.
 
-  * the C ABI loads and exports every symbol include/qasr.h declares;
+  * the C ABI loads and exports every symbol include/qasr.h and qasr_tune.h declare;
   * the segmenter (qasr_vad_timestamps_from_probabilities) vs FireRedVad._timestamps_from_probabilities
     outputs (firered_vad.py:121-191, golden vad_post.json);
   * pcm_s16le base64 decoding (server_common.py:145-187) and the linear resampler
@@ -20,11 +20,13 @@ from qasr import _lib
 from qasr.firered_vad import FireRedVadOptions, timestamps_from_probabilities
 
 G = os.path.join(os.path.dirname(__file__), "golden")
-HDR = os.path.join(os.path.dirname(__file__), "..", "include", "qasr.h")
+HDRS = [os.path.join(os.path.dirname(__file__), "..", "include", h) for h in ("qasr.h", "qasr_tune.h")]
 
 
 def test_header_symbols_exported():
-    declared = set(re.findall(r"QASR_API\s+[^;(]*?\b(qasr_\w+)\s*\(", open(HDR).read()))
+    declared = set()
+    for h in HDRS:   # the boundary (qasr.h) and the engine-internal tuning hooks (qasr_tune.h)
+        declared |= set(re.findall(r"QASR_API\s+[^;(]*?\b(qasr_\w+)\s*\(", open(h).read()))
     assert len(declared) >= 40
     assert declared == set(_lib.SIGNATURES), declared ^ set(_lib.SIGNATURES)
     missing = declared - _lib.exported_symbols()
