@@ -270,6 +270,9 @@ def main():
                          "(seed 2) VAD-segmented across the ranks (halo-sharded FireRedVAD, probability "
                          "all-gather), segments LPT-sharded for ASR — strong scaling")
     ap.add_argument("--c5-seconds", type=float, default=3600.0)
+    ap.add_argument("--batch-invariant", action="store_true",
+                    help="decode every segment with its single-utterance arithmetic (Session.set_batch_invariant: "
+                         "tokens independent of the batch and the GPU count); default: the batched GEMM tables")
     ap.add_argument("--dry-run-launch", action="store_true",
                     help="print the multi-rank launch command that --gpus N > 1 would run, and exit (tests)")
     args = ap.parse_args()
@@ -359,6 +362,8 @@ def main():
     if args.precision != "q8":
         model.set_precision(args.precision)
     sess = model.session(kv_type="f16", n_ctx=32768)
+    if args.batch_invariant:
+        sess.set_batch_invariant(True)
 
     c5_info = {}
     if args.workload == "c4":
@@ -480,6 +485,8 @@ def main():
                                     f"segments ({c5_info.get('speech_s')} s) LPT-sharded, {FORCE_TPS} forced "
                                     f"tokens/audio-s"),
                        "model": args.arch, "parallelism": f"dp{world}",
+                       "batch_invariant": bool(args.batch_invariant or os.environ.get("QASR_BATCH_INVARIANT", "0")
+                                               not in ("", "0")),
                        **({"segments_total": total_segments, "segments_rank0": len(lens),
                            "audio_s_rank0": round(audio_s, 1)}
                           if args.workload == "c4" else

@@ -143,6 +143,13 @@ QASR_API void qasr_tokenizer_close(qasr_tokenizer* t);
 QASR_API int qasr_session_set_draft(qasr_session* s, int32_t on);
 QASR_API int qasr_session_set_draft_noise(qasr_session* s, float rate, uint64_t seed);
 QASR_API int qasr_session_draft_stats(const qasr_session* s, int64_t* stats /* [4] */);
+/* Batch invariance (opt-in; QASR_BATCH_INVARIANT=1 in the environment sets the default): on = 1 makes every
+   utterance of a batch run (qasr_run_batch*) decode with the arithmetic of its own single-utterance run — the decode
+   rows on the exact-row linears and attention chunking of a 1-row step, the front end, encoder and decoder prefill
+   in the row-count-independent GEMM order — so its tokens are the same bits whatever else shares the batch or how
+   many GPUs the job is sharded over (the reference decodes each request alone, qwen3_asr_server.py:321).  Q8
+   precision only (ignored in MXFP8 mode).  Its cost on the C4 batch is measured in DESIGN.md §2. */
+QASR_API int qasr_session_set_batch_invariant(qasr_session* s, int32_t on);
 /* Streaming encoder cache: every single-utterance run encodes in a row-count-independent GEMM
    order (cache on or off), so a complete 8-chunk attention window's audio-embedding rows are a function of its
    samples and the request's log-mel maximum (Whisper-style normalisation; the conv stack is per 1 s chunk, the
@@ -283,7 +290,8 @@ QASR_API int qasr_op_gemv_fused(int32_t pro, const float* src, int32_t ld_src, c
 /* The draft verify passes' exact-row linear on the matrix core (engine.cpp, ≥ 5 rows): y = X·Wᵀ (epi 0) or y = res +
    X·Wᵀ (epi 1, y may alias res) with bit for bit the arithmetic of qasr_op_gemv_fused(pro 0) on each row alone — the
    exact-row contract that makes drafted decoding emit greedy's tokens (qwen3_asr_server.py:321's session.run is one
-   greedy decode).  M 1..32, K a multiple of 1,024 (K/1024 ∈ {1,2,3,4,6}). */
+   greedy decode; the batch-invariant decode's linears).  M ≥ 1 (32-row chunks in one launch), K a multiple of 1,024
+   (K/1024 ∈ {1,2,3,4,6}). */
 QASR_API int qasr_op_gemm_exact_rows(const int8_t* xq, const float* xd, int32_t M, const int8_t* wqs, const void* wsc,
                                      int32_t N, int32_t K, const float* res, float* y, int32_t ldy, int32_t epi,
                                      void* stream);

@@ -259,6 +259,13 @@ QASR_API int qasr_session_set_draft(qasr_session* s, int32_t on) {
     });
 }
 
+QASR_API int qasr_session_set_batch_invariant(qasr_session* s, int32_t on) {
+    return guard([&] {
+        QASR_CHECK(s, QASR_E_INVALID, "null argument");
+        s->s->set_batch_invariant(on != 0);
+    });
+}
+
 QASR_API int qasr_session_set_draft_noise(qasr_session* s, float rate, uint64_t seed) {
     return guard([&] {
         QASR_CHECK(s && rate >= 0.f && rate <= 1.f, QASR_E_INVALID, "bad arguments");

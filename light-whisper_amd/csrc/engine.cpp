@@ -124,9 +124,7 @@ Session::Session(Model* m, int n_ctx) : m_(m), n_ctx_(n_ctx) {
     // split-K decode attention scratch (≤ 4 rows over long key ranges): partial states + zeroed arrival counters
     const int nkv = m->hp.txt_kv_heads, G = nkv > 0 ? m->hp.txt_heads / nkv : 1;
     if (m->hp.head_dim == 128 && nkv > 0) {
-        QASR_HIP(hipMalloc(&attn_part_, attn_split_floats(kExactRows, nkv, G) * sizeof(float)));
-        QASR_HIP(hipMalloc(&attn_cnt_, (size_t)kExactRows * nkv * sizeof(int)));
-        QASR_HIP(hipMemset(attn_cnt_, 0, (size_t)kExactRows * nkv * sizeof(int)));
+        ensure_attn_split(kExactRows);
     }
     // split-K fix-up of the decode GEMMs: up to kFixSplits partial tiles of 256 rows × the widest decoder weight
     const qasr_hparams& hp = m->hp;
@@ -279,7 +277,7 @@ void Session::front_end(const float* dpcm, const std::vector<int64_t>& off, cons
     const int rows = chunks * 13, K = C * F3;
     // one utterance: the row-count-independent GEMM order, so its audio-embedding rows are the same bits whether a
     // window is computed in this run or reused from the encoder cache (cache on == cache off, bit for bit)
-    StableOrderScope order(count == 1);
+    StableOrderScope order(count == 1 || batch_inv_);
     int8_t* xq = (int8_t*)sc_.get(S_XQ, (size_t)rows * K);
     float* xd = (float*)sc_.get(S_XD, (size_t)rows * (K / QK) * sizeof(float));
     quant_rows(a3, rows, K, K, xq, xd, st_);
@@ -299,7 +297,8 @@ void Session::encoder(FrontEnd& fe, float* enc_out_dbg) {
     // so encoding it as an utterance of its own gives the same windows
     const int skip = fe.skip_tokens, N = fe.total_tokens - skip, d = h.enc_d, F = h.enc_ffn, H = h.txt_h;
     QASR_CHECK(skip == 0 || fe.n_tok.size() == 1, QASR_E_INTERNAL, "encoder cache: one utterance");
-    StableOrderScope order(fe.n_tok.size() == 1);   // one utterance: rows independent of the row count (front_end)
+    // one utterance (or batch invariance): rows independent of the row count (front_end)
+    StableOrderScope order(fe.n_tok.size() == 1 || batch_inv_);
     // attention windows (get_audio_cu_seqlens, modeling_qwen3_asr.py:276-315)
     std::vector<int> kvs(N), kvl(N);
     for (size_t u = 0; u < fe.n_tok.size(); u++) {
@@ -421,6 +420,24 @@ void Session::dump_rows(const char* what, int l, int rows, const void* p, size_t
     }
 }
 
+// the split decode attention's partial states + zeroed arrival counters for `rows` rows (grow-only; never while a step
+// graph is being captured — the eager sizing step of the largest bucket runs first)
+void Session::ensure_attn_split(int rows) {
+    if (rows <= attn_rows_) return;
+    QASR_CHECK(!sc_.capturing, QASR_E_INTERNAL, "split attention scratch growth during graph capture");
+    const int nkv = m_->hp.txt_kv_heads, G = m_->hp.txt_heads / nkv;
+    if (attn_part_) {
+        QASR_HIP(hipDeviceSynchronize());   // queued steps may still use the old buffers
+        QASR_HIP(hipFree(attn_part_));
+        QASR_HIP(hipFree(attn_cnt_));
+    }
+    QASR_HIP(hipMalloc(&attn_part_, attn_split_floats(rows, nkv, G) * sizeof(float)));
+    QASR_HIP(hipMalloc(&attn_cnt_, (size_t)rows * nkv * sizeof(int)));
+    QASR_HIP(hipMemset(attn_cnt_, 0, (size_t)rows * nkv * sizeof(int)));
+    attn_rows_ = rows;
+    attn_epoch_++;
+}
+
 void Session::decoder_layers(float* x, int rows, const int* d_pos, const int* d_slot, const int* d_kvs,
                              const int* d_kvl, int64_t total_keys, bool dense, bool rows_share_kv) {
     const qasr_hparams& h = m_->hp;
@@ -444,7 +461,9 @@ void Session::decoder_layers(float* x, int rows, const int* d_pos, const int* d_
     // exact rows (a draft verify pass): every row runs the arithmetic of a 1-row decode step — the fused GEMVs in
     // row groups against the same weight registers, the same per-row decode attention (split over the key range like a
     // single row) — so the accepted tokens are greedy's bit for bit, whatever the draft
-    const bool exact = rows_share_kv && rows <= kExactRows;
+    // batch invariance (set_batch_invariant): a batch's decode rows (different utterances) take the exact-row path too
+    const bool inv = batch_inv_ && !dense && !rows_share_kv && !m_->mx();
+    const bool exact = (rows_share_kv && rows <= kExactRows) || inv;
     const bool gv_shapes = gemv_fused_ok(GV_RMS, rows, H) && gemv_fused_ok(GV_NONE, rows, F) &&
                            gemv_fused_ok(GV_NONE, rows, QD);
     // GEMV row counts: the norms and the SwiGLU run inside the GEMVs' prologues (5 launches per layer, not 8)
@@ -457,6 +476,8 @@ void Session::decoder_layers(float* x, int rows, const int* d_pos, const int* d_
     const bool gv = !xm && gv_shapes && (exact || (rows <= gemv_layer_rows() && dec_fuse_));
     QASR_CHECK(!rows_share_kv || (exact && (gv || xm)), QASR_E_INTERNAL,
                "decoder: a verify pass needs the exact-row path (≤ kExactRows rows, GEMV shapes)");
+    QASR_CHECK(!inv || gv || xm, QASR_E_INTERNAL, "decoder: batch invariance needs the exact-row linears");
+    if (inv && fuse_qk && attn_split_) ensure_attn_split(rows);
     int8_t* hq2 = gv || xm ? (int8_t*)sc_.get(S_HQ, (size_t)rows * F) : nullptr;   // the SwiGLU Q8 rows
     float* hd2 = gv || xm ? (float*)sc_.get(S_HD, (size_t)rows * (F / QK) * sizeof(float)) : nullptr;
     float* gux = xm ? (float*)sc_.get(S_GU, (size_t)rows * 2 * F * sizeof(float)) : nullptr;
@@ -487,10 +508,12 @@ void Session::decoder_layers(float* x, int rows, const int* d_pos, const int* d_
                 qk_norm_rope(qkv, rows, nh, nkv, hd, d_pos, d_slot, L.q_norm, L.k_norm, rope_, h.rms_eps, qh, kc, vc,
                              st_);
             QkFuse fz{qkv, d_pos, d_slot, L.q_norm, L.k_norm, rope_, h.rms_eps, kc, vc};
-            if ((rows <= 4 || exact) && attn_part_ && attn_split_) {   // long key ranges split over workgroups
-                fz.part = attn_part_;
+            if ((rows <= 4 || exact) && attn_part_ && attn_split_ && rows <= attn_rows_) {   // long key ranges split
+                fz.part = attn_part_;                                                         // over workgroups
                 fz.cnt = attn_cnt_;
+                fz.part_rows = attn_rows_;
             }
+            fz.fixed_chunk = inv;   // the 1-row step's chunking for every row
             attention_decode_fused(fz, KD, d_kvs, d_kvl, rows, nh, nkv, hd, scale, xq, xd, st_, total_keys);
         } else {
             qk_norm_rope(qkv, rows, nh, nkv, hd, d_pos, d_slot, L.q_norm, L.k_norm, rope_, h.rms_eps, qh, kc, vc, st_);
@@ -594,7 +617,7 @@ void Session::decode_step(const DecState& ds, int B, bool sizing, int64_t keys) 
     embed_rows(tab, B, m_->tok_embd, nullptr, x, st_);
     decoder_layers(x, B, tab + B, tab + 2 * B, tab + 3 * B, tab + 4 * B, keys);
     float* logits = (float*)sc_.get(S_LOGITS, (size_t)B * V * sizeof(float));
-    lm_head_rows(x, B, H, logits);
+    lm_head_rows(x, B, H, logits, batch_inv_ && !m_->mx());
     int* d_tok = (int*)sc_.get(S_TOK, (size_t)B * sizeof(int));
     argmax_rows(logits, B, V, d_tok, st_, sc_.get(S_ARGP, argmax_scratch_bytes(B)));
     dec_accept(ds, B, tab + 5 * B, d_tok, st_);
@@ -621,7 +644,7 @@ void Session::draft_step(int B) {
 
 // bucket graphs hold scratch / KV / weight pointers: retire them whenever any of those moved
 void Session::draft_graphs_refresh() {
-    const uint64_t key[4] = {sc_.epoch, kv_epoch_, m_->precision_gen, deterministic_gen()};
+    const uint64_t key[5] = {sc_.epoch, kv_epoch_, m_->precision_gen, deterministic_gen(), attn_epoch_};
     if (memcmp(key, draft_key_, sizeof key) != 0) {
         for (auto& g : draft_graphs_) (void)hipGraphExecDestroy(g.second);
         draft_graphs_.clear();
@@ -880,6 +903,9 @@ void Session::run_batch(const float* dpcm, const std::vector<int64_t>& off, cons
     }
     {
         Timer t(st_, times ? &times->prefill : nullptr);
+        // a single utterance's decoder prefill — and a batch's under batch invariance — in the row-count-independent
+        // GEMM order (every output one block chain in K order), so a prompt row is the same bits in any batch
+        StableOrderScope order(count == 1 || batch_inv_);
         sc_.get(S_X, (size_t)std::max(T, P0) * H * sizeof(float));
         if (skip) {
             const std::vector<int32_t> full = build_prompt(h, 0, 0, context_);
@@ -914,7 +940,7 @@ void Session::run_batch(const float* dpcm, const std::vector<int64_t>& off, cons
         float* xn = (float*)sc_.get(S_XN, (size_t)count * H * sizeof(float));
         k_gather_rows<<<(unsigned)cdiv64((int64_t)count * H, 256), 256, 0, st_>>>(x, d_last, count, H, xn);
         float* logits = (float*)sc_.get(S_LOGITS, (size_t)count * V * sizeof(float));
-        lm_head_rows(xn, count, H, logits);
+        lm_head_rows(xn, count, H, logits, batch_inv_ && !m_->mx());
         int* d_tok = (int*)sc_.get(S_TOK, count * sizeof(int));
         argmax_rows(logits, count, V, d_tok, st_, sc_.get(S_ARGP, argmax_scratch_bytes(count)));
         // the first generated token of every utterance: plan (identity rows) + accept on the device
@@ -972,7 +998,8 @@ void Session::run_batch(const float* dpcm, const std::vector<int64_t>& off, cons
         QASR_HIP(hipEventRecord(step_ev_[0], st_));
     }
     // captured step graphs hold scratch, KV and weight pointers: any reallocation or precision change retires them
-    const uint64_t key[4] = {sc_.epoch, kv_epoch_, m_->precision_gen, deterministic_gen()};
+    const uint64_t key[5] = {sc_.epoch, kv_epoch_, m_->precision_gen, deterministic_gen(),
+                             attn_epoch_ * 2 + (batch_inv_ ? 1 : 0)};
     if (memcmp(key, graph_key_, sizeof key) != 0) {
         for (auto& g : graphs_) (void)hipGraphExecDestroy(g.second);
         graphs_.clear();

@@ -67,6 +67,13 @@ class Session {
     // transcripts (prompt-lookup: the tokens that followed the same bigram last time) and verify a whole draft in one
     // teacher-forced pass; the accepted tokens are exactly greedy's (up to near-ties of f32 summation order)
     void set_draft(bool on) { draft_ = on; }
+    // batch invariance (round 4): a batch's decode rows each run the 1-row decode step's arithmetic (the exact-row
+    // linears, the fixed-chunk split attention, the exact-row vocabulary projection) and its front end / encoder /
+    // decoder prefill the row-count-independent GEMM order, so an utterance's tokens are the bits of its own
+    // single-utterance run whatever else shares the batch (or the GPU count).  Q8 precision only.
+    // Default: QASR_BATCH_INVARIANT=1 in the environment.
+    void set_batch_invariant(bool on) { batch_inv_ = on; }
+    bool batch_invariant() const { return batch_inv_; }
     // benchmark / test hook: each proposed draft token is replaced by a random id with probability `rate` (draft
     // acceptance below the degenerate 100 % of synthetic weights; the output stays greedy's, only the speed changes)
     void set_draft_noise(float rate, uint64_t seed) {
@@ -143,7 +150,7 @@ class Session {
     hipEvent_t step_ev_[2] = {nullptr, nullptr};
     std::map<int, hipGraphExec_t> graphs_;
     std::map<int, hipGraphExec_t> draft_graphs_;
-    uint64_t draft_key_[4] = {~0ull, ~0ull, ~0ull, ~0ull};
+    uint64_t draft_key_[5] = {~0ull, ~0ull, ~0ull, ~0ull, ~0ull};
     bool draft_ = false;
     float draft_noise_ = 0.f;
     uint64_t noise_state_ = 0;
@@ -155,6 +162,13 @@ class Session {
     bool attn_split_ = getenv("QASR_NO_ATTN_SPLIT") == nullptr;
     float* attn_part_ = nullptr;
     int* attn_cnt_ = nullptr;
+    int attn_rows_ = 0;          // rows attn_part_ / attn_cnt_ are sized for
+    uint64_t attn_epoch_ = 0;    // bumped when they are reallocated (captured step graphs hold the pointers)
+    void ensure_attn_split(int rows);
+    bool batch_inv_ = [] {
+        const char* e = getenv("QASR_BATCH_INVARIANT");
+        return e && atoi(e) != 0;
+    }();
     // split-K fix-up workspace of the decode-step GEMMs (≤ 256 rows; QASR_NO_FIXUP=1: f32 atomics instead): partial
     // tiles + per-tile arrival counters (zeroed once; the kernels leave them zero)
     float* fix_part_ = nullptr;
@@ -179,7 +193,8 @@ class Session {
     size_t ec_cap_ = 0;
     EncCacheStats ecstats_;
     int last_audio_tokens_ = 0;
-    uint64_t graph_key_[4] = {~0ull, ~0ull, ~0ull, ~0ull};   // scratch epoch, KV epoch, precision gen, determinism gen
+    // scratch epoch, KV epoch, precision gen, determinism gen, split-attention scratch epoch + batch invariance
+    uint64_t graph_key_[5] = {~0ull, ~0ull, ~0ull, ~0ull, ~0ull};
     uint64_t kv_epoch_ = 0;
     int ucap_ = 0;
 };

@@ -46,7 +46,7 @@ void gemv_q8(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const flo
 // EPI_SWIGLU (GV_RMS only; W = interleaved gate/up, N % 64 == 0): h = Q8(silu(g)·u) into yq [M][N/2] / yd [M][N/64].
 enum GvPro : int { GV_NONE = 0, GV_RMS = 1 };
 // The draft verify passes' linears on the matrix core with EXACTLY k_gemv_wide's 1-row arithmetic (the same block fma
-// chains and wave-sum tree, run in-lane): rows 1..kExactRows, K a multiple of 1,024 (K/1024 ∈ {1,2,3,4,6}), epi store
+// chains and wave-sum tree, run in-lane): any row count (32-row chunks in one launch), K a multiple of 1,024 (K/1024 ∈ {1,2,3,4,6}), epi store
 // or residual — bit-identical to gemv_fused(GV_NONE) on the same Q8 rows, and to the fused norm / SwiGLU launches when
 // preceded by rmsnorm_q8 / followed by swiglu_q8(interleaved)
 bool gemm_exact_rows_ok(int M, const Q8Mat& W);
@@ -150,6 +150,10 @@ struct QkFuse {
     // workgroup per (row, KV head)
     float* part = nullptr;
     int* cnt = nullptr;
+    int part_rows = kExactRows;   // rows part / cnt are sized for
+    // the row-invariant decode (Session batch invariance): the 64-key chunk kernel whatever the row count, so a row's
+    // result is the bits of a 1-row step (many-row launches otherwise take the 32-key chunks)
+    bool fixed_chunk = false;
     // ranges up to split_min keys stay in one workgroup; longer ones get pieces of ≥ split_keys keys
     // (tools/graph_cost.py, profiles/r2_attn_split_min_sweep.jsonl: 300 / 400 keys 9.7 → 8.0 / 8.2 µs at 256)
     int split_min = 256;

@@ -826,13 +826,13 @@ void attention_decode_fused(const QkFuse& fz, int ldkv, const int* kv_start, con
     ProfScope ps(s, "attention_decode", 4.0 * hd * nh * (double)total_keys, 4.0 * hd * nkv * (double)total_keys);
     QASR_CHECK(hd == 128 && nkv > 0 && nh % nkv == 0, QASR_E_INVALID, "attention_decode_fused: hd 128 only");
     const int G = nh / nkv;
-    QASR_CHECK(!fz.part || (rows <= kExactRows && fz.cnt), QASR_E_INVALID,
-               "attention_decode_fused: split-K is for ≤ kExactRows rows");
+    QASR_CHECK(!fz.part || (rows <= fz.part_rows && fz.cnt), QASR_E_INVALID,
+               "attention_decode_fused: more split rows than the scratch holds");
     const unsigned b4 = (unsigned)(rows * nkv * (fz.part ? kAttnSplitMax : 1));
     // many rows (≥ 192: ≥ 1,536 workgroups) → the 32-key-chunk kernel, 103 VGPRs and 4 waves per SIMD instead of 3
     // (tools/attn_batch.py, profiles/r2_attn_batch_chunk.jsonl: 256 rows 35.9 → 31.2 µs); fewer rows → the 64-key
     // kernel, which still runs its ≤ 32-key waves in 32-key chunks (1 key 6.35 → 5.37 µs)
-    const bool ck32 = rows >= 192;
+    const bool ck32 = rows >= 192 && !fz.fixed_chunk;
     // (a 5-waves-per-SIMD build of the 32-key kernel, 95 VGPRs, streamed the same: 31.1 against 31.5 µs at 256
     // rows, profiles/r2s2_attn_occupancy_ab.jsonl — the kernel is not occupancy-bound)
     if (G == 2 && ck32)

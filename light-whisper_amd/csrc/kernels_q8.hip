@@ -489,6 +489,16 @@ __global__ __launch_bounds__(256, 2) void k_gemm_q8_exact(const int8_t* __restri
     // a workgroup per 16-column fragment and all RF 16-row fragments (the weight span loaded once for them); wave w
     // owns leaves 8w … 8w+7 (blocks 8w + 2j + {0,1} + 32t: spans 4w + j + 16t)
     __shared__ float hx[4][RF][4][64];   // [wave][row fragment][r][lane]: H_w = O_2w + O_2w+1 of each output
+    // rows past 16·RF: grid.y chunks of 16·RF rows, each with the arithmetic of a launch of its own rows (the per-row
+    // code depends on nothing but the row)
+    {
+        const int m0 = (int)blockIdx.y * 16 * RF;
+        X += (size_t)m0 * K;
+        Xd += (size_t)m0 * (K / QK);
+        y += (size_t)m0 * ldy;
+        if (res) res += (size_t)m0 * ldy;
+        M -= m0;
+    }
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int fr = lane & 15, g = lane >> 4;
     const int n0 = blockIdx.x * 16;
@@ -577,15 +587,16 @@ int exact_mfma_rows() {
 
 bool gemm_exact_rows_ok(int M, const Q8Mat& W) {
     const int T = W.K / 1024;
-    return M >= 1 && M <= kExactRows && W.K % 1024 == 0 && (T == 1 || T == 2 || T == 3 || T == 4 || T == 6) && !W.mx;
+    return M >= 1 && W.K % 1024 == 0 && (T == 1 || T == 2 || T == 3 || T == 4 || T == 6) && !W.mx;
 }
 
 void gemm_exact_rows(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const float* res, float* y, int ldy,
                      int epi, hipStream_t s) {
     ProfScope ps(s, "gemm_q8_exact", 2.0 * M * W.N * W.K, q8_bytes(M, W, epi));
-    QASR_CHECK(gemm_exact_rows_ok(M, W), QASR_E_INVALID, "gemm_exact_rows: rows 1..32, K a multiple of 1024 (T 1-4, 6)");
+    QASR_CHECK(gemm_exact_rows_ok(M, W), QASR_E_INVALID, "gemm_exact_rows: rows ≥ 1, K a multiple of 1024 (T 1-4, 6)");
     QASR_CHECK(epi == EPI_STORE || (epi == EPI_RESID && res), QASR_E_INVALID, "gemm_exact_rows: store or residual");
-    const dim3 grid(cdiv(W.N, 16));
+    // one launch for any row count: 32-row chunks along grid.y (≤ 16 rows: one 16-row chunk)
+    const dim3 grid(cdiv(W.N, 16), M <= 16 ? 1 : cdiv(M, 32));
 #define EXACT_GO(TT)                                                                                                   \
     do {                                                                                                               \
         if (M <= 16)                                                                                                   \

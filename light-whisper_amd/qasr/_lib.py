@@ -106,6 +106,7 @@ SIGNATURES = {
     "qasr_resample_linear": (C.c_int, [P, SZ, C.c_double, P, SZ, C.POINTER(SZ)]),
     "qasr_audio_load_path": (C.c_int, [C.c_char_p, P, SZ, C.POINTER(SZ)]),
     "qasr_session_set_draft": (C.c_int, [P, I32]),
+    "qasr_session_set_batch_invariant": (C.c_int, [P, I32]),
     "qasr_dist_unique_id": (C.c_int, [P, SZ]),
     "qasr_dist_init": (C.c_int, [P, I32, I32, I32, P]),
     "qasr_dist_close": (None, [P]),

@@ -206,6 +206,10 @@ class Session:
         """streaming decode: draft from this session's earlier transcripts, verify in one pass (greedy's tokens)"""
         check(_lib.load().qasr_session_set_draft(self._h, 1 if on else 0))
 
+    def set_batch_invariant(self, on: bool = True):
+        """batch runs decode every utterance with its single-utterance arithmetic (tokens independent of the batch)"""
+        check(_lib.load().qasr_session_set_batch_invariant(self._h, 1 if on else 0))
+
     def set_draft_noise(self, rate: float, seed: int = 0):
         """benchmark / test hook: replace each proposed draft token by a random id with probability `rate`"""
         check(_lib.load().qasr_session_set_draft_noise(self._h, float(rate), int(seed)))

@@ -287,6 +287,35 @@ def test_real_batch_c4_scale(pair):
            oracle_first_divergence=oracle_divs)
 
 
+def test_real_batch_invariant(pair):
+    """batch invariance (Session.set_batch_invariant): 1.7B, 48 segments of U[2,12] s (more than 32 decode
+    rows: two exact-row chunks per linear; the longest key ranges pass 256 keys: the split attention), 8 forced tokens
+    per audio-second — every segment's token stream equals its default single run's (session.run,
+    qwen3_asr_server.py:321) EXACTLY, with no near-tie allowance, and a batch of other composition (the odd segments
+    alone) gives the same streams again"""
+    arch, _, s, _ = pair
+    if arch != "qwen3-asr-1.7b":
+        pytest.skip("C4 is quoted on the 1.7B model")
+    rng = np.random.default_rng(13)
+    secs = rng.uniform(2.0, 12.0, size=48)
+    secs[5] = 12.0   # 15 prompt + 156 audio + 97 generated tokens: key ranges past the 256-key split threshold
+    clips = [clip(float(x), 900 + i) for i, x in enumerate(secs)]
+    singles = [s.run(c, force_tokens_per_s=8).tokens for c in clips]   # the default single-utterance path
+    s.set_batch_invariant(True)
+    try:
+        batch = [r.tokens for r in s.run_batch(clips, force_tokens_per_s=8)]
+        odd = [r.tokens for r in s.run_batch(clips[1::2], force_tokens_per_s=8)]
+    finally:
+        s.set_batch_invariant(False)
+    for i, c in enumerate(clips):
+        assert len(batch[i]) == len(singles[i]) == int(round(8 * c.size / 16000.0)) + 1, i
+    mism = [i for i in range(48) if batch[i] != singles[i]]
+    mism_odd = [i for i in range(1, 48, 2) if odd[i // 2] != singles[i]]
+    record(f"real_batch_invariant[{arch}]", segments=48, tokens=int(sum(len(b) for b in batch)),
+           batch_vs_single_mismatched_segments=len(mism), odd_batch_mismatched_segments=len(mism_odd))
+    assert not mism and not mism_odd, (mism, mism_odd)
+
+
 def test_real_mxfp8_against_q8(pair):
     """1.7B MXFP8 precision mode (C5; tolerance parity only) against the Q8 path on teacher-forced logits"""
     from qasr.transcribe_cpp import Model
