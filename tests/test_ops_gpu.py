@@ -862,7 +862,7 @@ def test_gemm_swiglu_q8_fixup(torch_dev, fixup, m, f, k, cfg):
     assert not host(fixup).any()
 
 
-@pytest.mark.parametrize("m", [1, 5, 16, 17, 32])
+@pytest.mark.parametrize("m", [1, 5, 16, 17, 32, 40, 97])
 @pytest.mark.parametrize("n,k,epi", [(4096, 2048, 0), (2048, 2048, 1), (2048, 6144, 1), (12288, 2048, 0),
                                      (1024, 1024, 0), (1024, 3072, 1), (300, 4096, 0)])
 def test_gemm_exact_rows_match_gemv(torch_dev, m, n, k, epi):

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Cost of batch-invariant C4 decode GEMMs: every batched decode row computed with the single-row
-decode's arithmetic (qasr_op_gemm_exact_rows: the GEMV's block fma chains and wave-sum tree, ≤ 32 rows per launch)
+decode's arithmetic (qasr_op_gemm_exact_rows: the GEMV's block fma chains and wave-sum tree, 32-row chunks)
 instead of the deterministic batched GEMM table (qasr_op_linear_q8 path 2 / qasr_op_gemm_swiglu_q8).  Times both per
 decoder matrix and row count with COLD weights (a ring of copies larger than the Infinity Cache, as in a decode step
 streaming 28 layers), then prices one C4 bench step: Σ over its decode steps of 28 × (exact − table) at that step's
@@ -65,13 +65,10 @@ def main():
                                                  N, K, None, y.data_ptr() if epi == 1 else None, y.data_ptr(), N,
                                                  epi, 2, None))
 
-            def run_exact(i):
-                for r0 in range(0, M, 32):
-                    m = min(32, M - r0)
-                    _lib.check(lib.qasr_op_gemm_exact_rows(
-                        xq.data_ptr() + r0 * K, xd.data_ptr() + r0 * (K // 32) * 4, m, wq[i].data_ptr(),
-                        ws[i].data_ptr(), N, K, y.data_ptr() + r0 * N * 4 if epi == 1 else None,
-                        y.data_ptr() + r0 * N * 4, N, 1 if epi == 1 else 0, None))
+            def run_exact(i):   # one launch: 32-row chunks along grid.y
+                _lib.check(lib.qasr_op_gemm_exact_rows(xq.data_ptr(), xd.data_ptr(), M, wq[i].data_ptr(),
+                                                       ws[i].data_ptr(), N, K, y.data_ptr() if epi == 1 else None,
+                                                       y.data_ptr(), N, 1 if epi == 1 else 0, None))
                 if epi == 3:
                     _lib.check(lib.qasr_op_swiglu_q8_interleaved(y.data_ptr(), M, N // 2, hq.data_ptr(),
                                                                  hd.data_ptr(), None))
