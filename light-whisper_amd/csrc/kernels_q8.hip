@@ -16,6 +16,10 @@
 #ifndef QASR_DIAG
 #define QASR_DIAG 0
 #endif
+// the exact-row kernel's d_x·d_w from outer-product MFMAs (1) or VALU multiplies (0): the same IEEE products
+#ifndef QASR_EXACT_MFMA_PROD
+#define QASR_EXACT_MFMA_PROD 1
+#endif
 #ifndef QASR_PIN
 #define QASR_PIN 1
 #endif
@@ -507,22 +511,29 @@ __global__ __launch_bounds__(256, 2) void k_gemm_q8_exact(const int8_t* __restri
     const uint32_t* sp = (const uint32_t*)(Wsc + (size_t)min(n0 + fr, N - 1) * nb);
     const int8_t* ap[RF];
     const float* dxp[RF][4];
+    const float* dxq[RF];   // QASR_EXACT_MFMA_PROD: the block scales of row fr of each fragment
 #pragma unroll
     for (int f = 0; f < RF; f++) {
         ap[f] = X + (size_t)min(16 * f + fr, M - 1) * K + 16 * g;
+        dxq[f] = Xd + (size_t)min(16 * f + fr, M - 1) * nb;
 #pragma unroll
         for (int r = 0; r < 4; r++) dxp[f][r] = Xd + (size_t)min(16 * f + 4 * g + r, M - 1) * nb;
     }
     constexpr int NS = 4 * T;                  // spans of this wave
     constexpr int G8 = RF == 1 && NS % 8 == 0 ? 8 : 4;   // spans loaded per group
+    // (the product path where its registers fit: K ≤ 4,096 with one row fragment, K ≤ 2,048 with two — the fully
+    // unrolled span groups spill beyond that)
+    constexpr bool MP = QASR_EXACT_MFMA_PROD && (RF == 1 ? T <= 4 : T <= 2);
     float leaf[RF][8][4];
     const bool lo = g < 2;
     const v4i zero = {0, 0, 0, 0};
+    const v16f zero16 = {};
 #pragma unroll
     for (int q0 = 0; q0 < NS; q0 += G8) {
         v4i wq[G8], aq[G8][RF];
         uint32_t ws[G8];
-        float2 dx[G8][RF][4];
+        float2 dx[MP ? 1 : G8][RF][4];
+        float dxv[G8 / 2][RF];   // MP: lane group g's operand of the span pair's outer product: row fr, block b_g
 #pragma unroll
         for (int u = 0; u < G8; u++) {
             const int i = q0 + u, s = 4 * wv + (i & 3) + 16 * (i >> 2);
@@ -531,9 +542,44 @@ __global__ __launch_bounds__(256, 2) void k_gemm_q8_exact(const int8_t* __restri
 #pragma unroll
             for (int f = 0; f < RF; f++) {
                 aq[u][f] = *(const v4i*)(ap[f] + 64 * (size_t)s);
+                if constexpr (MP) {
+                    // pair u/2 = spans (u & ~1, u | 1): block b_g = 2·s(u & ~1 | g >> 1) + (g & 1) feeds lane group g
+                    if ((u & 1) == (g >> 1)) dxv[u / 2][f] = dxq[f][2 * s + (g & 1)];
+                } else {
 #pragma unroll
-                for (int r = 0; r < 4; r++) dx[u][f][r] = *(const float2*)(dxp[f][r] + 2 * s);
+                    for (int r = 0; r < 4; r++) dx[u][f][r] = *(const float2*)(dxp[f][r] + 2 * s);
+                }
             }
+        }
+        if constexpr (MP) {
+            // per span pair and row fragment: d_x·d_w of its 4 blocks by one v_mfma_f32_16x16x1_4b_f32 (block k = lane
+            // group k's operands: row fr's d_x and column fr's d_w of block b_k; C_k[4g + r][fr] lands in lane
+            // fr + 16g, register 4k + r — the i8 MFMA's (row, col)).  Its f32 products are the VALU's dw·dx bit for bit
+            // (IEEE round-to-nearest, tools/micro/prod_check.hip), so the leaves keep the GEMV's bits; each leaf's
+            // chain still runs in t order (pairs in increasing span order).  One product set live at a time.
+#pragma unroll
+            for (int u0 = 0; u0 < G8; u0 += 2) {
+                const uint32_t wsg = ws[u0 + (g >> 1)];
+                const float dwv = __half2float(__ushort_as_half((unsigned short)((g & 1) ? wsg >> 16 : wsg & 0xffff)));
+#pragma unroll
+                for (int f = 0; f < RF; f++) {
+                    const v16f prod = __builtin_amdgcn_mfma_f32_16x16x1f32(dxv[u0 / 2][f], dwv, zero16, 0, 0, 0);
+#pragma unroll
+                    for (int uu = 0; uu < 2; uu++) {
+                        const int u = u0 + uu, i = q0 + u, j = i & 3, t = i >> 2;
+#pragma unroll
+                        for (int h = 0; h < 2; h++) {
+                            const v4i bm = (lo == (h == 0)) ? wq[u] : zero;
+                            const int l = 2 * j + h;
+                            const v4i c = __builtin_amdgcn_mfma_i32_16x16x64_i8(aq[u][f], bm, zero, 0, 0, 0);
+#pragma unroll
+                            for (int r = 0; r < 4; r++)
+                                leaf[f][l][r] = fmaf((float)c[r], prod[4 * (2 * uu + h) + r], t == 0 ? 0.f : leaf[f][l][r]);
+                        }
+                    }
+                }
+            }
+            continue;
         }
 #pragma unroll
         for (int u = 0; u < G8; u++) {
