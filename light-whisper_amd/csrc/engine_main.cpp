@@ -681,11 +681,15 @@ struct Server {
 };
 
 int usage() {
-    fprintf(stderr, "usage: engine serve --engine {qwen3-asr-0.6b,qwen3-asr-1.7b}\n");
+    fprintf(stderr, "usage: engine serve --engine {qwen3-asr-0.6b,qwen3-asr-1.7b}\n"
+                    "       engine longform --engine {qwen3-asr-0.6b,qwen3-asr-1.7b} [--force-tps K] [--max-new N] "
+                    "[--batch-invariant] recording.wav   (one process per GPU: RANK / WORLD_SIZE / LOCAL_RANK)\n");
     return 2;
 }
 
 }  // namespace
+
+int longform_main(const std::string& engine, const std::string& gguf, int argc, char** argv);   // engine_longform.cpp
 
 int main(int argc, char** argv) {
     signal(SIGTERM, on_signal);
@@ -698,6 +702,22 @@ int main(int argc, char** argv) {
         if (cmd == "download") {
             fprintf(stderr, "model download is not part of this engine; provision the GGUF into the HF cache\n");
             return 2;
+        }
+        if (cmd == "longform" && !engine.empty()) {
+            // the GGUF from the HF cache like `serve` (hf_cache_utils.find_hf_snapshot_file); QASR_SYNTHETIC=1 allows
+            // the seeded synthetic weights when it is absent
+            const ModelSpec* spec = nullptr;
+            for (const auto& m : kModels)
+                if (engine == m.id) spec = &m;
+            if (!spec) return usage();
+            const std::string path = find_snapshot_file(spec->repo, spec->file);
+            const bool synth = getenv("QASR_SYNTHETIC") && std::string(getenv("QASR_SYNTHETIC")) == "1";
+            if (path.empty() && !synth) {
+                fprintf(stderr, "Qwen3-ASR Q8 模型未下载: %s\n", spec->file);
+                return 1;
+            }
+            setvbuf(stdout, nullptr, _IOFBF, 1 << 16);
+            return longform_main(engine, path, argc - 2, argv + 2);
         }
         if (cmd != "serve" || engine.empty()) return usage();
     } else {

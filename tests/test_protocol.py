@@ -82,6 +82,21 @@ def test_models_not_downloaded_without_fake(tmp_path):
                      "type": "models_not_downloaded", "engine": "qwen3-asr-0.6b"}
 
 
+def test_longform_cli_arguments(tmp_path):
+    """`engine longform` (the native C5 host path): no recording → usage (2); no GGUF and no QASR_SYNTHETIC → the
+    reference's not-downloaded message (1); a bad RANK / WORLD_SIZE → an error before any GPU work (1)"""
+    env = {k: v for k, v in os.environ.items() if k not in ("QASR_SYNTHETIC", "RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    env.update(LIGHT_WHISPER_DATA_DIR=str(tmp_path), HF_HUB_CACHE=str(tmp_path))
+    run = lambda *a, **e: subprocess.run([_lib.ENGINE_PATH, "longform", "--engine", "qwen3-asr-0.6b", *a],
+                                         capture_output=True, text=True, env={**env, **e}, timeout=60)
+    res = run()
+    assert res.returncode == 1 and "Qwen3-ASR-0.6B-Q8_0.gguf" in res.stderr
+    res = run(QASR_SYNTHETIC="1")
+    assert res.returncode == 2 and "usage: engine longform" in res.stderr
+    res = run(str(tmp_path / "x.wav"), QASR_SYNTHETIC="1", RANK="3", WORLD_SIZE="2")
+    assert res.returncode == 1 and "bad RANK / WORLD_SIZE" in res.stderr
+
+
 def test_path_mode_requests(tmp_path):
     """audio_path requests (qwen3_asr_server.py:256-267, the app's WAV fallback funasr_service.rs:1296-1323): the reply
     carries input_mode "path" and the duration of the decoded 16 kHz audio; an undecodable file is a

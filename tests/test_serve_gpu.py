@@ -198,3 +198,39 @@ def test_serve_interim_replay(ref_arch, tmp_path):
         # the near-tie rule of every parity test: top-2 gap below 0.5 % of the row's range
         assert top2[1] - top2[0] < 0.005 * (lg[div].max() - lg[div].min()), (engine, div, got, list(toks))
     assert div >= min(4, n), (engine, got, list(toks))
+
+
+def _write_f32_wav(path, audio):
+    """IEEE-float mono 16 kHz WAV (format 3): the samples round-trip bit for bit through qasr_audio_load_path"""
+    data = np.asarray(audio, dtype="<f4").tobytes()
+    fmt = (3).to_bytes(2, "little") + (1).to_bytes(2, "little") + (16000).to_bytes(4, "little") + \
+        (64000).to_bytes(4, "little") + (4).to_bytes(2, "little") + (32).to_bytes(2, "little")
+    body = b"WAVE" + b"fmt " + len(fmt).to_bytes(4, "little") + fmt + b"data" + len(data).to_bytes(4, "little") + data
+    with open(path, "wb") as f:
+        f.write(b"RIFF" + len(body).to_bytes(4, "little") + body)
+
+
+def test_engine_longform_matches_python_pipeline(ref, tmp_path):
+    """`engine longform` — the native C5 host path (no PyTorch: file unique-id hand-off, halo-sharded VAD, segmenter,
+    LPT, one ASR batch, token gather; world 1 here) — gives the segments and token streams of the Python pipeline
+    (qasr.longform + Session.run_batch) on the same 40 s recording and weights, and the parsed text of each"""
+    from qasr import _lib, longform
+
+    s, v = ref
+    audio = recording(40.0, 5)
+    wav = tmp_path / "rec.wav"
+    _write_f32_wav(wav, audio)
+    env = {k: val for k, val in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    env.update(QASR_SYNTHETIC="1", HF_HUB_CACHE=str(tmp_path / "hf"))
+    out = subprocess.run([_lib.ENGINE_PATH, "longform", "--engine", ENGINE, "--force-tps", "8", str(wav)],
+                         capture_output=True, text=True, env=env, timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    got = json.loads(out.stdout)
+    probs = longform.shard_probabilities(v, audio, 0, 1)
+    segs = longform.segments(probs, audio.size)
+    assert len(segs) >= 3 and got["segments_total"] == len(segs) and got["world"] == 1
+    assert [(d["start"], d["end"]) for d in got["segments"]] == segs
+    res = s.run_batch([audio[a:b] for a, b in segs], force_tokens_per_s=8)
+    assert [d["tokens"] for d in got["segments"]] == [r.tokens for r in res]
+    assert [d["text"] for d in got["segments"]] == [r.text for r in res]
+    assert [d["language"] for d in got["segments"]] == [r.language for r in res]
