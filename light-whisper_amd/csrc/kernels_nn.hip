@@ -103,7 +103,10 @@ void rmsnorm_q8(const float* x, int M, int H, int ldx, const float* w, float eps
     QASR_CHECK(H % 32 == 0 && H <= RW_MAX * 256 && ldx % 4 == 0, QASR_E_INVALID, "rmsnorm_q8: unsupported width");
     QASR_CHECK(nzero % 4 == 0 && ((uintptr_t)zero & 15) == 0, QASR_E_INVALID, "rmsnorm_q8: zero range alignment");
     const int kc = cdiv(H, 1024);   // float4 chunks per thread with a workgroup per row
-    if (M <= 2048 && kc <= 4) {
+    // a workgroup per row for every row count (round 4): the wave-per-row kernel below sums the squares in another
+    // order, so a prefill of > 2,048 rows (a batch) rounded a row differently from the same row in a smaller one —
+    // the batch-invariant contract needs one reduction order per row width
+    if (kc <= 4) {
         float4* z = zero ? (float4*)zero : nullptr;
         const int64_t nz = zero ? nzero / 4 : 0;
         if (kc <= 1) k_rmsnorm_q8_wg<1><<<M, 256, 0, s>>>(x, H, ldx, w, eps, q, d, z, nz);
