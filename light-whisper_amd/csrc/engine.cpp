@@ -7,6 +7,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <array>
 #include <climits>
 #include <cstdio>
 #include <map>
@@ -478,6 +479,19 @@ void Session::decoder_layers(float* x, int rows, const int* d_pos, const int* d_
                "decoder: a verify pass needs the exact-row path (≤ kExactRows rows, GEMV shapes)");
     QASR_CHECK(!inv || gv || xm, QASR_E_INTERNAL, "decoder: batch invariance needs the exact-row linears");
     if (inv && fuse_qk && attn_split_) ensure_attn_split(rows);
+    // batched decode rows (the table path) of few rows: the exact-row kernel where it is the faster launch (cold
+    // weights, deterministic table: QKV 5.6 / 7.5 against 7.2 / 9.6 µs at 16 / 32 rows, O-projection 6.7–8.6 against
+    // 10.2–10.9 µs at 16–64 rows, down 12.9 against 15.0 µs at 16 rows; profiles/r4_exact_cost_*.json) — the strong-
+    // scaling regime (32 segments per GPU at N = 8).  QASR_XR_ROWS=q,o,d overrides the row limits (0 = never).
+    static const std::array<int, 3> xr_lim = [] {
+        std::array<int, 3> v{32, 64, 16};
+        if (const char* e = getenv("QASR_XR_ROWS")) sscanf(e, "%d,%d,%d", &v[0], &v[1], &v[2]);
+        return v;
+    }();
+    const bool xr = !dense && !gv && !xm && !m_->mx();
+    const bool xr_qkv = xr && rows <= xr_lim[0] && gemm_exact_rows_ok(rows, m_->dec[0].qkv);
+    const bool xr_o = xr && rows <= xr_lim[1] && gemm_exact_rows_ok(rows, m_->dec[0].o);
+    const bool xr_down = xr && rows <= xr_lim[2] && gemm_exact_rows_ok(rows, m_->dec[0].down);
     int8_t* hq2 = gv || xm ? (int8_t*)sc_.get(S_HQ, (size_t)rows * F) : nullptr;   // the SwiGLU Q8 rows
     float* hd2 = gv || xm ? (float*)sc_.get(S_HD, (size_t)rows * (F / QK) * sizeof(float)) : nullptr;
     float* gux = xm ? (float*)sc_.get(S_GU, (size_t)rows * 2 * F * sizeof(float)) : nullptr;
@@ -495,6 +509,9 @@ void Session::decoder_layers(float* x, int rows, const int* d_pos, const int* d_
         } else if (gv) {
             gemv_fused(GV_RMS, nullptr, nullptr, x, H, L.attn_norm, h.rms_eps, rows, L.qkv, nullptr, qkv, QD + 2 * KD,
                        EPI_STORE, nullptr, nullptr, st_);
+        } else if (xr_qkv) {
+            rmsnorm_q8(x, rows, H, H, L.attn_norm, h.rms_eps, xq, xd, st_);
+            gemm_exact_rows(xq, xd, rows, L.qkv, nullptr, qkv, QD + 2 * KD, EPI_STORE, st_);
         } else {
             rmsnorm_q8(x, rows, H, H, L.attn_norm, h.rms_eps, xq, xd, st_, zq ? qkv : nullptr,
                        zq ? (int64_t)rows * (QD + 2 * KD) : 0);
@@ -550,7 +567,10 @@ void Session::decoder_layers(float* x, int rows, const int* d_pos, const int* d_
                        st_);
             continue;
         }
-        linear_q8(xq, xd, rows, L.o, nullptr, x, x, H, EPI_RESID, st_);
+        if (xr_o)
+            gemm_exact_rows(xq, xd, rows, L.o, x, x, H, EPI_RESID, st_);
+        else
+            linear_q8(xq, xd, rows, L.o, nullptr, x, x, H, EPI_RESID, st_);
         rmsnorm_q8(x, rows, H, H, L.ffn_norm, h.rms_eps, xq, xd, st_);
         if (fused) {  // SwiGLU + Q8 in the gate-up GEMM epilogue (rows interleaved at load)
             gemm_q8(xq, xd, rows, L.gu, nullptr, nullptr, nullptr, 2 * F, EPI_SWIGLU, st_, -1, 0, hq, hd_);
@@ -560,7 +580,10 @@ void Session::decoder_layers(float* x, int rows, const int* d_pos, const int* d_
             linear_q8(xq, xd, rows, L.gu, nullptr, nullptr, gu, 2 * F, EPI_STORE, st_);
             swiglu_q8(gu, rows, F, xq, xd, st_, true);
         }
-        linear_q8(xq, xd, rows, L.down, nullptr, x, x, H, EPI_RESID, st_);
+        if (xr_down)
+            gemm_exact_rows(xq, xd, rows, L.down, x, x, H, EPI_RESID, st_);
+        else
+            linear_q8(xq, xd, rows, L.down, nullptr, x, x, H, EPI_RESID, st_);
         if (fused) {
             std::swap(xq, hq);
             std::swap(xd, hd_);

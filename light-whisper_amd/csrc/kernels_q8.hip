@@ -17,8 +17,10 @@
 #define QASR_DIAG 0
 #endif
 // the exact-row kernel's d_x·d_w from outer-product MFMAs (1) or VALU multiplies (0): the same IEEE products
+// (default 0: the 4-block f32 MFMA and its result latency cost more than the VALU multiplies it replaces — exact rows
+// 5.6 → 6.6 µs for QKV at 16 rows, 116 → 146 µs for the vocabulary projection: profiles/r4_exact_cost_*.json)
 #ifndef QASR_EXACT_MFMA_PROD
-#define QASR_EXACT_MFMA_PROD 1
+#define QASR_EXACT_MFMA_PROD 0
 #endif
 #ifndef QASR_PIN
 #define QASR_PIN 1
