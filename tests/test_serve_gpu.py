@@ -217,7 +217,7 @@ def test_engine_longform_matches_python_pipeline(ref, tmp_path):
     from qasr import _lib, longform
 
     s, v = ref
-    audio = recording(40.0, 5)
+    audio = recording(60.0, 5)
     wav = tmp_path / "rec.wav"
     _write_f32_wav(wav, audio)
     env = {k: val for k, val in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
@@ -228,7 +228,7 @@ def test_engine_longform_matches_python_pipeline(ref, tmp_path):
     got = json.loads(out.stdout)
     probs = longform.shard_probabilities(v, audio, 0, 1)
     segs = longform.segments(probs, audio.size)
-    assert len(segs) >= 3 and got["segments_total"] == len(segs) and got["world"] == 1
+    assert len(segs) >= 2 and got["segments_total"] == len(segs) and got["world"] == 1
     assert [(d["start"], d["end"]) for d in got["segments"]] == segs
     res = s.run_batch([audio[a:b] for a, b in segs], force_tokens_per_s=8)
     assert [d["tokens"] for d in got["segments"]] == [r.tokens for r in res]
