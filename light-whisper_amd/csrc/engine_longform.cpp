@@ -15,6 +15,8 @@
 //   6. the token streams all-gathered (qasr_dist_gather_tokens); rank 0 detokenises, splits language / text
 //      (qasr_parse_transcript) and prints one JSON object.
 // The reference handles one short utterance per request and has no long-form or multi-GPU mode.
+// A rank that fails exits non-zero without entering the next collective; the launcher (torchrun's agent, or the
+// Rust host's own supervisor) must then stop the other ranks, which would otherwise wait in that collective.
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
