@@ -213,7 +213,7 @@ def _write_f32_wav(path, audio):
 def test_engine_longform_matches_python_pipeline(ref, tmp_path):
     """`engine longform` — the native C5 host path (no PyTorch: file unique-id hand-off, halo-sharded VAD, segmenter,
     LPT, one ASR batch, token gather; world 1 here) — gives the segments and token streams of the Python pipeline
-    (qasr.longform + Session.run_batch) on the same 40 s recording and weights, and the parsed text of each"""
+    (qasr.longform + Session.run_batch) on the same 60 s recording and weights, and the parsed text of each"""
     from qasr import _lib, longform
 
     s, v = ref
@@ -233,4 +233,4 @@ def test_engine_longform_matches_python_pipeline(ref, tmp_path):
     res = s.run_batch([audio[a:b] for a, b in segs], force_tokens_per_s=8)
     assert [d["tokens"] for d in got["segments"]] == [r.tokens for r in res]
     assert [d["text"] for d in got["segments"]] == [r.text for r in res]
-    assert [d["language"] for d in got["segments"]] == [r.language for r in res]
+    assert [d["language"] for d in got["segments"]] == [r.language or "" for r in res]
