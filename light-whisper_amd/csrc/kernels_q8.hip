@@ -22,6 +22,13 @@
 #ifndef QASR_EXACT_MFMA_PROD
 #define QASR_EXACT_MFMA_PROD 0
 #endif
+#ifndef QASR_PREOFF_ALL
+#define QASR_PREOFF_ALL 1
+#endif
+// big tiles: unroll the K loop by the ring depth up to this depth (0 = only the pre-offset decode tiles)
+#ifndef QASR_UNR_RING
+#define QASR_UNR_RING 4
+#endif
 #ifndef QASR_PIN
 #define QASR_PIN 1
 #endif
@@ -1238,7 +1245,9 @@ __global__ __launch_bounds__(256 * KG, KG == 1 ? 2 : 1) void k_gemm_q8d(const in
     // ds_read2st64, whose 16-lane groups would conflict on this image), and the K loop is unrolled by the ring depth,
     // so each stage's LDS base is an immediate of its ds_reads — no per-read address VALU in the K loop (round 3:
     // 180 VALU per 16 MFMAs in the cfg-12 loop, 52 of them moves and adds for addresses)
-    constexpr bool PREOFF = TI * TJ <= 4;
+    // (round 4: every tile — the big tiles' per-read opacity copied each hoisted offset into a temporary, one v_mov per
+    // LDS read, 16 per stage of the 128×128 K-64 loop; QASR_PREOFF_ALL=0 restores the per-read form)
+    constexpr bool PREOFF = TI * TJ <= 4 || QASR_PREOFF_ALL;
     int offa[PREOFF ? KB : 1][PREOFF ? TI : 1], offb[PREOFF ? KB : 1][PREOFF ? TJ : 1];
     if constexpr (PREOFF) {
 #pragma unroll
@@ -1259,7 +1268,10 @@ __global__ __launch_bounds__(256 * KG, KG == 1 ? 2 : 1) void k_gemm_q8d(const in
 #pragma unroll
     for (int t = 0; t < D; t++)
         if (t < nsteps) issue(t, t);
-    constexpr int UNR = PREOFF ? NBUF : 1;   // stages per trip of the outer loop (one per ring buffer)
+    // stages per trip of the outer loop (one per ring buffer): each unrolled stage's ring slot is a constant, so its
+    // LDS base folds into the ds_read immediates (round 4: also the ≤ 4-deep rings of the big tiles, whose per-stage
+    // slot arithmetic cost two VALU per LDS read — 36 of the 128×128 K-64 loop's 311 VALU per stage)
+    constexpr int UNR = PREOFF || NBUF <= QASR_UNR_RING ? NBUF : 1;
     for (int s0 = 0; s0 < nsteps; s0 += UNR)
 #pragma unroll
     for (int ub = 0; ub < UNR; ub++) {
