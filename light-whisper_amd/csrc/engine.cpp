@@ -499,8 +499,9 @@ void Session::decoder_layers(float* x, int rows, const int* d_pos, const int* d_
         const DecLayer& L = m_->dec[l];
         __half* kc = kc_ + (size_t)l * layer_kv;
         __half* vc = vc_ + (size_t)l * layer_kv;
-        // decode-sized steps: the norm launch also clears the QKV output, so the split-K QKV GEMM needs no memset
-        const bool zq = rows <= 256;
+        // decode-sized steps: the norm launch also clears the QKV output, so the split-K QKV GEMM needs no memset —
+        // only with f32-atomic split-K (deterministic mode splits through the fix-up, which stores every output)
+        const bool zq = rows <= 256 && !deterministic();
         const bool dmp = g_dump && rows <= kExactRows;
         if (dmp) dump_rows("x_in", l, rows, x, (size_t)rows * H * sizeof(float));
         if (xm) {
