@@ -160,6 +160,11 @@ QASR_API int qasr_session_set_batch_invariant(qasr_session* s, int32_t on);
    reused, windows encoded by them. */
 QASR_API int qasr_session_set_encoder_cache(qasr_session* s, int32_t on);
 QASR_API int qasr_session_encoder_cache_stats(const qasr_session* s, int64_t* stats /* [3] */);
+/* With the encoder cache on, a run that reused the previous run's leading windows also keeps that run's K/V of the
+   prompt rows they cover (the chat prefix + the reused audio tokens: same tokens, same positions, bit-identical —
+   single-utterance prefill runs the row-count-independent GEMM order) and prefills only the rows after them
+   (interim.rs:135-146's growing window).  *rows_reused: prompt rows taken over so far. */
+QASR_API int qasr_session_prompt_kv_stats(const qasr_session* s, int64_t* rows_reused);
 /* The audio-embedding rows (projector output, [tokens][text hidden] f32) of the session's last run — a test /
    debugging hook (transcribe.cpp exposes no equivalent).  out = NULL: *n_out = the float count only. */
 QASR_API int qasr_session_audio_embeds(qasr_session* s, float* out, size_t cap, size_t* n_out);

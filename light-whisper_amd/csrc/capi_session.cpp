@@ -296,6 +296,13 @@ QASR_API int qasr_session_encoder_cache_stats(const qasr_session* s, int64_t* st
     });
 }
 
+QASR_API int qasr_session_prompt_kv_stats(const qasr_session* s, int64_t* rows_reused) {
+    return guard([&] {
+        QASR_CHECK(s && rows_reused, QASR_E_INVALID, "null argument");
+        *rows_reused = s->s->prompt_kv_stats().rows_reused;
+    });
+}
+
 QASR_API int qasr_session_audio_embeds(qasr_session* s, float* out, size_t cap, size_t* n_out) {
     return guard([&] {
         QASR_CHECK(s && n_out, QASR_E_INVALID, "null argument");

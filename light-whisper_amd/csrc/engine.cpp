@@ -855,7 +855,31 @@ void Session::run_batch(const float* dpcm, const std::vector<int64_t>& off, cons
     // tokens at the same positions for every utterance, so its K/V is computed once and copied into each
     // utterance's slots; the packed prefill then starts at position P0
     const int P0 = kPromptPrefix + (int)context_.size();
-    const int skip = count >= 4 ? P0 : 0;
+    const int shared = count >= 4 ? P0 : 0;
+    // prompt-KV reuse (round 4; a growing interim window, interim.rs:135-146): a single-utterance run whose encoder
+    // reused the previous run's leading windows (fe.skip_tokens audio rows, bit-identical embeddings) has the same
+    // prompt rows [0, P0 + skip_tokens) at the same positions as that run; single-utterance prefill runs the
+    // row-count-independent order, so their K/V — still in slots [0, …) of this session's cache, which nothing since
+    // has written — are the bits a recomputation would give: the prefill starts after them
+    int reuse = 0;
+    {
+        const uint64_t key[4] = {kv_epoch_, m_->precision_gen, deterministic_gen(), 0};
+        const std::vector<int32_t> head = build_prompt(h, 0, 0, context_);
+        const bool same = kvp_rows_ > 0 && !memcmp(key, kvp_key_, sizeof key) && count == 1 && ec_run_ &&
+                          kvp_prefix_ == std::vector<int32_t>(head.begin(), head.begin() + P0) && kv_reuse_;
+        if (same && fe.skip_tokens > 0) reuse = std::min(P0 + fe.skip_tokens, kvp_rows_);
+        kvp_rows_ = 0;   // valid again only once this run has completed (below)
+    }
+    const int skip = shared ? shared : reuse;
+    // a completed single-utterance run leaves its prompt rows' K/V in slots [0, n_prompt) for the next run
+    auto remember_prompt_kv = [&]() {
+        if (count != 1 || m_->mx()) return;
+        const std::vector<int32_t> head = build_prompt(h, 0, 0, context_);
+        kvp_prefix_.assign(head.begin(), head.begin() + P0);
+        const uint64_t key[4] = {kv_epoch_, m_->precision_gen, deterministic_gen(), 0};
+        memcpy(kvp_key_, key, sizeof key);
+        kvp_rows_ = n_prompt[0];
+    };
     int64_t slots = 0;
     for (int u = 0; u < count; u++) {
         std::vector<int32_t> p = build_prompt(h, fe.n_tok[u], fe.tok_base[u], context_);
@@ -875,7 +899,10 @@ void Session::run_batch(const float* dpcm, const std::vector<int64_t>& off, cons
         out[u].n_prompt = n_prompt[u];
     }
     const int64_t pref = slots + 1;          // slots: utterances, the dummy slot, the shared prefix
-    ensure_kv(slots + 1 + (skip ? P0 : 0));
+    const uint64_t kv_ep = kv_epoch_;
+    ensure_kv(slots + 1 + (shared ? P0 : 0));
+    QASR_CHECK(!reuse || kv_epoch_ == kv_ep, QASR_E_INTERNAL, "prompt-KV reuse across a KV reallocation");
+    kvp_stats_.rows_reused += reuse;
     const int T = (int)ids.size(), H = h.txt_h, V = h.vocab;
     std::vector<int> pos(T), slot(T), kvs(T), kvl(T), last(count);
     for (int u = 0; u < count; u++) {
@@ -931,7 +958,7 @@ void Session::run_batch(const float* dpcm, const std::vector<int64_t>& off, cons
         // GEMM order (every output one block chain in K order), so a prompt row is the same bits in any batch
         StableOrderScope order(count == 1 || batch_inv_);
         sc_.get(S_X, (size_t)std::max(T, P0) * H * sizeof(float));
-        if (skip) {
+        if (shared) {
             const std::vector<int32_t> full = build_prompt(h, 0, 0, context_);
             std::vector<int32_t> pid(full.begin(), full.begin() + P0);
             std::vector<int> ppos(P0), pslot(P0), pkvs(P0, (int)pref), pkvl(P0);
@@ -1002,6 +1029,7 @@ void Session::run_batch(const float* dpcm, const std::vector<int64_t>& off, cons
         UttResult& r = out[0];
         r.raw = m_->tok.decode(r.tokens.data(), (int)r.tokens.size());
         Tokenizer::parse(r.raw, r.language, r.text);
+        remember_prompt_kv();
         return;
     }
     // continuous-batching greedy decode: rows = a bucket of the active count (padding rows are dummies); the
@@ -1095,6 +1123,7 @@ void Session::run_batch(const float* dpcm, const std::vector<int64_t>& off, cons
         r.raw = m_->tok.decode(r.tokens.data(), (int)r.tokens.size());
         Tokenizer::parse(r.raw, r.language, r.text);
     }
+    remember_prompt_kv();
 }
 
 void Session::run_host(const std::vector<const float*>& pcm, const std::vector<int64_t>& len, int max_new,
@@ -1212,6 +1241,7 @@ void Session::encode_host(const float* mel, int t_pad, int t_valid, std::vector<
 }
 
 void Session::prefill_logits_host(const float* embeds, int n, std::vector<float>& logits) {
+    kvp_rows_ = 0;   // writes K/V rows from slot 0 (no prompt-KV reuse after it)
     const qasr_hparams& h = m_->hp;
     QASR_CHECK(n > 0 && n <= n_ctx_, QASR_E_CAPACITY, "prefill length exceeds n_ctx");
     ensure_kv(n);
@@ -1239,6 +1269,7 @@ void Session::prefill_logits_host(const float* embeds, int n, std::vector<float>
 // logits [n_forced + 1][V]
 void Session::forced_logits_host(const float* pcm, int64_t n, const int32_t* forced, int n_forced,
                                  std::vector<float>& logits, bool one_pass) {
+    kvp_rows_ = 0;   // writes K/V rows from slot 0 (no prompt-KV reuse after it)
     const qasr_hparams& h = m_->hp;
     const int H = h.txt_h, V = h.vocab;
     float* d = (float*)sc_.get(S_PCM, (size_t)n * sizeof(float));

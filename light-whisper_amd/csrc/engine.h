@@ -95,6 +95,11 @@ class Session {
         int64_t runs = 0, windows_reused = 0, windows_computed = 0;
     };
     const EncCacheStats& enc_cache_stats() const { return ecstats_; }
+    // prompt rows whose K/V a single-utterance run took from the previous run instead of prefilling them
+    struct PromptKvStats {
+        int64_t rows_reused = 0;
+    };
+    const PromptKvStats& prompt_kv_stats() const { return kvp_stats_; }
     // the audio-embedding rows (projector output, [tokens][H]) of the last single-utterance run (tests)
     std::vector<float> last_audio_embeds();
     hipStream_t stream() const { return st_; }
@@ -192,7 +197,14 @@ class Session {
     float* ec_emb_ = nullptr;
     size_t ec_cap_ = 0;
     EncCacheStats ecstats_;
+    PromptKvStats kvp_stats_;
     int last_audio_tokens_ = 0;
+    // prompt-KV reuse (run_batch): rows [0, kvp_rows_) of the KV cache hold the last completed single-utterance run's
+    // prompt K/V, valid while kvp_key_ (KV epoch, precision, determinism) and the prompt prefix still match
+    int kvp_rows_ = 0;
+    uint64_t kvp_key_[4] = {~0ull, ~0ull, ~0ull, ~0ull};
+    std::vector<int32_t> kvp_prefix_;
+    bool kv_reuse_ = getenv("QASR_NO_PROMPT_KV_REUSE") == nullptr;
     // scratch epoch, KV epoch, precision gen, determinism gen, split-attention scratch epoch + batch invariance
     uint64_t graph_key_[5] = {~0ull, ~0ull, ~0ull, ~0ull, ~0ull};
     uint64_t kv_epoch_ = 0;

@@ -120,6 +120,7 @@ SIGNATURES = {
     "qasr_session_draft_stats": (C.c_int, [P, C.POINTER(C.c_int64)]),
     "qasr_session_set_encoder_cache": (C.c_int, [P, I32]),
     "qasr_session_encoder_cache_stats": (C.c_int, [P, C.POINTER(C.c_int64)]),
+    "qasr_session_prompt_kv_stats": (C.c_int, [P, C.POINTER(C.c_int64)]),
     "qasr_session_audio_embeds": (C.c_int, [P, P, SZ, C.POINTER(SZ)]),
     "qasr_parse_transcript": (C.c_int, [C.c_char_p, SZ, C.c_char_p, SZ, C.POINTER(SZ), C.c_char_p, SZ,
                                         C.POINTER(SZ)]),

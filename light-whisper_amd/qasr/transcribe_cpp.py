@@ -228,6 +228,12 @@ class Session:
         check(_lib.load().qasr_session_encoder_cache_stats(self._h, st))
         return dict(zip(("runs", "windows_reused", "windows_computed"), list(st)))
 
+    def prompt_kv_rows_reused(self) -> int:
+        """prompt rows whose K/V runs took over from the previous run (growing windows with the encoder cache)"""
+        n = C.c_int64(0)
+        check(_lib.load().qasr_session_prompt_kv_stats(self._h, C.byref(n)))
+        return int(n.value)
+
     def audio_embeds(self) -> np.ndarray:
         """the audio-embedding rows [tokens][hidden] of this session's last run"""
         lib, n = _lib.load(), C.c_size_t(0)
