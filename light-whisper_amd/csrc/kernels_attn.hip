@@ -15,6 +15,12 @@
 #include "qk_rope.h"
 #include "xlane.h"
 
+// decode rows from which the fused decode attention takes the 32-key-chunk kernel (4 waves per SIMD) instead of the
+// 64-key one (3 per SIMD, one chunk for per-wave ranges of 33–64 keys)
+#ifndef QASR_ATTN_CK32_ROWS
+#define QASR_ATTN_CK32_ROWS 192
+#endif
+
 namespace qasr {
 
 __device__ __forceinline__ void wave_sync_lds() {
@@ -832,7 +838,7 @@ void attention_decode_fused(const QkFuse& fz, int ldkv, const int* kv_start, con
     // many rows (≥ 192: ≥ 1,536 workgroups) → the 32-key-chunk kernel, 103 VGPRs and 4 waves per SIMD instead of 3
     // (tools/attn_batch.py, profiles/r2_attn_batch_chunk.jsonl: 256 rows 35.9 → 31.2 µs); fewer rows → the 64-key
     // kernel, which still runs its ≤ 32-key waves in 32-key chunks (1 key 6.35 → 5.37 µs)
-    const bool ck32 = rows >= 192 && !fz.fixed_chunk;
+    const bool ck32 = rows >= QASR_ATTN_CK32_ROWS && !fz.fixed_chunk;
     // (a 5-waves-per-SIMD build of the 32-key kernel, 95 VGPRs, streamed the same: 31.1 against 31.5 µs at 256
     // rows, profiles/r2s2_attn_occupancy_ab.jsonl — the kernel is not occupancy-bound)
     if (G == 2 && ck32)
