@@ -805,7 +805,7 @@ static void launch_attention(int G, int rows, hipStream_t s, const __half* Q, in
         case 1: k_attention<HD, 1, 1><<<b1, 256, 0, s>>>(Q, ldq, K, V, ldkv, kv_start, kv_len, rows, nh, nkv, scale, o, oq, od); break;
         // the fused decode kernel's chunk policy (attention_decode_fused), so the two paths stay bit-identical
         case 2:
-            if (HD == 128 && rows >= 192)
+            if (HD == 128 && rows >= QASR_ATTN_CK32_ROWS)
                 k_attention<HD, 2, 4, false, 32><<<b4, 256, 0, s>>>(Q, ldq, K, V, ldkv, kv_start, kv_len, rows, nh, nkv,
                                                                      scale, o, oq, od);
             else
@@ -813,7 +813,7 @@ static void launch_attention(int G, int rows, hipStream_t s, const __half* Q, in
                                                          oq, od);
             break;
         case 4:
-            if (HD == 128 && rows >= 192)
+            if (HD == 128 && rows >= QASR_ATTN_CK32_ROWS)
                 k_attention<HD, 4, 4, false, 32><<<b4, 256, 0, s>>>(Q, ldq, K, V, ldkv, kv_start, kv_len, rows, nh, nkv,
                                                                      scale, o, oq, od);
             else
