@@ -2,7 +2,8 @@
 // Rust process drives over the C ABI, in C++ here because the image has no Rust toolchain.  One
 // process per GPU (RANK / WORLD_SIZE / LOCAL_RANK as torchrun sets them):
 //   1. the 128-byte RCCL unique id handed over through a file (qasr/dist.py file_exchange's protocol:
-//      <QASR_RDV_DIR|TMPDIR|/tmp>/qasr_uid_<TORCHELASTIC_RUN_ID>_<MASTER_PORT>.bin, written under a temporary name and
+//      <QASR_RDV_DIR|TMPDIR|/tmp>/qasr_uid_<TORCHELASTIC_RUN_ID>_<MASTER_PORT>_<launcher pid>.bin (or
+//      qasr_uid_<QASR_RDV_KEY>.bin), written under a temporary name and
 //      renamed), qasr_dist_init;
 //   2. rank 0 loads (or generates) the model, every other rank opens a shell of the same layout and receives the
 //      weight blob in ONE broadcast (qasr_dist_broadcast_weights: checksums compared);
@@ -60,9 +61,12 @@ std::string uid_path() {
     const char* dir = getenv("QASR_RDV_DIR");
     if (!dir || !*dir) dir = getenv("TMPDIR");
     if (!dir || !*dir) dir = "/tmp";
+    if (const char* k = getenv("QASR_RDV_KEY"); k && *k) return std::string(dir) + "/qasr_uid_" + k + ".bin";
     const char* run = getenv("TORCHELASTIC_RUN_ID");
     const char* port = getenv("MASTER_PORT");
-    return std::string(dir) + "/qasr_uid_" + (run && *run ? run : "run") + "_" + (port && *port ? port : "0") + ".bin";
+    // + the launcher's pid (torchrun's agent is every rank's parent): never a stale file of an earlier launch
+    return std::string(dir) + "/qasr_uid_" + (run && *run ? run : "run") + "_" + (port && *port ? port : "0") + "_" +
+           std::to_string(getppid()) + ".bin";
 }
 
 void exchange_uid(uint8_t id[128], int rank, const std::string& path, double timeout_s) {

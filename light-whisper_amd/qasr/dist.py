@@ -199,14 +199,19 @@ def file_exchange(rank: int, world: int, key: str | None = None, directory: str 
     publishes its bytes in `<directory>/qasr_uid_<key>.bin` — written under a temporary name and renamed, so a reader
     never sees a partial file — and every other rank polls for the file.  This is what a host without torch (the Rust
     app) does with a file or a pipe of its own.  `key` defaults to the launcher's rendezvous
-    (TORCHELASTIC_RUN_ID + MASTER_PORT, fresh for every launch), `directory` to $QASR_RDV_DIR or the temp dir.
+    (TORCHELASTIC_RUN_ID + MASTER_PORT + the launcher's pid, fresh for every launch; $QASR_RDV_KEY overrides),
+    `directory` to $QASR_RDV_DIR or the temp dir.
     Rank 0 removes the file once its communicator exists (ncclCommInitRank returns only when every rank joined, i.e.
     after every rank has read it): call `exchange.cleanup()` then."""
     import os
     import tempfile
 
     if key is None:
-        key = f"{os.environ.get('TORCHELASTIC_RUN_ID', 'run')}_{os.environ.get('MASTER_PORT', '0')}"
+        # the launch's rendezvous + the launcher's pid (torchrun's agent is every rank's parent): a file a crashed
+        # earlier launch left behind under the same run id and port is never taken for this one's.  QASR_RDV_KEY
+        # overrides (ranks started by separate launchers)
+        key = os.environ.get("QASR_RDV_KEY") or (f"{os.environ.get('TORCHELASTIC_RUN_ID', 'run')}_"
+                                                 f"{os.environ.get('MASTER_PORT', '0')}_{os.getppid()}")
     directory = directory or os.environ.get("QASR_RDV_DIR") or tempfile.gettempdir()
     path = os.path.join(directory, f"qasr_uid_{key}.bin")
 

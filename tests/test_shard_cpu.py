@@ -127,6 +127,30 @@ def test_file_unique_id_exchange(tmp_path):
     assert not os.path.exists(x.path) and not [f for f in os.listdir(tmp_path) if f.endswith(".tmp")]
 
 
+def test_file_unique_id_default_key_is_launch_unique(tmp_path):
+    """the default key (run id + master port + the launcher's pid): ranks started by one launcher agree on it (the
+    exchange goes through), and a stale file an earlier launch left under the same run id and port is not read"""
+    import multiprocessing as mp
+
+    sys.path.insert(0, os.path.join(ROOT, "light-whisper_amd"))
+    from qasr import dist as qdist
+
+    stale = os.path.join(str(tmp_path), "qasr_uid_run_0.bin")   # round 3's key format
+    with open(stale, "wb") as f:
+        f.write(bytes([7]) * 128)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_xchg_rank, args=(r, 2, None, str(tmp_path), q)) for r in (1, 0)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=60) for _ in range(2))
+    for p in procs:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    assert out[1] == bytes(range(128))
+    assert qdist.file_exchange(0, 2, directory=str(tmp_path)).path.endswith(f"_{os.getppid()}.bin")
+
+
 def test_workload_deterministic():
     a = bench.make_workload(2, 1)
     b = bench.make_workload(2, 1)
