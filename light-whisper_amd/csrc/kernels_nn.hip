@@ -97,63 +97,6 @@ __global__ __launch_bounds__(256) void k_rmsnorm_q8_wg(const float* __restrict__
     rms_row_q8_wg<KC>(x + (size_t)row * ldx, H, w, eps, q + (size_t)row * H, d + (size_t)row * (H / 32), part);
 }
 
-// One wave per row with EXACTLY the workgroup kernel's arithmetic (round 4): lane l plays threads l, l+64, l+128 and
-// l+192 of k_rmsnorm_q8_wg's 256 (their float4 chunks t + 256k), sums each one's squares in the same order, reduces
-// each of the four by the same wave tree and adds the four as the workgroup adds its waves' partials, then quantises
-// every chunk in the same 8-lane blocks — the same bits per row, without the LDS round trip and the barrier; all of a
-// lane's loads in flight at once.
-#ifndef QASR_RMS_WAVE
-#define QASR_RMS_WAVE 1
-#endif
-template <int KC>
-__global__ __launch_bounds__(256) void k_rmsnorm_q8_wv(const float* __restrict__ x, int M, int H, int ldx,
-                                                       const float* __restrict__ w, float eps, int8_t* __restrict__ q,
-                                                       float* __restrict__ d) {
-    const int lane = threadIdx.x & 63;
-    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (row >= M) return;   // wave-uniform
-    const int nc = H / 4;
-    const float4* x4 = (const float4*)(x + (size_t)row * ldx);
-    const float4* g4 = (const float4*)w;
-    float4 v[4][KC], gw[4][KC];
-#pragma unroll
-    for (int t4 = 0; t4 < 4; t4++)
-#pragma unroll
-        for (int k = 0; k < KC; k++) {
-            const int c = lane + 64 * t4 + 256 * k;
-            v[t4][k] = c < nc ? x4[c] : make_float4(0.f, 0.f, 0.f, 0.f);
-            gw[t4][k] = c < nc ? g4[c] : make_float4(0.f, 0.f, 0.f, 0.f);
-        }
-    float part[4];
-#pragma unroll
-    for (int t4 = 0; t4 < 4; t4++) {
-        float ss = 0.f;
-#pragma unroll
-        for (int k = 0; k < KC; k++)
-            ss = __fadd_rn(ss, __fadd_rn(__fadd_rn(__fmul_rn(v[t4][k].x, v[t4][k].x), __fmul_rn(v[t4][k].y, v[t4][k].y)),
-                                         __fadd_rn(__fmul_rn(v[t4][k].z, v[t4][k].z), __fmul_rn(v[t4][k].w, v[t4][k].w))));
-        part[t4] = wave_sum(ss);
-    }
-    const float ss = __fadd_rn(__fadd_rn(part[0], part[1]), __fadd_rn(part[2], part[3]));
-    const float inv = __fdiv_rn(1.0f, __fsqrt_rn(__fadd_rn(__fdiv_rn(ss, (float)H), eps)));
-    int8_t* qr = q + (size_t)row * H;
-    float* dr = d + (size_t)row * (H / 32);
-#pragma unroll
-    for (int t4 = 0; t4 < 4; t4++)
-#pragma unroll
-        for (int k = 0; k < KC; k++) {
-            const int c = lane + 64 * t4 + 256 * k;
-            if (256 * k + ((64 * t4 + lane) & ~7) < nc) {   // 8-lane blocks are all in or all out (nc % 8 == 0)
-                const float4 g = gw[t4][k];
-                const float4 y = make_float4(__fmul_rn(__fmul_rn(v[t4][k].x, inv), g.x),
-                                             __fmul_rn(__fmul_rn(v[t4][k].y, inv), g.y),
-                                             __fmul_rn(__fmul_rn(v[t4][k].z, inv), g.z),
-                                             __fmul_rn(__fmul_rn(v[t4][k].w, inv), g.w));
-                quant4_store(y, c, lane, qr, dr);
-            }
-        }
-}
-
 void rmsnorm_q8(const float* x, int M, int H, int ldx, const float* w, float eps, int8_t* q, float* d, hipStream_t s,
                 float* zero, int64_t nzero) {
     if (M <= 0) return;
@@ -163,11 +106,6 @@ void rmsnorm_q8(const float* x, int M, int H, int ldx, const float* w, float eps
     // a workgroup per row for every row count (round 4): the wave-per-row kernel below sums the squares in another
     // order, so a prefill of > 2,048 rows (a batch) rounded a row differently from the same row in a smaller one —
     // the batch-invariant contract needs one reduction order per row width
-    if (QASR_RMS_WAVE && kc <= 2 && !(zero && nzero)) {   // (a lane holds 8·kc float4 of the row and its weights)
-        if (kc <= 1) k_rmsnorm_q8_wv<1><<<cdiv(M, 4), 256, 0, s>>>(x, M, H, ldx, w, eps, q, d);
-        else k_rmsnorm_q8_wv<2><<<cdiv(M, 4), 256, 0, s>>>(x, M, H, ldx, w, eps, q, d);
-        return;
-    }
     if (kc <= 4) {
         float4* z = zero ? (float4*)zero : nullptr;
         const int64_t nz = zero ? nzero / 4 : 0;

@@ -214,7 +214,7 @@ def test_linear_fused_epilogues(torch_dev, m, n, k, cfg):
 
 @pytest.mark.parametrize("m,h", [(9, 2048), (256, 1024), (5, 896), (3000, 2048)])
 def test_rmsnorm_q8(torch_dev, m, h):
-    """the norm kernels: wave-per-row (H ≤ 2,048; the workgroup kernel's arithmetic) and workgroup-per-row (wider rows)"""
+    """workgroup-per-row kernel (M <= 2048) and wave-per-row kernel (larger M)"""
     import torch
 
     rng = np.random.default_rng(3)
