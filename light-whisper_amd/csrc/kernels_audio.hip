@@ -334,7 +334,15 @@ __global__ __launch_bounds__(256) void k_conv3x3_gelu_c32(const __half* __restri
 // 256×160: 20.6 → 16.1 → 15.0 ms per C4 step.  LDS image: 192-B rows (no pad), 16-B chunk c of row r at chunk
 // c ^ ((r >> 1) & 3): every ds_read_b128 fragment lane group ({0–3,12–15,20–27}, … — MI355X_MICROARCH.md §LDS) and
 // every ds_write_b128 8-lane group hits distinct banks (the previous 208-B padded rows were 2-way on both; r2 PMC:
-// 3.6 conflict cycles per LDS instruction).
+// 3.6 conflict cycles per LDS instruction).  Two LDS buffers (156 KB, one workgroup per CU as the 216 VGPRs allow
+// anyway): step st+1's registers go into the other buffer right after step st's MFMAs, so one barrier per step
+// instead of two; the MFMA order is unchanged (same bits).
+// Tile order: the ⌈C/160⌉ column tiles of one position tile are consecutive logical tiles, and logical tiles are
+// dealt to the XCDs in contiguous ranges (workgroup b runs on XCD b mod 8), so the column tiles that gather the same
+// activation panel run side by side behind one L2 instead of on three XCDs that each fetch it.
+#ifndef QASR_CONV_XCD
+#define QASR_CONV_XCD 1
+#endif
 constexpr int CV_BM = 256, CV_BN = 160, CV_BK = 96, CV_LD = CV_BK, CV_TJ = CV_BN / 32, CV_NT = 512;
 __device__ __forceinline__ int cv_swz(int row) { return (row >> 1) & 3; }
 constexpr int CV_ACH = CV_BM * (CV_BK / 8) / CV_NT;                  // 6 A chunks of 16 B per thread
@@ -343,13 +351,20 @@ constexpr int CV_BCH = (CV_BN * (CV_BK / 8) + CV_NT - 1) / CV_NT;            // 
 __global__ __launch_bounds__(CV_NT) void k_conv3x3_gelu(const __half* __restrict__ in, int n_chunks, int Hi, int Wi,
                                                       const __half* __restrict__ w, const float* __restrict__ bias,
                                                       int C, void* __restrict__ out, int out_mode) {
-    __shared__ __attribute__((aligned(16))) _Float16 As[1][CV_BM * CV_LD];
-    __shared__ __attribute__((aligned(16))) _Float16 Bs[1][CV_BN * CV_LD];
+    __shared__ __attribute__((aligned(16))) _Float16 As[2][CV_BM * CV_LD];
+    __shared__ __attribute__((aligned(16))) _Float16 Bs[2][CV_BN * CV_LD];
     const int Ho = (Hi + 1) / 2, Wo = (Wi + 1) / 2;
     const int M = n_chunks * Ho * Wo;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wr = wave >> 1, wc = wave & 1;
-    const int n0 = blockIdx.x * CV_BN, m0 = blockIdx.y * CV_BM;
+    const int nct = (C + CV_BN - 1) / CV_BN;
+#if QASR_CONV_XCD
+    const int total = gridDim.x, xcd = blockIdx.x % 8, q = total / 8, r = total % 8;
+    const int t = xcd * q + min(xcd, r) + blockIdx.x / 8;   // a bijection: XCD x holds q (+1 if x < r) tiles
+#else
+    const int t = blockIdx.x;
+#endif
+    const int n0 = (t % nct) * CV_BN, m0 = (t / nct) * CV_BM;
     constexpr int SEG = CV_BK / 8;   // 16-byte chunks per row per step
     // per staged A chunk: its output position, decoded once
     int a_base[CV_ACH], a_oy[CV_ACH], a_ox[CV_ACH];
@@ -419,8 +434,8 @@ __global__ __launch_bounds__(CV_NT) void k_conv3x3_gelu(const __half* __restrict
     __syncthreads();
     for (int st = 0; st < steps; st++) {
         gload(min(st + 1, steps - 1));   // unconditional (the last one is a harmless repeat)
-        const _Float16* as = As[0];
-        const _Float16* bs = Bs[0];
+        const _Float16* as = As[st & 1];
+        const _Float16* bs = Bs[st & 1];
 #pragma unroll
         for (int ks = 0; ks < CV_BK / 32; ks++) {
             v8h a[4], b[CV_TJ];
@@ -436,11 +451,9 @@ __global__ __launch_bounds__(CV_NT) void k_conv3x3_gelu(const __half* __restrict
                 for (int j = 0; j < CV_TJ; j++)
                     acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[i], b[j], acc[i][j], 0, 0, 0);
         }
+        // buffer (st+1)&1 was last read in step st−1, which every wave finished before the previous barrier
+        if (st + 1 < steps) lstore((st + 1) & 1);
         __syncthreads();
-        if (st + 1 < steps) {
-            lstore(0);
-            __syncthreads();
-        }
     }
 #pragma unroll
     for (int i = 0; i < 4; i++) {
@@ -472,8 +485,7 @@ void conv3x3_gelu(const __half* in, int n_chunks, int Hi, int Wi, const __half* 
     QASR_CHECK(C % 32 == 0, QASR_E_INVALID, "conv channels must be a multiple of 32");
     ProfScope ps(s, "conv3x3_f16", 2.0 * M * C * 9.0 * C, (double)M * 9 * C * 2 / 4 + (double)M * C * 2);
     if (C % CV_BK == 0) {
-        dim3 grid(cdiv(C, CV_BN), cdiv(M, CV_BM));
-        k_conv3x3_gelu<<<grid, CV_NT, 0, s>>>(in, n_chunks, Hi, Wi, w, b, C, out, out_mode);
+        k_conv3x3_gelu<<<cdiv(C, CV_BN) * cdiv(M, CV_BM), CV_NT, 0, s>>>(in, n_chunks, Hi, Wi, w, b, C, out, out_mode);
     } else {
         dim3 grid(cdiv(C, CT), cdiv(M, CT));
         k_conv3x3_gelu_c32<<<grid, 256, 0, s>>>(in, n_chunks, Hi, Wi, w, b, C, out, out_mode);
