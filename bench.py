@@ -220,6 +220,12 @@ def pmc_evidence(kernel):
             "hbm_bytes_per_launch": round(hbm_bytes / launches) if launches else None}
 
 
+def share_cards():
+    """QASR_DIST_SHARE_CARDS=1 (test only): ranks beyond the visible GPUs share cards with any backend — with the
+    native backend RCCL then refuses the communicator on every rank, which exercises the agreed fallback below."""
+    return os.environ.get("QASR_DIST_SHARE_CARDS") == "1"
+
+
 def launch_ranks(argv, n, dry_run=False):
     """`bench.py --gpus N` started without WORLD_SIZE (N > 1): run N fresh child ranks under torch.distributed.run
     (127.0.0.1 rendezvous) and return their exit code.  Called BEFORE this process touches the GPU (counting devices
@@ -229,7 +235,7 @@ def launch_ranks(argv, n, dry_run=False):
     import subprocess
 
     backend = os.environ.get("QASR_DIST_BACKEND", "native")
-    if not dry_run and backend != "gloo":
+    if not dry_run and backend != "gloo" and not share_cards():
         import torch
 
         have = torch.cuda.device_count()
@@ -311,7 +317,7 @@ def main():
     if backend not in ("native", "torch-nccl", "gloo"):
         print(f"bench.py: unknown QASR_DIST_BACKEND={backend}", file=sys.stderr, flush=True)
         sys.exit(2)
-    if backend == "gloo":
+    if backend == "gloo" or share_cards():
         local = local % torch.cuda.device_count()
     torch.cuda.set_device(local)
     coll_dev = torch.device("cuda", local) if backend == "torch-nccl" else torch.device("cpu")
@@ -352,13 +358,32 @@ def main():
 
         model = Model.synthetic(args.arch, seed=0) if rank == 0 else Model.shell(args.arch)
         if backend == "native":
-            xchg = qdist.file_exchange(rank, world)
-            comm = qdist.NativeComm(rank, world, local, xchg)
-            xchg.cleanup()
-            collectives["weight_broadcast"] = comm.broadcast_weights(model)
+            # an error on any rank (communicator or broadcast) is agreed over the gloo group, which does not depend
+            # on RCCL, and every rank then falls back to the host-staged gloo collectives together — a rank that
+            # went on alone into an RCCL collective would block the job
+            err = None
+            try:
+                xchg = qdist.file_exchange(rank, world)
+                comm = qdist.NativeComm(rank, world, local, xchg)
+                xchg.cleanup()   # after the collective init: every rank has read the id
+                collectives["weight_broadcast"] = comm.broadcast_weights(model)
+            except Exception as e:  # noqa: BLE001 — reported in the line, never silent
+                err = f"{type(e).__name__}: {e}"
+            ok = torch.tensor([0 if err else 1], dtype=torch.int32)
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+            if not int(ok.item()):
+                if comm is not None:
+                    comm.close()
+                    comm = None
+                print(f"bench.py rank {rank}: native RCCL collectives failed ({err or 'on another rank'}); "
+                      "falling back to host-staged gloo collectives", file=sys.stderr, flush=True)
+                collectives["native_error"] = err or "failed on another rank"
+                backend = "native-fallback"
+                collectives["weight_broadcast"] = qdist.broadcast_weights(model, rank, torch.device("cuda", local))
         else:
             collectives["weight_broadcast"] = qdist.broadcast_weights(model, rank, torch.device("cuda", local))
         collectives["backend"] = {"native": "libqasr-rccl (file unique-id hand-off) + gloo barrier",
+                                  "native-fallback": "gloo (host-staged) after the native RCCL path failed",
                                   "torch-nccl": "torch nccl", "gloo": "gloo rehearsal"}[backend]
     else:
         model = Model.synthetic(args.arch, seed=0)
