@@ -361,23 +361,24 @@ def main():
             # an error on any rank (communicator or broadcast) is agreed over the gloo group, which does not depend
             # on RCCL, and every rank then falls back to the host-staged gloo collectives together — a rank that
             # went on alone into an RCCL collective would block the job
-            err = None
-            try:
+            def native():
                 xchg = qdist.file_exchange(rank, world)
-                comm = qdist.NativeComm(rank, world, local, xchg)
+                c = qdist.NativeComm(rank, world, local, xchg)
                 xchg.cleanup()   # after the collective init: every rank has read the id
-                collectives["weight_broadcast"] = comm.broadcast_weights(model)
-            except Exception as e:  # noqa: BLE001 — reported in the line, never silent
-                err = f"{type(e).__name__}: {e}"
-            ok = torch.tensor([0 if err else 1], dtype=torch.int32)
-            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
-            if not int(ok.item()):
-                if comm is not None:
-                    comm.close()
-                    comm = None
-                print(f"bench.py rank {rank}: native RCCL collectives failed ({err or 'on another rank'}); "
+                holder.append(c)
+                return c.broadcast_weights(model)
+
+            holder = []
+            info, err = qdist.agreed_attempt(native)
+            if err is None:
+                comm = holder[0]
+                collectives["weight_broadcast"] = info
+            else:
+                if holder:
+                    holder[0].close()
+                print(f"bench.py rank {rank}: native RCCL collectives failed ({err}); "
                       "falling back to host-staged gloo collectives", file=sys.stderr, flush=True)
-                collectives["native_error"] = err or "failed on another rank"
+                collectives["native_error"] = err
                 backend = "native-fallback"
                 collectives["weight_broadcast"] = qdist.broadcast_weights(model, rank, torch.device("cuda", local))
         else:

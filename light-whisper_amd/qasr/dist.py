@@ -87,6 +87,27 @@ def broadcast_weights(model, rank: int, device, src: int = 0) -> dict:
     return info
 
 
+def agreed_attempt(attempt, group=None):
+    """Run `attempt()` on every rank and agree on the outcome over `group` (default: the default process group — a
+    gloo group, so the agreement does not depend on the RCCL path being tried).  Returns (result, None) on every rank
+    when every rank succeeded, else (None, error text) on every rank — the failing rank's exception, or "failed on
+    another rank" — so all ranks take the fallback together instead of one going on alone into a collective that
+    would block the job (bench.py: the native communicator + weight broadcast)."""
+    import torch
+    import torch.distributed as dist
+
+    result, err = None, None
+    try:
+        result = attempt()
+    except Exception as e:  # noqa: BLE001 — returned to the caller, never silent
+        err = f"{type(e).__name__}: {e}"
+    ok = torch.tensor([0 if err else 1], dtype=torch.int32)
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=group)
+    if int(ok.item()):
+        return result, None
+    return None, err or "failed on another rank"
+
+
 def gather_token_streams(streams: list[list[int]], device) -> list[list[list[int]]]:
     """All-gather every rank's per-segment token ids; returns, on every rank, [rank][segment] -> ids."""
     import torch

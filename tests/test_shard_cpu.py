@@ -200,6 +200,54 @@ def test_weight_broadcast_and_token_gather_gloo(world):
         assert got == want
 
 
+def _agree_rank(rank, world, port, fail_rank, q):
+    import torch.distributed as dist
+
+    sys.path.insert(0, os.path.join(ROOT, "light-whisper_amd"))
+    from qasr import dist as qdist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    def attempt():
+        if rank == fail_rank:
+            raise RuntimeError("ncclCommInitRank: invalid usage")
+        return {"rank": rank}
+
+    got = qdist.agreed_attempt(attempt)
+    # the ranks must still be in step afterwards: one more collective completes on all of them
+    after = qdist.gather_token_streams([[rank]], __import__("torch").device("cpu"))
+    q.put((rank, got, after))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,fail_rank", [(2, 1), (3, 0), (3, -1)])
+def test_native_failure_is_agreed_by_every_rank(world, fail_rank):
+    """bench.py's native-RCCL attempt (communicator + weight broadcast) is agreed over the gloo group: an error on
+    ANY rank makes every rank return the fallback verdict together (no rank goes on alone into a collective that
+    would block), and with no error every rank keeps its own result"""
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_agree_rank, args=(r, world, port, fail_rank, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = sorted((q.get(timeout=120) for _ in range(world)), key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, (res, err), after in out:
+        assert after == [[[r]] for r in range(world)]
+        if fail_rank < 0:
+            assert res == {"rank": rank} and err is None
+        else:
+            assert res is None
+            assert err == ("RuntimeError: ncclCommInitRank: invalid usage" if rank == fail_rank
+                           else "failed on another rank")
+
+
 def _prob_gather_rank(rank, world, port, q):
     import torch
     import torch.distributed as dist
