@@ -358,24 +358,16 @@ def main():
 
         model = Model.synthetic(args.arch, seed=0) if rank == 0 else Model.shell(args.arch)
         if backend == "native":
-            # an error on any rank (communicator or broadcast) is agreed over the gloo group, which does not depend
-            # on RCCL, and every rank then falls back to the host-staged gloo collectives together — a rank that
-            # went on alone into an RCCL collective would block the job
-            def native():
-                xchg = qdist.file_exchange(rank, world)
-                c = qdist.NativeComm(rank, world, local, xchg)
-                xchg.cleanup()   # after the collective init: every rank has read the id
-                holder.append(c)
-                return c.broadcast_weights(model)
-
-            holder = []
-            info, err = qdist.agreed_attempt(native)
+            # the native path in three steps, each agreed over the gloo group (which does not depend on RCCL) before
+            # the next collective starts: (1) the unique-id hand-off through the file, (2) the communicator init,
+            # (3) the weight broadcast.  An error on any rank makes every rank fall back to the host-staged gloo
+            # collectives together, and no rank enters RCCL's init unless every rank holds the id (a rank alone in
+            # a blocking collective would hang the job).  A rank that fails INSIDE RCCL's blocking init is the one
+            # case this cannot cover.
+            comm, info, err = qdist.native_setup(rank, world, local, model, qdist.file_exchange(rank, world))
             if err is None:
-                comm = holder[0]
                 collectives["weight_broadcast"] = info
             else:
-                if holder:
-                    holder[0].close()
                 print(f"bench.py rank {rank}: native RCCL collectives failed ({err}); "
                       "falling back to host-staged gloo collectives", file=sys.stderr, flush=True)
                 collectives["native_error"] = err

@@ -362,7 +362,13 @@ QASR_API int qasr_get_deterministic(int32_t* on);
    qasr_dist_gather_tokens: every rank's segments' token ids ([n_seg] lengths + the flat ids, host arrays) to every
    rank, in rank order: rank_segs [world] = segments per rank; with all_lens / all_tokens NULL only the totals are
    reported (*n_segs_out, *n_tokens_out), then call again with buffers of that size.  Not in the reference (it runs
-   one process, one device, one utterance). */
+   one process, one device, one utterance).
+   qasr_dist_agree: status agreement before a collective — every rank passes its local status (0 = this rank's
+   previous step succeeded, anything else = it failed) and gets *any_failed = 1 on every rank if any rank's was
+   nonzero (one all-gather of an int32).  A host calls it before each collective after the communicator exists
+   (weight broadcast, probability gather, token gather): a rank whose VAD or batch failed then makes every rank
+   return an error instead of leaving the others blocked inside the next collective (the reference's crash
+   detection, funasr_service.rs:1367-1385, sees one process exit; engine_longform.cpp is the worked example). */
 typedef struct qasr_comm qasr_comm;
 typedef struct {
     uint64_t bytes;      /* blob bytes broadcast */
@@ -379,6 +385,7 @@ QASR_API int qasr_dist_broadcast_weights(qasr_comm* c, qasr_model* m, int32_t ro
 QASR_API int qasr_dist_gather_tokens(qasr_comm* c, const int32_t* lens, int32_t n_seg, const int32_t* tokens,
                                      int32_t* rank_segs /* [world] */, int32_t* all_lens, size_t lens_cap,
                                      int32_t* all_tokens, size_t tokens_cap, size_t* n_segs_out, size_t* n_tokens_out);
+QASR_API int qasr_dist_agree(qasr_comm* c, int32_t local_status, int32_t* any_failed);
 
 /* -------------------------------------------------------------------------------------------- profiling */
 /* live per-kernel-class timing (hipEvents on each instrumented launch's stream) + algorithmic FLOPs/bytes;

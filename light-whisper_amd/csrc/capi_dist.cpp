@@ -5,7 +5,8 @@
 //     it, the others hold shells of the identical layout, qasr_model_open_shell) — a single large message, the shape
 //     a per-link-bound ring over xGMI wants — then a wrapping 64-bit checksum per rank, all-gathered and compared;
 //   * qasr_dist_gather_tokens: every rank's per-segment token ids to every rank (two all-gathers: the counts, then
-//     the ragged payload padded to the largest rank).
+//     the ragged payload padded to the largest rank);
+//   * qasr_dist_agree: one int32 all-gather of every rank's local status before a collective (failure agreement).
 // Neither runs inside a timed step.  The reference has no multi-GPU path.
 #include <string.h>
 
@@ -212,6 +213,20 @@ QASR_API int qasr_dist_gather_tokens(qasr_comm* c, const int32_t* lens, int32_t 
             os += (size_t)counts[2 * r];
             ot += (size_t)counts[2 * r + 1];
         }
+    });
+}
+
+QASR_API int qasr_dist_agree(qasr_comm* c, int32_t local_status, int32_t* any_failed) {
+    return guard([&] {
+        QASR_CHECK(c && any_failed, QASR_E_INVALID, "bad arguments");
+        const int32_t mine = local_status != 0 ? 1 : 0;
+        DevBuf<int32_t> sts((size_t)c->world);
+        QASR_HIP(hipMemcpyAsync(sts.p + c->rank, &mine, sizeof mine, hipMemcpyHostToDevice, c->st));
+        QASR_NCCL(ncclAllGather(sts.p + c->rank, sts.p, 1, ncclInt32, c->c, c->st));
+        std::vector<int32_t> every((size_t)c->world);
+        QASR_HIP(hipMemcpyAsync(every.data(), sts.p, every.size() * 4, hipMemcpyDeviceToHost, c->st));
+        QASR_HIP(hipStreamSynchronize(c->st));
+        *any_failed = *std::max_element(every.begin(), every.end());
     });
 }
 

@@ -16,8 +16,14 @@
 //   6. the token streams all-gathered (qasr_dist_gather_tokens); rank 0 detokenises, splits language / text
 //      (qasr_parse_transcript) and prints one JSON object.
 // The reference handles one short utterance per request and has no long-form or multi-GPU mode.
-// A rank that fails exits non-zero without entering the next collective; the launcher (torchrun's agent, or the
-// Rust host's own supervisor) must then stop the other ranks, which would otherwise wait in that collective.
+// Failure agreement: once the communicator exists, every step that precedes a collective (model load, VAD, the ASR
+// batch) is a stage whose local outcome all ranks agree on first (qasr_dist_agree: one int32 all-gather) — a rank
+// whose stage failed makes EVERY rank exit non-zero with the failing rank's reason instead of leaving the others
+// blocked in the collective (the reference sees one crashed process, funasr_service.rs:1367-1385).  The stages can be
+// failed on purpose for tests: QASR_FAIL_STAGE=model|vad|asr [QASR_FAIL_RANK=r, default every rank].  At world 1,
+// QASR_LONGFORM_COMM=1 opens a one-rank communicator so the same agreement path runs.  Not covered: a rank that dies
+// inside a collective itself (the launcher's supervisor stops the job then), and a failure before the communicator
+// exists (the unique-id hand-off: rank 0 leaves a ".fail" marker, so the other ranks stop polling at once).
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -69,6 +75,11 @@ std::string uid_path() {
            std::to_string(getppid()) + ".bin";
 }
 
+// rank 0 could not create or publish the id: a marker next to the id file, so the other ranks stop polling at once
+void publish_uid_failure(const std::string& path) {
+    if (FILE* f = fopen((path + ".fail").c_str(), "wb")) fclose(f);
+}
+
 void exchange_uid(uint8_t id[128], int rank, const std::string& path, double timeout_s) {
     if (rank == 0) {
         const std::string tmp = path + "." + std::to_string(getpid()) + ".tmp";
@@ -86,6 +97,10 @@ void exchange_uid(uint8_t id[128], int rank, const std::string& path, double tim
             const size_t got = fread(id, 1, 128, f);
             fclose(f);
             if (got == 128) return;
+        }
+        if (FILE* f = fopen((path + ".fail").c_str(), "rb")) {
+            fclose(f);
+            throw Fail("rank " + std::to_string(rank) + ": rank 0 failed to publish the unique id");
         }
         if (now_ms() - t0 > timeout_s * 1e3) throw Fail("rank " + std::to_string(rank) + ": no unique id at " + path);
         std::this_thread::sleep_for(std::chrono::milliseconds(10));
@@ -165,21 +180,53 @@ int longform_main(const std::string& engine, const std::string& gguf, int argc, 
         ck(qasr_set_device(local), "device");
         const double t_start = now_ms();
         Value info = Value::object();
-        if (world > 1) {
+        if (world > 1 || env_int("QASR_LONGFORM_COMM", 0) != 0) {
             uint8_t id[128] = {0};
             const std::string path = uid_path();
-            if (rank == 0) ck(qasr_dist_unique_id(id, sizeof id), "unique id");
-            exchange_uid(id, rank, path, 600.0);
+            if (rank == 0) {
+                try {
+                    ck(qasr_dist_unique_id(id, sizeof id), "unique id");
+                    exchange_uid(id, rank, path, 600.0);
+                } catch (...) {
+                    publish_uid_failure(path);
+                    throw;
+                }
+            } else {
+                exchange_uid(id, rank, path, 600.0);
+            }
             ck(qasr_dist_init(id, rank, world, local, &comm), "communicator");
             if (rank == 0) remove(path.c_str());   // every rank has joined: the file has been read
         }
+        // a stage: run locally, then (with a communicator) agree on every rank's outcome before the next collective
+        const char* inject_stage = getenv("QASR_FAIL_STAGE");
+        const int inject_rank = env_int("QASR_FAIL_RANK", -1);
+        auto stage = [&](const char* what, auto&& fn) {
+            std::string err;
+            try {
+                if (inject_stage && strcmp(inject_stage, what) == 0 && (inject_rank < 0 || inject_rank == rank))
+                    throw Fail(std::string("injected failure (QASR_FAIL_STAGE=") + what + ")");
+                fn();
+            } catch (const std::exception& e) {
+                err = e.what();
+            }
+            if (comm) {
+                int32_t any = 0;
+                ck(qasr_dist_agree(comm, err.empty() ? 0 : 1, &any), "status agreement");
+                if (any) throw Fail(err.empty() ? std::string(what) + ": failed on another rank" : err);
+            } else if (!err.empty()) {
+                throw Fail(err);
+            }
+        };
         // the model: rank 0 loads / generates, the others receive it into a shell
         const char* arch = engine.c_str();
-        if (rank == 0)
-            ck(gguf.empty() ? qasr_model_open_synthetic(arch, nullptr, 0, &model) : qasr_model_open(gguf.c_str(), "hip", &model),
-               "model");
-        else
-            ck(qasr_model_open_shell(gguf.empty() ? nullptr : gguf.c_str(), arch, nullptr, &model), "model shell");
+        stage("model", [&] {
+            if (rank == 0)
+                ck(gguf.empty() ? qasr_model_open_synthetic(arch, nullptr, 0, &model)
+                                : qasr_model_open(gguf.c_str(), "hip", &model),
+                   "model");
+            else
+                ck(qasr_model_open_shell(gguf.empty() ? nullptr : gguf.c_str(), arch, nullptr, &model), "model shell");
+        });
         if (comm) {
             qasr_dist_info di;
             ck(qasr_dist_broadcast_weights(comm, model, 0, &di), "weight broadcast");
@@ -189,30 +236,34 @@ int longform_main(const std::string& engine, const std::string& gguf, int argc, 
             b.set("checksums_agree", Value::boolean(di.checksums_agree != 0));
             info.set("weight_broadcast", b);
         }
-        ck(qasr_session_open(model, "f16", 32768, &sess), "session");
-        if (inv) ck(qasr_session_set_batch_invariant(sess, 1), "batch invariance");
-        // the recording (every rank reads it: a file, like the app's path-mode requests)
         size_t n = 0;
-        ck(qasr_audio_load_path(wav.c_str(), nullptr, 0, &n), "audio");
-        std::vector<float> pcm(std::max<size_t>(n, 1));
-        ck(qasr_audio_load_path(wav.c_str(), pcm.data(), pcm.size(), &n), "audio");
-        pcm.resize(n);
-        const double t_loaded = now_ms();
-        // 3. halo-sharded VAD
-        ck(qasr_vad_open(nullptr, &vad), "vad");
-        const int64_t T = n_frames((int64_t)n);
-        const int64_t f0 = T * rank / world, f1 = T * (rank + 1) / world;
-        const int64_t h0 = std::max<int64_t>(0, f0 - kHalo), h1 = std::min<int64_t>(T, f1 + kHalo);
-        std::vector<float> core;
-        if (f1 > f0) {
-            std::vector<float> p(h1 - h0);
-            size_t nf = 0;
-            ck(qasr_vad_probabilities(vad, pcm.data() + h0 * kShift, (size_t)((h1 - 1) * kShift + kLen - h0 * kShift),
-                                      p.data(), p.size(), &nf),
-               "vad probabilities");
-            if ((int64_t)nf != h1 - h0) throw Fail("vad: frame count of the halo range");
-            core.assign(p.begin() + (f0 - h0), p.begin() + (f1 - h0));
-        }
+        std::vector<float> pcm, core;
+        double t_loaded = 0;
+        int64_t T = 0;
+        stage("vad", [&] {
+            ck(qasr_session_open(model, "f16", 32768, &sess), "session");
+            if (inv) ck(qasr_session_set_batch_invariant(sess, 1), "batch invariance");
+            // the recording (every rank reads it: a file, like the app's path-mode requests)
+            ck(qasr_audio_load_path(wav.c_str(), nullptr, 0, &n), "audio");
+            pcm.resize(std::max<size_t>(n, 1));
+            ck(qasr_audio_load_path(wav.c_str(), pcm.data(), pcm.size(), &n), "audio");
+            pcm.resize(n);
+            t_loaded = now_ms();
+            // 3. halo-sharded VAD
+            ck(qasr_vad_open(nullptr, &vad), "vad");
+            T = n_frames((int64_t)n);
+            const int64_t f0 = T * rank / world, f1 = T * (rank + 1) / world;
+            const int64_t h0 = std::max<int64_t>(0, f0 - kHalo), h1 = std::min<int64_t>(T, f1 + kHalo);
+            if (f1 > f0) {
+                std::vector<float> p(h1 - h0);
+                size_t nf = 0;
+                ck(qasr_vad_probabilities(vad, pcm.data() + h0 * kShift,
+                                          (size_t)((h1 - 1) * kShift + kLen - h0 * kShift), p.data(), p.size(), &nf),
+                   "vad probabilities");
+                if ((int64_t)nf != h1 - h0) throw Fail("vad: frame count of the halo range");
+                core.assign(p.begin() + (f0 - h0), p.begin() + (f1 - h0));
+            }
+        });
         std::vector<float> probs;
         if (comm) {
             std::vector<int32_t> bits(core.size()), per;
@@ -224,31 +275,37 @@ int longform_main(const std::string& engine, const std::string& gguf, int argc, 
             probs = core;
         }
         if ((int64_t)probs.size() != T) throw Fail("vad: gathered frame count");
-        // 4. segments (the reference's post-processing), LPT over the ranks
-        qasr_vad_options vo;
-        qasr_vad_default_options(&vo);
-        std::vector<qasr_segment> segs((size_t)T / 2 + 2);
+        // 4. segments (the reference's post-processing), LPT over the ranks; 5. this rank's share through one batch
+        std::vector<qasr_segment> segs;
         size_t nseg = 0;
-        ck(qasr_vad_timestamps_from_probabilities(probs.data(), probs.size(), (int64_t)n, &vo, segs.data(), segs.size(),
-                                                  &nseg),
-           "segments");
-        segs.resize(nseg);
-        std::vector<int64_t> seg_len(nseg);
-        for (size_t i = 0; i < nseg; i++) seg_len[i] = segs[i].end - segs[i].start;
-        const std::vector<std::vector<int>> shard = lpt_shard(seg_len, world);
+        std::vector<int64_t> seg_len;
+        std::vector<std::vector<int>> shard;
+        double t_vad = 0;
+        stage("asr", [&] {
+            qasr_vad_options vo;
+            qasr_vad_default_options(&vo);
+            segs.resize((size_t)T / 2 + 2);
+            ck(qasr_vad_timestamps_from_probabilities(probs.data(), probs.size(), (int64_t)n, &vo, segs.data(),
+                                                      segs.size(), &nseg),
+               "segments");
+            segs.resize(nseg);
+            seg_len.resize(nseg);
+            for (size_t i = 0; i < nseg; i++) seg_len[i] = segs[i].end - segs[i].start;
+            shard = lpt_shard(seg_len, world);
+            const std::vector<int>& mine = shard[rank];
+            t_vad = now_ms();
+            std::vector<const float*> ptrs;
+            std::vector<size_t> lens;
+            for (int i : mine) {
+                ptrs.push_back(pcm.data() + segs[i].start);
+                lens.push_back((size_t)seg_len[i]);
+            }
+            res.assign(mine.size(), qasr_result{});
+            qasr_run_opts ro{max_new, force_tps, 0};
+            if (!mine.empty())
+                ck(qasr_run_batch(sess, ptrs.data(), lens.data(), (int32_t)mine.size(), &ro, res.data()), "asr batch");
+        });
         const std::vector<int>& mine = shard[rank];
-        const double t_vad = now_ms();
-        // 5. this rank's share through one batch
-        std::vector<const float*> ptrs;
-        std::vector<size_t> lens;
-        for (int i : mine) {
-            ptrs.push_back(pcm.data() + segs[i].start);
-            lens.push_back((size_t)seg_len[i]);
-        }
-        res.assign(mine.size(), qasr_result{});
-        qasr_run_opts ro{max_new, force_tps, 0};
-        if (!mine.empty()) ck(qasr_run_batch(sess, ptrs.data(), lens.data(), (int32_t)mine.size(), &ro, res.data()),
-                              "asr batch");
         const double t_asr = now_ms();
         // 6. token streams to rank 0 (every rank gets them; rank 0 prints)
         std::vector<std::vector<int32_t>> streams(nseg);

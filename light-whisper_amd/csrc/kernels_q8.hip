@@ -8,6 +8,7 @@
 #include <atomic>
 #include <type_traits>
 
+#include "exact_rows.h"
 #include "kernels.h"
 #include "lds_dma.h"
 #include "rowops.h"
@@ -15,12 +16,6 @@
 
 #ifndef QASR_DIAG
 #define QASR_DIAG 0
-#endif
-// the exact-row kernel's d_x·d_w from outer-product MFMAs (1) or VALU multiplies (0): the same IEEE products
-// (default 0: the 4-block f32 MFMA and its result latency cost more than the VALU multiplies it replaces — exact rows
-// 5.6 → 6.6 µs for QKV at 16 rows, 116 → 146 µs for the vocabulary projection: profiles/r4_exact_cost_*.json)
-#ifndef QASR_EXACT_MFMA_PROD
-#define QASR_EXACT_MFMA_PROD 0
 #endif
 #ifndef QASR_PREOFF_ALL
 #define QASR_PREOFF_ALL 1
@@ -485,22 +480,13 @@ bool gemv_fused_ok(int pro, int M, int K) {
 }
 
 // ------------------------------------------------------------------------------------------------ exact-row GEMM (MFMA)
-// The draft verify passes' linears (5–32 rows of one utterance) with EXACTLY the arithmetic of k_gemv_wide's 1-row
-// launch (the exact-row contract, engine.cpp), but with the block dots on the matrix core instead of v_dot4 per row.
-// The GEMV's result for output (m, n), K = 1024·T, is: lane ℓ = 2l (l = 0…31) accumulates the blocks b = l + 32t in t
-// order, leaf_l = fma((float)Σ_b q·q, d_w[n][b]·d_x[m][b], leaf_l) from 0, the odd lanes hold 0, and wave_sum's DPP
-// tree adds them as ((H0 + H1) + (H2 + H3)), H_h = O_2h + O_2h+1, O_g = ((l'_4g + l'_4g+1) + (l'_4g+2 + l'_4g+3)), l'
-// = leaf + 0 (the xor-1 step's add of an odd lane's 0: -0 → +0).  Here a wave owns one 16 × 16 output fragment over
-// the whole K: the exact int32 block sums come from v_mfma_i32_16x16x64_i8 on 64-byte spans (the weight span masked to
-// lane groups 0–1 / 2–3 gives blocks 2s / 2s+1), each lane keeps the 32 leaves of its 4 outputs in registers, and the
-// same fma chains and the same tree run in-lane — the same bits, whatever the row count (test_gemm_exact_rows_match
-// _gemv).  Rows past M are computed on clamped inputs and not stored.
+// The draft verify passes' (and the batch-invariant decode's) linears with EXACTLY the arithmetic of k_gemv_wide's
+// 1-row launch, the block dots on the matrix core: exact_rows.h (exact_frag) holds the arithmetic and its derivation.
+// A workgroup per 16-column fragment and all RF 16-row fragments (the weight span loaded once for them).
 template <int T, int RF>
 __global__ __launch_bounds__(256, 2) void k_gemm_q8_exact(const int8_t* __restrict__ X, const float* __restrict__ Xd, int M,
                                                        const int8_t* __restrict__ W, const __half* __restrict__ Wsc,
                                                        int N, int K, const float* res, float* y, int ldy, int epi) {
-    // a workgroup per 16-column fragment and all RF 16-row fragments (the weight span loaded once for them); wave w
-    // owns leaves 8w … 8w+7 (blocks 8w + 2j + {0,1} + 32t: spans 4w + j + 16t)
     __shared__ float hx[4][RF][4][64];   // [wave][row fragment][r][lane]: H_w = O_2w + O_2w+1 of each output
     // rows past 16·RF: grid.y chunks of 16·RF rows, each with the arithmetic of a launch of its own rows (the per-row
     // code depends on nothing but the row)
@@ -513,125 +499,15 @@ __global__ __launch_bounds__(256, 2) void k_gemm_q8_exact(const int8_t* __restri
         M -= m0;
     }
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int fr = lane & 15, g = lane >> 4;
     const int n0 = blockIdx.x * 16;
-    const int nb = K / QK;
-    const int8_t* wp = W + (size_t)min(n0 + fr, N - 1) * K + 16 * g;
-    const uint32_t* sp = (const uint32_t*)(Wsc + (size_t)min(n0 + fr, N - 1) * nb);
-    const int8_t* ap[RF];
-    const float* dxp[RF][4];
-    const float* dxq[RF];   // QASR_EXACT_MFMA_PROD: the block scales of row fr of each fragment
-#pragma unroll
-    for (int f = 0; f < RF; f++) {
-        ap[f] = X + (size_t)min(16 * f + fr, M - 1) * K + 16 * g;
-        dxq[f] = Xd + (size_t)min(16 * f + fr, M - 1) * nb;
-#pragma unroll
-        for (int r = 0; r < 4; r++) dxp[f][r] = Xd + (size_t)min(16 * f + 4 * g + r, M - 1) * nb;
-    }
-    constexpr int NS = 4 * T;                  // spans of this wave
-    constexpr int G8 = RF == 1 && NS % 8 == 0 ? 8 : 4;   // spans loaded per group
-    // (the product path where its registers fit: K ≤ 4,096 with one row fragment, K ≤ 2,048 with two — the fully
-    // unrolled span groups spill beyond that)
-    constexpr bool MP = QASR_EXACT_MFMA_PROD && (RF == 1 ? T <= 4 : T <= 2);
-    float leaf[RF][8][4];
-    const bool lo = g < 2;
-    const v4i zero = {0, 0, 0, 0};
-    const v16f zero16 = {};
-#pragma unroll
-    for (int q0 = 0; q0 < NS; q0 += G8) {
-        v4i wq[G8], aq[G8][RF];
-        uint32_t ws[G8];
-        float2 dx[MP ? 1 : G8][RF][4];
-        float dxv[G8 / 2][RF];   // MP: lane group g's operand of the span pair's outer product: row fr, block b_g
-#pragma unroll
-        for (int u = 0; u < G8; u++) {
-            const int i = q0 + u, s = 4 * wv + (i & 3) + 16 * (i >> 2);
-            wq[u] = __builtin_nontemporal_load((const v4i*)(wp + 64 * (size_t)s));
-            ws[u] = sp[s];
-#pragma unroll
-            for (int f = 0; f < RF; f++) {
-                aq[u][f] = *(const v4i*)(ap[f] + 64 * (size_t)s);
-                if constexpr (MP) {
-                    // pair u/2 = spans (u & ~1, u | 1): block b_g = 2·s(u & ~1 | g >> 1) + (g & 1) feeds lane group g
-                    if ((u & 1) == (g >> 1)) dxv[u / 2][f] = dxq[f][2 * s + (g & 1)];
-                } else {
-#pragma unroll
-                    for (int r = 0; r < 4; r++) dx[u][f][r] = *(const float2*)(dxp[f][r] + 2 * s);
-                }
-            }
-        }
-        if constexpr (MP) {
-            // per span pair and row fragment: d_x·d_w of its 4 blocks by one v_mfma_f32_16x16x1_4b_f32 (block k = lane
-            // group k's operands: row fr's d_x and column fr's d_w of block b_k; C_k[4g + r][fr] lands in lane
-            // fr + 16g, register 4k + r — the i8 MFMA's (row, col)).  Its f32 products are the VALU's dw·dx bit for bit
-            // (IEEE round-to-nearest, tools/micro/prod_check.hip), so the leaves keep the GEMV's bits; each leaf's
-            // chain still runs in t order (pairs in increasing span order).  One product set live at a time.
-#pragma unroll
-            for (int u0 = 0; u0 < G8; u0 += 2) {
-                const uint32_t wsg = ws[u0 + (g >> 1)];
-                const float dwv = __half2float(__ushort_as_half((unsigned short)((g & 1) ? wsg >> 16 : wsg & 0xffff)));
-#pragma unroll
-                for (int f = 0; f < RF; f++) {
-                    const v16f prod = __builtin_amdgcn_mfma_f32_16x16x1f32(dxv[u0 / 2][f], dwv, zero16, 0, 0, 0);
-#pragma unroll
-                    for (int uu = 0; uu < 2; uu++) {
-                        const int u = u0 + uu, i = q0 + u, j = i & 3, t = i >> 2;
-#pragma unroll
-                        for (int h = 0; h < 2; h++) {
-                            const v4i bm = (lo == (h == 0)) ? wq[u] : zero;
-                            const int l = 2 * j + h;
-                            const v4i c = __builtin_amdgcn_mfma_i32_16x16x64_i8(aq[u][f], bm, zero, 0, 0, 0);
-#pragma unroll
-                            for (int r = 0; r < 4; r++)
-                                leaf[f][l][r] = fmaf((float)c[r], prod[4 * (2 * uu + h) + r], t == 0 ? 0.f : leaf[f][l][r]);
-                        }
-                    }
-                }
-            }
-            continue;
-        }
-#pragma unroll
-        for (int u = 0; u < G8; u++) {
-            const int i = q0 + u, j = i & 3, t = i >> 2;   // blocks 8w + 2j + h + 32t → leaves 2j + h (of this wave)
-#pragma unroll
-            for (int h = 0; h < 2; h++) {
-                const v4i bm = (lo == (h == 0)) ? wq[u] : zero;
-                const float dw = __half2float(__ushort_as_half((unsigned short)(h ? ws[u] >> 16 : ws[u] & 0xffff)));
-                const int l = 2 * j + h;
-#pragma unroll
-                for (int f = 0; f < RF; f++) {
-                    const v4i c = __builtin_amdgcn_mfma_i32_16x16x64_i8(aq[u][f], bm, zero, 0, 0, 0);
-#pragma unroll
-                    for (int r = 0; r < 4; r++) {
-                        const float dxr = h ? dx[u][f][r].y : dx[u][f][r].x;
-                        leaf[f][l][r] = fmaf((float)c[r], dw * dxr, t == 0 ? 0.f : leaf[f][l][r]);
-                    }
-                }
-            }
-        }
-    }
-    // this wave's leaves l' = leaf + 0 (the GEMV's xor-1 add of an odd lane's 0), O_2w, O_2w+1, H_w
-#pragma unroll
-    for (int f = 0; f < RF; f++)
-#pragma unroll
-        for (int r = 0; r < 4; r++) {
-            float o[2];
-#pragma unroll
-            for (int gq = 0; gq < 2; gq++) {
-                const float a0 = leaf[f][4 * gq][r] + 0.f, a1 = leaf[f][4 * gq + 1][r] + 0.f;
-                const float a2 = leaf[f][4 * gq + 2][r] + 0.f, a3 = leaf[f][4 * gq + 3][r] + 0.f;
-                o[gq] = (a0 + a1) + (a2 + a3);
-            }
-            hx[wv][f][r][lane] = o[0] + o[1];
-        }
-    __syncthreads();
+    float v[4];
+    exact_frag<T, RF, XS_PLAIN>(X, Xd, M, W, Wsc, N, K, n0, hx, v);
     if (wv >= RF) return;
     const int f = wv;   // wave f stores row fragment f
 #pragma unroll
     for (int r = 0; r < 4; r++) {
-        const float v = (hx[0][f][r][lane] + hx[1][f][r][lane]) + (hx[2][f][r][lane] + hx[3][f][r][lane]);
-        const int row = 16 * f + 4 * g + r, col = n0 + fr;
-        if (row < M && col < N) y[(size_t)row * ldy + col] = epi_apply(epi, v, row, col, nullptr, res, ldy);
+        const int row = 16 * f + 4 * (lane >> 4) + r, col = n0 + (lane & 15);
+        if (row < M && col < N) y[(size_t)row * ldy + col] = epi_apply(epi, v[r], row, col, nullptr, res, ldy);
     }
 }
 

@@ -3,12 +3,15 @@
 // prologue is bit-identical to the one the separate launch writes (the decode-fusion parity contract).
 #pragma once
 #include "common.h"
+#include "wt.h"
 #include "xlane.h"
 
 namespace qasr {
 
 // one float4 chunk c of a row → 4 int8 of its Q8 block (8 consecutive lanes = one 32-block: amax by three DPP
 // steps); the block's first lane writes the scale.  q / d may point to global memory or LDS.
+// WT: stored write-through (sc1, wt.h: qrow / drow wave-uniform), for a hand-off inside one launch
+template <bool WT = false>
 __device__ __forceinline__ void quant4_store(float4 v, int c, int lane, int8_t* qrow, float* drow) {
     const float am = max8(fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
     const float dd = am / 127.f;
@@ -17,8 +20,13 @@ __device__ __forceinline__ void quant4_store(float4 v, int c, int lane, int8_t* 
         w = ((int)roundf(v.x / dd) & 0xff) | (((int)roundf(v.y / dd) & 0xff) << 8) |
             (((int)roundf(v.z / dd) & 0xff) << 16) | (((int)roundf(v.w / dd) & 0xff) << 24);
     }
-    ((int32_t*)qrow)[c] = w;
-    if ((lane & 7) == 0) drow[c >> 3] = __half2float(f2h(dd));
+    if constexpr (WT) {
+        wt_st32(qrow, (uint32_t)c * 4u, w);
+        if ((lane & 7) == 0) wt_stf(drow, (uint32_t)(c >> 3) * 4u, __half2float(f2h(dd)));
+    } else {
+        ((int32_t*)qrow)[c] = w;
+        if ((lane & 7) == 0) drow[c >> 3] = __half2float(f2h(dd));
+    }
 }
 
 // RMSNorm(x)·w of one row of H (H % 32 == 0, H ≤ 1024·KC) → Q8 (q [H], d [H/32]) by a whole 256-thread workgroup:
@@ -26,24 +34,28 @@ __device__ __forceinline__ void quant4_store(float4 v, int c, int lane, int8_t* 
 // waves through part[4] (LDS).  Split in two so a caller can issue the row's loads before other memory traffic:
 // rms_row_load (registers) then rms_row_q8_finish, which ends with every thread past one workgroup barrier (part may
 // be reused only after another barrier).  Threads 256+ of a larger workgroup pass active = false (barrier only).
-template <int KC>
+// WT: the row is read write-through (sc1: it was written by another workgroup of the same launch; xr wave-uniform)
+// (tid < 0: threadIdx.x; the persistent kernel passes its per-layer opaque thread index)
+template <int KC, bool WT = false>
 __device__ __forceinline__ void rms_row_load(const float* __restrict__ xr, int H, const float* __restrict__ w,
-                                             float4 (&v)[KC], float4 (&gw)[KC]) {
-    const int tid = threadIdx.x, nc = H / 4;
+                                             float4 (&v)[KC], float4 (&gw)[KC], int tid_ = -1) {
+    const int tid = tid_ < 0 ? (int)threadIdx.x : tid_, nc = H / 4;
     const float4* x4 = (const float4*)xr;
     const float4* g4 = (const float4*)w;
 #pragma unroll
     for (int k = 0; k < KC; k++) {
         const int c = tid + 256 * k;
-        v[k] = c < nc ? x4[c] : make_float4(0.f, 0.f, 0.f, 0.f);
+        if constexpr (WT) v[k] = c < nc ? wt_ldf4(xr, (uint32_t)c * 16u) : make_float4(0.f, 0.f, 0.f, 0.f);
+        else v[k] = c < nc ? x4[c] : make_float4(0.f, 0.f, 0.f, 0.f);
         gw[k] = c < nc ? g4[c] : make_float4(0.f, 0.f, 0.f, 0.f);
     }
 }
 
-template <int KC>
+template <int KC, bool WT = false>
 __device__ __forceinline__ void rms_row_q8_finish(const float4 (&v)[KC], const float4 (&gw)[KC], int H, float eps,
-                                                  int8_t* q, float* d, float* part, bool active = true) {
-    const int tid = threadIdx.x, lane = tid & 63, nc = H / 4;
+                                                  int8_t* q, float* d, float* part, bool active = true,
+                                                  int tid_ = -1) {
+    const int tid = tid_ < 0 ? (int)threadIdx.x : tid_, lane = tid & 63, nc = H / 4;
     if (!active) {   // waves past the first four of a larger workgroup: only the barrier
         __syncthreads();
         return;
@@ -68,7 +80,7 @@ __device__ __forceinline__ void rms_row_q8_finish(const float4 (&v)[KC], const f
             const float4 g = gw[k];
             const float4 y = make_float4(__fmul_rn(__fmul_rn(v[k].x, inv), g.x), __fmul_rn(__fmul_rn(v[k].y, inv), g.y),
                                          __fmul_rn(__fmul_rn(v[k].z, inv), g.z), __fmul_rn(__fmul_rn(v[k].w, inv), g.w));
-            quant4_store(y, c, lane, q, d);
+            quant4_store<WT>(y, c, lane, q, d);
         }
     }
 }
@@ -84,7 +96,8 @@ __device__ __forceinline__ void rms_row_q8_wg(const float* __restrict__ xr, int 
 // SwiGLU of element j (0..31) of one h block from the block's 64 gate/up values in the interleaved layout
 // ([g 16 | u 16 | g 16 | u 16]) → its Q8 value; one lane per element, a 32-lane group = one Q8 block (every lane of
 // the group active).  Writes *q and, from the block's first lane, *d.
-__device__ __forceinline__ void swiglu_q8_block(const float* blk64, int j, int8_t* q, float* d) {
+// the value form: element j's Q8 value, dq = the block's scale (f16-rounded)
+__device__ __forceinline__ int swiglu_q8_value(const float* blk64, int j, float& dq) {
     const int c = j < 16 ? j : j + 16;
     const float g = blk64[c], u = blk64[c + 16];
     const float v = g / (1.f + expf(-g)) * u;
@@ -92,8 +105,13 @@ __device__ __forceinline__ void swiglu_q8_block(const float* blk64, int j, int8_
 #pragma unroll
     for (int o = 16; o >= 1; o >>= 1) amax = fmaxf(amax, __shfl_xor(amax, o));
     const float dd = amax / 127.f;
-    *q = (int8_t)(amax == 0.f ? 0 : (int)roundf(v / dd));
-    if (j == 0) *d = __half2float(f2h(dd));
+    dq = __half2float(f2h(dd));
+    return amax == 0.f ? 0 : (int)roundf(v / dd);
+}
+__device__ __forceinline__ void swiglu_q8_block(const float* blk64, int j, int8_t* q, float* d) {
+    float dq;
+    *q = (int8_t)swiglu_q8_value(blk64, j, dq);
+    if (j == 0) *d = dq;
 }
 
 // SwiGLU of element f of a gate/up row (interleaved by 16, or [gate F | up F]) → q[f] / d[f/32]; as above

@@ -113,6 +113,7 @@ SIGNATURES = {
     "qasr_dist_broadcast": (C.c_int, [P, P, P, SZ, I32]),
     "qasr_dist_broadcast_weights": (C.c_int, [P, P, I32, P]),
     "qasr_dist_gather_tokens": (C.c_int, [P, P, I32, P, P, P, SZ, P, SZ, P, P]),
+    "qasr_dist_agree": (C.c_int, [P, I32, P]),
     "qasr_tokenizer_open": (C.c_int, [P, I32, P, P, I32, P]),
     "qasr_tokenizer_encode": (C.c_int, [P, C.c_char_p, SZ, P, SZ, P]),
     "qasr_tokenizer_close": (None, [P]),

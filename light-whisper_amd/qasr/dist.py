@@ -108,6 +108,76 @@ def agreed_attempt(attempt, group=None):
     return None, err or "failed on another rank"
 
 
+def gloo_agree(failed: bool, group=None) -> bool:
+    """`agree` over a torch.distributed group: True on every rank if any rank's `failed` is set"""
+    import torch
+    import torch.distributed as dist
+
+    t = torch.tensor([1 if failed else 0], dtype=torch.int32)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return bool(int(t.item()))
+
+
+class StageFailed(RuntimeError):
+    pass
+
+
+def agreed_stage(name: str, fn, agree, rank: int = 0):
+    """engine_longform.cpp's failure-agreement protocol (the Rust host copies it): run `fn()` locally, then agree on
+    every rank's outcome — `agree(failed) -> any_failed`, NativeComm.agree (qasr_dist_agree over RCCL) or gloo_agree —
+    before the collective that follows; if any rank failed, EVERY rank raises StageFailed (the failing rank with its
+    own reason), so no rank goes on alone into a collective that would block.  QASR_FAIL_STAGE=<name>
+    [QASR_FAIL_RANK=r] injects a failure (tests)."""
+    import os
+
+    err = None
+    try:
+        inj = os.environ.get("QASR_FAIL_STAGE")
+        if inj == name and int(os.environ.get("QASR_FAIL_RANK", "-1")) in (-1, rank):
+            raise RuntimeError(f"injected failure (QASR_FAIL_STAGE={name})")
+        result = fn()
+    except Exception as e:  # noqa: BLE001 — agreed on, then raised on every rank
+        err, result = f"{type(e).__name__}: {e}", None
+    if agree(err is not None):
+        raise StageFailed(err or f"{name}: failed on another rank")
+    return result
+
+
+def native_setup(rank: int, world: int, device: int, model, exchange, comm_cls=None, agree_group=None):
+    """bench.py's native collectives, each step agreed over the gloo group (which does not depend on RCCL) before the
+    next collective starts: (1) the unique-id hand-off (`exchange`, e.g. file_exchange), (2) the communicator init,
+    (3) the weight broadcast.  Returns (comm, broadcast info, None) or (None, None, error text) — the same verdict on
+    every rank, so all ranks take the fallback together, and no rank enters RCCL's blocking init unless every rank
+    holds the id.  (A rank that fails INSIDE RCCL's init is the one case this cannot cover.)"""
+    comm_cls = comm_cls or NativeComm
+    holder = []
+
+    def get_uid():
+        if rank != 0:
+            return exchange(bytes(128))
+        try:
+            return exchange(comm_cls.unique_id())
+        except Exception:
+            if hasattr(exchange, "fail"):
+                exchange.fail()
+            raise
+
+    uid, err = agreed_attempt(get_uid, group=agree_group)
+    if err is None:
+        _, err = agreed_attempt(lambda: holder.append(comm_cls(rank, world, device, uid=uid)), group=agree_group)
+    if err is None:
+        if hasattr(exchange, "cleanup"):
+            exchange.cleanup()   # after the collective init: every rank has read the id
+        info, err = agreed_attempt(lambda: holder[0].broadcast_weights(model), group=agree_group)
+        if err is None:
+            return holder[0], info, None
+    if hasattr(exchange, "cleanup"):
+        exchange.cleanup()
+    if holder:
+        holder[0].close()
+    return None, None, err
+
+
 def gather_token_streams(streams: list[list[int]], device) -> list[list[list[int]]]:
     """All-gather every rank's per-segment token ids; returns, on every rank, [rank][segment] -> ids."""
     import torch
@@ -143,20 +213,34 @@ class NativeComm:
     """libqasr's RCCL communicator (qasr_dist_*).  Rank 0 creates the unique id; `exchange` (any callable that
     returns rank 0's bytes on every rank, e.g. torch.distributed.broadcast_object_list) distributes it."""
 
-    def __init__(self, rank: int, world: int, device: int, exchange):
+    def __init__(self, rank: int, world: int, device: int, exchange=None, uid: bytes | None = None):
+        """either `exchange` (rank 0 creates the id here and the callable distributes it) or `uid` (the 128 bytes,
+        already on every rank — the caller then agrees on the hand-off before this collective init)"""
         import ctypes as C
 
         from . import _lib
 
         self._lib = _lib.load()
-        uid = (C.c_uint8 * 128)()
-        if rank == 0:
-            _lib.check(self._lib.qasr_dist_unique_id(uid, 128))
-        got = exchange(bytes(uid))
+        if uid is None:
+            got = exchange(NativeComm.unique_id() if rank == 0 else bytes(128))
+        else:
+            got = uid
         uid = (C.c_uint8 * 128).from_buffer_copy(got)
         self._h = C.c_void_p()
         _lib.check(self._lib.qasr_dist_init(uid, rank, world, device, C.byref(self._h)))
         self.rank, self.world = rank, world
+
+    @staticmethod
+    def unique_id() -> bytes:
+        """rank 0: a fresh 128-byte RCCL unique id (qasr_dist_unique_id)"""
+        import ctypes as C
+
+        from . import _lib
+
+        lib = _lib.load()
+        uid = (C.c_uint8 * 128)()
+        _lib.check(lib.qasr_dist_unique_id(uid, 128))
+        return bytes(uid)
 
     def close(self):
         if getattr(self, "_h", None):
@@ -178,6 +262,16 @@ class NativeComm:
         return {"bytes": int(info.bytes), "ms": round(info.ms, 3), "native_rccl": True,
                 "GB_per_s": round(info.bytes / info.ms / 1e6, 1) if info.ms > 0 else None,
                 "checksums_agree": bool(info.checksums_agree)}
+
+    def agree(self, failed: bool) -> bool:
+        """qasr_dist_agree: every rank's local outcome over RCCL; True on every rank if any rank failed"""
+        import ctypes as C
+
+        from . import _lib
+
+        anyf = C.c_int32(0)
+        _lib.check(self._lib.qasr_dist_agree(self._h, 1 if failed else 0, C.byref(anyf)))
+        return bool(anyf.value)
 
     def broadcast(self, send_ptr, recv_ptr: int, nbytes: int, root: int = 0):
         from . import _lib
@@ -256,18 +350,28 @@ def file_exchange(rank: int, world: int, key: str | None = None, directory: str 
                     return got
             except FileNotFoundError:
                 pass
+            if os.path.exists(path + ".fail"):
+                raise RuntimeError(f"rank {rank}: rank 0 failed to publish the unique id")
             if time.monotonic() - t0 > timeout_s:
                 raise TimeoutError(f"rank {rank}: no unique id at {path} after {timeout_s:.0f} s")
             time.sleep(0.01)
 
     def cleanup():
         if rank == 0:
-            try:
-                os.remove(path)
-            except FileNotFoundError:
+            for p in (path, path + ".fail"):
+                try:
+                    os.remove(p)
+                except FileNotFoundError:
+                    pass
+
+    def fail():
+        """rank 0 could not create or publish the id: a marker file, so the other ranks stop polling at once"""
+        if rank == 0:
+            with open(path + ".fail", "wb"):
                 pass
 
     exchange.cleanup = cleanup
+    exchange.fail = fail
     exchange.path = path
     return exchange
 

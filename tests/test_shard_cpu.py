@@ -248,6 +248,137 @@ def test_native_failure_is_agreed_by_every_rank(world, fail_rank):
                            else "failed on another rank")
 
 
+def _setup_rank(rank, world, port, fail, rdv, q):
+    """bench.py's native setup (qasr.dist.native_setup) with a fake communicator whose init is a BLOCKING collective
+    (a gloo barrier, like ncclCommInitRank): `fail` = ("uid", rank) injects an error in the id hand-off (rank 0
+    cannot create it, or another rank cannot read it)"""
+    import torch.distributed as dist
+
+    sys.path.insert(0, os.path.join(ROOT, "light-whisper_amd"))
+    from qasr import dist as qdist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    step, frank = fail
+    inits = []
+
+    class FakeComm:
+        @staticmethod
+        def unique_id():
+            if step == "uid" and frank == 0:
+                raise RuntimeError("qasr_dist_unique_id failed")
+            return bytes(range(128))
+
+        def __init__(self, r, w, dev, uid=None):
+            assert uid == bytes(range(128))
+            dist.barrier()   # the blocking collective every rank must enter together
+            inits.append(r)
+
+        def broadcast_weights(self, model):
+            dist.barrier()
+            return {"ok": True}
+
+        def close(self):
+            pass
+
+    xchg = qdist.file_exchange(rank, world, key=f"t{port}", directory=rdv, timeout_s=60.0)
+    if step == "uid" and frank > 0 and rank == frank:   # this rank cannot read the id (e.g. another host)
+        xchg = lambda payload: (_ for _ in ()).throw(TimeoutError("no unique id"))  # noqa: E731
+    comm, info, err = qdist.native_setup(rank, world, 0, None, xchg, comm_cls=FakeComm)
+    after = qdist.gather_token_streams([[rank]], __import__("torch").device("cpu"))
+    q.put((rank, comm is not None, info, err, inits, after))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,fail", [(2, ("uid", 0)), (3, ("uid", 0)), (3, ("uid", 2)), (2, ("uid", 1)),
+                                        (3, ("none", -1))])
+def test_native_setup_agrees_before_each_collective(world, fail, tmp_path):
+    """the native setup agrees after the id hand-off and before the (blocking) communicator init, and again
+    before the broadcast — a rank that fails to get the id (rank 0 cannot create it: the others stop polling at the
+    marker file; or a rank cannot read it) never leaves the others waiting inside the init, and every rank returns the
+    same verdict within seconds"""
+    import time
+
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_setup_rank, args=(r, world, port, fail, str(tmp_path), q)) for r in range(world)]
+    t0 = time.monotonic()
+    for p in procs:
+        p.start()
+    out = sorted((q.get(timeout=120) for _ in range(world)), key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert time.monotonic() - t0 < 90
+    step, frank = fail
+    for rank, ok, info, err, inits, after in out:
+        assert after == [[[r]] for r in range(world)]   # still in step afterwards
+        if step == "none":
+            assert ok and info == {"ok": True} and err is None and inits == [rank]
+            continue
+        assert not ok and info is None and err
+        if rank == frank:
+            assert "qasr_dist_unique_id failed" in err or "no unique id" in err, err
+        else:
+            assert err == "failed on another rank" or "rank 0 failed to publish" in err, err
+        assert inits == []   # nobody entered the blocking init
+    assert not os.listdir(tmp_path) or all(not f.endswith(".bin") for f in os.listdir(tmp_path))
+
+
+def _stage_rank(rank, world, port, fail_rank, stage, q):
+    import torch.distributed as dist
+
+    sys.path.insert(0, os.path.join(ROOT, "light-whisper_amd"))
+    from qasr import dist as qdist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    if fail_rank is not None:
+        os.environ.update(QASR_FAIL_STAGE=stage, QASR_FAIL_RANK=str(fail_rank))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    done = []
+    err = None
+    try:
+        for name in ("model", "vad", "asr"):
+            qdist.agreed_stage(name, lambda: done.append(name), qdist.gloo_agree, rank=rank)
+            dist.barrier()   # the collective that follows the stage
+    except qdist.StageFailed as e:
+        err = str(e)
+    q.put((rank, done, err))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,fail_rank,stage", [(2, 0, "vad"), (2, 1, "asr"), (3, 0, "asr"), (3, 2, "vad"),
+                                                   (3, 2, "model"), (3, None, "asr")])
+def test_longform_stage_agreement_gloo(world, fail_rank, stage):
+    """engine_longform.cpp's failure agreement (qasr_dist_agree before each collective), in its Python mirror
+    qasr.dist.agreed_stage over gloo: one rank's stage failure (first rank and last rank) makes EVERY rank stop at that
+    stage with an error — none is left in the collective that follows"""
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_stage_rank, args=(r, world, port, fail_rank, stage, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = sorted((q.get(timeout=120) for _ in range(world)), key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    order = ["model", "vad", "asr"]
+    for rank, done, err in out:
+        if fail_rank is None:
+            assert done == order and err is None
+            continue
+        k = order.index(stage)
+        assert done == order[:k + (0 if rank == fail_rank else 1)], (rank, done)
+        assert err == (f"RuntimeError: injected failure (QASR_FAIL_STAGE={stage})" if rank == fail_rank
+                       else f"{stage}: failed on another rank"), err
+
+
 def _prob_gather_rank(rank, world, port, q):
     import torch
     import torch.distributed as dist
