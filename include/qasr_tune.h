@@ -33,10 +33,22 @@ QASR_API int qasr_op_set_gemm_fixup(void* part, int64_t part_bytes, void* cnt, i
 QASR_API int qasr_op_set_gemm_ws_rows(int32_t rows, int32_t all_shapes);
 /* Regrouped stage scales of a Q8 matrix (sc [N][K/32] f16 → out [K/128][N][4] f16, K % 128 == 0): a K-128 GEMM
    stage's column scales as one contiguous run (the decode GEMMs' 16-byte scale DMA; a model's decoder matrices
-   carry theirs).  qasr_op_register_stage_scales(wsc, out) makes the qasr_op_* GEMM entry points use `out` for the
-   matrix whose scale pointer is `wsc` (NULL unregisters) — tests and tuning tools. */
+   carry theirs).  qasr_op_register_stage_scales(wsc, N, K, out) makes the qasr_op_* GEMM entry points use `out` for
+   the N × K matrix whose scale pointer is `wsc` (out NULL unregisters; a call with another N or K at that address
+   finds no registration) — tests and tuning tools. */
 QASR_API int qasr_op_stage_scales(const void* wsc, int32_t N, int32_t K, void* out, void* stream);
-QASR_API int qasr_op_register_stage_scales(const void* wsc, const void* sc4);
+QASR_API int qasr_op_register_stage_scales(const void* wsc, int32_t N, int32_t K, const void* sc4);
+/* The ≤ 32-row decode's exact-row launches (kernels_persist.hip, xr_*): the same outputs bit for bit as
+   qasr_op_gemm_exact_rows (and, with src, as qasr_op_rmsnorm_q8 + it), one workgroup per 16-column fragment with its
+   weights loaded up front and the rows staged once in LDS.  qasr_op_xr_linear: y = X·Wᵀ (+ y when resid); src != NULL
+   (M ≤ 8, K ≤ 2,048): X = Q8(RMSNorm(src)·nw) computed inside.  qasr_op_xr_gu_swiglu: W = interleaved gate/up [2F][K],
+   hq / hd = Q8(silu(g)·u) (qasr_op_swiglu_q8_interleaved's arithmetic).  M 1-32, K ∈ {1,024, 2,048, 3,072, 6,144}. */
+QASR_API int qasr_op_xr_linear(const int8_t* xq, const float* xd, const float* src, const float* nw, float eps,
+                               int32_t M, const int8_t* wqs, const void* wsc, int32_t N, int32_t K, float* y,
+                               int32_t ldy, int32_t resid, void* stream);
+QASR_API int qasr_op_xr_gu_swiglu(const int8_t* xq, const float* xd, const float* src, const float* nw, float eps,
+                                  int32_t M, const int8_t* wqs, const void* wsc, int32_t N, int32_t K, int8_t* hq,
+                                  float* hd, void* stream);
 #ifdef __cplusplus
 }
 #endif

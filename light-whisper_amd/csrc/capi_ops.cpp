@@ -29,13 +29,19 @@ QASR_API int qasr_op_quant_rows(const float* x, int32_t M, int32_t K, int32_t ld
 }
 
 // Tests and tuning tools: the regrouped stage scales (Q8Mat::sc4, [K/128][N][4]) of a raw weight matrix given to the
-// qasr_op_* GEMM entry points, registered by its scale pointer (a model's matrices carry theirs, model.cpp)
+// qasr_op_* GEMM entry points, registered by its scale pointer AND shape (a model's matrices carry theirs, model.cpp):
+// a later matrix of another shape at a recycled address never picks up a stale registration
+struct S4Reg {
+    const void* wsc;
+    int32_t N, K;
+    const __half* sc4;
+};
 static std::mutex g_s4_mu;
-static std::vector<std::pair<const void*, const __half*>> g_s4;
-static const __half* stage_scales_of(const void* wsc) {
+static std::vector<S4Reg> g_s4;
+static const __half* stage_scales_of(const void* wsc, int32_t N, int32_t K) {
     std::lock_guard<std::mutex> lk(g_s4_mu);
     for (auto& e : g_s4)
-        if (e.first == wsc) return e.second;
+        if (e.wsc == wsc && e.N == N && e.K == K) return e.sc4;
     return nullptr;
 }
 
@@ -46,16 +52,16 @@ QASR_API int qasr_op_stage_scales(const void* wsc, int32_t N, int32_t K, void* o
     });
 }
 
-QASR_API int qasr_op_register_stage_scales(const void* wsc, const void* sc4) {
+QASR_API int qasr_op_register_stage_scales(const void* wsc, int32_t N, int32_t K, const void* sc4) {
     return guard([&] {
-        QASR_CHECK(wsc, QASR_E_INVALID, "null scale pointer");
+        QASR_CHECK(wsc && N > 0 && K > 0 && K % 128 == 0, QASR_E_INVALID, "stage scales: scale pointer, N, K % 128");
         std::lock_guard<std::mutex> lk(g_s4_mu);
         for (size_t i = 0; i < g_s4.size(); i++)
-            if (g_s4[i].first == wsc) {
+            if (g_s4[i].wsc == wsc) {   // one registration per address (whatever shape it had)
                 g_s4.erase(g_s4.begin() + (long)i);
                 break;
             }
-        if (sc4) g_s4.emplace_back(wsc, (const __half*)sc4);
+        if (sc4) g_s4.push_back(S4Reg{wsc, N, K, (const __half*)sc4});
     });
 }
 
@@ -76,7 +82,7 @@ QASR_API int qasr_op_linear_q8(const int8_t* xq, const float* xd, int32_t M, con
         Q8Mat W;
         W.qs = (int8_t*)wqs;
         W.sc = (__half*)wsc;
-        W.sc4 = stage_scales_of(wsc);
+        W.sc4 = stage_scales_of(wsc, N, K);
         W.N = N;
         W.K = K;
         if (path == 1 || (path >= 3 && path <= 5)) {   // GEMV: auto, or 1 / 2 / 4 columns per wave
@@ -132,7 +138,7 @@ QASR_API int qasr_op_linear_q8_ex(const int8_t* xq, const float* xd, int32_t M, 
         Q8Mat W;
         W.qs = (int8_t*)wqs;
         W.sc = (__half*)wsc;
-        W.sc4 = stage_scales_of(wsc);
+        W.sc4 = stage_scales_of(wsc, N, K);
         W.N = N;
         W.K = K;
         gemm_q8(xq, xd, M, W, bias, nullptr, (float*)y, ldy, epi, S(stream), cfg, 0, yq, yd);
@@ -187,7 +193,7 @@ QASR_API int qasr_op_gemm_swiglu_q8(const int8_t* xq, const float* xd, int32_t M
         Q8Mat W;
         W.qs = (int8_t*)wqs;
         W.sc = (__half*)wsc;
-        W.sc4 = stage_scales_of(wsc);
+        W.sc4 = stage_scales_of(wsc, N, K);
         W.N = N;
         W.K = K;
         gemm_q8(xq, xd, M, W, nullptr, nullptr, nullptr, N, EPI_SWIGLU, S(stream), -1, 0, hq, hd);
@@ -203,7 +209,7 @@ QASR_API int qasr_op_gemm_swiglu_q8_cfg(const int8_t* xq, const float* xd, int32
         Q8Mat W;
         W.qs = (int8_t*)wqs;
         W.sc = (__half*)wsc;
-        W.sc4 = stage_scales_of(wsc);
+        W.sc4 = stage_scales_of(wsc, N, K);
         W.N = N;
         W.K = K;
         // cfg + 32·splits (cfg < 31), or 4096 + cfg + 256·splits (any configuration index)
@@ -223,10 +229,40 @@ QASR_API int qasr_op_gemm_exact_rows(const int8_t* xq, const float* xd, int32_t 
         Q8Mat W;
         W.qs = (int8_t*)wqs;
         W.sc = (__half*)wsc;
-        W.sc4 = stage_scales_of(wsc);
+        W.sc4 = stage_scales_of(wsc, N, K);
         W.N = N;
         W.K = K;
         gemm_exact_rows(xq, xd, M, W, res, y, ldy, epi, S(stream));
+        launched();
+    });
+}
+
+QASR_API int qasr_op_xr_linear(const int8_t* xq, const float* xd, const float* src, const float* nw, float eps,
+                               int32_t M, const int8_t* wqs, const void* wsc, int32_t N, int32_t K, float* y,
+                               int32_t ldy, int32_t resid, void* stream) {
+    return guard([&] {
+        QASR_CHECK(N > 0 && ldy >= N && (src || (xq && xd)), QASR_E_INVALID, "xr_linear: bad arguments");
+        Q8Mat W;
+        W.qs = (int8_t*)wqs;
+        W.sc = (__half*)wsc;
+        W.N = N;
+        W.K = K;
+        xr_linear(xq, xd, src, nw, eps, M, W, y, ldy, resid != 0, S(stream));
+        launched();
+    });
+}
+
+QASR_API int qasr_op_xr_gu_swiglu(const int8_t* xq, const float* xd, const float* src, const float* nw, float eps,
+                                  int32_t M, const int8_t* wqs, const void* wsc, int32_t N, int32_t K, int8_t* hq,
+                                  float* hd, void* stream) {
+    return guard([&] {
+        QASR_CHECK(N > 0 && (src || (xq && xd)) && hq && hd, QASR_E_INVALID, "xr_gu_swiglu: bad arguments");
+        Q8Mat W;
+        W.qs = (int8_t*)wqs;
+        W.sc = (__half*)wsc;
+        W.N = N;
+        W.K = K;
+        xr_gu_swiglu(xq, xd, src, nw, eps, M, W, hq, hd, S(stream));
         launched();
     });
 }
@@ -262,7 +298,7 @@ QASR_API int qasr_op_gemv_fused(int32_t pro, const float* src, int32_t ld_src, c
         Q8Mat W;
         W.qs = (int8_t*)wqs;
         W.sc = (__half*)wsc;
-        W.sc4 = stage_scales_of(wsc);
+        W.sc4 = stage_scales_of(wsc, N, K);
         W.N = N;
         W.K = K;
         gemv_fused(pro, xq, xd, src, ld_src, nw, eps, M, W, res, y, ldy, epi, hq, hd, S(stream));
@@ -347,7 +383,6 @@ QASR_API int qasr_op_embed_rows(const int32_t* ids, int32_t n, const int8_t* wqs
         Q8Mat W;
         W.qs = (int8_t*)wqs;
         W.sc = (__half*)wsc;
-        W.sc4 = stage_scales_of(wsc);
         W.K = K;
         embed_rows(ids, n, W, alt, out, S(stream));
         launched();

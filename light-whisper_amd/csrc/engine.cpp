@@ -540,9 +540,10 @@ void Session::decoder_layers(float* x, int rows, const int* d_pos, const int* d_
     // batched decode rows (the table path) of few rows: the exact-row kernel where it is the faster launch (cold
     // weights, deterministic table: QKV 5.6 / 7.5 against 7.2 / 9.6 µs at 16 / 32 rows, O-projection 6.7–8.6 against
     // 10.2–10.9 µs at 16–64 rows, down 12.9 against 15.0 µs at 16 rows; profiles/r4_exact_cost_*.json) — the strong-
-    // scaling regime (32 segments per GPU at N = 8).  QASR_XR_ROWS=q,o,d overrides the row limits (0 = never).
+    // scaling regime (32 segments per GPU at N = 8); round 5: down to 32 rows too (the xr launch, 13.0 against the table's
+    // 13.6 µs at 32 rows, profiles/r5_xr_cost.log).  QASR_XR_ROWS=q,o,d overrides the row limits (0 = never).
     static const std::array<int, 3> xr_lim = [] {
-        std::array<int, 3> v{32, 64, 16};
+        std::array<int, 3> v{32, 64, 32};
         if (const char* e = getenv("QASR_XR_ROWS")) sscanf(e, "%d,%d,%d", &v[0], &v[1], &v[2]);
         return v;
     }();
@@ -588,11 +589,22 @@ void Session::decoder_layers(float* x, int rows, const int* d_pos, const int* d_
         a.timeout_ticks = 100000000;   // 1 s per grid wait (a decode step takes ~1 ms)
         a.grid = pgrid_[rows <= 16 ? 0 : 1];
         a.stamps = pstamps_;
-        static const int fold = getenv("QASR_PERSIST_FOLD") ? atoi(getenv("QASR_PERSIST_FOLD")) : 32;
+        static const int fold = getenv("QASR_PERSIST_FOLD") ? atoi(getenv("QASR_PERSIST_FOLD")) : 8;
         a.fold_rows = fold;
         decoder_persistent(a, st_);
         return;
     }
+    // ≤ 32 rows: the exact-row linears as the per-phase launches (xr_linear: weights loaded up front, rows staged in
+    // LDS; bit-identical to gemm_exact_rows — tests/test_ops_gpu.py::test_xr_linear_bit_identical_to_exact_rows),
+    // faster at 2-32 rows on O / down and from 24 rows on QKV (profiles/r5_xr_cost.log); QASR_NO_XR=1 keeps
+    // gemm_exact_rows
+    static const bool no_xr = getenv("QASR_NO_XR") != nullptr;
+    auto exact_linear = [&](const int8_t* q, const float* d, const Q8Mat& W, const float* res, float* y, int ldy,
+                            int epi) {
+        if (!no_xr && xr_ok(rows, W.K) && W.N % 16 == 0) xr_linear(q, d, nullptr, nullptr, 0.f, rows, W, y, ldy,
+                                                                   epi == EPI_RESID, st_);
+        else gemm_exact_rows(q, d, rows, W, res, y, ldy, epi, st_);
+    };
     int8_t* hq2 = gv || xm ? (int8_t*)sc_.get(S_HQ, (size_t)rows * F) : nullptr;   // the SwiGLU Q8 rows
     float* hd2 = gv || xm ? (float*)sc_.get(S_HD, (size_t)rows * (F / QK) * sizeof(float)) : nullptr;
     float* gux = xm ? (float*)sc_.get(S_GU, (size_t)rows * 2 * F * sizeof(float)) : nullptr;
@@ -607,13 +619,13 @@ void Session::decoder_layers(float* x, int rows, const int* d_pos, const int* d_
         if (dmp) dump_rows("x_in", l, rows, x, (size_t)rows * H * sizeof(float));
         if (xm) {
             rmsnorm_q8(x, rows, H, H, L.attn_norm, h.rms_eps, xq, xd, st_);
-            gemm_exact_rows(xq, xd, rows, L.qkv, nullptr, qkv, QD + 2 * KD, EPI_STORE, st_);
+            exact_linear(xq, xd, L.qkv, nullptr, qkv, QD + 2 * KD, EPI_STORE);
         } else if (gv) {
             gemv_fused(GV_RMS, nullptr, nullptr, x, H, L.attn_norm, h.rms_eps, rows, L.qkv, nullptr, qkv, QD + 2 * KD,
                        EPI_STORE, nullptr, nullptr, st_);
         } else if (xr_qkv) {
             rmsnorm_q8(x, rows, H, H, L.attn_norm, h.rms_eps, xq, xd, st_);
-            gemm_exact_rows(xq, xd, rows, L.qkv, nullptr, qkv, QD + 2 * KD, EPI_STORE, st_);
+            exact_linear(xq, xd, L.qkv, nullptr, qkv, QD + 2 * KD, EPI_STORE);
         } else {
             rmsnorm_q8(x, rows, H, H, L.attn_norm, h.rms_eps, xq, xd, st_, zq ? qkv : nullptr,
                        zq ? (int64_t)rows * (QD + 2 * KD) : 0);
@@ -644,16 +656,16 @@ void Session::decoder_layers(float* x, int rows, const int* d_pos, const int* d_
             dump_rows("att_d", l, rows, xd, (size_t)rows * (QD / QK) * sizeof(float));
         }
         if (xm) {   // the same four steps as separate launches with the exact-row MFMA linears
-            gemm_exact_rows(xq, xd, rows, L.o, x, x, H, EPI_RESID, st_);
+            exact_linear(xq, xd, L.o, x, x, H, EPI_RESID);
             if (dmp) dump_rows("x_mid", l, rows, x, (size_t)rows * H * sizeof(float));
             rmsnorm_q8(x, rows, H, H, L.ffn_norm, h.rms_eps, xq, xd, st_);
-            gemm_exact_rows(xq, xd, rows, L.gu, nullptr, gux, 2 * F, EPI_STORE, st_);
+            exact_linear(xq, xd, L.gu, nullptr, gux, 2 * F, EPI_STORE);
             swiglu_q8(gux, rows, F, hq2, hd2, st_, /*interleaved=*/true);
             if (dmp) {
                 dump_rows("h_q", l, rows, hq2, (size_t)rows * F);
                 dump_rows("h_d", l, rows, hd2, (size_t)rows * (F / QK) * sizeof(float));
             }
-            gemm_exact_rows(hq2, hd2, rows, L.down, x, x, H, EPI_RESID, st_);
+            exact_linear(hq2, hd2, L.down, x, x, H, EPI_RESID);
             continue;
         }
         if (gv) {   // O-projection + residual; norm + gate/up + SwiGLU + Q8; down-projection + residual
@@ -670,7 +682,7 @@ void Session::decoder_layers(float* x, int rows, const int* d_pos, const int* d_
             continue;
         }
         if (xr_o)
-            gemm_exact_rows(xq, xd, rows, L.o, x, x, H, EPI_RESID, st_);
+            exact_linear(xq, xd, L.o, x, x, H, EPI_RESID);
         else
             linear_q8(xq, xd, rows, L.o, nullptr, x, x, H, EPI_RESID, st_);
         rmsnorm_q8(x, rows, H, H, L.ffn_norm, h.rms_eps, xq, xd, st_);
@@ -683,7 +695,7 @@ void Session::decoder_layers(float* x, int rows, const int* d_pos, const int* d_
             swiglu_q8(gu, rows, F, xq, xd, st_, true);
         }
         if (xr_down)
-            gemm_exact_rows(xq, xd, rows, L.down, x, x, H, EPI_RESID, st_);
+            exact_linear(xq, xd, L.down, x, x, H, EPI_RESID);
         else
             linear_q8(xq, xd, rows, L.down, nullptr, x, x, H, EPI_RESID, st_);
         if (fused) {
@@ -971,7 +983,6 @@ void Session::run_batch(const float* dpcm, const std::vector<int64_t>& off, cons
         if (same && fe.skip_tokens > 0) reuse = std::min(P0 + fe.skip_tokens, kvp_rows_);
         kvp_rows_ = 0;   // valid again only once this run has completed (below)
     }
-    const int skip = shared ? shared : reuse;
     // a completed single-utterance run leaves its prompt rows' K/V in slots [0, n_prompt) for the next run
     auto remember_prompt_kv = [&]() {
         if (count != 1 || m_->mx()) return;
@@ -982,11 +993,10 @@ void Session::run_batch(const float* dpcm, const std::vector<int64_t>& off, cons
         kvp_rows_ = n_prompt[0];
     };
     int64_t slots = 0;
+    std::vector<std::vector<int32_t>> prompts(count);
     for (int u = 0; u < count; u++) {
-        std::vector<int32_t> p = build_prompt(h, fe.n_tok[u], fe.tok_base[u], context_);
-        n_prompt[u] = (int)p.size();
-        row0[u] = (int)ids.size();
-        ids.insert(ids.end(), p.begin() + skip, p.end());
+        prompts[u] = build_prompt(h, fe.n_tok[u], fe.tok_base[u], context_);
+        n_prompt[u] = (int)prompts[u].size();
         const double secs = (double)len[u] / 16000.0;
         // one utterance decodes until EOS or n_ctx, like the reference's session.run; a batch caps each utterance
         // (its KV slot range is reserved up front)
@@ -1002,7 +1012,12 @@ void Session::run_batch(const float* dpcm, const std::vector<int64_t>& off, cons
     const int64_t pref = slots + 1;          // slots: utterances, the dummy slot, the shared prefix
     const uint64_t kv_ep = kv_epoch_;
     ensure_kv(slots + 1 + (shared ? P0 : 0));
-    QASR_CHECK(!reuse || kv_epoch_ == kv_ep, QASR_E_INTERNAL, "prompt-KV reuse across a KV reallocation");
+    if (kv_epoch_ != kv_ep) reuse = 0;   // a reallocated cache holds none of the previous run's rows: prefill them all
+    const int skip = shared ? shared : reuse;
+    for (int u = 0; u < count; u++) {
+        row0[u] = (int)ids.size();
+        ids.insert(ids.end(), prompts[u].begin() + skip, prompts[u].end());
+    }
     kvp_stats_.rows_reused += reuse;
     const int T = (int)ids.size(), H = h.txt_h, V = h.vocab;
     std::vector<int> pos(T), slot(T), kvs(T), kvl(T), last(count);

@@ -31,8 +31,11 @@ void linear_q8(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const f
 // epilogues (tools/gemv_tune.py: at 8 rows the GEMM is faster on every decoder shape, at 4 the GEMV mostly is)
 constexpr int kGemvRows = 4;
 // rows up to which the decoder layer runs on the fused weight-streaming GEMVs (gemv_fused: norm prologue, SwiGLU
-// epilogue, 5 launches per layer) instead of the MFMA GEMMs (QASR_GV_ROWS overrides, for A/B timing)
-constexpr int kGemvWideRows = 8;
+// epilogue, 5 launches per layer) instead of the MFMA GEMMs (QASR_GV_ROWS overrides, for A/B timing).  Round 5: 4 —
+// the 5–8-row GEMV group (v_dot4 rows, 8 rows against the weight registers) cost 19–26 µs per QKV / down / gate-up
+// launch in the 32-segment share; the MFMA paths take 5–15 µs (32-segment share 1,107 → 1,188 audio-s/s,
+// profiles/r5_seg32_*.log)
+constexpr int kGemvWideRows = 4;
 // rows up to which gemv_fused runs (groups of 8 against the weights held in registers, each row with the per-row
 // arithmetic of a 1-row launch): the draft verify passes of the streaming decode, whose rows must be the same bits
 // as one-token greedy steps (engine.cpp, exact rows)
@@ -210,6 +213,15 @@ bool persist_supported(int H, int F, int nh, int nkv, int hd);
 // workgroups the persistent launch uses on this device (0: the occupancy check failed)
 int persist_grid(int H, int F, int nh, int nkv, int R);
 void decoder_persistent(const PersistArgs& a, hipStream_t s);
+// the same item bodies as one launch per linear (≤ 32 rows; kernels_persist.hip): exact-row arithmetic, bit-identical
+// to gemm_exact_rows / the 1-row GEMVs.  src != nullptr (≤ 8 rows, K ≤ 2,048): the input rows are RMSNorm(src)·nw
+// quantised inside the launch (rmsnorm_q8's arithmetic) instead of xq / xd.
+bool xr_ok(int R, int K);
+void xr_linear(const int8_t* xq, const float* xd, const float* src, const float* nw, float eps, int R, const Q8Mat& W,
+               float* y, int ldy, bool resid, hipStream_t s);
+// interleaved gate/up (N = 2F) + SwiGLU + Q8 → hq [R][F] / hd [R][F/32]
+void xr_gu_swiglu(const int8_t* xq, const float* xd, const float* src, const float* nw, float eps, int R,
+                  const Q8Mat& W, int8_t* hq, float* hd, hipStream_t s);
 
 // ---- device-resident decode state (kernels_decode.hip)
 struct DecState {

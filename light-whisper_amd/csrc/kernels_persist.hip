@@ -141,18 +141,18 @@ __device__ __forceinline__ void stage_tile(const int8_t* X, const float* Xd, int
 // RMSNorm(x rows [0, R))·w → Q8 into the LDS tile (rmsnorm_q8's arithmetic: rms_row_q8_finish into LDS), eight rows'
 // loads in flight at a time; part: [8][4] floats
 template <int KC>
-__device__ __forceinline__ void norm_tile(const PersistArgs& a, int R, const float* w, int8_t* sX, int ldx, float* sXd,
-                                          float (*part)[4], int tid) {
+__device__ __forceinline__ void norm_tile(const float* x, int H, float eps, int R, const float* w, int8_t* sX, int ldx,
+                                          float* sXd, float (*part)[4], int tid) {
     for (int r0 = 0; r0 < R; r0 += 8) {
         float4 v[8][KC], gw[KC];
 #pragma unroll
         for (int u = 0; u < 8; u++)
-            if (r0 + u < R) rms_row_load<KC, true>(a.x + (size_t)(r0 + u) * a.H, a.H, w, v[u], gw, tid);
+            if (r0 + u < R) rms_row_load<KC, true>(x + (size_t)(r0 + u) * H, H, w, v[u], gw, tid);
 #pragma unroll
         for (int u = 0; u < 8; u++)
             if (r0 + u < R)
-                rms_row_q8_finish<KC, false>(v[u], gw, a.H, a.eps, sX + (r0 + u) * ldx, sXd + (r0 + u) * (a.H / QK),
-                                             part[u], true, tid);
+                rms_row_q8_finish<KC, false>(v[u], gw, H, eps, sX + (r0 + u) * ldx, sXd + (r0 + u) * (H / QK), part[u],
+                                             true, tid);
         __syncthreads();   // part reuse
     }
 }
@@ -273,7 +273,7 @@ __global__ __launch_bounds__(256, 1) void k_dec_persist(PersistArgs a) {
         // ---- QKV
         if (b < nQ) {
             float* sXd = (float*)(tile + 16 * RF * LX_H);
-            if (fold) norm_tile<TH>(a, R, Ly.attn_norm, sX, LX_H, sXd, part, tl);
+            if (fold) norm_tile<TH>(a.x, H, a.eps, R, Ly.attn_norm, sX, LX_H, sXd, part, tl);
             else stage_tile(a.xq, a.xd, H, 0, R, sX, LX_H, sXd, tl);
             __syncthreads();
             // (the first item on the prefetched weights, further ones — fewer CUs than items — on their own: one
@@ -354,7 +354,7 @@ __global__ __launch_bounds__(256, 1) void k_dec_persist(PersistArgs a) {
 #pragma unroll
             for (int c = 2; c < 4; c++) exact_load_w<TH>(wg[c], Ly.gu_q, Ly.gu_s, 2 * F, H, 64 * b + 16 * c, tl);
             float* sXd = (float*)(tile + 16 * RF * LX_H);
-            if (fold) norm_tile<TH>(a, R, Ly.ffn_norm, sX, LX_H, sXd, part, tl);
+            if (fold) norm_tile<TH>(a.x, H, a.eps, R, Ly.ffn_norm, sX, LX_H, sXd, part, tl);
             else stage_tile(a.xq, a.xd, H, 0, R, sX, LX_H, sXd, tl);
             __syncthreads();
             auto g_item = [&](int it, const XWeights<TH>(&w)[4]) {
@@ -437,6 +437,147 @@ __global__ __launch_bounds__(256, 1) void k_dec_persist(PersistArgs a) {
             __hip_atomic_store(a.sync + kExitWord, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
+}
+
+// ------------------------------------------------------------------------------------------------ per-phase launches
+// The persistent kernel's item bodies as plain launches (a kernel boundary instead of a grid wait): the ≤ 32-row decode
+// linears with exact-row arithmetic (bit-identical to the 1-row GEMV step and to gemm_exact_rows), every weight span
+// of a workgroup's fragment(s) loaded at its start, the activation rows staged once into LDS (or, FOLD, normalised
+// there from x: rmsnorm_q8's arithmetic — no separate norm launch).  One workgroup per CU (512 registers).
+//   k_xr_linear: a 16-column fragment × the rows of blockIdx.y's slice (16·RF rows), + residual (RESID)
+//   k_xr_gu:     one h block = 64 interleaved gate/up columns (4 fragments) + SwiGLU + Q8
+template <int T, int RF, bool FOLD, bool RESID>
+__global__ __launch_bounds__(256, 1) void k_xr_linear(const int8_t* X, const float* Xd, const float* src,
+                                                      const float* nw, float eps, int R, const int8_t* Wq,
+                                                      const __half* Ws, int N, float* y, int ldy) {
+    constexpr int K = 1024 * T, LX = K + 16;
+    __shared__ __align__(16) int8_t tile[16 * RF * LX + 16 * RF * (K / QK) * 4];
+    __shared__ float hx[4][RF][4][64];
+    __shared__ float part[8][4];
+    const int tid = threadIdx.x;
+    const int n0 = 16 * blockIdx.x, r0 = 16 * RF * blockIdx.y, rn = min(16 * RF, R - r0);
+    XWeights<T> w;
+    exact_load_w<T>(w, Wq, Ws, N, K, n0, tid);
+    float rv[4] = {0.f, 0.f, 0.f, 0.f}, v[4];
+    if (RESID) resid_load<RF>(rv, r0, R, n0, N, y, ldy, tid);
+    float* sXd = (float*)(tile + 16 * RF * LX);
+    if constexpr (FOLD) norm_tile<T>(src + (size_t)r0 * K, K, eps, rn, nw, tile, LX, sXd, part, tid);
+    else stage_tile(X, Xd, K, r0, rn, tile, LX, sXd, tid);
+    __syncthreads();
+    exact_frag_lds<T, RF>(w, tile, LX, sXd, rn, hx, v, tid);
+    item_store<RF, RESID>(v, rv, r0, R, n0, N, y, ldy, tid);
+}
+
+template <int T, int RF, bool FOLD>
+__global__ __launch_bounds__(256, 1) void k_xr_gu(const int8_t* X, const float* Xd, const float* src, const float* nw,
+                                                  float eps, int R, const int8_t* Wq, const __half* Ws, int F,
+                                                  int8_t* hq, float* hd) {
+    constexpr int K = 1024 * T, LX = K + 16;
+    __shared__ __align__(16) int8_t tile[16 * RF * LX + 16 * RF * (K / QK) * 4];
+    __shared__ float hx[4][RF][4][64];
+    __shared__ float part[8][4];
+    __shared__ float gub[16 * RF][64];
+    __shared__ __align__(16) int8_t hqb[16 * RF][32];
+    __shared__ float hdb[16 * RF];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int it = blockIdx.x;
+    XWeights<T> w[4];
+#pragma unroll
+    for (int c = 0; c < 4; c++) exact_load_w<T>(w[c], Wq, Ws, 2 * F, K, 64 * it + 16 * c, tid);
+    float* sXd = (float*)(tile + 16 * RF * LX);
+    if constexpr (FOLD) norm_tile<T>(src, K, eps, R, nw, tile, LX, sXd, part, tid);
+    else stage_tile(X, Xd, K, 0, R, tile, LX, sXd, tid);
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+        float v[4];
+        exact_frag_lds<T, RF>(w[c], tile, LX, sXd, R, hx, v, tid);
+        if (wv < RF) {
+#pragma unroll
+            for (int r = 0; r < 4; r++) gub[16 * wv + 4 * (lane >> 4) + r][16 * c + (lane & 15)] = v[r];
+        }
+        __syncthreads();
+    }
+    const int grp = tid >> 5, j = tid & 31;   // row m on the 32-lane group m % 8 (swiglu_q8_block's arithmetic)
+    for (int m = grp; m < 16 * RF; m += 8) {
+        float dq;
+        const int q = swiglu_q8_value(gub[m], j, dq);
+        hqb[m][j] = (int8_t)q;
+        if (j == 0) hdb[m] = dq;
+    }
+    __syncthreads();
+    if (tid < R * 8) {
+        const int m = tid >> 3, w4 = tid & 7;
+        ((int32_t*)(hq + (size_t)m * F + 32 * it))[w4] = ((const int32_t*)hqb[m])[w4];
+    }
+    if (tid < R) hd[(size_t)tid * (F / QK) + it] = hdb[tid];
+}
+
+bool xr_ok(int R, int K) { return R >= 1 && R <= 32 && (K == 1024 || K == 2048 || K == 3072 || K == 6144); }
+
+void xr_linear(const int8_t* xq, const float* xd, const float* src, const float* nw, float eps, int R, const Q8Mat& W,
+               float* y, int ldy, bool resid, hipStream_t s) {
+    const bool fold = src != nullptr;
+    ProfScope ps(s, fold ? "xr_linear_rms" : "xr_linear", 2.0 * R * W.N * W.K,
+                 (double)W.N * W.K * (1.0 + 2.0 / 32) + (double)R * W.K * (fold ? 4.0 : 1.125) +
+                     (double)R * W.N * 4.0 * (resid ? 2 : 1));
+    QASR_CHECK(xr_ok(R, W.K) && W.N % 16 == 0 && (!fold || (R <= 8 && nw)), QASR_E_INVALID,
+               "xr_linear: rows 1-32 (fold: ≤ 8), K 1,024 / 2,048 / 3,072 / 6,144");
+    // rows > 16: two 16-row slices (one row fragment each) where a 32-row tile would not fit LDS (K 6,144), else one
+    // 32-row slice
+    const bool two = R > 16 && W.K > 3072;
+    const int rf = R > 16 && !two ? 2 : 1;
+    const dim3 g(W.N / 16, two ? 2 : 1);
+#define XR_GO(TT, RFF, FF, RR)                                                                                        \
+    k_xr_linear<TT, RFF, FF, RR><<<g, 256, 0, s>>>(xq, xd, src, nw, eps, R, W.qs, W.sc, W.N, y, ldy)
+#define XR_RF(TT, FF, RR)                      \
+    do {                                       \
+        if (rf == 2) XR_GO(TT, 2, FF, RR);     \
+        else XR_GO(TT, 1, FF, RR);             \
+    } while (0)
+#define XR_T(FF, RR)                                        \
+    do {                                                    \
+        switch (W.K) {                                      \
+            case 1024: XR_RF(1, FF, RR); break;             \
+            case 2048: XR_RF(2, FF, RR); break;             \
+            case 3072: XR_RF(3, FF, RR); break;             \
+            default: XR_GO(6, 1, FF, RR); break;            \
+        }                                                   \
+    } while (0)
+    if (fold) {
+        QASR_CHECK(W.K <= 2048 && !resid, QASR_E_INVALID, "xr_linear: the norm fold is for the QKV input (K ≤ 2,048)");
+        if (W.K == 1024) XR_GO(1, 1, true, false);
+        else XR_GO(2, 1, true, false);
+    } else if (resid) {
+        XR_T(false, true);
+    } else {
+        XR_T(false, false);
+    }
+#undef XR_T
+#undef XR_RF
+#undef XR_GO
+    QASR_HIP(hipGetLastError());
+}
+
+void xr_gu_swiglu(const int8_t* xq, const float* xd, const float* src, const float* nw, float eps, int R,
+                  const Q8Mat& W, int8_t* hq, float* hd, hipStream_t s) {
+    const bool fold = src != nullptr;
+    ProfScope ps(s, fold ? "xr_gu_rms" : "xr_gu", 2.0 * R * W.N * W.K,
+                 (double)W.N * W.K * (1.0 + 2.0 / 32) + (double)R * W.K * (fold ? 4.0 : 1.125) + R * W.N * 0.5625);
+    QASR_CHECK(xr_ok(R, W.K) && W.K <= 2048 && W.N % 64 == 0 && (!fold || (R <= 8 && nw)), QASR_E_INVALID,
+               "xr_gu_swiglu: rows 1-32 (fold: ≤ 8), K 1,024 / 2,048, interleaved gate/up");
+    const int F = W.N / 2;
+    const dim3 g(F / 32);
+    if (W.K == 1024) {
+        if (fold) k_xr_gu<1, 1, true><<<g, 256, 0, s>>>(xq, xd, src, nw, eps, R, W.qs, W.sc, F, hq, hd);
+        else if (R <= 16) k_xr_gu<1, 1, false><<<g, 256, 0, s>>>(xq, xd, src, nw, eps, R, W.qs, W.sc, F, hq, hd);
+        else k_xr_gu<1, 2, false><<<g, 256, 0, s>>>(xq, xd, src, nw, eps, R, W.qs, W.sc, F, hq, hd);
+    } else {
+        if (fold) k_xr_gu<2, 1, true><<<g, 256, 0, s>>>(xq, xd, src, nw, eps, R, W.qs, W.sc, F, hq, hd);
+        else if (R <= 16) k_xr_gu<2, 1, false><<<g, 256, 0, s>>>(xq, xd, src, nw, eps, R, W.qs, W.sc, F, hq, hd);
+        else k_xr_gu<2, 2, false><<<g, 256, 0, s>>>(xq, xd, src, nw, eps, R, W.qs, W.sc, F, hq, hd);
+    }
+    QASR_HIP(hipGetLastError());
 }
 
 namespace {

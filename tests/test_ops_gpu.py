@@ -139,14 +139,14 @@ def _linear_case(torch_dev, m, n, k, path, epi, seed=0, exact=False, s4=False):
     if s4:
         s4t = empty((n, k // 32), torch.float16, torch_dev)
         _lib.check(L().qasr_op_stage_scales(ptr(ws), n, k, ptr(s4t), None))
-        _lib.check(L().qasr_op_register_stage_scales(ptr(ws), ptr(s4t)))
+        _lib.check(L().qasr_op_register_stage_scales(ptr(ws), n, k, ptr(s4t)))
     try:
         _lib.check(L().qasr_op_linear_q8(ptr(xq), ptr(xdd), m, ptr(wq), ptr(ws), n, k, ptr(bt),
                                          ptr(y) if epi == 1 else None, ptr(y), n, epi, path, None))
         out = host(y)
     finally:
         if s4:
-            _lib.check(L().qasr_op_register_stage_scales(ptr(ws), None))
+            _lib.check(L().qasr_op_register_stage_scales(ptr(ws), n, k, None))
     return out, ref.astype(np.float32)
 
 
@@ -288,14 +288,14 @@ def test_gemm_swiglu_q8(torch_dev, m, f, k, cfg, s4):
     if s4:
         s4t = empty((2 * f, k // 32), torch.float16, torch_dev)
         _lib.check(L().qasr_op_stage_scales(ptr(ws), 2 * f, k, ptr(s4t), None))
-        _lib.check(L().qasr_op_register_stage_scales(ptr(ws), ptr(s4t)))
+        _lib.check(L().qasr_op_register_stage_scales(ptr(ws), 2 * f, k, ptr(s4t)))
     try:
         _lib.check(L().qasr_op_gemm_swiglu_q8_cfg(ptr(xq), ptr(xdd), m, ptr(wq), ptr(ws), 2 * f, k, ptr(hq), ptr(hd),
                                                   cfg, None))
         torch.cuda.synchronize()
     finally:
         if s4:
-            _lib.check(L().qasr_op_register_stage_scales(ptr(ws), None))
+            _lib.check(L().qasr_op_register_stage_scales(ptr(ws), 2 * f, k, None))
     assert np.allclose(host(hd), dr, rtol=2e-3)
     assert (np.abs(host(hq).astype(int) - qr) <= 1).all()
     # the unfused path (GEMV rows) on the interleaved layout
@@ -983,3 +983,69 @@ def test_attention_verify_rows_exact(torch_dev, split, P, R):
     bad = [i for i in range(R) if not np.array_equal(a[i], b[i])]
     assert not bad, bad
     assert np.array_equal(host(od_s), host(od_v))
+
+
+# the ≤ 32-row decode's per-phase launches (kernels_persist.hip xr_*): bit-identical to the exact-row chain
+@pytest.mark.parametrize("m", [1, 3, 8, 16, 17, 32])
+@pytest.mark.parametrize("n,k,epi", [(4096, 2048, 0), (2048, 2048, 1), (2048, 6144, 1), (1024, 3072, 1), (4096, 1024, 0)])
+def test_xr_linear_bit_identical_to_exact_rows(torch_dev, m, n, k, epi):
+    """qasr_op_xr_linear (weights loaded up front, rows staged in LDS) == qasr_op_gemm_exact_rows, bit for bit, and
+    for ≤ 8 rows with the norm folded in (src rows, K ≤ 2,048) == qasr_op_rmsnorm_q8 + qasr_op_gemm_exact_rows"""
+    rng = np.random.default_rng(m * 7 + n + k)
+    xq = dev(rng.integers(-127, 128, (m, k), dtype=np.int8), torch_dev)
+    xd = dev((rng.random((m, k // 32)) * 0.02).astype(np.float32), torch_dev)
+    xd[0, 3] = 0.0
+    res = dev((rng.standard_normal((m, n)) * 3).astype(np.float32), torch_dev)
+    wq, ws = _q8_weights(torch_dev, n, k, 11)
+    y_ref, y = res.clone(), res.clone()
+    _lib.check(L().qasr_op_gemm_exact_rows(ptr(xq), ptr(xd), m, ptr(wq), ptr(ws), n, k, ptr(y_ref) if epi else None,
+                                           ptr(y_ref), n, epi, None))
+    _lib.check(L().qasr_op_xr_linear(ptr(xq), ptr(xd), None, None, 0.0, m, ptr(wq), ptr(ws), n, k, ptr(y), n, epi,
+                                     None))
+    assert np.array_equal(host(y), host(y_ref))
+    if m <= 8 and k <= 2048 and epi == 0:
+        src = dev((rng.standard_normal((m, k)) * 2).astype(np.float32), torch_dev)
+        nw = dev((1 + 0.1 * rng.standard_normal(k)).astype(np.float32), torch_dev)
+        q2 = empty((m, k), __import__("torch").int8, torch_dev)
+        d2 = empty((m, k // 32), __import__("torch").float32, torch_dev)
+        _lib.check(L().qasr_op_rmsnorm_q8(ptr(src), m, k, ptr(nw), C.c_float(1e-6), ptr(q2), ptr(d2), None))
+        _lib.check(L().qasr_op_gemm_exact_rows(ptr(q2), ptr(d2), m, ptr(wq), ptr(ws), n, k, None, ptr(y_ref), n, 0,
+                                               None))
+        _lib.check(L().qasr_op_xr_linear(None, None, ptr(src), ptr(nw), C.c_float(1e-6), m, ptr(wq), ptr(ws), n, k,
+                                         ptr(y), n, 0, None))
+        assert np.array_equal(host(y), host(y_ref))
+
+
+@pytest.mark.parametrize("m", [1, 5, 8, 16, 32])
+@pytest.mark.parametrize("f,k", [(6144, 2048), (3072, 1024)])
+def test_xr_gu_swiglu_bit_identical(torch_dev, m, f, k):
+    """qasr_op_xr_gu_swiglu (an h block per workgroup: 4 exact fragments + SwiGLU + Q8) == gemm_exact_rows on the
+    interleaved gate/up + swiglu_q8_interleaved, bit for bit; with the norm folded in (≤ 8 rows) == rmsnorm_q8 first"""
+    import torch
+
+    rng = np.random.default_rng(m + f + k)
+    xq = dev(rng.integers(-127, 128, (m, k), dtype=np.int8), torch_dev)
+    xd = dev((rng.random((m, k // 32)) * 0.02).astype(np.float32), torch_dev)
+    wq, ws = _q8_weights(torch_dev, 2 * f, k, 13)
+    gu = empty((m, 2 * f), torch.float32, torch_dev)
+    hq_ref, hd_ref = empty((m, f), torch.int8, torch_dev), empty((m, f // 32), torch.float32, torch_dev)
+    hq, hd = empty((m, f), torch.int8, torch_dev), empty((m, f // 32), torch.float32, torch_dev)
+
+    def ref(q, d):
+        _lib.check(L().qasr_op_gemm_exact_rows(ptr(q), ptr(d), m, ptr(wq), ptr(ws), 2 * f, k, None, ptr(gu), 2 * f, 0,
+                                               None))
+        _lib.check(L().qasr_op_swiglu_q8_interleaved(ptr(gu), m, f, ptr(hq_ref), ptr(hd_ref), None))
+
+    ref(xq, xd)
+    _lib.check(L().qasr_op_xr_gu_swiglu(ptr(xq), ptr(xd), None, None, 0.0, m, ptr(wq), ptr(ws), 2 * f, k, ptr(hq),
+                                        ptr(hd), None))
+    assert np.array_equal(host(hq), host(hq_ref)) and np.array_equal(host(hd), host(hd_ref))
+    if m <= 8:
+        src = dev((rng.standard_normal((m, k)) * 2).astype(np.float32), torch_dev)
+        nw = dev((1 + 0.1 * rng.standard_normal(k)).astype(np.float32), torch_dev)
+        q2, d2 = empty((m, k), torch.int8, torch_dev), empty((m, k // 32), torch.float32, torch_dev)
+        _lib.check(L().qasr_op_rmsnorm_q8(ptr(src), m, k, ptr(nw), C.c_float(1e-6), ptr(q2), ptr(d2), None))
+        ref(q2, d2)
+        _lib.check(L().qasr_op_xr_gu_swiglu(None, None, ptr(src), ptr(nw), C.c_float(1e-6), m, ptr(wq), ptr(ws), 2 * f,
+                                            k, ptr(hq), ptr(hd), None))
+        assert np.array_equal(host(hq), host(hq_ref)) and np.array_equal(host(hd), host(hd_ref))

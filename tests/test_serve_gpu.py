@@ -234,3 +234,28 @@ def test_engine_longform_matches_python_pipeline(ref, tmp_path):
     assert [d["tokens"] for d in got["segments"]] == [r.tokens for r in res]
     assert [d["text"] for d in got["segments"]] == [r.text for r in res]
     assert [d["language"] for d in got["segments"]] == [r.language or "" for r in res]
+
+
+@pytest.mark.parametrize("stage", ["model", "vad", "asr"])
+def test_engine_longform_failure_is_agreed(stage, tmp_path):
+    """`engine longform` with an injected stage failure (QASR_FAIL_STAGE) at world 1 through the agreement path
+    (QASR_LONGFORM_COMM=1: a one-rank communicator, qasr_dist_agree before each collective): the engine exits
+    non-zero with the stage's reason and prints no result (the N-rank protocol itself: tests/test_shard_cpu.py::
+    test_longform_stage_agreement_gloo); and with the communicator but no failure it still succeeds"""
+    from qasr import _lib
+
+    audio = recording(8.0, 6)
+    wav = tmp_path / "rec.wav"
+    _write_f32_wav(wav, audio)
+    env = {k: val for k, val in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    env.update(QASR_SYNTHETIC="1", HF_HUB_CACHE=str(tmp_path / "hf"), QASR_LONGFORM_COMM="1",
+               QASR_RDV_KEY=f"t{os.getpid()}_{stage}", QASR_RDV_DIR=str(tmp_path), QASR_FAIL_STAGE=stage)
+    args = [_lib.ENGINE_PATH, "longform", "--engine", "qwen3-asr-0.6b", "--force-tps", "8", str(wav)]
+    out = subprocess.run(args, capture_output=True, text=True, env=env, timeout=300)
+    assert out.returncode == 1 and out.stdout == "", (out.returncode, out.stdout[:200], out.stderr[-2000:])
+    assert f"injected failure (QASR_FAIL_STAGE={stage})" in out.stderr, out.stderr[-2000:]
+    if stage == "asr":
+        env.pop("QASR_FAIL_STAGE")
+        ok = subprocess.run(args, capture_output=True, text=True, env=env, timeout=300)
+        assert ok.returncode == 0, ok.stderr[-2000:]
+        assert json.loads(ok.stdout)["world"] == 1
