@@ -1330,286 +1330,6 @@ __global__ __launch_bounds__(256 * KG, KG == 1 ? 2 : 1) void k_gemm_q8d(const in
     gemm_epilogue<TI, TJ>(acc, M, N, m0, n0, arow, bcol, fr, fq, bias, res, y, ldy, epi, yq, yd);
 }
 
-// ------------------------------------------------------------------------------------------------ GEMM (32×32×32 i8)
-typedef int v16i __attribute__((ext_vector_type(16)));
-typedef float v32f __attribute__((ext_vector_type(32)));
-
-// The Q8 W8A8 GEMM on v_mfma_i32_32x32x32_i8 (round 4): K = 32 = ONE Q8 block per MFMA for a 32×32 tile — the exact
-// int32 block sums at twice the per-output rate of the CDNA3-form 16x16x32_i8 (tools/micro/mfma_rate.hip, MI355X:
-// ~33 cycles per 1,024 outputs against ~18 per 256) and one MFMA latency per 16 outputs of a lane.
-//  * Scales (OPS): the products d_x(row)·d_w(col) of a 32-row × 64-column pair of tiles come from ONE
-//    v_mfma_f32_32x32x1_2b_f32 (an outer product per block: lanes 0–31 give block 0, 32–63 block 1; d_x·d_w of two
-//    f16-valued scales is exact in f32, so it is the multiply the GEMV does), whose result registers line up with the
-//    i8 MFMA's 32×32 layout — the rescale is cvt + fma per output and block, acc = fma((float)Σq·q, d_x·d_w, acc),
-//    the arithmetic of every Q8 GEMM here (same bits per output for the same block order).  !OPS: 16 VALU
-//    multiplies per tile instead.
-//  * Tiles: a wave owns 32 × 32·TN outputs; WM × WN waves per K group, KG K groups (group g takes blocks
-//    [g·KB/KG, (g+1)·KB/KG) of every stage; partials added through LDS in group order).  Staging is k_gemm_q8d's:
-//    every operand byte by LDS-DMA into an NBUF-stage ring, 16-B chunks XOR-swizzled (conflict-free for the
-//    ds_read_b128 fragment reads of both 64- and 128-byte rows), WS4 stage scales.
-//  * Schedule, pinned by sched_barrier(0): slot q = MFMA q, then (at a block's last tile) the next block's fragment
-//    and scale reads into the other register slot, then the rescale of MFMA q−1 (whose result has landed behind the
-//    previous slot's 32 VALU); the next block's outer product goes out at its first slot.
-//  * Epilogue: each wave's f32 tile → LDS (column-major) → the 16×16 fragment layout → gemm_epilogue, i.e. the
-//    epilogue code of the 16×16 kernels (bias, residual, GELU, GELU + Q8, SwiGLU + Q8, f16 store).
-template <int WM, int WN, int TN, int NBUF, int BK, int KG, bool WS4, bool OPS>
-__global__ __launch_bounds__(64 * WM * WN * KG) void k_q8mm(const int8_t* __restrict__ X, const float* __restrict__ Xd,
-                                                          int M, const int8_t* __restrict__ W,
-                                                          const __half* __restrict__ Wsc,
-                                                          const __half* __restrict__ Wsc4, int N, int K,
-                                                          const float* __restrict__ bias, const float* res, float* y,
-                                                          int ldy, int epi, int8_t* __restrict__ yq,
-                                                          float* __restrict__ yd) {
-    static_assert(BK == 64 || BK == 128, "k_q8mm: a stage is 2 or 4 Q8 blocks");
-    static_assert(!OPS || TN == 2, "k_q8mm: the outer-product scales cover two 32-column tiles");
-    static_assert(!WS4 || BK == 128, "k_q8mm: WS4 stages are K = 128");
-    constexpr int NWG = WM * WN, NW = NWG * KG;
-    constexpr int KB = BK / 32;
-    static_assert(KB % KG == 0, "k_q8mm: K groups split a stage's blocks");
-    constexpr int KBG = KB / KG;
-    constexpr int BM = 32 * WM, BN = 32 * TN * WN;
-    constexpr int RP = 1024 / BK;   // rows per 1-KB DMA piece
-    constexpr int PA = BM / RP, PB = BN / RP;
-    static_assert(PA * RP == BM && PB * RP == BN && (PA + PB) % NW == 0, "k_q8mm: DMA pieces per wave");
-    constexpr int PP = (PA + PB) / NW;
-    constexpr int OB = BM * BK, OSA = OB + BN * BK, OSB = OSA + KB * BM * 4, STAGE = OSB + (KB / 2) * BN * 4;
-    constexpr int SAW = KB * BM / NW, ASI = (SAW + 63) / 64;
-    constexpr int SBW = BN * KB / (2 * NW), BSI = (SBW + 63) / 64;
-    static_assert(WS4 || (SAW * NW == KB * BM && SBW * 2 * NW == BN * KB), "k_q8mm: scale gathers per wave");
-    constexpr int AR4 = BM / NW, BL4 = BN / (2 * NW);
-    static_assert(!WS4 || (AR4 * NW == BM && AR4 <= 64 && BL4 * 2 * NW == BN && BL4 >= 1), "k_q8mm: WS4 tile");
-    constexpr int SCI = WS4 ? 2 : ASI + BSI;
-    constexpr int NPW = PP + SCI;   // DMA instructions per wave per stage
-    constexpr int D = NBUF - 1;
-    constexpr int F = 16 * TN;                         // accumulators per lane
-    constexpr int TP = 32 + 4;                         // epilogue transpose: [column][TP floats] per wave
-    constexpr int EPI_B = NWG * 32 * TN * TP * 4;
-    constexpr int RED_B = (KG - 1) * NWG * 64 * F * 4;
-    constexpr int SMEM = std::max(NBUF * STAGE, std::max(EPI_B, RED_B));
-    __shared__ __attribute__((aligned(1024))) char smem[SMEM];
-
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int kg = wave / NWG, lw = wave % NWG, wr = lw / WN, wc = lw % WN;
-    const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM;
-    const int nb = K / QK;
-    const int nsteps = K / BK;
-    auto swz = [](int r) { return BK == 64 ? (r >> 2) & 3 : (r >> 1) & 7; };
-
-    // ---- DMA sources: the stage's A and B pieces as one list, PP per wave; scales as k_gemm_q8d
-    const int8_t* u_src[PP];
-    uint32_t u_dst[PP];
-#pragma unroll
-    for (int u = 0; u < PP; u++) {
-        const int p = wave * PP + u;
-        const bool isa = p < PA;
-        const int row = RP * (isa ? p : p - PA) + lane / (BK / 16), c = (lane % (BK / 16)) ^ swz(row);
-        u_src[u] = isa ? X + (size_t)min(m0 + row, M - 1) * K + 16 * c : W + (size_t)min(n0 + row, N - 1) * K + 16 * c;
-        u_dst[u] = isa ? 1024 * p : OB + 1024 * (p - PA);
-    }
-    const float* sa_src[ASI];
-#pragma unroll
-    for (int u = 0; u < ASI; u++) {
-        const int p = wave * SAW + min(64 * u + lane, SAW - 1);
-        sa_src[u] = Xd + (size_t)min(m0 + p % BM, M - 1) * nb + p / BM;
-    }
-    const uint32_t* sb_src[BSI];
-#pragma unroll
-    for (int u = 0; u < BSI; u++) {
-        const int p = wave * SBW + min(64 * u + lane, SBW - 1);
-        sb_src[u] = (const uint32_t*)Wsc + (size_t)min(n0 + p % BN, N - 1) * (nb / 2) + p / BN;
-    }
-    const float* sa4_src = Xd + (size_t)min(m0 + wave * AR4 + min(lane, AR4 - 1), M - 1) * nb;
-    const __half* sb4_src = WS4 ? Wsc4 + (size_t)4 * min(n0 + 2 * (wave * BL4 + min(lane, BL4 - 1)), N - 2) : nullptr;
-    const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
-    const uint32_t wsa = __builtin_amdgcn_readfirstlane(lds0 + OSA + (WS4 ? wave * AR4 * 16 : wave * SAW * 4));
-    const uint32_t wsb = __builtin_amdgcn_readfirstlane(lds0 + OSB + (WS4 ? wave * BL4 * 16 : wave * SBW * 4));
-    auto issue = [&](int s, int buf) {
-        const int k0 = s * BK;
-        const uint32_t so = buf * STAGE;
-#pragma unroll
-        for (int u = 0; u < PP; u++) dma_lds16(u_src[u] + k0, __builtin_amdgcn_readfirstlane(lds0 + u_dst[u]) + so);
-        if constexpr (WS4) {
-            if (lane < AR4) dma_lds16(sa4_src + k0 / QK, wsa + so);
-            if (lane < BL4) dma_lds16(sb4_src + (size_t)(k0 / 128) * N * 4, wsb + so);
-        } else {
-#pragma unroll
-            for (int u = 0; u < ASI; u++)
-                if (64 * u + lane < SAW) dma_lds4(sa_src[u] + k0 / QK, wsa + so + 256 * u);
-#pragma unroll
-            for (int u = 0; u < BSI; u++)
-                if (64 * u + lane < SBW) dma_lds4(sb_src[u] + k0 / 64, wsb + so + 256 * u);
-        }
-    };
-
-    const int l31 = lane & 31, hh = lane >> 5;
-    const int arow = 32 * wr, bcol = 32 * TN * wc;
-    const bool active = m0 + arow < M;   // wave-uniform: waves past the last row skip the math, still stage
-    const int kb0 = kg * KBG;
-    // fragment offsets (k-independent): lane (l31, hh) reads row / column l31's 16 bytes [16·hh, 16·hh + 16) of block kb
-    int offa[KBG], offb[KBG][TN];
-#pragma unroll
-    for (int b = 0; b < KBG; b++) {
-        const int ra = arow + l31;
-        offa[b] = ra * BK + 16 * ((2 * (kb0 + b) + hh) ^ swz(ra));
-        asm volatile("" : "+v"(offa[b]));
-#pragma unroll
-        for (int j = 0; j < TN; j++) {
-            const int rb = bcol + 32 * j + l31;
-            offb[b][j] = OB + rb * BK + 16 * ((2 * (kb0 + b) + hh) ^ swz(rb));
-            asm volatile("" : "+v"(offb[b][j]));
-        }
-    }
-
-    float acc[F];
-#pragma unroll
-    for (int e = 0; e < F; e++) acc[e] = 0.f;
-
-#pragma unroll
-    for (int t = 0; t < D; t++)
-        if (t < nsteps) issue(t, t);
-    for (int s = 0; s < nsteps; s++) {
-        wait_stages<NPW, D>(min(D - 1, nsteps - 1 - s));
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-        if (s + D < nsteps) issue(s + D, (s + D) % NBUF);
-        if (!active) continue;
-        const char* st = smem + (s % NBUF) * STAGE;
-        v4i a[2], b[2][TN];
-        float dx[2], dw[2], dxv[OPS ? 1 : 2][16], dwj[OPS ? 1 : 2][TN];
-        auto load = [&](int sl, int bb) {   // block kb0 + bb of this stage into register slot sl
-            const int kb = kb0 + bb;
-            a[sl] = *(const v4i*)(st + offa[bb]);
-#pragma unroll
-            for (int j = 0; j < TN; j++) b[sl][j] = *(const v4i*)(st + offb[bb][j]);
-            if constexpr (OPS) {
-                if constexpr (WS4) {
-                    dx[sl] = *(const float*)(st + OSA + 16 * (arow + l31) + 4 * kb);
-                    dw[sl] = __half2float(*(const __half*)(st + OSB + 8 * (bcol + lane) + 2 * kb));
-                } else {
-                    dx[sl] = *(const float*)(st + OSA + 4 * (kb * BM + arow + l31));
-                    const uint32_t v = *(const uint32_t*)(st + OSB + 4 * ((kb >> 1) * BN + bcol + lane));
-                    dw[sl] = __half2float(__ushort_as_half((unsigned short)((kb & 1) ? v >> 16 : v & 0xffff)));
-                }
-            } else {
-#pragma unroll
-                for (int g = 0; g < 4; g++) {   // rows 8g + 4hh … + 3 of this wave's 32
-                    if constexpr (WS4) {
-#pragma unroll
-                        for (int r = 0; r < 4; r++)
-                            dxv[sl][4 * g + r] = *(const float*)(st + OSA + 16 * (arow + 8 * g + 4 * hh + r) + 4 * kb);
-                    } else {
-                        const float4 v = *(const float4*)(st + OSA + 4 * (kb * BM + arow + 8 * g + 4 * hh));
-                        dxv[sl][4 * g] = v.x, dxv[sl][4 * g + 1] = v.y, dxv[sl][4 * g + 2] = v.z, dxv[sl][4 * g + 3] = v.w;
-                    }
-                }
-#pragma unroll
-                for (int j = 0; j < TN; j++) {
-                    const int col = bcol + 32 * j + l31;
-                    if constexpr (WS4) {
-                        dwj[sl][j] = __half2float(*(const __half*)(st + OSB + 8 * col + 2 * kb));
-                    } else {
-                        const uint32_t v = *(const uint32_t*)(st + OSB + 4 * ((kb >> 1) * BN + col));
-                        dwj[sl][j] = __half2float(__ushort_as_half((unsigned short)((kb & 1) ? v >> 16 : v & 0xffff)));
-                    }
-                }
-            }
-        };
-        v16i c[2];
-        v32f prod[OPS ? 2 : 1];
-        auto rescale = [&](int q) {
-            const int bb = q / TN, j = q % TN;
-#pragma unroll
-            for (int r = 0; r < 16; r++) {
-                if constexpr (OPS)
-                    acc[16 * j + r] = fmaf((float)c[q & 1][r], prod[bb & 1][16 * j + r], acc[16 * j + r]);
-                else
-                    acc[16 * j + r] = fmaf((float)c[q & 1][r], dxv[bb & 1][r] * dwj[bb & 1][j], acc[16 * j + r]);
-            }
-        };
-        constexpr int NQ = KBG * TN;
-        load(0, 0);
-#pragma unroll
-        for (int q = 0; q < NQ; q++) {
-            const int bb = q / TN, j = q % TN;
-            if constexpr (OPS) {
-                if (j == 0) {
-                    const v32f z = {};
-                    prod[bb & 1] = __builtin_amdgcn_mfma_f32_32x32x1f32(dx[bb & 1], dw[bb & 1], z, 0, 0, 0);
-                }
-            }
-            const v16i z16 = {};
-            c[q & 1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[bb & 1], b[bb & 1][j], z16, 0, 0, 0);
-            // the MFMA issues first: left free inside the slot the scheduler put it behind the slot's VALU, so the
-            // next slot's rescale consumed it right away (s_nop 9 per MFMA)
-            __builtin_amdgcn_sched_barrier(0);
-            if (j == TN - 1 && bb + 1 < KBG) load((bb + 1) & 1, bb + 1);
-            if (q > 0) rescale(q - 1);
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        rescale(NQ - 1);
-        __builtin_amdgcn_sched_barrier(0);
-    }
-    __syncthreads();   // every wave is out of the ring: its LDS takes the K-group partials / the epilogue transpose
-    if constexpr (KG > 1) {
-        float* red = (float*)smem;   // [KG-1][NWG][F][64]
-        if (kg > 0 && active) {
-#pragma unroll
-            for (int e = 0; e < F; e++) red[(((size_t)(kg - 1) * NWG + lw) * F + e) * 64 + lane] = acc[e];
-        }
-        __syncthreads();
-        if (kg > 0) return;
-        if (active) {
-#pragma unroll
-            for (int g = 1; g < KG; g++)
-#pragma unroll
-                for (int e = 0; e < F; e++) acc[e] += red[(((size_t)(g - 1) * NWG + lw) * F + e) * 64 + lane];
-        }
-        __syncthreads();   // (group 0 only) the partials are read before the transpose image overwrites them
-    }
-    // epilogue: 32×32 layout (lane: column l31, rows (r&3) + 8(r>>2) + 4hh) → LDS [column][row] → 16×16 fragments
-    // (lane (fr, kh): column fr, rows 4kh … 4kh+3 of each fragment) → gemm_epilogue
-    float* tp = (float*)smem + (size_t)lw * 32 * TN * TP;
-    if (active) {
-#pragma unroll
-        for (int j = 0; j < TN; j++)
-#pragma unroll
-            for (int g = 0; g < 4; g++)
-                *(float4*)(tp + (32 * j + l31) * TP + 8 * g + 4 * hh) =
-                    make_float4(acc[16 * j + 4 * g], acc[16 * j + 4 * g + 1], acc[16 * j + 4 * g + 2],
-                                acc[16 * j + 4 * g + 3]);
-    }
-    __builtin_amdgcn_wave_barrier();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (!active) return;
-    constexpr int TI = 2, TJ = 2 * TN;
-    const int fr = lane & 15, kh = lane >> 4, fq = 4 * kh;
-    float o[TI][TJ][4];
-#pragma unroll
-    for (int i = 0; i < TI; i++)
-#pragma unroll
-        for (int jj = 0; jj < TJ; jj++) {
-            const float4 v = *(const float4*)(tp + (16 * jj + fr) * TP + 16 * i + fq);
-            o[i][jj][0] = v.x, o[i][jj][1] = v.y, o[i][jj][2] = v.z, o[i][jj][3] = v.w;
-        }
-    gemm_epilogue<TI, TJ, true>(o, M, N, m0, n0, arow, bcol, fr, fq, bias, res, y, ldy, epi, yq, yd);
-}
-
-template <int WM, int WN, int TN, int NBUF, int BK, int KG, bool OPS>
-static void launch_q8mm(hipStream_t s, const int8_t* xq, const float* xd, int M, const Q8Mat& W, const float* bias,
-                        const float* res, float* y, int ldy, int epi, int8_t* yq, float* yd) {
-    constexpr int BM = 32 * WM, BN = 32 * TN * WN;
-    const dim3 grid(cdiv(W.N, BN), cdiv(M, BM));
-    if constexpr (BK == 128) {
-        if (W.sc4 && g_ws4 && W.N % 2 == 0) {
-            k_q8mm<WM, WN, TN, NBUF, BK, KG, true, OPS><<<grid, 64 * WM * WN * KG, 0, s>>>(
-                xq, xd, M, W.qs, W.sc, W.sc4, W.N, W.K, bias, res, y, ldy, epi, yq, yd);
-            return;
-        }
-    }
-    k_q8mm<WM, WN, TN, NBUF, BK, KG, false, OPS><<<grid, 64 * WM * WN * KG, 0, s>>>(
-        xq, xd, M, W.qs, W.sc, nullptr, W.N, W.K, bias, res, y, ldy, epi, yq, yd);
-}
-
 // ------------------------------------------------------------------------------------------------ GEMM (decode, K over waves)
 // Decode-sized Q8 W8A8 GEMM (a decode step's M ≤ 256 rows; every weight byte is read once per step).  One workgroup
 // owns a (16·TI)×(16·TJ) output tile over the WHOLE K and its NW waves split K into equal slices: each wave loads its
@@ -1937,8 +1657,8 @@ static void launch_gemm_dma(dim3 grid, hipStream_t s, const int8_t* xq, const fl
 
 // GEMM configurations: 0..3 register-staged kernel (any K % 32 == 0), 4..11 LDS-DMA kernel, 2×2 waves, stages of
 // 64 (4..7) or 128 (8..11) K (K % bk == 0); 12..13 LDS-DMA, 4×1 waves (64-column wave tiles), K-128 stages.
-// ks: waves of the K-over-waves decode kernel (bk unused); mm: the 32×32×32 kernel k_q8mm (no split-K)
-struct GemmCfg { int bm, bn, bk; bool dma; int ks = 0; bool mm = false; };
+// ks: waves of the K-over-waves decode kernel (bk unused)
+struct GemmCfg { int bm, bn, bk; bool dma; int ks = 0; };
 static const GemmCfg kGemmCfgs[] = {
     {128, 128, 128, false}, {64, 128, 128, false}, {64, 64, 128, false}, {32, 64, 128, false},   // 0..3
     {128, 128, 64, true}, {64, 128, 64, true}, {64, 64, 64, true}, {128, 64, 64, true},          // 4..7
@@ -1953,17 +1673,11 @@ static const GemmCfg kGemmCfgs[] = {
     {32, 16, 0, false, 16}, {32, 32, 0, false, 16}, {64, 16, 0, false, 16}, {64, 32, 0, false, 8},
     {16, 64, 0, false, 16}, {32, 64, 0, false, 8}, {64, 64, 0, false, 8},
     {0, 0, 0, false},   // 31: reserved (the ops' "auto" code)
-    // round 4, K-128 stages: 32..35 four K groups (16 waves: 4 per SIMD) — 64×64 2×2 / 4×1 (64-column wave tiles:
-    // SwiGLU, fix-up) with rings of 3 / 6; 36..37 one K group, ring 6 — 64×32, 32×64 (256 tiles of N 2,048 at 256
-    // rows); 38..39 two K groups — 128×64 4×1, 128×128 2×2
-    {64, 64, 128, true}, {64, 64, 128, true}, {64, 64, 128, true}, {64, 64, 128, true},      // 32..35
+    // 32..35: reserved (round 4's four-K-group 16-wave tiles: never faster, removed in round 5 — DESIGN §10)
+    {0, 0, 0, false}, {0, 0, 0, false}, {0, 0, 0, false}, {0, 0, 0, false},
+    // round 4, K-128 stages: 36..37 one K group, ring 6 — 64×32, 32×64 (256 tiles of N 2,048 at 256 rows); 38..39 two
+    // K groups — 128×64 4×1, 128×128 2×2.  (40..48, round 4's 32×32×32 kernel k_q8mm: never picked, removed in round 5)
     {64, 32, 128, true}, {32, 64, 128, true}, {128, 64, 128, true}, {128, 128, 128, true},   // 36..39
-    // 40..48: k_q8mm (32×32×32 i8 MFMA + outer-product scales; wave tile 32×64): 40 128×128 8 waves K-64 ring 3,
-    // 41 the same with K-128 stages, 42 128×64 4 waves K-64, 43 64×64 2 waves × 2 K groups, 44 32×64 × 4 K groups,
-    // 45 64×64 × 4 K groups (8 waves), 46 64×128 4 waves; 47 / 48 = 40 / 43 with VALU scale products
-    {128, 128, 64, true, 0, true}, {128, 128, 128, true, 0, true}, {128, 64, 64, true, 0, true},
-    {64, 64, 128, true, 0, true}, {32, 64, 128, true, 0, true}, {64, 64, 128, true, 0, true},
-    {64, 128, 128, true, 0, true}, {128, 128, 64, true, 0, true}, {64, 64, 128, true, 0, true},
 };
 constexpr int kNumGemmCfgs = sizeof(kGemmCfgs) / sizeof(kGemmCfgs[0]);
 
@@ -1986,21 +1700,6 @@ static void launch_ks_cfg(int cfg, hipStream_t s, const int8_t* xq, const float*
         case 28: launch_ks<1, 4, 16>(s, xq, xd, M, W, bias, res, y, ldy, epi, yq, yd); break;
         case 29: launch_ks<2, 4, 8>(s, xq, xd, M, W, bias, res, y, ldy, epi, yq, yd); break;
         default: launch_ks<4, 4, 8>(s, xq, xd, M, W, bias, res, y, ldy, epi, yq, yd); break;
-    }
-}
-
-static void launch_mm_cfg(int cfg, hipStream_t s, const int8_t* xq, const float* xd, int M, const Q8Mat& W,
-                          const float* bias, const float* res, float* y, int ldy, int epi, int8_t* yq, float* yd) {
-    switch (cfg) {
-        case 40: launch_q8mm<4, 2, 2, 3, 64, 1, true>(s, xq, xd, M, W, bias, res, y, ldy, epi, yq, yd); break;
-        case 41: launch_q8mm<4, 2, 2, 3, 128, 1, true>(s, xq, xd, M, W, bias, res, y, ldy, epi, yq, yd); break;
-        case 42: launch_q8mm<4, 1, 2, 3, 64, 1, true>(s, xq, xd, M, W, bias, res, y, ldy, epi, yq, yd); break;
-        case 43: launch_q8mm<2, 1, 2, 3, 128, 2, true>(s, xq, xd, M, W, bias, res, y, ldy, epi, yq, yd); break;
-        case 44: launch_q8mm<1, 1, 2, 4, 128, 4, true>(s, xq, xd, M, W, bias, res, y, ldy, epi, yq, yd); break;
-        case 45: launch_q8mm<2, 1, 2, 3, 128, 4, true>(s, xq, xd, M, W, bias, res, y, ldy, epi, yq, yd); break;
-        case 46: launch_q8mm<2, 2, 2, 3, 128, 1, true>(s, xq, xd, M, W, bias, res, y, ldy, epi, yq, yd); break;
-        case 47: launch_q8mm<4, 2, 2, 3, 64, 1, false>(s, xq, xd, M, W, bias, res, y, ldy, epi, yq, yd); break;
-        default: launch_q8mm<2, 1, 2, 3, 128, 2, false>(s, xq, xd, M, W, bias, res, y, ldy, epi, yq, yd); break;
     }
 }
 
@@ -2033,10 +1732,6 @@ static void launch_cfg(int cfg, dim3 grid, hipStream_t s, const int8_t* xq, cons
         case 21: launch_gemm_dma<2, 2, 2, 2, 6, 128>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd, fp, fc); break;
         case 22: launch_gemm_dma<4, 1, 1, 4, 6, 128>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd, fp, fc); break;
         case 23: launch_gemm_dma<2, 2, 1, 4, 4, 128>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd, fp, fc); break;
-        case 32: launch_gemm_dma<2, 2, 2, 2, 3, 128, 4>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd, fp, fc); break;
-        case 33: launch_gemm_dma<4, 1, 1, 4, 3, 128, 4>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd, fp, fc); break;
-        case 34: launch_gemm_dma<2, 2, 2, 2, 6, 128, 4>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd, fp, fc); break;
-        case 35: launch_gemm_dma<4, 1, 1, 4, 6, 128, 4>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd, fp, fc); break;
         case 36: launch_gemm_dma<2, 2, 2, 1, 6, 128>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd, fp, fc); break;
         case 37: launch_gemm_dma<2, 2, 1, 2, 6, 128>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd, fp, fc); break;
         case 38: launch_gemm_dma<4, 1, 2, 4, 3, 128, 2>(grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd, fp, fc); break;
@@ -2427,13 +2122,6 @@ void gemm_q8(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const flo
     }
     if (force_cfg >= 0 && force_cfg < kNumGemmCfgs && usable(force_cfg)) pick = force_cfg;
     const GemmCfg& cf = kGemmCfgs[pick];
-    if (cf.mm) {   // the 32×32×32 kernel: one launch over the whole K, no split-K (the epilogue stores every output)
-        QASR_CHECK(epi != EPI_SWIGLU || (W.N % 64 == 0 && yq && yd), QASR_E_INVALID,
-                   "gemm_q8: SwiGLU epilogue needs N % 64 == 0");
-        QASR_CHECK(epi != EPI_GELU_Q8 || (W.N % 32 == 0 && yq && yd), QASR_E_INVALID, "gemm_q8: GELU+Q8 epilogue shape");
-        launch_mm_cfg(pick, s, xq, xd, M, W, bias, res, y, ldy, epi, yq, yd);
-        return;
-    }
     if (cf.ks) {   // decode kernel: one launch over the whole K, no split-K, no memset
         QASR_CHECK(epi != EPI_SWIGLU || (cf.bn == 64 && W.N % 64 == 0 && yq && yd), QASR_E_INVALID,
                    "gemm_q8: SwiGLU epilogue needs a 64-column wave tile");
@@ -2445,8 +2133,7 @@ void gemm_q8(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const flo
     const int tiles = cdiv(W.N, cf.bn) * cdiv(M, cf.bm);
     // split-K through the fix-up workspace (any epilogue, deterministic): a forced / table split count of a DMA tile
     auto fixup_ok = [&](int sp) {
-        const bool wave64 = pick == 12 || pick == 15 || pick == 20 || pick == 22 || pick == 23 || pick == 33 ||
-                            pick == 35;   // TJ = 4 tiles
+        const bool wave64 = pick == 12 || pick == 15 || pick == 20 || pick == 22 || pick == 23;   // TJ = 4 tiles
         return cf.dma && wave64 && sp > 1 && g_fix_part && tiles <= g_fix_ncnt &&
                (size_t)tiles * sp * cf.bm * cf.bn <= g_fix_floats;
     };
@@ -2460,16 +2147,15 @@ void gemm_q8(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const flo
         dim3 grid(cdiv(W.N, cf.bn), cdiv(M, cf.bm), cdiv(steps, sps));
         if (epi == EPI_SWIGLU)
             QASR_CHECK(W.N % 64 == 0 && yq && yd && (cf.bn == 128 || pick == 12 || pick == 13 || pick == 15 ||
-                                                     pick == 20 || pick == 22 || pick == 33 || pick == 35 ||
-                                                     pick == 38),
+                                                     pick == 20 || pick == 22 || pick == 38),
                        QASR_E_INVALID, "gemm_q8: SwiGLU epilogue needs a 64-column wave tile");
         launch_cfg(pick, grid, s, xq, xd, M, W, bias, res, y, ldy, epi, sps, yq, yd, g_fix_part, g_fix_cnt);
         return;
     }
     if (epi == EPI_SWIGLU) {
         QASR_CHECK(W.N % 64 == 0 && yq && yd, QASR_E_INVALID, "gemm_q8: SwiGLU epilogue needs N % 64 == 0");
-        QASR_CHECK(cf.bn == 128 || pick == 12 || pick == 13 || pick == 15 || pick == 20 || pick == 22 || pick == 33 ||
-                       pick == 35 || pick == 38, QASR_E_INVALID,
+        QASR_CHECK(cf.bn == 128 || pick == 12 || pick == 13 || pick == 15 || pick == 20 || pick == 22 || pick == 38,
+                   QASR_E_INVALID,
                    "gemm_q8: SwiGLU epilogue needs a 64-column wave tile");
         dim3 grid(cdiv(W.N, cf.bn), cdiv(M, cf.bm), 1);
         launch_cfg(pick, grid, s, xq, xd, M, W, bias, res, y, ldy, epi, steps, yq, yd);

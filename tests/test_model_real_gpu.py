@@ -246,8 +246,8 @@ def test_real_batch_equals_single_and_oracle(pair):
 
 def test_real_batch_c4_scale(pair):
     """C4 at scale (1.7B, 64 segments of U[2,12] s like bench.py, 8 forced tokens per audio-second: up to 97 tokens,
-    EOS ignored): the batch's token streams against the 64 single runs, and the two shortest segments against the
-    oracle.  The mismatch count and every first divergence are recorded ($QASR_PARITY_LOG); a divergence is allowed
+    EOS ignored): the batch's token streams against the 64 single runs, and 8 segments (the two shortest, the longest,
+    five length quantiles) against the oracle.  The mismatch count and every first divergence are recorded ($QASR_PARITY_LOG); a divergence is allowed
     only at a near-tie (0.5 % of the row's range) of the single run's teacher-forced logits (batch vs single) or of
     the oracle's logits (batch vs oracle)."""
     arch, _, s, o = pair
@@ -270,9 +270,12 @@ def test_real_batch_c4_scale(pair):
         divs[i] = d
         lg = s.forced_logits(clips[i], np.asarray(b[:d], np.int32))   # row d: the single path's logits at the split
         assert _near_tie(lg[d]), f"segment {i}: batch/single diverge at token {d} of {len(a)} without a near-tie"
-    # the oracle on the two shortest segments (forced length, EOS ignored, as the batch)
+    # the oracle on 8 segments (forced length, EOS ignored, as the batch): the two shortest, the longest (12 s class:
+    # ~97 tokens, key ranges past the 256-key split) and five at evenly spaced length quantiles between them
+    order = np.argsort(secs)
+    pick = [int(i) for i in order[:2]] + [int(order[-1])] + [int(order[q]) for q in (13, 25, 38, 50, 57)]
     oracle_divs = []
-    for i in np.argsort(secs)[:2]:
+    for i in pick:
         ids, remb = _prompt_embeds(o, clips[i])
         n_new = len(batch[i])
         ref, lg = oracle.KV(o, len(ids) + n_new + 8).generate(ids, SP["tok_audio_pad"], remb, eos=(), max_new=n_new,
@@ -284,7 +287,9 @@ def test_real_batch_c4_scale(pair):
         assert d >= min(8, n_new), (i, d)
     record(f"real_batch_c4[{arch}]", segments=64, tokens=int(sum(len(b) for b in batch)),
            batch_vs_single_mismatched_segments=len(divs), first_divergences=sorted(divs.items()),
-           oracle_first_divergence=oracle_divs)
+           oracle_first_divergence=oracle_divs,
+           oracle_mismatched_segments=sum(1 for _, d, n in oracle_divs if d < n),
+           oracle_tokens_compared=int(sum(n for *_, n in oracle_divs)))
 
 
 def test_real_batch_invariant(pair):

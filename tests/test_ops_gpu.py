@@ -441,8 +441,7 @@ def test_gemv_exact_rows(torch_dev, pro, n, k, epi):
             assert np.array_equal(host(y)[0], single[r][0]), r
 
 
-GEMM_CHAIN_CFGS = [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 16, 17, 18, 21, 22, 23,
-                   40, 41, 42, 46, 47]   # 40..: the 32×32×32 kernel (k_q8mm), one K group: the same chain
+GEMM_CHAIN_CFGS = [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 16, 17, 18, 21, 22, 23, 36, 37]
 
 
 @pytest.mark.parametrize("m,n,k,epi", [(13, 1024, 1024, 0), (104, 3072, 1024, 0), (160, 1024, 4096, 1),
@@ -798,12 +797,10 @@ def test_linear_q8_fixup_vs_oracle(torch_dev, fixup, path, epi, m, n, k):
     assert not host(fixup).any()
 
 
-# round 4: K-128 tiles with the stage scales by 16-byte DMA (WS4), the 16-wave tiles (four K groups; their A and B
-# DMA pieces as one list) and the one-group deep-ring 64×32 / 32×64 tiles; 4096 + cfg + 256·splits
+# round 4: K-128 tiles with the stage scales by 16-byte DMA (WS4) and the one-group deep-ring 64×32 / 32×64 tiles;
+# 4096 + cfg + 256·splits
 S4_PATHS = [4096 + c + 256 * sp for c, sp in [(8, 1), (10, 1), (12, 1), (14, 1), (15, 1), (16, 1), (17, 1), (18, 1),
-                                              (23, 1), (32, 1), (33, 1), (34, 1), (35, 1), (36, 1), (37, 1), (38, 1),
-                                              (39, 1), (12, 3), (15, 4), (33, 2), (35, 4)] +
-            [(c, 1) for c in range(40, 49)]]   # the 32×32×32 kernel
+                                              (23, 1), (36, 1), (37, 1), (38, 1), (39, 1), (12, 3), (15, 4)]]
 
 
 @pytest.mark.parametrize("path", S4_PATHS)

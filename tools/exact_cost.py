@@ -47,7 +47,7 @@ def main():
         for w in ws:   # the decoder matrices carry their regrouped stage scales (model.cpp ensure_stage_scales)
             o = torch.empty_like(w)
             _lib.check(lib.qasr_op_stage_scales(w.data_ptr(), N, K, o.data_ptr(), None))
-            _lib.check(lib.qasr_op_register_stage_scales(w.data_ptr(), o.data_ptr()))
+            _lib.check(lib.qasr_op_register_stage_scales(w.data_ptr(), N, K, o.data_ptr()))
             s4.append(o)
         for M in MS:
             xq = torch.randint(-127, 128, (M, K), dtype=torch.int8, device=dev)
@@ -87,7 +87,7 @@ def main():
             print(f"{tag:5s} M={M:4d} table {table[(tag, M)]:8.1f}us exact {exact[(tag, M)]:8.1f}us "
                   f"x{exact[(tag, M)] / table[(tag, M)]:.2f}", flush=True)
         for w in ws:
-            _lib.check(lib.qasr_op_register_stage_scales(w.data_ptr(), None))
+            _lib.check(lib.qasr_op_register_stage_scales(w.data_ptr(), N, K, None))
         del wq, ws, s4
         torch.cuda.empty_cache()
 

@@ -44,7 +44,7 @@ def main():
         if os.environ.get("S4", "0") == "1" and K % 128 == 0:   # the regrouped stage scales (Q8Mat::sc4)
             s4 = torch.empty_like(ws)
             _lib.check(lib.qasr_op_stage_scales(ws.data_ptr(), N, K, s4.data_ptr(), None))
-            _lib.check(lib.qasr_op_register_stage_scales(ws.data_ptr(), s4.data_ptr()))
+            _lib.check(lib.qasr_op_register_stage_scales(ws.data_ptr(), N, K, s4.data_ptr()))
         y = torch.zeros(M, N, device=dev)
         res = y if epi == 1 else None
         hq = torch.empty(M, N // 2, dtype=torch.int8, device=dev)
@@ -79,7 +79,7 @@ def main():
             out.append(f"{path}:{us:8.1f}us {flops / us / 1e6:6.0f}TF")
         print(f"{tag:14s} M={M:6d} N={N:6d} K={K:5d} | " + " ".join(out), flush=True)
         if s4 is not None:
-            _lib.check(lib.qasr_op_register_stage_scales(ws.data_ptr(), None))
+            _lib.check(lib.qasr_op_register_stage_scales(ws.data_ptr(), N, K, None))
 
 
 if __name__ == "__main__":
