@@ -132,6 +132,8 @@ Session::Session(Model* m, int n_ctx) : m_(m), n_ctx_(n_ctx) {
     const qasr_hparams& hp = m->hp;
     const size_t widest = (size_t)std::max(std::max(2 * hp.txt_ffn, hp.txt_h),
                                            (hp.txt_heads + 2 * hp.txt_kv_heads) * hp.head_dim);
+    QASR_HIP(hipMalloc(&xr_cnt_, 4 * sizeof(unsigned)));
+    QASR_HIP(hipMemset(xr_cnt_, 0, 4 * sizeof(unsigned)));
     const char* nofix = getenv("QASR_NO_FIXUP");
     if (!nofix || atoi(nofix) == 0) {
         fix_floats_ = (size_t)256 * ((widest + 127) / 128 * 128) * kFixSplits;
@@ -152,6 +154,7 @@ Session::~Session() {
     if (fix_cnt_) (void)hipFree(fix_cnt_);
     if (d_players_) (void)hipFree(d_players_);
     if (psync_) (void)hipFree(psync_);
+    if (xr_cnt_) (void)hipFree(xr_cnt_);
     if (pstamps_) (void)hipFree(pstamps_);
     if (pin_) (void)hipHostFree(pin_);
     for (auto& g : graphs_) (void)hipGraphExecDestroy(g.second);
@@ -497,6 +500,16 @@ void Session::persist_check_abort() {
     }
 }
 
+// the fused-norm residual launches flag a wait that timed out (never with the grid resident) in xr_cnt_[2]
+void Session::xr_check() {
+    unsigned e = 0;
+    QASR_HIP(hipMemcpy(&e, xr_cnt_ + 2, sizeof e, hipMemcpyDeviceToHost));
+    if (e != 0) {
+        QASR_HIP(hipMemset(xr_cnt_, 0, 4 * sizeof(unsigned)));
+        throw Error(QASR_E_INTERNAL, "decoder: a fused-norm wait timed out (workgroups not co-resident)");
+    }
+}
+
 void Session::decoder_layers(float* x, int rows, const int* d_pos, const int* d_slot, const int* d_kvs,
                              const int* d_kvl, int64_t total_keys, bool dense, bool rows_share_kv) {
     const qasr_hparams& h = m_->hp;
@@ -597,14 +610,30 @@ void Session::decoder_layers(float* x, int rows, const int* d_pos, const int* d_
     // ≤ 32 rows: the exact-row linears as the per-phase launches (xr_linear: weights loaded up front, rows staged in
     // LDS; bit-identical to gemm_exact_rows — tests/test_ops_gpu.py::test_xr_linear_bit_identical_to_exact_rows),
     // faster at 2-32 rows on O / down and from 24 rows on QKV (profiles/r5_xr_cost.log); QASR_NO_XR=1 keeps
-    // gemm_exact_rows
-    static const bool no_xr = getenv("QASR_NO_XR") != nullptr;
+    // gemm_exact_rows (read per call, like QASR_XR_NORM below: tests switch it between sessions)
+    const bool no_xr = getenv("QASR_NO_XR") != nullptr;
+    auto xr_path = [&](const Q8Mat& W) { return !no_xr && xr_ok(rows, W.K) && W.N % 16 == 0; };
     auto exact_linear = [&](const int8_t* q, const float* d, const Q8Mat& W, const float* res, float* y, int ldy,
                             int epi) {
-        if (!no_xr && xr_ok(rows, W.K) && W.N % 16 == 0) xr_linear(q, d, nullptr, nullptr, 0.f, rows, W, y, ldy,
-                                                                   epi == EPI_RESID, st_);
+        if (xr_path(W)) xr_linear(q, d, nullptr, nullptr, 0.f, rows, W, y, ldy, epi == EPI_RESID, st_);
         else gemm_exact_rows(q, d, rows, W, res, y, ldy, epi, st_);
     };
+    // a residual exact-row launch that also leaves RMSNorm(x)·nw as the next launch's Q8 rows in (nq, nd) — the norm
+    // fused into its tail (xr_norm_tail: no separate rmsnorm_q8 launch).  Returns false (and runs the plain residual
+    // launch) where the fused form does not apply.  Opt-in (QASR_XR_NORM=1): bit-identical, but the tail's wait for
+    // the last column tile plus one row per norm workgroup costs more than the rmsnorm_q8 launch it replaces — 32-
+    // segment share 1137 vs 1183 audio-s/s with it off (profiles/r5_seg32_xrnorm.json).
+    const bool no_xr_norm = getenv("QASR_XR_NORM") == nullptr;
+    auto resid_norm = [&](const int8_t* q, const float* d, const Q8Mat& W, const float* nw, int8_t* nq, float* nd) {
+        if (!no_xr_norm && nw && rows >= 5 && xr_path(W) && (H == 1024 || H == 2048) && xr_cnt_) {
+            const XrNorm nm{nw, h.rms_eps, nq, nd, xr_cnt_};
+            xr_linear(q, d, nullptr, nullptr, 0.f, rows, W, x, H, true, st_, &nm);
+            return true;
+        }
+        exact_linear(q, d, W, x, x, H, EPI_RESID);
+        return false;
+    };
+    bool normed = false;   // xq / xd already hold this layer's RMSNorm(x)·attn_norm (fused into the last down launch)
     int8_t* hq2 = gv || xm ? (int8_t*)sc_.get(S_HQ, (size_t)rows * F) : nullptr;   // the SwiGLU Q8 rows
     float* hd2 = gv || xm ? (float*)sc_.get(S_HD, (size_t)rows * (F / QK) * sizeof(float)) : nullptr;
     float* gux = xm ? (float*)sc_.get(S_GU, (size_t)rows * 2 * F * sizeof(float)) : nullptr;
@@ -617,16 +646,18 @@ void Session::decoder_layers(float* x, int rows, const int* d_pos, const int* d_
         const bool zq = rows <= 256 && !deterministic();
         const bool dmp = g_dump && rows <= kExactRows;
         if (dmp) dump_rows("x_in", l, rows, x, (size_t)rows * H * sizeof(float));
+        const float* next_norm = l + 1 < h.txt_layers ? m_->dec[l + 1].attn_norm : nullptr;
         if (xm) {
-            rmsnorm_q8(x, rows, H, H, L.attn_norm, h.rms_eps, xq, xd, st_);
+            if (!normed) rmsnorm_q8(x, rows, H, H, L.attn_norm, h.rms_eps, xq, xd, st_);
             exact_linear(xq, xd, L.qkv, nullptr, qkv, QD + 2 * KD, EPI_STORE);
         } else if (gv) {
             gemv_fused(GV_RMS, nullptr, nullptr, x, H, L.attn_norm, h.rms_eps, rows, L.qkv, nullptr, qkv, QD + 2 * KD,
                        EPI_STORE, nullptr, nullptr, st_);
         } else if (xr_qkv) {
-            rmsnorm_q8(x, rows, H, H, L.attn_norm, h.rms_eps, xq, xd, st_);
+            if (!normed) rmsnorm_q8(x, rows, H, H, L.attn_norm, h.rms_eps, xq, xd, st_);
             exact_linear(xq, xd, L.qkv, nullptr, qkv, QD + 2 * KD, EPI_STORE);
         } else {
+            QASR_CHECK(!normed, QASR_E_INTERNAL, "decoder: a fused norm feeds the table QKV path");
             rmsnorm_q8(x, rows, H, H, L.attn_norm, h.rms_eps, xq, xd, st_, zq ? qkv : nullptr,
                        zq ? (int64_t)rows * (QD + 2 * KD) : 0);
             linear_q8(xq, xd, rows, L.qkv, nullptr, nullptr, qkv, QD + 2 * KD, EPI_STORE, st_, zq);
@@ -655,17 +686,20 @@ void Session::decoder_layers(float* x, int rows, const int* d_pos, const int* d_
             dump_rows("att_q", l, rows, xq, (size_t)rows * QD);
             dump_rows("att_d", l, rows, xd, (size_t)rows * (QD / QK) * sizeof(float));
         }
-        if (xm) {   // the same four steps as separate launches with the exact-row MFMA linears
-            exact_linear(xq, xd, L.o, x, x, H, EPI_RESID);
+        if (xm) {   // the same steps with the exact-row linears (≤ 32 rows: the xr launches, norms fused in)
+            if (!resid_norm(xq, xd, L.o, L.ffn_norm, xq, xd)) rmsnorm_q8(x, rows, H, H, L.ffn_norm, h.rms_eps, xq, xd, st_);
             if (dmp) dump_rows("x_mid", l, rows, x, (size_t)rows * H * sizeof(float));
-            rmsnorm_q8(x, rows, H, H, L.ffn_norm, h.rms_eps, xq, xd, st_);
-            exact_linear(xq, xd, L.gu, nullptr, gux, 2 * F, EPI_STORE);
-            swiglu_q8(gux, rows, F, hq2, hd2, st_, /*interleaved=*/true);
+            if (xr_path(L.gu) && L.gu.K <= 2048) {   // gate/up + SwiGLU + Q8 in one exact launch
+                xr_gu_swiglu(xq, xd, nullptr, nullptr, 0.f, rows, L.gu, hq2, hd2, st_);
+            } else {
+                exact_linear(xq, xd, L.gu, nullptr, gux, 2 * F, EPI_STORE);
+                swiglu_q8(gux, rows, F, hq2, hd2, st_, /*interleaved=*/true);
+            }
             if (dmp) {
                 dump_rows("h_q", l, rows, hq2, (size_t)rows * F);
                 dump_rows("h_d", l, rows, hd2, (size_t)rows * (F / QK) * sizeof(float));
             }
-            exact_linear(hq2, hd2, L.down, x, x, H, EPI_RESID);
+            normed = !g_dump && resid_norm(hq2, hd2, L.down, next_norm, xq, xd);
             continue;
         }
         if (gv) {   // O-projection + residual; norm + gate/up + SwiGLU + Q8; down-projection + residual
@@ -681,11 +715,12 @@ void Session::decoder_layers(float* x, int rows, const int* d_pos, const int* d_
                        st_);
             continue;
         }
+        bool o_normed = false;
         if (xr_o)
-            exact_linear(xq, xd, L.o, x, x, H, EPI_RESID);
+            o_normed = resid_norm(xq, xd, L.o, L.ffn_norm, xq, xd);
         else
             linear_q8(xq, xd, rows, L.o, nullptr, x, x, H, EPI_RESID, st_);
-        rmsnorm_q8(x, rows, H, H, L.ffn_norm, h.rms_eps, xq, xd, st_);
+        if (!o_normed) rmsnorm_q8(x, rows, H, H, L.ffn_norm, h.rms_eps, xq, xd, st_);
         if (fused) {  // SwiGLU + Q8 in the gate-up GEMM epilogue (rows interleaved at load)
             gemm_q8(xq, xd, rows, L.gu, nullptr, nullptr, nullptr, 2 * F, EPI_SWIGLU, st_, -1, 0, hq, hd_);
             std::swap(xq, hq);
@@ -694,8 +729,10 @@ void Session::decoder_layers(float* x, int rows, const int* d_pos, const int* d_
             linear_q8(xq, xd, rows, L.gu, nullptr, nullptr, gu, 2 * F, EPI_STORE, st_);
             swiglu_q8(gu, rows, F, xq, xd, st_, true);
         }
+        // the next layer's QKV reads the fused norm only on its exact-row path (xr_qkv)
         if (xr_down)
-            exact_linear(xq, xd, L.down, x, x, H, EPI_RESID);
+            normed = resid_norm(xq, xd, L.down, xr_qkv && !g_dump ? next_norm : nullptr, fused ? hq : xq,
+                                fused ? hd_ : xd);
         else
             linear_q8(xq, xd, rows, L.down, nullptr, x, x, H, EPI_RESID, st_);
         if (fused) {
@@ -1143,6 +1180,7 @@ void Session::run_batch(const float* dpcm, const std::vector<int64_t>& off, cons
         }
         dstats_.tokens += (int64_t)toks.size();
         UttResult& r = out[0];
+        xr_check();
         r.raw = m_->tok.decode(r.tokens.data(), (int)r.tokens.size());
         Tokenizer::parse(r.raw, r.language, r.text);
         remember_prompt_kv();
@@ -1181,9 +1219,11 @@ void Session::run_batch(const float* dpcm, const std::vector<int64_t>& off, cons
         decode_step(ds, bmax, true);  // also sizes the layer scratch
         QASR_HIP(hipEventRecord(step_ev_[0], st_));
     }
-    // captured step graphs hold scratch, KV and weight pointers: any reallocation or precision change retires them
+    // captured step graphs hold scratch, KV and weight pointers: any reallocation or precision change retires them;
+    // so does a switch of the per-call launch-path variables (QASR_NO_XR / QASR_XR_NORM, read in decoder_layers)
+    const uint64_t launch_path = (getenv("QASR_NO_XR") ? 1 : 0) + (getenv("QASR_XR_NORM") ? 2 : 0);
     const uint64_t key[5] = {sc_.epoch, kv_epoch_, m_->precision_gen, deterministic_gen(),
-                             attn_epoch_ * 4 + (batch_inv_ ? 1 : 0) + (persist_run_ ? 2 : 0)};
+                             attn_epoch_ * 16 + launch_path * 4 + (batch_inv_ ? 1 : 0) + (persist_run_ ? 2 : 0)};
     if (memcmp(key, graph_key_, sizeof key) != 0) {
         for (auto& g : graphs_) (void)hipGraphExecDestroy(g.second);
         graphs_.clear();
@@ -1234,6 +1274,7 @@ void Session::run_batch(const float* dpcm, const std::vector<int64_t>& off, cons
     }
     QASR_HIP(hipStreamSynchronize(st_));
     if (persist_run_) persist_check_abort();
+    xr_check();
     if (hist) {
         fprintf(stderr, "decode steps per row bucket:");
         for (auto& kv : steps_per_bucket) fprintf(stderr, " %d:%d", kv.first, kv.second);

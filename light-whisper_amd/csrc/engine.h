@@ -189,6 +189,8 @@ class Session {
     int pgrid_[2] = {0, 0};      // workgroups for ≤ 16 / ≤ 32 rows
     uint64_t* pstamps_ = nullptr;   // QASR_PERSIST_STAMPS=<file>: the last launch's grid-wait stamps, written there
     bool persist_prepare();
+    unsigned* xr_cnt_ = nullptr;   // the residual xr launches' fused-norm counters (3 words, zero between launches)
+    void xr_check();
     void persist_check_abort();
     // split-K fix-up workspace of the decode-step GEMMs (≤ 256 rows; QASR_NO_FIXUP=1: f32 atomics instead): partial
     // tiles + per-tile arrival counters (zeroed once; the kernels leave them zero)

@@ -217,8 +217,17 @@ void decoder_persistent(const PersistArgs& a, hipStream_t s);
 // to gemm_exact_rows / the 1-row GEMVs.  src != nullptr (≤ 8 rows, K ≤ 2,048): the input rows are RMSNorm(src)·nw
 // quantised inside the launch (rmsnorm_q8's arithmetic) instead of xq / xd.
 bool xr_ok(int R, int K);
+// norm (residual launches of whole rows, N = H ∈ {1,024, 2,048}): RMSNorm(y)·w → Q8 rows q / d inside the launch
+// (rmsnorm_q8's arithmetic, by the last workgroups to finish); cnt: 3 words, zero between launches
+struct XrNorm {
+    const float* w = nullptr;
+    float eps = 0.f;
+    int8_t* q = nullptr;
+    float* d = nullptr;
+    unsigned* cnt = nullptr;
+};
 void xr_linear(const int8_t* xq, const float* xd, const float* src, const float* nw, float eps, int R, const Q8Mat& W,
-               float* y, int ldy, bool resid, hipStream_t s);
+               float* y, int ldy, bool resid, hipStream_t s, const XrNorm* norm = nullptr);
 // interleaved gate/up (N = 2F) + SwiGLU + Q8 → hq [R][F] / hd [R][F/32]
 void xr_gu_swiglu(const int8_t* xq, const float* xd, const float* src, const float* nw, float eps, int R,
                   const Q8Mat& W, int8_t* hq, float* hd, hipStream_t s);

@@ -446,10 +446,53 @@ __global__ __launch_bounds__(256, 1) void k_dec_persist(PersistArgs a) {
 // there from x: rmsnorm_q8's arithmetic — no separate norm launch).  One workgroup per CU (512 registers).
 //   k_xr_linear: a 16-column fragment × the rows of blockIdx.y's slice (16·RF rows), + residual (RESID)
 //   k_xr_gu:     one h block = 64 interleaved gate/up columns (4 fragments) + SwiGLU + Q8
+// The residual launches' fused RMSNorm (XrNorm::w != nullptr; the output rows are whole rows of H = N): once every
+// workgroup has stored its columns (write-through, counted on cnt[0]), the last R workgroups to arrive wait
+// for the count to reach the grid and normalise the rows into q / d — rmsnorm_q8's arithmetic on the finished rows,
+// so the next launch needs no norm launch of its own.  The grid (≤ 256 workgroups, one per CU) is resident as a
+// whole, so the wait ends; it is bounded anyway (cnt[2] = 1 flags a timeout, the engine checks it).  cnt[1] counts
+// the finished norm workgroups; the last one leaves cnt[0..1] zero for the next launch.
+template <int KC>
+__device__ __forceinline__ void xr_norm_tail(const XrNorm& nm, const float* x, int H, int R, float* part, int tid) {
+    __shared__ int s_prev;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's write-through stores of x have completed
+    __syncthreads();
+    const unsigned G = gridDim.x * gridDim.y;
+    if (tid == 0) s_prev = (int)__hip_atomic_fetch_add(nm.cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const int NL = R, k = s_prev - (int)(G - (unsigned)NL);   // one row per norm workgroup (8 rows each: slower than a launch)
+    if (k < 0) return;   // uniform: not one of the norm workgroups
+    if (tid == 0) {
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        while (__hip_atomic_load(nm.cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < G) {
+            if (__builtin_amdgcn_s_memrealtime() - t0 > 20000000ull) {   // 0.2 s: never, with the grid resident
+                __hip_atomic_store(nm.cnt + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+    }
+    __syncthreads();
+    for (int r = k; r < R; r += NL) {
+        float4 v[KC], gw[KC];
+        rms_row_load<KC, true>(x + (size_t)r * H, H, nm.w, v, gw, tid);
+        rms_row_q8_finish<KC, false>(v, gw, H, nm.eps, nm.q + (size_t)r * H, nm.d + (size_t)r * (H / QK), part, true,
+                                     tid);
+        __syncthreads();
+    }
+    if (tid == 0) {
+        const unsigned d = __hip_atomic_fetch_add(nm.cnt + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (d == (unsigned)NL - 1) {   // every norm workgroup is past its wait
+            __hip_atomic_store(nm.cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(nm.cnt + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
 template <int T, int RF, bool FOLD, bool RESID>
 __global__ __launch_bounds__(256, 1) void k_xr_linear(const int8_t* X, const float* Xd, const float* src,
                                                       const float* nw, float eps, int R, const int8_t* Wq,
-                                                      const __half* Ws, int N, float* y, int ldy) {
+                                                      const __half* Ws, int N, float* y, int ldy, XrNorm nm) {
     constexpr int K = 1024 * T, LX = K + 16;
     __shared__ __align__(16) int8_t tile[16 * RF * LX + 16 * RF * (K / QK) * 4];
     __shared__ float hx[4][RF][4][64];
@@ -466,6 +509,12 @@ __global__ __launch_bounds__(256, 1) void k_xr_linear(const int8_t* X, const flo
     __syncthreads();
     exact_frag_lds<T, RF>(w, tile, LX, sXd, rn, hx, v, tid);
     item_store<RF, RESID>(v, rv, r0, R, n0, N, y, ldy, tid);
+    if constexpr (RESID) {
+        if (nm.w) {   // uniform
+            if (N == 1024) xr_norm_tail<1>(nm, y, N, R, part[0], tid);
+            else xr_norm_tail<2>(nm, y, N, R, part[0], tid);
+        }
+    }
 }
 
 template <int T, int RF, bool FOLD>
@@ -516,20 +565,24 @@ __global__ __launch_bounds__(256, 1) void k_xr_gu(const int8_t* X, const float* 
 bool xr_ok(int R, int K) { return R >= 1 && R <= 32 && (K == 1024 || K == 2048 || K == 3072 || K == 6144); }
 
 void xr_linear(const int8_t* xq, const float* xd, const float* src, const float* nw, float eps, int R, const Q8Mat& W,
-               float* y, int ldy, bool resid, hipStream_t s) {
+               float* y, int ldy, bool resid, hipStream_t s, const XrNorm* norm) {
     const bool fold = src != nullptr;
     ProfScope ps(s, fold ? "xr_linear_rms" : "xr_linear", 2.0 * R * W.N * W.K,
                  (double)W.N * W.K * (1.0 + 2.0 / 32) + (double)R * W.K * (fold ? 4.0 : 1.125) +
                      (double)R * W.N * 4.0 * (resid ? 2 : 1));
     QASR_CHECK(xr_ok(R, W.K) && W.N % 16 == 0 && (!fold || (R <= 8 && nw)), QASR_E_INVALID,
                "xr_linear: rows 1-32 (fold: ≤ 8), K 1,024 / 2,048 / 3,072 / 6,144");
+    QASR_CHECK(!norm || (resid && ldy == W.N && (W.N == 1024 || W.N == 2048) && norm->w && norm->q && norm->d &&
+                         norm->cnt),
+               QASR_E_INVALID, "xr_linear: the fused norm needs whole residual rows of 1,024 / 2,048");
+    const XrNorm nm = norm ? *norm : XrNorm{};
     // rows > 16: two 16-row slices (one row fragment each) where a 32-row tile would not fit LDS (K 6,144), else one
     // 32-row slice
     const bool two = R > 16 && W.K > 3072;
     const int rf = R > 16 && !two ? 2 : 1;
     const dim3 g(W.N / 16, two ? 2 : 1);
 #define XR_GO(TT, RFF, FF, RR)                                                                                        \
-    k_xr_linear<TT, RFF, FF, RR><<<g, 256, 0, s>>>(xq, xd, src, nw, eps, R, W.qs, W.sc, W.N, y, ldy)
+    k_xr_linear<TT, RFF, FF, RR><<<g, 256, 0, s>>>(xq, xd, src, nw, eps, R, W.qs, W.sc, W.N, y, ldy, nm)
 #define XR_RF(TT, FF, RR)                      \
     do {                                       \
         if (rf == 2) XR_GO(TT, 2, FF, RR);     \

@@ -434,3 +434,29 @@ def test_real_teacher_forced_100_tokens(pair):
     assert e < 2e-2
     assert agree[clear].all(), np.nonzero(~agree & clear)
     assert clear.mean() >= 0.8
+
+
+def test_real_fused_norm_and_xr_bit_identical(pair, monkeypatch):
+    """round 5's ≤ 32-row decode launches — the exact-row linears as per-phase xr launches and the RMSNorm fused into
+    the residual launches' tails (opt-in QASR_XR_NORM=1) — against the round-4 launch chain (QASR_NO_XR=1:
+    gemm_exact_rows + rmsnorm_q8): a batch-invariant batch of 20 segments (rows 20 → 1) gives the same token streams, and the same
+    streams as the segments' single runs"""
+    arch, m, s, _ = pair
+    rng = np.random.default_rng(31)
+    secs = rng.uniform(2.0, 8.0, size=20)
+    clips = [clip(float(x), 700 + i) for i, x in enumerate(secs)]
+    singles = [s.run(c, force_tokens_per_s=8).tokens for c in clips[:6]]
+    s.set_batch_invariant(True)
+    try:
+        monkeypatch.setenv("QASR_XR_NORM", "1")
+        new = [r.tokens for r in s.run_batch(clips, force_tokens_per_s=8)]
+        monkeypatch.delenv("QASR_XR_NORM")
+        monkeypatch.setenv("QASR_NO_XR", "1")
+        s2 = m.session(kv_type="f16", n_ctx=4096)
+        s2.set_batch_invariant(True)
+        old = [r.tokens for r in s2.run_batch(clips, force_tokens_per_s=8)]
+        s2.close()
+    finally:
+        s.set_batch_invariant(False)
+    assert new == old
+    assert new[:6] == singles
