@@ -159,6 +159,9 @@ def class_roofline(name, p):
         r = {"bound": "hbm", "achieved": round(ach, 1), "peak": 8000.0, "unit": "GB/s", "frac": round(ach / 8000.0, 4),
              "traffic": None}
     r.update(base)
+    gr = graph_replayed(name, p)
+    if gr:
+        r["graph_replayed"] = gr
     ev = pmc_evidence(name)
     if ev:
         r["committed_pmc"] = ev
@@ -218,6 +221,44 @@ def pmc_evidence(kernel):
             "mfma_busy": round(busy / (1024 * grbm / 8), 4) if grbm else None,
             "hbm_gbps": round(hbm_bytes / time_ns, 1) if time_ns else None,
             "hbm_bytes_per_launch": round(hbm_bytes / launches) if launches else None}
+
+
+def graph_replayed(kernel, p):
+    """the class's average launch duration in GRAPH-REPLAYED bench steps (the timed steps replay captured decode-step
+    graphs, where per-launch events would perturb them) from the committed kernel trace of `bench.py --no-prof`
+    (profiles/*trace_classes*.json, tools/trace_classes.py), priced with this run's algorithmic work per launch: the
+    same launches run eagerly in the instrumented step.  Prefers the file recorded for the loaded libqasr.so
+    (matches_build true).  None if absent."""
+    import glob
+
+    files = glob.glob(os.path.join(ROOT, "profiles", "*trace_classes*.json"))
+    if not files:
+        return None
+    sha = lib_sha16()
+    meta = {}
+    for fpath in files:
+        with open(fpath) as f:
+            meta[fpath] = json.load(f).get("_meta", {})
+    same = [fp for fp in files if sha and meta[fp].get("lib_sha256_16") == sha]
+    pick = max(same or files, key=lambda fp: (meta[fp].get("generated_utc", ""), os.path.basename(fp)))
+    with open(pick) as f:
+        tr = json.load(f)
+    names = [c for c in PMC_CLASSES.get(kernel, (kernel,)) if c in tr]
+    if not names:
+        return None
+    launches = sum(tr[c]["launches"] for c in names)
+    avg_s = sum(tr[c]["avg_us"] * tr[c]["launches"] for c in names) / launches / 1e6
+    r = {"source": os.path.relpath(pick, ROOT), "matches_build": bool(same),
+         "note": "committed rocprofv3 kernel trace of bench.py --no-prof (graph-replayed steps), not measured by this run",
+         "avg_launch_us": round(avg_s * 1e6, 2),
+         "launches_per_step": round(sum(tr[c]["launches_per_step"] for c in names), 1)}
+    if kernel in MFMA_PEAK_TF:
+        ach = p["flops"] / p["count"] / avg_s / 1e12
+        r.update(achieved=round(ach, 2), unit="TFLOP/s", frac=round(ach / MFMA_PEAK_TF[kernel], 4))
+    else:
+        ach = p["bytes"] / p["count"] / avg_s / 1e9
+        r.update(achieved=round(ach, 1), unit="GB/s", frac=round(ach / 8000.0, 4))
+    return r
 
 
 def share_cards():

@@ -26,11 +26,6 @@ QASR_API int qasr_op_gemm_swiglu_q8_cfg(const int8_t* xq, const float* xd, int32
    register their own for the decode steps (used there for the SwiGLU epilogue).  Not in
    the reference (an engine-internal tuning / test hook). */
 QASR_API int qasr_op_set_gemm_fixup(void* part, int64_t part_bytes, void* cnt, int32_t ncnt);
-/* Rows (0..64) up to which the Q8 GEMM's automatic choice streams the weights straight into the matrix core's operand
-   registers (k_gemm_q8_ws: decode rows, every weight byte read once, no LDS staging); 0 = never.  all_shapes = 0: only
-   on the wide decoder matrices where it is faster (QKV, gate/up); 1: every shape it supports (tests).  Process-wide;
-   default 16 rows (QASR_WS_ROWS).  Tuning / A/B hook, not in the reference. */
-QASR_API int qasr_op_set_gemm_ws_rows(int32_t rows, int32_t all_shapes);
 /* Regrouped stage scales of a Q8 matrix (sc [N][K/32] f16 → out [K/128][N][4] f16, K % 128 == 0): a K-128 GEMM
    stage's column scales as one contiguous run (the decode GEMMs' 16-byte scale DMA; a model's decoder matrices
    carry theirs).  qasr_op_register_stage_scales(wsc, N, K, out) makes the qasr_op_* GEMM entry points use `out` for

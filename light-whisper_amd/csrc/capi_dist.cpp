@@ -8,7 +8,9 @@
 //     the ragged payload padded to the largest rank);
 //   * qasr_dist_agree: one int32 all-gather of every rank's local status before a collective (failure agreement).
 // Neither runs inside a timed step.  The reference has no multi-GPU path.
+#include <stdio.h>
 #include <string.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <chrono>
@@ -78,12 +80,29 @@ struct DevBuf {
 
 }  // namespace
 
+// RCCL prints its version banner on stdout the first time it initialises; stdout is the protocol channel of the
+// engine (`engine longform` JSON, the server's replies) and of bench.py's one JSON line, so RCCL's init runs with fd 1
+// pointed at stderr.
+struct StdoutToStderr {
+    int saved = -1;
+    StdoutToStderr() {
+        fflush(stdout);
+        saved = dup(1);
+        if (saved >= 0) dup2(2, 1);
+    }
+    ~StdoutToStderr() {
+        fflush(stdout);
+        if (saved >= 0) dup2(saved, 1), close(saved);
+    }
+};
+
 extern "C" {
 
 QASR_API int qasr_dist_unique_id(uint8_t* out, size_t cap) {
     return guard([&] {
         QASR_CHECK(out && cap >= NCCL_UNIQUE_ID_BYTES, QASR_E_INVALID, "unique id buffer: 128 bytes");
         ncclUniqueId id;
+        StdoutToStderr quiet;
         QASR_NCCL(ncclGetUniqueId(&id));
         memcpy(out, id.internal, NCCL_UNIQUE_ID_BYTES);
     });
@@ -96,7 +115,10 @@ QASR_API int qasr_dist_init(const uint8_t* id, int32_t rank, int32_t world, int3
         QASR_HIP(hipSetDevice(device));
         ncclUniqueId uid;
         memcpy(uid.internal, id, NCCL_UNIQUE_ID_BYTES);
-        QASR_NCCL(ncclCommInitRank(&c->c, world, uid, rank));
+        {
+            StdoutToStderr quiet;
+            QASR_NCCL(ncclCommInitRank(&c->c, world, uid, rank));
+        }
         QASR_HIP(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
         c->rank = rank, c->world = world, c->device = device;
         *out = c.release();

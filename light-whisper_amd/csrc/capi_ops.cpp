@@ -267,13 +267,6 @@ QASR_API int qasr_op_xr_gu_swiglu(const int8_t* xq, const float* xd, const float
     });
 }
 
-QASR_API int qasr_op_set_gemm_ws_rows(int32_t rows, int32_t all_shapes) {
-    return guard([&] {
-        QASR_CHECK(rows >= 0 && rows <= 64, QASR_E_INVALID, "set_gemm_ws_rows: 0..64");
-        set_gemm_ws_rows(rows, all_shapes != 0);
-    });
-}
-
 QASR_API int qasr_op_set_gemm_fixup(void* part, int64_t part_bytes, void* cnt, int32_t ncnt) {
     return guard([&] {
         QASR_CHECK(part_bytes >= 0 && ncnt >= 0, QASR_E_INVALID, "set_gemm_fixup: bad size");

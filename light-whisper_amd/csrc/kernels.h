@@ -94,7 +94,6 @@ void set_mx_workspace(void* p, size_t bytes);
 void set_gemm_fixup(float* part, size_t floats, unsigned* cnt, int ncnt, bool all_epilogues = false);
 // rows up to which gemm_q8's automatic choice takes the weight-streaming kernel (≤ 64; 0 = never); all_shapes: on
 // every shape it supports, not only the wide decoder matrices where it is faster (tests)
-void set_gemm_ws_rows(int rows, bool all_shapes = false);
 constexpr int kFixSplits = 8, kFixCounters = 8192;
 struct FixupScope {   // registers a fix-up workspace for the calls in its scope, unregisters on exit (throws included)
     FixupScope(float* part, size_t floats, unsigned* cnt, int ncnt) { set_gemm_fixup(part, floats, cnt, ncnt); }

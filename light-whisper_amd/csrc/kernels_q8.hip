@@ -1435,205 +1435,6 @@ __global__ __launch_bounds__(64 * NW) void k_gemm_q8_ks(const int8_t* __restrict
     gemm_epilogue<1, TJ>(out, M, N, m0, n0, 16 * wave, 0, fr, fq, bias, res, y, ldy, epi, yq, yd);
 }
 
-// ------------------------------------------------------------------------------------------------ GEMM (weight stream)
-// Decode rows 9–64 (C3 draft verify passes, the tail of a C4 batch): the layer is a weight stream (53.5 MB per 1.7B
-// layer against ≤ 64 activation rows), so the weights go straight from HBM into the matrix core's operand registers —
-// no LDS staging, no ring, no barrier in the K loop.  A wave owns 16 output columns and a K range; lane (fr, g)
-// loads the 16 bytes [16g, 16g+16) of column fr's 64-byte span (two Q8 blocks) — a coalesced 16-byte load, every
-// weight byte read once.  v_mfma_i32_16x16x64_i8 pairs byte j of lane group g in A with byte j of lane group g in B,
-// so with the activation span loaded the same way and zeroed in groups 2–3 (block 2s) or 0–1 (block 2s+1), two
-// MFMAs give the two blocks' exact int32 sums, rescaled into f32 as everywhere ((float)sum · (d_x·d_w), one fma).
-// The activation rows are L2/L1-resident (≤ 64 × K bytes) and read directly; their block scales sit in LDS
-// block-major ([b][row], one ds_read_b128 per 4 rows).  KS waves split K per column group, their partial tiles are
-// summed through LDS in wave order (deterministic); CG column groups per workgroup (4 for the SwiGLU epilogue: the
-// 64 interleaved gate/up columns of one 32-wide h block → swiglu_q8_block, the GEMM path's arithmetic).
-template <int TI, int CG, int KS>
-__global__ __launch_bounds__(64 * CG * KS) void k_gemm_q8_ws(const int8_t* __restrict__ X, const float* __restrict__ Xd,
-                                                           int M, const int8_t* __restrict__ W,
-                                                           const __half* __restrict__ Wsc, int N, int K,
-                                                           const float* __restrict__ bias, const float* res, float* y,
-                                                           int ldy, int epi, int8_t* __restrict__ yq,
-                                                           float* __restrict__ yd) {
-    constexpr int U = TI >= 4 ? 2 : 4;   // spans per load group (two groups in flight)
-    extern __shared__ float4 smem_ws[];
-    float* sxd = (float*)smem_ws;   // [nb][16·TI] activation scales, then the KS partial tiles / SwiGLU block
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int cg = wave % CG, ks = wave / CG;
-    const int nb = K / QK, ns = nb / 2, per = ns / KS, s0 = ks * per;   // host: ns % (KS·U) == 0
-    constexpr int BM = 16 * TI;
-    const int n0 = (blockIdx.x * CG + cg) * 16;
-    const int fr = lane & 15, g = lane >> 4;
-    const int col = min(n0 + fr, N - 1);
-    const int8_t* wp = W + (size_t)col * K + 16 * g;
-    const uint32_t* sp = (const uint32_t*)(Wsc + (size_t)col * nb);
-    const int8_t* ap[TI];
-#pragma unroll
-    for (int i = 0; i < TI; i++) ap[i] = X + (size_t)min(16 * i + fr, M - 1) * K + 16 * g;
-    float acc[TI][4];
-#pragma unroll
-    for (int i = 0; i < TI; i++)
-#pragma unroll
-        for (int r = 0; r < 4; r++) acc[i][r] = 0.f;
-    v4i wv[2][U], av[2][U][TI];
-    uint32_t sw[2][U];
-    // two load groups in flight; the buffer index is a compile-time constant at every use (a runtime index would put
-    // the operand arrays in scratch)
-    auto load = [&](auto bufc, int s) {
-        constexpr int buf = decltype(bufc)::value;
-#pragma unroll
-        for (int u = 0; u < U; u++) {
-            wv[buf][u] = __builtin_nontemporal_load((const v4i*)(wp + 64 * (size_t)(s + u)));
-            sw[buf][u] = sp[s + u];
-#pragma unroll
-            for (int i = 0; i < TI; i++) av[buf][u][i] = *(const v4i*)(ap[i] + 64 * (size_t)(s + u));
-        }
-    };
-    const bool lo = g < 2;
-    const v4i zero = {0, 0, 0, 0};
-    auto compute = [&](auto bufc, int s) {
-        constexpr int buf = decltype(bufc)::value;
-#pragma unroll
-        for (int u = 0; u < U; u++) {
-            const uint32_t h2 = sw[buf][u];
-            const float dw0 = __half2float(__ushort_as_half((unsigned short)(h2 & 0xffff)));
-            const float dw1 = __half2float(__ushort_as_half((unsigned short)(h2 >> 16)));
-            const int b0 = 2 * (s + u);
-#pragma unroll
-            for (int i = 0; i < TI; i++) {
-                const v4i a = av[buf][u][i];
-                const v4i c0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(lo ? a : zero, wv[buf][u], zero, 0, 0, 0);
-                const v4i c1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(lo ? zero : a, wv[buf][u], zero, 0, 0, 0);
-                const float4 x0 = *(const float4*)(sxd + b0 * BM + 16 * i + 4 * g);
-                const float4 x1 = *(const float4*)(sxd + (b0 + 1) * BM + 16 * i + 4 * g);
-                const float xs0[4] = {x0.x, x0.y, x0.z, x0.w}, xs1[4] = {x1.x, x1.y, x1.z, x1.w};
-#pragma unroll
-                for (int r = 0; r < 4; r++) {
-                    acc[i][r] = fmaf((float)c0[r], xs0[r] * dw0, acc[i][r]);
-                    acc[i][r] = fmaf((float)c1[r], xs1[r] * dw1, acc[i][r]);
-                }
-            }
-        }
-    };
-    using B0 = std::integral_constant<int, 0>;
-    using B1 = std::integral_constant<int, 1>;
-    const int end = s0 + per;   // per % (2·U) need not hold: the loop may stop after either group
-    load(B0{}, s0);   // the first weight group flies while the workgroup stages the activation scales
-    for (int idx = threadIdx.x; idx < nb * BM; idx += 64 * CG * KS) {
-        const int row = idx / nb, blk = idx % nb;
-        sxd[blk * BM + row] = Xd[(size_t)min(row, M - 1) * nb + blk];
-    }
-    __syncthreads();
-    for (int s = s0; s < end; s += 2 * U) {
-        if (s + U < end) load(B1{}, s + U);
-        compute(B0{}, s);
-        if (s + U >= end) break;
-        if (s + 2 * U < end) load(B0{}, s + 2 * U);
-        compute(B1{}, s + U);
-    }
-    // lane (fr, g) holds rows 16i + 4g + r of column n0 + fr; the KS partial tiles of a column group are summed in
-    // wave order through LDS (the scale image is dead once every wave has left the K loop)
-    __syncthreads();
-    float4* red = smem_ws;   // [KS][CG][TI][64]
-    if constexpr (KS > 1) {
-#pragma unroll
-        for (int i = 0; i < TI; i++)
-            red[((ks * CG + cg) * TI + i) * 64 + lane] = make_float4(acc[i][0], acc[i][1], acc[i][2], acc[i][3]);
-        __syncthreads();
-        if (ks != 0) return;
-#pragma unroll
-        for (int i = 0; i < TI; i++) {
-#pragma unroll
-            for (int w = 1; w < KS; w++) {
-                const float4 v = red[((w * CG + cg) * TI + i) * 64 + lane];
-                acc[i][0] += v.x, acc[i][1] += v.y, acc[i][2] += v.z, acc[i][3] += v.w;
-            }
-        }
-    }
-    if (epi == EPI_SWIGLU) {
-        if constexpr (CG == 4) {
-            // the workgroup's 64 interleaved columns [g 16 | u 16 | g 16 | u 16] of every row → LDS → SwiGLU + Q8 of
-            // the 32-wide h block (one lane per element, one 32-lane group per row)
-            float* blk = (float*)(red + (size_t)KS * CG * TI * 64);   // [BM][64]
-#pragma unroll
-            for (int i = 0; i < TI; i++)
-#pragma unroll
-                for (int r = 0; r < 4; r++) blk[(16 * i + 4 * g + r) * 64 + 16 * cg + fr] = acc[i][r];
-            __syncthreads();   // (only the ks = 0 waves are left)
-            const int F = N / 2, hb = blockIdx.x * 32;
-            for (int m = 2 * cg + (lane >> 5); m < min(M, BM); m += 2 * CG)
-                swiglu_q8_block(blk + m * 64, lane & 31, yq + (size_t)m * F + hb + (lane & 31), yd + (size_t)m * (F / QK) + hb / QK);
-        }
-        return;
-    }
-    if (n0 + fr >= N) return;
-#pragma unroll
-    for (int i = 0; i < TI; i++)
-#pragma unroll
-        for (int r = 0; r < 4; r++) {
-            const int row = 16 * i + 4 * g + r;
-            if (row < M) y[(size_t)row * ldy + n0 + fr] = epi_apply(epi, acc[i][r], row, n0 + fr, bias, res, ldy);
-        }
-}
-
-template <int TI, int CG, int KS>
-static void launch_ws(hipStream_t s, const int8_t* xq, const float* xd, int M, const Q8Mat& W, const float* bias,
-                      const float* res, float* y, int ldy, int epi, int8_t* yq, float* yd) {
-    const int BM = 16 * TI;
-    const size_t lds = std::max((size_t)(W.K / QK) * BM * 4,
-                                (size_t)KS * CG * TI * 64 * 16 + (epi == EPI_SWIGLU ? (size_t)BM * 64 * 4 : 0));
-    QASR_CHECK(lds <= 160 * 1024, QASR_E_INVALID, "gemm_q8_ws: LDS");
-    k_gemm_q8_ws<TI, CG, KS><<<cdiv(W.N, 16 * CG), 64 * CG * KS, lds, s>>>(xq, xd, M, W.qs, W.sc, W.N, W.K, bias, res, y,
-                                                                          ldy, epi, yq, yd);
-}
-
-static bool g_ws_all = false;   // set_gemm_ws_rows(…, true) — tests: every shape the kernel supports
-
-// rows ≤ 64, K % (128·KS·4) == 0 (spans of two blocks, U-span load groups per wave); the SwiGLU epilogue takes four
-// 16-column groups per workgroup (N % 64 == 0).  Returns false when the shape does not fit.
-static bool gemm_q8_ws(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const float* bias, const float* res,
-                       float* y, int ldy, int epi, hipStream_t s, int8_t* yq, float* yd, int ks_force) {
-    if (M < 1 || M > 64 || !(epi == EPI_STORE || epi == EPI_RESID || epi == EPI_SWIGLU)) return false;
-    // measured (tools/ws_probe.py, profiles/r2s2_ws_probe.jsonl): the activation rows are re-read per 16-column group
-    // straight from L2, so the kernel wins only while they are few — at ≤ 16 rows on the wide decoder matrices (QKV
-    // 9.2 → 5.6 µs at 8 rows, gate/up 16.2 → 12.3 µs), not on the 2,048-wide projections or the vocabulary
-    if (ks_force <= 0 && !g_ws_all && !(epi == EPI_SWIGLU || (W.N >= 4096 && W.N < 32768))) return false;
-    // round 4: with the pinned LDS-DMA tile the SwiGLU shape at 9–16 rows is faster on the table's cfg 12 / 4 splits
-    // (11.8 against 14.3 µs at 16 rows, profiles/r4b_sweep.log)
-    if (ks_force <= 0 && !g_ws_all && epi == EPI_SWIGLU && M > 8) return false;
-    const int TI = (M + 15) / 16, U = TI >= 3 ? 2 : 4;
-    const bool swi = epi == EPI_SWIGLU;
-    // K split over waves: fill ≈ 1,024 waves (4 per CU) — 16-column groups × KS (SwiGLU: 4 groups, ≤ 8 waves: 16
-    // would cap the registers at 128 and spill)
-    static const int ks_env = getenv("QASR_WS_KS") ? atoi(getenv("QASR_WS_KS")) : 0;   // tuning (tools/ws_probe.py)
-    int ks = ks_force > 0 ? ks_force : ks_env > 0 ? ks_env : swi ? 2 : 8;
-    ks = std::min(ks, swi ? 2 : 8);
-    while (ks > 1 && (W.K / 64) % (ks * U) != 0) ks /= 2;
-    if (W.K % 64 != 0 || (W.K / 64) % (ks * U) != 0 || (swi && (W.N % 64 != 0 || !yq || !yd))) return false;
-#define WS_GO(T, C, S) launch_ws<T, C, S>(s, xq, xd, M, W, bias, res, y, ldy, epi, yq, yd)
-#define WS_KS2(T, C)                                \
-    switch (ks) {                                   \
-        case 1: WS_GO(T, C, 1); break;              \
-        default: WS_GO(T, C, 2); break;             \
-    }
-#define WS_KS8(T, C)                                \
-    switch (ks) {                                   \
-        case 1: WS_GO(T, C, 1); break;              \
-        case 2: WS_GO(T, C, 2); break;              \
-        case 4: WS_GO(T, C, 4); break;              \
-        default: WS_GO(T, C, 8); break;             \
-    }
-    if (swi) {
-        if (TI == 1) { WS_KS2(1, 4) } else if (TI == 2) { WS_KS2(2, 4) } else { WS_KS2(4, 4) }
-    } else {
-        if (TI == 1) { WS_KS8(1, 1) } else if (TI == 2) { WS_KS8(2, 1) } else { WS_KS8(4, 1) }
-    }
-#undef WS_KS2
-#undef WS_KS8
-#undef WS_GO
-    return true;
-}
-
-
 template <int TI, int TJ>
 static void launch_gemm(dim3 grid, hipStream_t s, const int8_t* xq, const float* xd, int M, const Q8Mat& W,
                         const float* bias, const float* res, float* y, int ldy, int epi, int sps, int8_t* yq,
@@ -2043,16 +1844,6 @@ static bool dec_table_pick(int M, const Q8Mat& W, int epi, int& cfg, int& splits
     return false;
 }
 
-// rows up to which the auto path takes the weight-streaming kernel (k_gemm_q8_ws); QASR_WS_ROWS / set_gemm_ws_rows
-static int g_ws_rows = [] {
-    const char* e = getenv("QASR_WS_ROWS");
-    return e ? std::max(0, std::min(64, atoi(e))) : 16;
-}();
-void set_gemm_ws_rows(int rows, bool all_shapes) {
-    g_ws_rows = std::max(0, std::min(64, rows));
-    g_ws_all = all_shapes;
-}
-
 // The configurations whose outputs are each one fma chain over the K blocks in order (one K group, no split): the
 // register-staged tiles 0–3 and the LDS-DMA tiles 4–13, 16–18, 21–23.  Stable order picks among them (K % 128 == 0):
 // 128×128 for prefill-sized M, else the largest of 64×64 / 32×64 / 32×32 that fills the chip (≥ 256 tiles) — the
@@ -2080,9 +1871,6 @@ void gemm_q8(const int8_t* xq, const float* xd, int M, const Q8Mat& W, const flo
     // two classes for the bench's roofline: prefill / encoder shapes (M > 256 rows, MFMA-bound) and decode-step
     // shapes (≤ 256 rows, bound by the weight stream and the per-block rescale)
     ProfScope ps(s, M > 256 ? "gemm_q8_prefill" : "gemm_q8_decode", 2.0 * M * W.N * W.K, q8_bytes(M, W, epi));
-    if (force_cfg < 0 && force_splits <= 0 && !g_stable && M <= g_ws_rows &&
-        gemm_q8_ws(xq, xd, M, W, bias, res, y, ldy, epi, s, yq, yd, 0))
-        return;
     auto usable = [&](int c) {
         const GemmCfg& g = kGemmCfgs[c];
         if (g.bm == 0) return false;   // reserved slot

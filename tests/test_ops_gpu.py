@@ -884,46 +884,6 @@ def test_gemm_exact_rows_match_gemv(torch_dev, m, n, k, epi):
         assert np.array_equal(host(y)[r], host(y1)[0]), r
 
 
-@pytest.fixture
-def ws_all():
-    """the weight-streaming kernel on every shape it supports up to 64 rows (restored to the default afterwards)"""
-    _lib.check(L().qasr_op_set_gemm_ws_rows(64, 1))
-    yield
-    _lib.check(L().qasr_op_set_gemm_ws_rows(16, 0))
-
-
-# the decoder's shapes at decode row counts (1.7B / 0.6B widths): QKV store, O / down residual, K = 6,144
-@pytest.mark.parametrize("m", [5, 9, 16, 31, 33, 48, 64])
-@pytest.mark.parametrize("n,k,epi", [(4096, 2048, 0), (2048, 2048, 1), (2048, 6144, 1), (1024, 3072, 1), (384, 1024, 0)])
-def test_linear_q8_weight_stream(torch_dev, ws_all, m, n, k, epi):
-    """k_gemm_q8_ws (rows ≤ 64: weights straight into the MFMA operands, two zero-masked 16x16x64 MFMAs per two Q8
-    blocks) against the oracle, on the automatic path (path 2)"""
-    y, ref = _linear_case(torch_dev, m, n, k, 2, epi, seed=m + n + k)
-    scale = np.abs(ref).max() + 1e-6
-    assert np.abs(y - ref).max() <= 2e-5 * scale * np.sqrt(k / 256)
-    ye, refe = _linear_case(torch_dev, m, n, k, 2, 0, seed=m + k, exact=True)
-    assert np.array_equal(ye, refe)
-
-
-@pytest.mark.parametrize("m", [9, 16, 33, 64])
-@pytest.mark.parametrize("f,k", [(6144, 2048), (3072, 1024), (512, 1024)])
-def test_gemm_swiglu_q8_weight_stream(torch_dev, ws_all, m, f, k):
-    """the weight-streaming kernel's SwiGLU + Q8 epilogue (four 16-column groups = one 32-wide h block)"""
-    test_gemm_swiglu_q8(torch_dev, m, f, k, -1, False)
-
-
-def test_linear_q8_weight_stream_vs_gemm(torch_dev):
-    """the same decode GEMM with and without the weight-streaming kernel: equal up to f32 summation order"""
-    m, n, k = 16, 4096, 2048
-    y1, _ = _linear_case(torch_dev, m, n, k, 2, 0, seed=3)   # default: the weight stream at ≤ 16 rows
-    _lib.check(L().qasr_op_set_gemm_ws_rows(0, 0))
-    try:
-        y0, _ = _linear_case(torch_dev, m, n, k, 2, 0, seed=3)
-    finally:
-        _lib.check(L().qasr_op_set_gemm_ws_rows(16, 0))
-    assert np.abs(y1 - y0).max() <= 1e-5 * np.abs(y0).max()
-
-
 @pytest.mark.parametrize("split,P,R", [(True, 275, 17), (False, 275, 17), (True, 40, 9), (False, 600, 8)])
 def test_attention_verify_rows_exact(torch_dev, split, P, R):
     """exact-row contract of the draft verify pass (engine.cpp decoder_layers, rows_share_kv): R consecutive positions
