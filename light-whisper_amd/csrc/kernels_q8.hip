@@ -1849,8 +1849,8 @@ static bool dec_table_pick(int M, const Q8Mat& W, int epi, int& cfg, int& splits
 // 128×128 for prefill-sized M, else the largest of 64×64 / 32×64 / 32×32 that fills the chip (≥ 256 tiles) — the
 // smallest otherwise; the SwiGLU epilogue needs 64-column wave tiles (12), GELU+Q8 64-column workgroup tiles.
 static int stable_pick(int M, int N, int epi) {
-    if (epi == EPI_SWIGLU) return M > 256 ? 13 : 12;
-    if (M > 256) return N >= 32768 ? 8 : 4;
+    if (M > 256) return N >= 32768 ? 8 : 4;   // (the SwiGLU epilogue too: cfg 4's wave tiles are 64 columns wide)
+    if (epi == EPI_SWIGLU) return 12;
     const int cand[3] = {10, 17, 16};
     const int n = epi == EPI_GELU_Q8 ? 2 : 3;
     for (int i = 0; i < n; i++) {

@@ -261,6 +261,9 @@ def test_real_batch_c4_scale(pair):
     for i, c in enumerate(clips):
         n_want = int(round(8 * c.size / 16000.0)) + 1
         assert len(batch[i]) == n_want and len(singles[i]) == n_want, (i, len(batch[i]), len(singles[i]), n_want)
+    # every prefill runs the row-count-independent order and the first token's projection the 1-row arithmetic
+    # (engine.cpp run_batch): the first tokens are the single runs' exactly, with no near-tie allowance
+    assert [b[0] for b in batch] == [x[0] for x in singles]
     divs = {}
     for i in range(64):
         a, b = batch[i], singles[i]

@@ -444,6 +444,34 @@ def test_gemv_exact_rows(torch_dev, pro, n, k, epi):
 GEMM_CHAIN_CFGS = [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 16, 17, 18, 21, 22, 23, 36, 37]
 
 
+@pytest.mark.parametrize("m,f,k", [(300, 1024, 1024), (520, 3072, 2048)])
+def test_gemm_swiglu_stable_tiles_bit_identical(torch_dev, m, f, k):
+    """the row-count-independent order's SwiGLU tile above 256 rows (stable_pick: cfg 4, 128×128 with 64-column wave
+    tiles, K-64 stages) gives the bits of cfg 13 (128×64, 4×1 waves, K-128 stages) and cfg 12 — each output one block
+    chain in K order, the SwiGLU + Q8 epilogue per 64-column wave tile (every prefill of round 5 runs this order)"""
+    import torch
+
+    rng = np.random.default_rng(m + 3 * f)
+    x = rng.standard_normal((m, k)).astype(np.float32)
+    qs, sc = q8_split(oracle.synth_q8(11, "gu", 2 * f, k, 0.05), 2 * f, k)
+    wq, ws = dev(qs, torch_dev), dev(sc, torch_dev)
+    _lib.check(L().qasr_op_interleave_gate_up(ptr(wq), ptr(ws), 2 * f, k, None))
+    xq = empty((m, k), torch.int8, torch_dev)
+    xdd = empty((m, k // 32), torch.float32, torch_dev)
+    xt = dev(x, torch_dev)
+    _lib.check(L().qasr_op_quant_rows(ptr(xt), m, k, k, ptr(xq), ptr(xdd), None))
+    outs = []
+    for cfg in (4, 13, 12):
+        hq = empty((m, f), torch.int8, torch_dev)
+        hd = empty((m, f // 32), torch.float32, torch_dev)
+        _lib.check(L().qasr_op_gemm_swiglu_q8_cfg(ptr(xq), ptr(xdd), m, ptr(wq), ptr(ws), 2 * f, k, ptr(hq), ptr(hd),
+                                                  cfg, None))
+        torch.cuda.synchronize()
+        outs.append((host(hq), host(hd)))
+    for hq, hd in outs[1:]:
+        assert np.array_equal(hq, outs[0][0]) and np.array_equal(hd.view(np.uint32), outs[0][1].view(np.uint32))
+
+
 @pytest.mark.parametrize("m,n,k,epi", [(13, 1024, 1024, 0), (104, 3072, 1024, 0), (160, 1024, 4096, 1),
                                        (300, 4096, 1024, 0), (7, 2048, 2048, 1)])
 def test_gemm_chain_configs_bit_identical(torch_dev, m, n, k, epi):
