@@ -26,10 +26,6 @@ QASR_API int qasr_op_gemm_swiglu_q8_cfg(const int8_t* xq, const float* xd, int32
    register their own for the decode steps (used there for the SwiGLU epilogue).  Not in
    the reference (an engine-internal tuning / test hook). */
 QASR_API int qasr_op_set_gemm_fixup(void* part, int64_t part_bytes, void* cnt, int32_t ncnt);
-/* Decode rows (≥ 1; 0 = never) from which the decode attention (fused and unfused, not split, not batch-invariant)
-   runs one wave per (row, KV head) over the whole key range instead of four waves merged through LDS — same per-key
-   arithmetic, another summation order.  Process-wide; default QASR_ATTN_WAVE_ROWS.  Tuning / A/B hook. */
-QASR_API int qasr_op_set_attn_wave_rows(int32_t rows);
 /* Regrouped stage scales of a Q8 matrix (sc [N][K/32] f16 → out [K/128][N][4] f16, K % 128 == 0): a K-128 GEMM
    stage's column scales as one contiguous run (the decode GEMMs' 16-byte scale DMA; a model's decoder matrices
    carry theirs).  qasr_op_register_stage_scales(wsc, N, K, out) makes the qasr_op_* GEMM entry points use `out` for

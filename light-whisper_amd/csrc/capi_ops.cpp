@@ -267,13 +267,6 @@ QASR_API int qasr_op_xr_gu_swiglu(const int8_t* xq, const float* xd, const float
     });
 }
 
-QASR_API int qasr_op_set_attn_wave_rows(int32_t rows) {
-    return guard([&] {
-        QASR_CHECK(rows >= 0, QASR_E_INVALID, "set_attn_wave_rows: rows >= 0");
-        set_attn_wave_rows(rows);
-    });
-}
-
 QASR_API int qasr_op_set_gemm_fixup(void* part, int64_t part_bytes, void* cnt, int32_t ncnt) {
     return guard([&] {
         QASR_CHECK(part_bytes >= 0 && ncnt >= 0, QASR_E_INVALID, "set_gemm_fixup: bad size");

@@ -91,7 +91,6 @@ void set_mx_workspace(void* p, size_t bytes);
 // split-K fix-up workspace for gemm_q8 (thread-local): `floats` partial-tile floats and `ncnt` arrival counters that
 // are zero between launches (the kernels keep them so); nullptr = split-K adds with f32 atomics.  The fix-up serves
 // the SwiGLU epilogue (deterministic), or every split epilogue with all_epilogues (op-level tests / tuning).
-void set_attn_wave_rows(int rows);   // one-wave decode attention from this many rows (0 = never)
 void set_gemm_fixup(float* part, size_t floats, unsigned* cnt, int ncnt, bool all_epilogues = false);
 // rows up to which gemm_q8's automatic choice takes the weight-streaming kernel (≤ 64; 0 = never); all_shapes: on
 // every shape it supports, not only the wide decoder matrices where it is faster (tests)

@@ -36,213 +36,6 @@ __global__ __launch_bounds__(256) void k_attention(const __half* __restrict__ Q,
 }
 
 
-// ------------------------------------------------------------------------------------------------ one wave per item
-// Decode rows of many-row steps (round 5): ONE wave per (row, KV head) over its whole key range, 4
-// items per workgroup, no LDS merge and no workgroup barrier — the 4-wave kernel's chain (prologue → barrier → K → V
-// → merge barrier) per item is replaced by a per-wave chunk loop in which chunk c+1's K loads are issued as soon as
-// chunk c's scores are out of the K registers, so K(c+1) and V(c) are in flight together (one memory round trip per
-// 32-key chunk).  Same per-key arithmetic as the decode chunk loop of attention_rows (v_dot2 q·k, f32 online softmax,
-// v_fma_mix PV over 4 key groups of 16 lanes), one key range instead of four merged quarters: NOT bit-identical to
-// the 4-wave kernel, so it runs only where the engine's contract is tolerance-level (the table path's batched decode
-// rows; exact rows, verify passes and batch invariance keep attention_rows).  FUSED: the q/k RMSNorm + RoPE and the
-// new K/V row in the wave's prologue (qk_rope.h arithmetic); the new row's K and V are patched in from LDS.
-template <int G, bool FUSED>
-__global__ __launch_bounds__(256) void k_attn_wave(const __half* __restrict__ Q, int ldq, __half* K, __half* V,
-                                                   int ldkv, const int* __restrict__ kv_start,
-                                                   const int* __restrict__ kv_len, int rows, int nh, int nkv,
-                                                   float scale, int8_t* __restrict__ oq, float* __restrict__ od,
-                                                   QkFuse fz) {
-    constexpr int HD = 128, QD = 16, C = 32;
-    __shared__ float sp_all[4][G][C];
-    __shared__ __align__(16) float qs_all[FUSED ? 4 : 1][G][HD + HD / 4];
-    __shared__ __align__(16) __half2 kn_all[FUSED ? 4 : 1][HD / 2];
-    __shared__ __align__(16) __half2 vn_all[FUSED ? 4 : 1][HD / 2];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int gw = blockIdx.x * 4 + w;
-    if (gw >= rows * nkv) return;   // whole wave (no workgroup barrier below)
-    const int r = gw / nkv, kvh = gw % nkv;
-    const int L = kv_len[r], s0 = kv_start[r];
-    const int sub = lane & 7, kk = lane >> 3, vg = lane >> 4, vd = 8 * (lane & 15);
-    float (*sp)[C] = sp_all[w];
-    const __half* kbase = K + (size_t)kvh * HD + sub * QD;
-    const __half* vbase = V + (size_t)kvh * HD + vd;
-    int4 ka[4], kb[4];
-    auto load_k = [&](int c0) {
-        const int n = min(C, L - c0);
-        const __half* kc = kbase + (size_t)(s0 + c0) * ldkv;
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const int j = min(8 * u + kk, n - 1);   // rows past n re-read row n-1 (their scores are dropped)
-            ka[u] = *(const int4*)(kc + (size_t)j * ldkv);
-            kb[u] = *(const int4*)(kc + (size_t)j * ldkv + 8);
-        }
-    };
-    if (L > 0) load_k(0);   // chunk 0's K goes out before the prologue (the new row is patched from LDS below)
-    h2v qv[G][QD / 2];
-    int sl_new = -1;
-    if constexpr (FUSED) {
-        float* qs = &qs_all[w][0][0];
-        const int nslot = nh + 2 * nkv, kvd = nkv * HD;
-        const float* src = fz.qkv + (size_t)r * nslot * HD;
-        const int p = fz.pos[r], sl = fz.slot[r];
-        sl_new = sl;
-        const int e0 = (2 * lane) & (HD / 2 - 1);
-        const float4 cs = *(const float4*)(fz.rope_cs + ((size_t)p * (HD / 2) + e0) * 2);
-        const bool lo = 2 * lane < HD / 2;
-        float2 v[G + 2];
-#pragma unroll
-        for (int t = 0; t < G + 2; t++) {
-            const int h = t < G ? kvh * G + t : t == G ? nh + kvh : nh + nkv + kvh;
-            v[t] = *(const float2*)(src + h * HD + 2 * lane);
-        }
-        const float2 gq = *(const float2*)(fz.qnw + 2 * lane), gk = *(const float2*)(fz.knw + 2 * lane);
-#pragma unroll
-        for (int t = 0; t < G + 1; t++) {
-            const __half2 hv = norm_rope_hd128(v[t], t < G ? gq : gk, cs, lo, fz.eps);
-            if (t < G) {
-                const float2 back = __half22float2(hv);
-                *(float2*)&qs[t * (HD + HD / 4) + 2 * lane + 4 * (lane >> 3)] = make_float2(back.x, back.y);
-            } else {
-                *(__half2*)(fz.kc + (size_t)sl * kvd + kvh * HD + 2 * lane) = hv;
-                kn_all[w][lane] = hv;
-            }
-        }
-        const __half2 vh = __floats2half2_rn(v[G + 1].x, v[G + 1].y);
-        *(__half2*)(fz.vc + (size_t)sl * kvd + kvh * HD + 2 * lane) = vh;
-        vn_all[w][lane] = vh;
-        wave_sync_lds();
-#pragma unroll
-        for (int g = 0; g < G; g++)
-#pragma unroll
-            for (int j = 0; j < QD / 2; j++)
-                qv[g][j] = (h2v){(_Float16)qs[g * (HD + HD / 4) + sub * (QD + 4) + 2 * j],
-                                 (_Float16)qs[g * (HD + HD / 4) + sub * (QD + 4) + 2 * j + 1]};
-    } else {
-#pragma unroll
-        for (int g = 0; g < G; g++) {
-            const __half* qp = Q + (size_t)r * ldq + (kvh * G + g) * HD + sub * QD;
-#pragma unroll
-            for (int j = 0; j < QD / 2; j++) qv[g][j] = *(const h2v*)(qp + 2 * j);
-        }
-    }
-    float m[G], lsum[G], av[G][8];
-#pragma unroll
-    for (int g = 0; g < G; g++) {
-        m[g] = -INFINITY;
-        lsum[g] = 0.f;
-#pragma unroll
-        for (int j = 0; j < 8; j++) av[g][j] = 0.f;
-    }
-    for (int c0 = 0; c0 < L; c0 += C) {
-        const int n = min(C, L - c0);
-        if constexpr (FUSED) {
-            if (sl_new >= s0 + c0 && sl_new < s0 + c0 + n) {   // this chunk holds the new row: K from LDS
-#pragma unroll
-                for (int u = 0; u < 4; u++) {
-                    if (s0 + c0 + min(8 * u + kk, n - 1) == sl_new) {
-                        ka[u] = *(const int4*)(&kn_all[w][0] + sub * (QD / 2));
-                        kb[u] = *(const int4*)(&kn_all[w][0] + sub * (QD / 2) + 4);
-                    }
-                }
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const int j = 8 * u + kk;
-#pragma unroll
-            for (int g = 0; g < G; g++) {
-                const float p = sum8(qk_dot16(qv[g], ka[u], kb[u]));
-                if (sub == 0 && j < n) sp[g][j] = p * scale;
-            }
-        }
-        // the K registers are free: the next chunk's K loads go out now, beside this chunk's V loads
-        if (c0 + C < L) load_k(c0 + C);
-        int4 vr[8];
-        const __half* vc = vbase + (size_t)(s0 + c0) * ldkv;
-#pragma unroll
-        for (int u = 0; u < 8; u++) {
-            const int j = min(4 * u + vg, n - 1);   // rows past n: weight p = 0
-            vr[u] = *(const int4*)(vc + (size_t)j * ldkv);
-        }
-        wave_sync_lds();
-#pragma unroll
-        for (int g = 0; g < G; g++) {
-            const float x = lane < n ? sp[g][lane] : -INFINITY;
-            const float mnew = fmaxf(m[g], wave_max(x));
-            const float alpha = expf(m[g] - mnew);
-            const float p = lane < n ? expf(x - mnew) : 0.f;
-            lsum[g] = fmaf(lsum[g], alpha, wave_sum(p));
-            m[g] = mnew;
-            if (lane < C) sp[g][lane] = p;
-#pragma unroll
-            for (int j = 0; j < 8; j++) av[g][j] *= alpha;
-        }
-        wave_sync_lds();
-        if constexpr (FUSED) {
-            if (sl_new >= s0 + c0 && sl_new < s0 + c0 + n) {   // the new row's V from LDS
-#pragma unroll
-                for (int u = 0; u < 8; u++)
-                    if (s0 + c0 + min(4 * u + vg, n - 1) == sl_new) vr[u] = *(const int4*)(&vn_all[w][0] + vd / 2);
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < 8; u++) {
-            const uint32_t* hv = (const uint32_t*)&vr[u];
-#pragma unroll
-            for (int g = 0; g < G; g++) {
-                const float p = sp[g][4 * u + vg];
-#pragma unroll
-                for (int t = 0; t < 4; t++) {
-                    av[g][2 * t] = fma_mix_lo(p, hv[t], av[g][2 * t]);
-                    av[g][2 * t + 1] = fma_mix_hi(p, hv[t], av[g][2 * t + 1]);
-                }
-            }
-        }
-        wave_sync_lds();
-    }
-    const int D = nh * HD;
-#pragma unroll
-    for (int g = 0; g < G; g++) {
-        const int h = kvh * G + g;
-        const float inv = L > 0 ? 1.f / lsum[g] : 0.f;
-        float out[8];
-#pragma unroll
-        for (int j = 0; j < 8; j++) {
-            float a = av[g][j];
-            a += __shfl_xor(a, 16);
-            a += __shfl_xor(a, 32);
-            out[j] = a * inv;
-        }
-        // lane (lane & 15) holds dims vd … vd+7: a Q8 block = 32 dims = 4 lanes
-        float amax = 0.f;
-#pragma unroll
-        for (int j = 0; j < 8; j++) amax = fmaxf(amax, fabsf(out[j]));
-        amax = fmaxf(amax, __shfl_xor(amax, 1));
-        amax = fmaxf(amax, __shfl_xor(amax, 2));
-        const float d = amax / 127.f;
-        if (lane < 16) {
-            uint32_t lo4 = 0, hi4 = 0;
-#pragma unroll
-            for (int j = 0; j < 8; j++) {
-                const uint32_t b = (uint32_t)(uint8_t)(int8_t)(amax == 0.f ? 0 : (int)roundf(out[j] / d));
-                if (j < 4) lo4 |= b << (8 * j);
-                else hi4 |= b << (8 * (j - 4));
-            }
-            *(uint2*)(oq + (size_t)r * D + h * HD + vd) = make_uint2(lo4, hi4);
-            if ((lane & 3) == 0) od[(size_t)r * (D / 32) + (h * HD + vd) / 32] = __half2float(f2h(d));
-        }
-    }
-}
-
-// the one-wave kernel from this many decode rows (engine's table path; QASR_ATTN_WAVE_ROWS / set_attn_wave_rows,
-// 0 = never)
-static int g_attn_wave_rows = [] {
-    const char* e = getenv("QASR_ATTN_WAVE_ROWS");
-    return e ? atoi(e) : 0;
-}();
-static int attn_wave_rows() { return g_attn_wave_rows; }
-void set_attn_wave_rows(int rows) { g_attn_wave_rows = rows < 0 ? 0 : rows; }
-
 // ------------------------------------------------------------------------------------------------ tiled (MFMA)
 // Prefill / encoder attention: rows come in runs that share their key range (an utterance's causal prompt rows,
 // an encoder window), so 16 consecutive rows form one tile and every K/V chunk loaded is used by all 16.
@@ -490,16 +283,6 @@ static void launch_attention(int G, int rows, hipStream_t s, const __half* Q, in
                              const __half* V, int ldkv, const int* kv_start, const int* kv_len, int nh, int nkv,
                              float scale, float* o, int8_t* oq, float* od) {
     const unsigned b4 = (unsigned)(rows * nkv), b1 = (unsigned)cdiv(rows * nkv, 4);
-    // the fused decode kernel's one-wave policy (attention_decode_fused), so the two paths stay bit-identical
-    if (HD == 128 && !o && oq && (G == 2 || G == 4) && attn_wave_rows() > 0 && rows >= attn_wave_rows()) {
-        if (G == 2)
-            k_attn_wave<2, false><<<b1, 256, 0, s>>>(Q, ldq, (__half*)K, (__half*)V, ldkv, kv_start, kv_len, rows, nh,
-                                                     nkv, scale, oq, od, QkFuse{});
-        else
-            k_attn_wave<4, false><<<b1, 256, 0, s>>>(Q, ldq, (__half*)K, (__half*)V, ldkv, kv_start, kv_len, rows, nh,
-                                                     nkv, scale, oq, od, QkFuse{});
-        return;
-    }
     switch (G) {
         case 1: k_attention<HD, 1, 1><<<b1, 256, 0, s>>>(Q, ldq, K, V, ldkv, kv_start, kv_len, rows, nh, nkv, scale, o, oq, od); break;
         // the fused decode kernel's chunk policy (attention_decode_fused), so the two paths stay bit-identical
@@ -538,16 +321,6 @@ void attention_decode_fused(const QkFuse& fz, int ldkv, const int* kv_start, con
     // (tools/attn_batch.py, profiles/r2_attn_batch_chunk.jsonl: 256 rows 35.9 → 31.2 µs); fewer rows → the 64-key
     // kernel, which still runs its ≤ 32-key waves in 32-key chunks (1 key 6.35 → 5.37 µs)
     const bool ck32 = rows >= QASR_ATTN_CK32_ROWS && !fz.fixed_chunk;
-    if (!fz.part && !fz.fixed_chunk && attn_wave_rows() > 0 && rows >= attn_wave_rows() && (G == 2 || G == 4)) {
-        const unsigned b1 = (unsigned)cdiv(rows * nkv, 4);
-        if (G == 2)
-            k_attn_wave<2, true><<<b1, 256, 0, s>>>(nullptr, 0, fz.kc, fz.vc, ldkv, kv_start, kv_len, rows, nh, nkv,
-                                                    scale, oq, od, fz);
-        else
-            k_attn_wave<4, true><<<b1, 256, 0, s>>>(nullptr, 0, fz.kc, fz.vc, ldkv, kv_start, kv_len, rows, nh, nkv,
-                                                    scale, oq, od, fz);
-        return;
-    }
     // (a 5-waves-per-SIMD build of the 32-key kernel, 95 VGPRs, streamed the same: 31.1 against 31.5 µs at 256
     // rows, profiles/r2s2_attn_occupancy_ab.jsonl — the kernel is not occupancy-bound)
     if (G == 2 && ck32)

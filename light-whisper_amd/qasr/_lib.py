@@ -134,7 +134,6 @@ SIGNATURES = {
     "qasr_op_interleave_gate_up": (C.c_int, [P, P, I32, I32, P]),
     "qasr_op_gemm_swiglu_q8": (C.c_int, [P, P, I32, P, P, I32, I32, P, P, P]),
     "qasr_op_gemm_swiglu_q8_cfg": (C.c_int, [P, P, I32, P, P, I32, I32, P, P, I32, P]),
-    "qasr_op_set_attn_wave_rows": (C.c_int, [I32]),
     "qasr_op_set_gemm_fixup": (C.c_int, [P, C.c_int64, P, I32]),
     "qasr_op_gemm_exact_rows": (C.c_int, [P, P, I32, P, P, I32, I32, P, P, I32, I32, P]),
     "qasr_op_swiglu_q8_interleaved": (C.c_int, [P, I32, I32, P, P, P]),

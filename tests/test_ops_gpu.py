@@ -607,74 +607,6 @@ def test_attention_decode_fused(torch_dev, nh, nkv, rows):
 
 
 @pytest.mark.parametrize("nh,nkv", [(16, 8), (16, 4)])
-def test_attention_decode_wave(torch_dev, nh, nkv):
-    """the one-wave decode attention (k_attn_wave: one wave per (row, KV head) over the whole key range, K(c+1)
-    in flight with V(c)): fused == qk_norm_rope + unfused bit for bit (Q8 rows and both caches), and the Q8 output
-    within one Q8 step of an f64 reference over the written caches, on ragged ranges of 1 … 300 keys (chunk edges
-    31 / 32 / 33 / 64 / 65)"""
-    import torch
-
-    hd, rows = 128, 200
-    rng = np.random.default_rng(17)
-    lens = rng.integers(1, 300, rows).astype(np.int32)
-    lens[:6] = [1, 31, 32, 33, 64, 65]
-    starts = np.concatenate([[3], 3 + np.cumsum(lens[:-1] + 2)]).astype(np.int32)
-    slots = int(starts[-1] + lens[-1] + 4)
-    qkv = rng.standard_normal((rows, (nh + 2 * nkv) * hd)).astype(np.float32)
-    pos = (lens - 1).astype(np.int32)
-    slot = (starts + lens - 1).astype(np.int32)
-    qnw = (1 + 0.1 * rng.standard_normal(hd)).astype(np.float32)
-    knw = (1 + 0.1 * rng.standard_normal(hd)).astype(np.float32)
-    tab = np.empty((512, hd // 2, 2), np.float32)
-    _lib.check(L().qasr_op_rope_table(512, hd, 1e6, tab.ctypes.data_as(C.c_void_p)))
-    kc0 = rng.standard_normal((slots, nkv * hd)).astype(np.float16)
-    vc0 = rng.standard_normal((slots, nkv * hd)).astype(np.float16)
-    keep = [dev(a, torch_dev) for a in (qkv, pos, slot, qnw, knw, tab, starts, lens)]
-    scale = 1.0 / np.sqrt(hd)
-    outs = []
-    _lib.check(L().qasr_op_set_attn_wave_rows(1))
-    try:
-        for fused in (False, True):
-            kc, vc = dev(kc0, torch_dev), dev(vc0, torch_dev)
-            oq = torch.zeros((rows, nh * hd), dtype=torch.int8, device=torch_dev)
-            od = torch.zeros((rows, nh * hd // 32), dtype=torch.float32, device=torch_dev)
-            qo = torch.zeros((rows, nh * hd), dtype=torch.float16, device=torch_dev)
-            if fused:
-                _lib.check(L().qasr_op_attention_decode_fused(ptr(keep[0]), rows, nh, nkv, hd, ptr(keep[1]),
-                                                              ptr(keep[2]), ptr(keep[3]), ptr(keep[4]), ptr(keep[5]),
-                                                              1e-6, ptr(kc), ptr(vc), ptr(keep[6]), ptr(keep[7]), scale,
-                                                              ptr(oq), ptr(od), None))
-            else:
-                _lib.check(L().qasr_op_qk_norm_rope(ptr(keep[0]), rows, nh, nkv, hd, ptr(keep[1]), ptr(keep[2]),
-                                                    ptr(keep[3]), ptr(keep[4]), ptr(keep[5]), 1e-6, ptr(qo), ptr(kc),
-                                                    ptr(vc), None))
-                _lib.check(L().qasr_op_attention(ptr(qo), nh * hd, ptr(kc), ptr(vc), nkv * hd, ptr(keep[6]),
-                                                 ptr(keep[7]), rows, nh, nkv, hd, scale, None, ptr(oq), ptr(od), None))
-            torch.cuda.synchronize()
-            outs.append([host(x) for x in (oq, od, kc, vc, qo)])
-    finally:
-        _lib.check(L().qasr_op_set_attn_wave_rows(0))
-    for name, a, b in zip(("oq", "od", "kc", "vc"), outs[0][:4], outs[1][:4]):
-        bad = np.argwhere(a != b)
-        assert bad.size == 0, f"{name}: {len(bad)} differ, first {bad[:4].tolist()}"
-    oq, od, kc, vc, q = outs[0]
-    G = nh // nkv
-    ref = np.zeros((rows, nh * hd), np.float64)
-    for r in range(rows):
-        for h in range(nh):
-            g = h // G
-            kk = kc[starts[r]:starts[r] + lens[r], g * hd:(g + 1) * hd].astype(np.float64)
-            vv = vc[starts[r]:starts[r] + lens[r], g * hd:(g + 1) * hd].astype(np.float64)
-            s = kk @ q[r, h * hd:(h + 1) * hd].astype(np.float64) * scale
-            p = np.exp(s - s.max())
-            ref[r, h * hd:(h + 1) * hd] = p @ vv / p.sum()
-    deq = oq.astype(np.float64) * np.repeat(od, 32, axis=1)
-    step = np.repeat(od, 32, axis=1)
-    # rounding to the Q8 grid (0.5 step) + the f16-rounded stored scale (≤ 127 · 2^-11 step) + f32 arithmetic
-    assert (np.abs(deq - ref) <= 0.57 * step + 1e-4 * np.abs(ref).max() + 1e-7).all()
-
-
-@pytest.mark.parametrize("nh,nkv", [(16, 8), (16, 4)])
 def test_attention_decode_split(torch_dev, nh, nkv):
     """≤ 4 decode rows over long key ranges split over workgroups (flash-decoding, pieces merged by the last to
     arrive): the same K/V cache writes as one workgroup per row, outputs within f32 merge-order noise of it and of an
