@@ -7,10 +7,10 @@ root=$(pwd)
 out=$root/gpurun_out
 mkdir -p $out
 cd /tmp && export TMPDIR=/tmp
-# graph-replayed steps only (--no-prof: no eager instrumented step): 1 warm-up + 2 timed = 3 steps in the trace
+# graph-replayed steps only (--no-prof: no eager instrumented step): 1 warm-up + 2 timed + the results step = 4
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d /tmp/kt_$tag -o run --output-format csv -- python3 $root/bench.py --no-cpu-baseline --no-prof --steps 2 --warmup 1 > $out/${tag}_prof_bench.log 2>&1 || { tail -n 20 $out/${tag}_prof_bench.log; exit 1; }
 cp $(find /tmp/kt_$tag -name '*kernel_stats.csv' | head -n 1) $out/${tag}_kernel_stats.csv
-python3 $root/tools/trace_classes.py $out/${tag}_trace_classes.json 3 $(find /tmp/kt_$tag -name '*kernel_trace.csv' | head -n 1) > /dev/null || exit 1
+python3 $root/tools/trace_classes.py $out/${tag}_trace_classes.json 4 $(find /tmp/kt_$tag -name '*kernel_trace.csv' | head -n 1) > /dev/null || exit 1
 echo "kernel trace done" >> $out/${tag}_progress.log
 cd $root
 bash tools/pmc_round.sh $tag > $out/${tag}_pmc.log 2>&1 || { tail -n 20 $out/${tag}_pmc.log; exit 1; }
