@@ -247,7 +247,18 @@ QASR_API int qasr_op_xr_linear(const int8_t* xq, const float* xd, const float* s
         W.sc = (__half*)wsc;
         W.N = N;
         W.K = K;
-        xr_linear(xq, xd, src, nw, eps, M, W, y, ldy, resid != 0, S(stream));
+        // the leaf split's scratch: one process-wide buffer for the op entry points (tests / tools, one stream)
+        static XrSplit xs = [] {
+            XrSplit v;
+            void* mem = nullptr;
+            QASR_HIP(hipMalloc(&mem, xr_split_bytes()));
+            QASR_HIP(hipMemset(mem, 0, xr_split_bytes()));
+            v.part = (float*)mem;
+            v.cnt = (unsigned*)((char*)mem + (size_t)kXrSplitItems * 2 * 2 * 256 * sizeof(float));
+            v.items = kXrSplitItems;
+            return v;
+        }();
+        xr_linear(xq, xd, src, nw, eps, M, W, y, ldy, resid != 0, S(stream), nullptr, &xs);
         launched();
     });
 }

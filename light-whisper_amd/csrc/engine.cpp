@@ -134,6 +134,12 @@ Session::Session(Model* m, int n_ctx) : m_(m), n_ctx_(n_ctx) {
                                            (hp.txt_heads + 2 * hp.txt_kv_heads) * hp.head_dim);
     QASR_HIP(hipMalloc(&xr_cnt_, 4 * sizeof(unsigned)));
     QASR_HIP(hipMemset(xr_cnt_, 0, 4 * sizeof(unsigned)));
+    // the xr launches' leaf split (two workgroups per 16-column fragment): partial trees + arrival counters
+    QASR_HIP(hipMalloc(&xr_split_mem_, xr_split_bytes()));
+    QASR_HIP(hipMemset(xr_split_mem_, 0, xr_split_bytes()));
+    xr_split_.part = (float*)xr_split_mem_;
+    xr_split_.cnt = (unsigned*)((char*)xr_split_mem_ + (size_t)kXrSplitItems * 2 * 2 * 256 * sizeof(float));
+    xr_split_.items = kXrSplitItems;
     const char* nofix = getenv("QASR_NO_FIXUP");
     if (!nofix || atoi(nofix) == 0) {
         fix_floats_ = (size_t)256 * ((widest + 127) / 128 * 128) * kFixSplits;
@@ -155,6 +161,7 @@ Session::~Session() {
     if (d_players_) (void)hipFree(d_players_);
     if (psync_) (void)hipFree(psync_);
     if (xr_cnt_) (void)hipFree(xr_cnt_);
+    if (xr_split_mem_) (void)hipFree(xr_split_mem_);
     if (pstamps_) (void)hipFree(pstamps_);
     if (pin_) (void)hipHostFree(pin_);
     for (auto& g : graphs_) (void)hipGraphExecDestroy(g.second);
@@ -616,7 +623,7 @@ void Session::decoder_layers(float* x, int rows, const int* d_pos, const int* d_
     auto xr_path = [&](const Q8Mat& W) { return !no_xr && xr_ok(rows, W.K) && W.N % 16 == 0; };
     auto exact_linear = [&](const int8_t* q, const float* d, const Q8Mat& W, const float* res, float* y, int ldy,
                             int epi) {
-        if (xr_path(W)) xr_linear(q, d, nullptr, nullptr, 0.f, rows, W, y, ldy, epi == EPI_RESID, st_);
+        if (xr_path(W)) xr_linear(q, d, nullptr, nullptr, 0.f, rows, W, y, ldy, epi == EPI_RESID, st_, nullptr, &xr_split_);
         else gemm_exact_rows(q, d, rows, W, res, y, ldy, epi, st_);
     };
     // a residual exact-row launch that also leaves RMSNorm(x)·nw as the next launch's Q8 rows in (nq, nd) — the norm

@@ -189,6 +189,8 @@ class Session {
     int pgrid_[2] = {0, 0};      // workgroups for ≤ 16 / ≤ 32 rows
     uint64_t* pstamps_ = nullptr;   // QASR_PERSIST_STAMPS=<file>: the last launch's grid-wait stamps, written there
     bool persist_prepare();
+    void* xr_split_mem_ = nullptr;   // the xr launches' leaf-split scratch (kernels.h XrSplit)
+    XrSplit xr_split_{};
     unsigned* xr_cnt_ = nullptr;   // the residual xr launches' fused-norm counters (3 words, zero between launches)
     void xr_check();
     void persist_check_abort();

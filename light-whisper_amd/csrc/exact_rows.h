@@ -126,19 +126,27 @@ __device__ __forceinline__ void exact_frag(const int8_t* __restrict__ X, const f
 // ---- the persistent kernel's form: weights held in registers (loaded ahead, before a grid wait), activations from an
 // LDS tile (staged once per phase).  Same lanes, spans, chains and tree as exact_frag: the same bits.
 
-// one wave's weight spans of a 16-column fragment: spans 4w + j + 16t, i = 4t + j (NS = 4T)
-template <int T>
+// one wave's weight spans of a 16-column fragment: spans 4w + j + 16t, i = 4t + j (NS = 4T).  XS = 2 (the leaf split
+// of the per-phase launches): the fragment's 32 leaves are shared by TWO workgroups, half h taking leaves 16h … 16h+15
+// (wave w: leaves 16h + 4w … +3 = O_{4h+w}; spans 8h + 2w + j + 16t, i = 2t + j, NS = 2T); each half's workgroup
+// tree gives H_{2h} + H_{2h+1}, and the two halves are added in half order — ((H0 + H1) + (H2 + H3)), the same bits.
+template <int T, int XS = 1>
 struct XWeights {
-    xr_v4i wq[4 * T];
-    uint32_t ws[4 * T];
+    xr_v4i wq[4 * T / XS];
+    uint32_t ws[4 * T / XS];
 };
+template <int XS>
+__device__ __forceinline__ int xr_span(int i, int wv, int half) {
+    return XS == 1 ? 4 * wv + (i & 3) + 16 * (i >> 2) : 8 * half + 2 * wv + (i & 1) + 16 * (i >> 1);
+}
 
 // tid: the thread index (the persistent kernel passes a per-layer opaque copy, so per-lane addresses are not hoisted
 // out of its layer loop and kept live across every phase)
 // spans [I0, I1) only (a caller that loads a matrix in two parts, e.g. half ahead of a grid wait)
-template <int T, int I0 = 0, int I1 = 4 * T>
-__device__ __forceinline__ void exact_load_w(XWeights<T>& w, const int8_t* __restrict__ W,
-                                             const __half* __restrict__ Wsc, int N, int K, int n0, int tid) {
+template <int T, int I0 = 0, int I1 = 4 * T, int XS = 1>
+__device__ __forceinline__ void exact_load_w(XWeights<T, XS>& w, const int8_t* __restrict__ W,
+                                             const __half* __restrict__ Wsc, int N, int K, int n0, int tid,
+                                             int half = 0) {
     const int lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int fr = lane & 15, g = lane >> 4;
     const int nb = K / QK;
@@ -146,7 +154,7 @@ __device__ __forceinline__ void exact_load_w(XWeights<T>& w, const int8_t* __res
     const uint32_t* sp = (const uint32_t*)(Wsc + (size_t)min(n0 + fr, N - 1) * nb);
 #pragma unroll
     for (int i = I0; i < I1; i++) {
-        const int s = 4 * wv + (i & 3) + 16 * (i >> 2);
+        const int s = xr_span<XS>(i, wv, half);
         w.wq[i] = __builtin_nontemporal_load((const xr_v4i*)(wp + 64 * (size_t)s));
         w.ws[i] = sp[s];
     }
@@ -154,9 +162,12 @@ __device__ __forceinline__ void exact_load_w(XWeights<T>& w, const int8_t* __res
 
 // sX: the tile's int8 rows (row stride ldx bytes, 16-B aligned, ldx ≡ 16 mod 256 so the 16 rows of a fragment read
 // conflict-free), sXd: its f32 block scales (row stride nb = K/32); rows [0, M) valid (later rows clamped to M − 1)
-template <int T, int RF>
-__device__ __forceinline__ void exact_frag_lds(const XWeights<T>& w, const int8_t* sX, int ldx, const float* sXd,
-                                               int M, float (*hx)[RF][4][64], float (&out)[4], int tid) {
+// XS = 2: this workgroup's half of the leaves (XWeights above); out = H_{2h} + H_{2h+1} of half h
+template <int T, int RF, int XS = 1>
+__device__ __forceinline__ void exact_frag_lds(const XWeights<T, XS>& w, const int8_t* sX, int ldx, const float* sXd,
+                                               int M, float (*hx)[RF][4][64], float (&out)[4], int tid,
+                                               int half = 0) {
+    constexpr int LW = 8 / XS;   // leaves per wave
     const int lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int fr = lane & 15, g = lane >> 4;
     constexpr int nb = 32 * T;   // K / 32
@@ -168,21 +179,21 @@ __device__ __forceinline__ void exact_frag_lds(const XWeights<T>& w, const int8_
 #pragma unroll
         for (int r = 0; r < 4; r++) dp[f][r] = sXd + min(16 * f + 4 * g + r, M - 1) * nb;
     }
-    float leaf[RF][8][4];
+    float leaf[RF][LW][4];
 #pragma unroll
     for (int f = 0; f < RF; f++)
 #pragma unroll
-        for (int l = 0; l < 8; l++)
+        for (int l = 0; l < LW; l++)
 #pragma unroll
             for (int r = 0; r < 4; r++) leaf[f][l][r] = 0.f;   // fma(c, p, +0) = the chains' first step
     const bool lo = g < 2;
     const xr_v4i zero = {0, 0, 0, 0};
 #pragma unroll
-    for (int i = 0; i < 4 * T; i++) {
+    for (int i = 0; i < 4 * T / XS; i++) {
         // a scheduling fence every two spans: unfenced, the scheduler hoisted every span's LDS reads (and the weights
         // of the next fragment) and spilled at 512 registers
         if (i % 2 == 0) __builtin_amdgcn_sched_barrier(0);
-        const int j = i & 3, s = 4 * wv + j + 16 * (i >> 2);
+        const int j = i & (4 / XS - 1), s = xr_span<XS>(i, wv, half);
         xr_v4i aq[RF];
         float2 dx[RF][4];
 #pragma unroll
@@ -213,12 +224,12 @@ __device__ __forceinline__ void exact_frag_lds(const XWeights<T>& w, const int8_
         for (int r = 0; r < 4; r++) {
             float o[2];
 #pragma unroll
-            for (int gq = 0; gq < 2; gq++) {
+            for (int gq = 0; gq < LW / 4; gq++) {
                 const float a0 = leaf[f][4 * gq][r] + 0.f, a1 = leaf[f][4 * gq + 1][r] + 0.f;
                 const float a2 = leaf[f][4 * gq + 2][r] + 0.f, a3 = leaf[f][4 * gq + 3][r] + 0.f;
                 o[gq] = (a0 + a1) + (a2 + a3);
             }
-            hx[wv][f][r][lane] = o[0] + o[1];
+            hx[wv][f][r][lane] = XS == 1 ? o[0] + o[1] : o[0];   // H_w, or (XS = 2) O_{4h+w}
         }
     __syncthreads();
     if (wv < RF) {

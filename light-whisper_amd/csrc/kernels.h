@@ -225,8 +225,18 @@ struct XrNorm {
     float* d = nullptr;
     unsigned* cnt = nullptr;
 };
+// the leaf split's scratch (k_xr_linear XS = 2): two workgroups per 16-column fragment; the second to arrive adds the
+// first's partial tree (write-through, one arrival counter per fragment and row slice, zero between launches)
+struct XrSplit {
+    float* part = nullptr;      // [items][2][RF·256] floats, RF ≤ 2
+    unsigned* cnt = nullptr;    // [items]
+    int items = 0;
+};
+constexpr int kXrSplitItems = 256;
+size_t xr_split_bytes();        // part + counters for kXrSplitItems items (counters zeroed by the owner)
 void xr_linear(const int8_t* xq, const float* xd, const float* src, const float* nw, float eps, int R, const Q8Mat& W,
-               float* y, int ldy, bool resid, hipStream_t s, const XrNorm* norm = nullptr);
+               float* y, int ldy, bool resid, hipStream_t s, const XrNorm* norm = nullptr,
+               const XrSplit* split = nullptr);
 // interleaved gate/up (N = 2F) + SwiGLU + Q8 → hq [R][F] / hd [R][F/32]
 void xr_gu_swiglu(const int8_t* xq, const float* xd, const float* src, const float* nw, float eps, int R,
                   const Q8Mat& W, int8_t* hq, float* hd, hipStream_t s);

@@ -489,25 +489,54 @@ __device__ __forceinline__ void xr_norm_tail(const XrNorm& nm, const float* x, i
     }
 }
 
-template <int T, int RF, bool FOLD, bool RESID>
+template <int T, int RF, bool FOLD, bool RESID, int XS = 1>
 __global__ __launch_bounds__(256, 1) void k_xr_linear(const int8_t* X, const float* Xd, const float* src,
                                                       const float* nw, float eps, int R, const int8_t* Wq,
-                                                      const __half* Ws, int N, float* y, int ldy, XrNorm nm) {
+                                                      const __half* Ws, int N, float* y, int ldy, XrNorm nm,
+                                                      XrSplit xs) {
     constexpr int K = 1024 * T, LX = K + 16;
     __shared__ __align__(16) int8_t tile[16 * RF * LX + 16 * RF * (K / QK) * 4];
     __shared__ float hx[4][RF][4][64];
     __shared__ float part[8][4];
+    __shared__ unsigned s_prev;
     const int tid = threadIdx.x;
-    const int n0 = 16 * blockIdx.x, r0 = 16 * RF * blockIdx.y, rn = min(16 * RF, R - r0);
-    XWeights<T> w;
-    exact_load_w<T>(w, Wq, Ws, N, K, n0, tid);
+    // XS = 2: blockIdx.x = 2·fragment + half (the halves of a fragment are neighbours, dispatched together)
+    const int half = XS == 2 ? (int)(blockIdx.x & 1) : 0, frag = XS == 2 ? (int)(blockIdx.x >> 1) : (int)blockIdx.x;
+    const int n0 = 16 * frag, r0 = 16 * RF * blockIdx.y, rn = min(16 * RF, R - r0);
+    XWeights<T, XS> w;
+    exact_load_w<T, 0, 4 * T / XS, XS>(w, Wq, Ws, N, K, n0, tid, half);
     float rv[4] = {0.f, 0.f, 0.f, 0.f}, v[4];
     if (RESID) resid_load<RF>(rv, r0, R, n0, N, y, ldy, tid);
     float* sXd = (float*)(tile + 16 * RF * LX);
     if constexpr (FOLD) norm_tile<T>(src + (size_t)r0 * K, K, eps, rn, nw, tile, LX, sXd, part, tid);
     else stage_tile(X, Xd, K, r0, rn, tile, LX, sXd, tid);
     __syncthreads();
-    exact_frag_lds<T, RF>(w, tile, LX, sXd, rn, hx, v, tid);
+    exact_frag_lds<T, RF, XS>(w, tile, LX, sXd, rn, hx, v, tid, half);
+    if constexpr (XS == 2) {
+        // hand-off (MI355X_MICROARCH.md inter-workgroup visibility, table row 1): this half's tree stored write-through,
+        // the storing waves' vmcnt(0), a barrier, one agent-scope add; the second to arrive reads the first's with sc1
+        // loads and adds the two in half order
+        const int lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+        const int item = frag * (int)gridDim.y + (int)blockIdx.y;
+        float* pp = xs.part + (size_t)item * 2 * (RF * 256);
+        if (wv < RF) {
+#pragma unroll
+            for (int r = 0; r < 4; r++) wt_stf(pp, (uint32_t)(((half * RF + wv) * 4 + r) * 64 + lane) * 4u, v[r]);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) s_prev = __hip_atomic_fetch_add(xs.cnt + item, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+        if (s_prev == 0) return;   // uniform: the first half to arrive is done
+        if (tid == 0) __hip_atomic_store(xs.cnt + item, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // next launch
+        if (wv < RF) {
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const float o = wt_ldf(pp, (uint32_t)((((1 - half) * RF + wv) * 4 + r) * 64 + lane) * 4u);
+                v[r] = half == 0 ? v[r] + o : o + v[r];
+            }
+        }
+    }
     item_store<RF, RESID>(v, rv, r0, R, n0, N, y, ldy, tid);
     if constexpr (RESID) {
         if (nm.w) {   // uniform
@@ -564,8 +593,16 @@ __global__ __launch_bounds__(256, 1) void k_xr_gu(const int8_t* X, const float* 
 
 bool xr_ok(int R, int K) { return R >= 1 && R <= 32 && (K == 1024 || K == 2048 || K == 3072 || K == 6144); }
 
+size_t xr_split_bytes() { return (size_t)kXrSplitItems * (2 * 2 * 256 * sizeof(float) + sizeof(unsigned)); }
+
+// QASR_XR_SPLIT=0 turns the leaf split off (A/B)
+static bool xr_split_on() {
+    static const bool on = !(getenv("QASR_XR_SPLIT") && atoi(getenv("QASR_XR_SPLIT")) == 0);
+    return on;
+}
+
 void xr_linear(const int8_t* xq, const float* xd, const float* src, const float* nw, float eps, int R, const Q8Mat& W,
-               float* y, int ldy, bool resid, hipStream_t s, const XrNorm* norm) {
+               float* y, int ldy, bool resid, hipStream_t s, const XrNorm* norm, const XrSplit* split) {
     const bool fold = src != nullptr;
     ProfScope ps(s, fold ? "xr_linear_rms" : "xr_linear", 2.0 * R * W.N * W.K,
                  (double)W.N * W.K * (1.0 + 2.0 / 32) + (double)R * W.K * (fold ? 4.0 : 1.125) +
@@ -580,9 +617,26 @@ void xr_linear(const int8_t* xq, const float* xd, const float* src, const float*
     // 32-row slice
     const bool two = R > 16 && W.K > 3072;
     const int rf = R > 16 && !two ? 2 : 1;
-    const dim3 g(W.N / 16, two ? 2 : 1);
+    // the leaf split (two workgroups per fragment) where one per fragment leaves CUs idle and the doubled grid is
+    // still resident at once (LDS: the activation tile bounds the workgroups per CU), on the long-K projection only:
+    // down (K 6,144) 11.5 / 12.8 → 9.5 / 10.8 µs at 8 / 16 rows, but QKV and O (K 2,048) 5.5 / 5.5 → 7.5 / 7.0 µs at
+    // 8 rows — there the hand-off's round trip costs more than the halved weight stream saves (profiles/
+    // r5_xr_cost_split.log)
+    const int slices = two ? 2 : 1, items = W.N / 16 * slices;
+    const size_t lds = (size_t)16 * rf * (W.K + 16) + (size_t)16 * rf * (W.K / QK) * 4 + 8192;
+    const int per_cu = (int)std::min<size_t>(2, 160 * 1024 / lds);
+    const bool xs2 = split && split->part && split->cnt && !norm && !fold && W.K > 3072 && items <= split->items &&
+                     items < 256 * per_cu && 2 * items <= 256 * per_cu && xr_split_on();
+    const XrSplit xsp = xs2 ? *split : XrSplit{};
+    const dim3 g(W.N / 16 * (xs2 ? 2 : 1), slices);
 #define XR_GO(TT, RFF, FF, RR)                                                                                        \
-    k_xr_linear<TT, RFF, FF, RR><<<g, 256, 0, s>>>(xq, xd, src, nw, eps, R, W.qs, W.sc, W.N, y, ldy, nm)
+    do {                                                                                                              \
+        if (xs2 && !FF)                                                                                               \
+            k_xr_linear<TT, RFF, FF, RR, 2><<<g, 256, 0, s>>>(xq, xd, src, nw, eps, R, W.qs, W.sc, W.N, y, ldy, nm,   \
+                                                              xsp);                                                   \
+        else                                                                                                          \
+            k_xr_linear<TT, RFF, FF, RR><<<g, 256, 0, s>>>(xq, xd, src, nw, eps, R, W.qs, W.sc, W.N, y, ldy, nm, xsp); \
+    } while (0)
 #define XR_RF(TT, FF, RR)                      \
     do {                                       \
         if (rf == 2) XR_GO(TT, 2, FF, RR);     \
