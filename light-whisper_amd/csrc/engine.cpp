@@ -641,19 +641,6 @@ void Session::decoder_layers(float* x, int rows, const int* d_pos, const int* d_
         exact_linear(q, d, W, x, x, H, EPI_RESID);
         return false;
     };
-    // RMSNorm + QKV of ≤ 32 exact rows: one launch (xr_norm_linear: the norm workgroups dispatched first, the column
-    // workgroups' weight stream overlapping the norm) where it applies, else rmsnorm_q8 + the exact-row linear.
-    // Opt-in (QASR_XR_QKV_NORM=1): bit-identical, measured slower (32-segment share 1,122 against 1,201 audio-s/s,
-    // profiles/r5_seg32_xr_norm_qkv.json) — the in-launch hand-off costs more than the launch boundary it removes
-    const bool qkv_norm_on = getenv("QASR_XR_QKV_NORM") && atoi(getenv("QASR_XR_QKV_NORM")) != 0;
-    auto norm_qkv = [&](const DecLayer& L) {
-        if (qkv_norm_on && xr_path(L.qkv) && xr_norm_linear_ok(rows, L.qkv.K, L.qkv.N) && xr_cnt_ && !g_dump) {
-            xr_norm_linear(x, L.attn_norm, h.rms_eps, rows, xq, xd, L.qkv, qkv, QD + 2 * KD, xr_cnt_, st_);
-            return;
-        }
-        rmsnorm_q8(x, rows, H, H, L.attn_norm, h.rms_eps, xq, xd, st_);
-        exact_linear(xq, xd, L.qkv, nullptr, qkv, QD + 2 * KD, EPI_STORE);
-    };
     bool normed = false;   // xq / xd already hold this layer's RMSNorm(x)·attn_norm (fused into the last down launch)
     int8_t* hq2 = gv || xm ? (int8_t*)sc_.get(S_HQ, (size_t)rows * F) : nullptr;   // the SwiGLU Q8 rows
     float* hd2 = gv || xm ? (float*)sc_.get(S_HD, (size_t)rows * (F / QK) * sizeof(float)) : nullptr;
@@ -669,14 +656,14 @@ void Session::decoder_layers(float* x, int rows, const int* d_pos, const int* d_
         if (dmp) dump_rows("x_in", l, rows, x, (size_t)rows * H * sizeof(float));
         const float* next_norm = l + 1 < h.txt_layers ? m_->dec[l + 1].attn_norm : nullptr;
         if (xm) {
-            if (normed) exact_linear(xq, xd, L.qkv, nullptr, qkv, QD + 2 * KD, EPI_STORE);
-            else norm_qkv(L);
+            if (!normed) rmsnorm_q8(x, rows, H, H, L.attn_norm, h.rms_eps, xq, xd, st_);
+            exact_linear(xq, xd, L.qkv, nullptr, qkv, QD + 2 * KD, EPI_STORE);
         } else if (gv) {
             gemv_fused(GV_RMS, nullptr, nullptr, x, H, L.attn_norm, h.rms_eps, rows, L.qkv, nullptr, qkv, QD + 2 * KD,
                        EPI_STORE, nullptr, nullptr, st_);
         } else if (xr_qkv) {
-            if (normed) exact_linear(xq, xd, L.qkv, nullptr, qkv, QD + 2 * KD, EPI_STORE);
-            else norm_qkv(L);
+            if (!normed) rmsnorm_q8(x, rows, H, H, L.attn_norm, h.rms_eps, xq, xd, st_);
+            exact_linear(xq, xd, L.qkv, nullptr, qkv, QD + 2 * KD, EPI_STORE);
         } else {
             QASR_CHECK(!normed, QASR_E_INTERNAL, "decoder: a fused norm feeds the table QKV path");
             rmsnorm_q8(x, rows, H, H, L.attn_norm, h.rms_eps, xq, xd, st_, zq ? qkv : nullptr,
@@ -1245,10 +1232,9 @@ void Session::run_batch(const float* dpcm, const std::vector<int64_t>& off, cons
     }
     // captured step graphs hold scratch, KV and weight pointers: any reallocation or precision change retires them;
     // so does a switch of the per-call launch-path variables (QASR_NO_XR / QASR_XR_NORM, read in decoder_layers)
-    const uint64_t launch_path = (getenv("QASR_NO_XR") ? 1 : 0) + (getenv("QASR_XR_NORM") ? 2 : 0) +
-                                 (getenv("QASR_XR_QKV_NORM") ? 4 : 0);
+    const uint64_t launch_path = (getenv("QASR_NO_XR") ? 1 : 0) + (getenv("QASR_XR_NORM") ? 2 : 0);
     const uint64_t key[5] = {sc_.epoch, kv_epoch_, m_->precision_gen, deterministic_gen(),
-                             attn_epoch_ * 64 + launch_path * 4 + (batch_inv_ ? 1 : 0) + (persist_run_ ? 2 : 0)};
+                             attn_epoch_ * 16 + launch_path * 4 + (batch_inv_ ? 1 : 0) + (persist_run_ ? 2 : 0)};
     if (memcmp(key, graph_key_, sizeof key) != 0) {
         for (auto& g : graphs_) (void)hipGraphExecDestroy(g.second);
         graphs_.clear();

@@ -237,11 +237,6 @@ size_t xr_split_bytes();        // part + counters for kXrSplitItems items (coun
 void xr_linear(const int8_t* xq, const float* xd, const float* src, const float* nw, float eps, int R, const Q8Mat& W,
                float* y, int ldy, bool resid, hipStream_t s, const XrNorm* norm = nullptr,
                const XrSplit* split = nullptr);
-// RMSNorm(x rows)·nw → Q8 (xq / xd, rmsnorm_q8's bits) and the exact-row linear of those rows in ONE launch (the
-// norm workgroups dispatched first; cnt: 3 words, zero between launches, cnt[2] = 1 flags a wait timeout)
-bool xr_norm_linear_ok(int R, int K, int N);
-void xr_norm_linear(const float* x, const float* nw, float eps, int R, int8_t* xq, float* xd, const Q8Mat& W, float* y,
-                    int ldy, unsigned* cnt, hipStream_t s);
 // interleaved gate/up (N = 2F) + SwiGLU + Q8 → hq [R][F] / hd [R][F/32]
 void xr_gu_swiglu(const int8_t* xq, const float* xd, const float* src, const float* nw, float eps, int R,
                   const Q8Mat& W, int8_t* hq, float* hd, hipStream_t s);

@@ -546,81 +546,6 @@ __global__ __launch_bounds__(256, 1) void k_xr_linear(const int8_t* X, const flo
     }
 }
 
-// RMSNorm + the QKV exact-row linear in ONE launch: workgroups 0 … R−1 (dispatched first) each normalise one row of x
-// into Q8 (rmsnorm_q8's arithmetic, write-through) and count it on cnt[0]; the column workgroups issue their weight
-// spans first — independent of the norm — then wait for cnt[0] = R, stage the Q8 rows (sc1 loads) and run the exact
-// fragment.  The norm's load and reduction overlap the weight stream, and the launch of its own is gone.  The last
-// column workgroup (cnt[1]) leaves cnt[0..1] zero; a wait that never ends (workgroups not co-resident — the norm
-// workgroups are dispatched first, so it does not happen) is bounded: cnt[2] = 1 flags it, the engine checks.
-template <int T, int RF>
-__global__ __launch_bounds__(256, 1) void k_xr_norm_linear(const float* x, const float* nw, float eps, int R,
-                                                           int8_t* xq, float* xd, const int8_t* Wq, const __half* Ws,
-                                                           int N, float* y, int ldy, unsigned* cnt) {
-    constexpr int K = 1024 * T, LX = K + 16, KC = T;
-    __shared__ __align__(16) int8_t tile[16 * RF * LX + 16 * RF * (K / QK) * 4];
-    __shared__ float hx[4][RF][4][64];
-    __shared__ float part[4];
-    const int tid = threadIdx.x;
-    if ((int)blockIdx.x < R) {   // norm workgroup: row blockIdx.x
-        const int r = blockIdx.x;
-        float4 v[KC], gw[KC];
-        rms_row_load<KC>(x + (size_t)r * K, K, nw, v, gw, tid);
-        rms_row_q8_finish<KC, true>(v, gw, K, eps, xq + (size_t)r * K, xd + (size_t)r * (K / QK), part, true, tid);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's write-through stores have completed
-        __syncthreads();
-        if (tid == 0) __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        return;
-    }
-    const int frag = (int)blockIdx.x - R, n0 = 16 * frag;
-    XWeights<T> w;
-    exact_load_w<T>(w, Wq, Ws, N, K, n0, tid);
-    if (tid == 0) {
-        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)R) {
-            if (__builtin_amdgcn_s_memrealtime() - t0 > 20000000ull) {   // 0.2 s
-                __hip_atomic_store(cnt + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-        }
-    }
-    __syncthreads();
-    float* sXd = (float*)(tile + 16 * RF * LX);
-    stage_tile(xq, xd, K, 0, R, tile, LX, sXd, tid);
-    __syncthreads();
-    float v[4], rv[4] = {0.f, 0.f, 0.f, 0.f};
-    exact_frag_lds<T, RF>(w, tile, LX, sXd, R, hx, v, tid);
-    item_store<RF, false>(v, rv, 0, R, n0, N, y, ldy, tid);
-    if (tid == 0) {
-        const unsigned d = __hip_atomic_fetch_add(cnt + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (d == gridDim.x - (unsigned)R - 1) {   // every column workgroup is past its wait
-            __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(cnt + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
-}
-
-bool xr_norm_linear_ok(int R, int K, int N) {
-    return R >= 1 && R <= 32 && (K == 1024 || K == 2048) && N % 16 == 0 && N / 16 + R <= 1024;
-}
-
-void xr_norm_linear(const float* x, const float* nw, float eps, int R, int8_t* xq, float* xd, const Q8Mat& W, float* y,
-                    int ldy, unsigned* cnt, hipStream_t s) {
-    ProfScope ps(s, "xr_norm_linear", 2.0 * R * W.N * W.K,
-                 (double)W.N * W.K * (1.0 + 2.0 / 32) + (double)R * W.K * (4.0 + 1.125) + (double)R * W.N * 4.0);
-    QASR_CHECK(xr_norm_linear_ok(R, W.K, W.N) && cnt && nw, QASR_E_INVALID,
-               "xr_norm_linear: rows 1-32, K 1,024 / 2,048 (the QKV input), N % 16 == 0");
-    const dim3 g(R + W.N / 16);
-    if (W.K == 1024) {
-        if (R > 16) k_xr_norm_linear<1, 2><<<g, 256, 0, s>>>(x, nw, eps, R, xq, xd, W.qs, W.sc, W.N, y, ldy, cnt);
-        else k_xr_norm_linear<1, 1><<<g, 256, 0, s>>>(x, nw, eps, R, xq, xd, W.qs, W.sc, W.N, y, ldy, cnt);
-    } else {
-        if (R > 16) k_xr_norm_linear<2, 2><<<g, 256, 0, s>>>(x, nw, eps, R, xq, xd, W.qs, W.sc, W.N, y, ldy, cnt);
-        else k_xr_norm_linear<2, 1><<<g, 256, 0, s>>>(x, nw, eps, R, xq, xd, W.qs, W.sc, W.N, y, ldy, cnt);
-    }
-    QASR_HIP(hipGetLastError());
-}
-
 template <int T, int RF, bool FOLD>
 __global__ __launch_bounds__(256, 1) void k_xr_gu(const int8_t* X, const float* Xd, const float* src, const float* nw,
                                                   float eps, int R, const int8_t* Wq, const __half* Ws, int F,
