@@ -14,7 +14,7 @@ sys.path.insert(0, os.path.join(ROOT, "light-whisper_amd"))
 from qasr import _lib  # noqa: E402
 
 SHAPES = [("qkv", 4096, 2048, 0), ("o", 2048, 2048, 1), ("gu", 12288, 2048, 3), ("down", 2048, 6144, 1)]
-MS = [1, 2, 4, 8, 12, 16, 24, 32]
+MS = [int(v) for v in os.environ.get("XR_COST_MS", "1,2,4,8,12,16,24,32").split(",")]
 
 
 def main():
@@ -74,8 +74,20 @@ def main():
                                                      1 if epi == 1 else 0, None))
                 return True
 
+            def tile(i):
+                # the multi-fragment exact tile (qasr_op_xr_tile; gate/up: + swiglu_q8_interleaved)
+                _lib.check(lib.qasr_op_xr_tile(p(xq), p(xd), M, p(wq[i]), p(ws[i]), N, K, p(y), N,
+                                               1 if epi == 1 else 0, None))
+                if epi == 3:
+                    _lib.check(lib.qasr_op_swiglu_q8_interleaved(p(y), M, N // 2, p(hq), p(hd), None))
+                return True
+
             row = {}
-            for name, fn in (("table", table), ("exact", exact), ("xr", xr), ("xr_fold", lambda i: xr(i, True))):
+            big = M > 32
+            for name, fn in (("table", table), ("exact", exact), ("xr", None if big else xr), ("tile", tile),
+                             ("xr_fold", None if big else (lambda i: xr(i, True)))):
+                if fn is None:
+                    continue
                 if fn(0) is None:
                     continue
                 torch.cuda.synchronize()
