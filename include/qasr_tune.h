@@ -44,11 +44,6 @@ QASR_API int qasr_op_xr_linear(const int8_t* xq, const float* xd, const float* s
 QASR_API int qasr_op_xr_gu_swiglu(const int8_t* xq, const float* xd, const float* src, const float* nw, float eps,
                                   int32_t M, const int8_t* wqs, const void* wsc, int32_t N, int32_t K, int8_t* hq,
                                   float* hd, void* stream);
-/* Any row count (M ≥ 1, N % 64 == 0): the exact-row linear as tiles of 4 (K 6,144: 2) fragments over 32-row chunks
-   (16 at K 6,144), the chunk's rows staged into LDS once per tile — the bits of qasr_op_gemm_exact_rows.  y = X·Wᵀ
-   (+ y when resid). */
-QASR_API int qasr_op_xr_tile(const int8_t* xq, const float* xd, int32_t M, const int8_t* wqs, const void* wsc,
-                             int32_t N, int32_t K, float* y, int32_t ldy, int32_t resid, void* stream);
 #ifdef __cplusplus
 }
 #endif

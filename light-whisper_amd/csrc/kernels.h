@@ -237,10 +237,6 @@ size_t xr_split_bytes();        // part + counters for kXrSplitItems items (coun
 void xr_linear(const int8_t* xq, const float* xd, const float* src, const float* nw, float eps, int R, const Q8Mat& W,
                float* y, int ldy, bool resid, hipStream_t s, const XrNorm* norm = nullptr,
                const XrSplit* split = nullptr);
-// any row count: the exact-row linear as NF-fragment tiles over 16·RF-row chunks, activations staged once per tile
-// (k_xr_tile; the bits of gemm_exact_rows / the 1-row GEMV)
-bool xr_tile_ok(int M, int K, int N);
-void xr_tile(const int8_t* xq, const float* xd, int M, const Q8Mat& W, float* y, int ldy, bool resid, hipStream_t s);
 // interleaved gate/up (N = 2F) + SwiGLU + Q8 → hq [R][F] / hd [R][F/32]
 void xr_gu_swiglu(const int8_t* xq, const float* xd, const float* src, const float* nw, float eps, int R,
                   const Q8Mat& W, int8_t* hq, float* hd, hipStream_t s);

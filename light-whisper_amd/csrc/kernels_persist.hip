@@ -489,40 +489,6 @@ __device__ __forceinline__ void xr_norm_tail(const XrNorm& nm, const float* x, i
     }
 }
 
-// Many rows (any M, the batch-invariant decode and the tile path): NF fragments (16·NF columns) per workgroup over
-// a 16·RF-row chunk (blockIdx.y), the chunk's Q8 rows staged into LDS ONCE for all NF fragments (k_gemm_q8_exact
-// re-reads them from L2 for every 16-column fragment), every fragment's weight spans issued at the start; the same
-// exact_frag_lds arithmetic per fragment — the 1-row GEMV's bits for every row.
-template <int T, int RF, int NF, bool RESID>
-__global__ __launch_bounds__(256, 1) void k_xr_tile(const int8_t* X, const float* Xd, int M, const int8_t* Wq,
-                                                    const __half* Ws, int N, float* y, int ldy) {
-    constexpr int K = 1024 * T, LX = K + 16;
-    __shared__ __align__(16) int8_t tile[16 * RF * LX + 16 * RF * (K / QK) * 4];
-    __shared__ float hx[4][RF][4][64];
-    const int tid = threadIdx.x;
-    const int r0 = 16 * RF * blockIdx.y, rn = min(16 * RF, M - r0);
-    XWeights<T> w[NF];
-#pragma unroll
-    for (int c = 0; c < NF; c++) exact_load_w<T>(w[c], Wq, Ws, N, K, 16 * (NF * (int)blockIdx.x + c), tid);
-    float rv[NF][4];
-#pragma unroll
-    for (int c = 0; c < NF; c++) {
-#pragma unroll
-        for (int r = 0; r < 4; r++) rv[c][r] = 0.f;
-        if (RESID) resid_load<RF>(rv[c], r0, M, 16 * (NF * (int)blockIdx.x + c), N, y, ldy, tid);
-    }
-    float* sXd = (float*)(tile + 16 * RF * LX);
-    stage_tile(X, Xd, K, r0, rn, tile, LX, sXd, tid);
-    __syncthreads();
-#pragma unroll
-    for (int c = 0; c < NF; c++) {
-        float v[4];
-        exact_frag_lds<T, RF>(w[c], tile, LX, sXd, rn, hx, v, tid);
-        item_store<RF, RESID>(v, rv[c], r0, M, 16 * (NF * (int)blockIdx.x + c), N, y, ldy, tid);
-        __syncthreads();   // hx is rewritten by the next fragment
-    }
-}
-
 template <int T, int RF, bool FOLD, bool RESID, int XS = 1>
 __global__ __launch_bounds__(256, 1) void k_xr_linear(const int8_t* X, const float* Xd, const float* src,
                                                       const float* nw, float eps, int R, const int8_t* Wq,
@@ -697,47 +663,6 @@ void xr_linear(const int8_t* xq, const float* xd, const float* src, const float*
 #undef XR_T
 #undef XR_RF
 #undef XR_GO
-    QASR_HIP(hipGetLastError());
-}
-
-bool xr_tile_ok(int M, int K, int N) {
-    return M >= 1 && (K == 1024 || K == 2048 || K == 3072 || K == 6144) && N % 64 == 0;
-}
-
-// QASR_XR_TILE_NF: fragments per workgroup (1, 2 or 4; tuning)
-static int xr_tile_nf(int K) {
-    static const int e = getenv("QASR_XR_TILE_NF") ? atoi(getenv("QASR_XR_TILE_NF")) : 0;
-    if (e == 1 || e == 2 || e == 4) return e;
-    return K >= 6144 ? 2 : 4;
-}
-
-void xr_tile(const int8_t* xq, const float* xd, int M, const Q8Mat& W, float* y, int ldy, bool resid,
-             hipStream_t s) {
-    ProfScope ps(s, "xr_tile", 2.0 * M * W.N * W.K,
-                 (double)W.N * W.K * (1.0 + 2.0 / 32) + (double)M * W.K * 1.125 + (double)M * W.N * 4.0 * (resid ? 2 : 1));
-    QASR_CHECK(xr_tile_ok(M, W.K, W.N), QASR_E_INVALID, "xr_tile: K 1,024 / 2,048 / 3,072 / 6,144, N % 64 == 0");
-    // 32-row chunks (K ≤ 3,072; 16-row chunks at 6,144, where a 32-row tile would not fit LDS)
-    const int rf = W.K > 3072 || M <= 16 ? 1 : 2, nf = xr_tile_nf(W.K);
-    const dim3 g(W.N / (16 * nf), cdiv(M, 16 * rf));
-#define XT_GO(TT, RFF, NFF)                                                                                             \
-    do {                                                                                                                \
-        if (resid) k_xr_tile<TT, RFF, NFF, true><<<g, 256, 0, s>>>(xq, xd, M, W.qs, W.sc, W.N, y, ldy);                \
-        else k_xr_tile<TT, RFF, NFF, false><<<g, 256, 0, s>>>(xq, xd, M, W.qs, W.sc, W.N, y, ldy);                     \
-    } while (0)
-#define XT_NF(TT, RFF)                             \
-    do {                                           \
-        if (nf == 4) XT_GO(TT, RFF, 4);            \
-        else if (nf == 2) XT_GO(TT, RFF, 2);       \
-        else XT_GO(TT, RFF, 1);                    \
-    } while (0)
-    switch (W.K) {
-        case 1024: if (rf == 2) XT_NF(1, 2); else XT_NF(1, 1); break;
-        case 2048: if (rf == 2) XT_NF(2, 2); else XT_NF(2, 1); break;
-        case 3072: if (rf == 2) XT_NF(3, 2); else XT_NF(3, 1); break;
-        default: if (nf >= 2) XT_GO(6, 1, 2); else XT_GO(6, 1, 1); break;
-    }
-#undef XT_NF
-#undef XT_GO
     QASR_HIP(hipGetLastError());
 }
 

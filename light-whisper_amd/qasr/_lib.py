@@ -143,7 +143,6 @@ SIGNATURES = {
     "qasr_op_stage_scales": (C.c_int, [P, I32, I32, P, P]),
     "qasr_op_register_stage_scales": (C.c_int, [P, I32, I32, P]),
     "qasr_op_xr_linear": (C.c_int, [P, P, P, P, C.c_float, I32, P, P, I32, I32, P, I32, I32, P]),
-    "qasr_op_xr_tile": (C.c_int, [P, P, I32, P, P, I32, I32, P, I32, I32, P]),
     "qasr_op_xr_gu_swiglu": (C.c_int, [P, P, P, P, C.c_float, I32, P, P, I32, I32, P, P, P]),
     "qasr_op_gemm_mx": (C.c_int, [P, P, I32, P, P, I32, I32, P, P, P, I32, I32, P, P, I32, P]),
     "qasr_op_linear_q8_ex": (C.c_int, [P, P, I32, P, P, I32, I32, P, P, I32, I32, P, P, I32, P]),

@@ -1001,24 +1001,6 @@ def test_xr_linear_bit_identical_to_exact_rows(torch_dev, m, n, k, epi):
         assert np.array_equal(host(y), host(y_ref))
 
 
-@pytest.mark.parametrize("m", [1, 17, 33, 64, 100, 256])
-@pytest.mark.parametrize("n,k,epi", [(4096, 2048, 0), (2048, 2048, 1), (2048, 6144, 1), (1024, 3072, 1), (12288, 2048, 0)])
-def test_xr_tile_bit_identical_to_exact_rows(torch_dev, m, n, k, epi):
-    """qasr_op_xr_tile (4 / 2 fragments per workgroup over 32 / 16-row chunks, the chunk's rows staged in LDS once)
-    == qasr_op_gemm_exact_rows bit for bit, at the batched decode's row counts (incl. ragged last chunks)"""
-    rng = np.random.default_rng(m * 5 + n + k)
-    xq = dev(rng.integers(-127, 128, (m, k), dtype=np.int8), torch_dev)
-    xd = dev((rng.random((m, k // 32)) * 0.02).astype(np.float32), torch_dev)
-    xd[0, 3] = 0.0
-    res = dev((rng.standard_normal((m, n)) * 3).astype(np.float32), torch_dev)
-    wq, ws = _q8_weights(torch_dev, n, k, 13)
-    y_ref, y = res.clone(), res.clone()
-    _lib.check(L().qasr_op_gemm_exact_rows(ptr(xq), ptr(xd), m, ptr(wq), ptr(ws), n, k, ptr(y_ref) if epi else None,
-                                           ptr(y_ref), n, epi, None))
-    _lib.check(L().qasr_op_xr_tile(ptr(xq), ptr(xd), m, ptr(wq), ptr(ws), n, k, ptr(y), n, epi, None))
-    assert np.array_equal(host(y), host(y_ref))
-
-
 @pytest.mark.parametrize("m", [1, 5, 8, 16, 32])
 @pytest.mark.parametrize("f,k", [(6144, 2048), (3072, 1024)])
 def test_xr_gu_swiglu_bit_identical(torch_dev, m, f, k):
