@@ -91,8 +91,6 @@ def main():
                              ("xr_fold", None if big else (lambda i: xr(i, True)))):
                 if fn is None or fn(0) is None:
                     continue
-                if fn(0) is None:
-                    continue
                 torch.cuda.synchronize()
                 n = copies * max(1, 16 // copies)
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
