@@ -23,8 +23,8 @@ if [ "$phase" = a ]; then
   echo "bench done" >> $out/${tag}_progress.log
 else
   cd $root
-  timeout -k 10 400 python3 -u bench.py > $out/${tag}_bench.log 2>&1 || exit 1
-  echo "bench done" >> $out/${tag}_progress.log
+  timeout -k 10 400 python3 -u bench.py > $out/${tag}_bench_b.log 2>&1 || exit 1   # (phase a's line is ${tag}_bench.log)
+  echo "bench (repeat) done" >> $out/${tag}_progress.log
   timeout -k 10 300 python3 -u bench.py --segments 32 --no-cpu-baseline > $out/${tag}_seg32.log 2>&1 || exit 1
   timeout -k 10 300 python3 -u bench.py --segments 64 --no-cpu-baseline > $out/${tag}_seg64.log 2>&1 || exit 1
   echo "shares done" >> $out/${tag}_progress.log
