@@ -379,6 +379,15 @@ typedef struct {
 QASR_API int qasr_dist_unique_id(uint8_t* out /* 128 bytes */, size_t cap);
 QASR_API int qasr_dist_init(const uint8_t* id /* 128 bytes */, int32_t rank, int32_t world, int32_t device,
                             qasr_comm** out);
+/* qasr_dist_init with an explicit deadline (ms; <= 0: QASR_DIST_TIMEOUT_MS from the environment, else 300,000) for
+   the init and for every later collective on the communicator.  The communicator is non-blocking inside: a rank
+   that never calls init (it crashed before it) or never enters a collective makes the others return
+   QASR_E_BACKEND at the deadline instead of blocking forever; the communicator is then aborted and every later call
+   on it fails at once.  qasr_dist_init = this with timeout_ms 0.  RCCL may print its version banner on stdout during
+   qasr_dist_unique_id / init: a host whose stdout is a protocol channel points fd 1 elsewhere around these calls
+   (the library does not touch process-wide file descriptors; engine_longform.cpp and qasr/dist.py do it). */
+QASR_API int qasr_dist_init_deadline(const uint8_t* id /* 128 bytes */, int32_t rank, int32_t world, int32_t device,
+                                     double timeout_ms, qasr_comm** out);
 QASR_API void qasr_dist_close(qasr_comm* c);
 QASR_API int qasr_dist_broadcast(qasr_comm* c, const void* send, void* recv, size_t bytes, int32_t root);
 QASR_API int qasr_dist_broadcast_weights(qasr_comm* c, qasr_model* m, int32_t root, qasr_dist_info* info);

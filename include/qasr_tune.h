@@ -33,7 +33,7 @@ QASR_API int qasr_op_set_gemm_fixup(void* part, int64_t part_bytes, void* cnt, i
    finds no registration) — tests and tuning tools. */
 QASR_API int qasr_op_stage_scales(const void* wsc, int32_t N, int32_t K, void* out, void* stream);
 QASR_API int qasr_op_register_stage_scales(const void* wsc, int32_t N, int32_t K, const void* sc4);
-/* The ≤ 32-row decode's exact-row launches (kernels_persist.hip, xr_*): the same outputs bit for bit as
+/* The ≤ 32-row decode's exact-row launches (kernels_xr.hip, xr_*): the same outputs bit for bit as
    qasr_op_gemm_exact_rows (and, with src, as qasr_op_rmsnorm_q8 + it), one workgroup per 16-column fragment with its
    weights loaded up front and the rows staged once in LDS.  qasr_op_xr_linear: y = X·Wᵀ (+ y when resid); src != NULL
    (M ≤ 8, K ≤ 2,048): X = Q8(RMSNorm(src)·nw) computed inside.  qasr_op_xr_gu_swiglu: W = interleaved gate/up [2F][K],

@@ -1,7 +1,6 @@
 // The per-row attention body (decode rows, encoder windows, the fused decode q/k prologue and the split key range),
-// shared by the k_attention launches (kernels_attn.hip) and the persistent decode kernel (kernels_persist.hip), so
-// both run one definition of the arithmetic.  `bid` is the work item (the launch's blockIdx.x); WT: the QKV rows are
-// read and the Q8 output written write-through (sc1, wt.h), for hand-offs between workgroups of one launch.  Every
+// of the k_attention launches (kernels_attn.hip; round 5's persistent decode kernel ran it too, hence the header).
+// `bid` is the work item (the launch's blockIdx.x).  Every
 // early `return` is either uniform over the workgroup (before any barrier) or leaves wave 0 alone past the last
 // barrier, so a caller that runs items back to back needs only a workgroup barrier between them.  `tid` is the thread
 // index.
@@ -67,7 +66,7 @@ __device__ __forceinline__ float qk_dot16(const h2v* qh, int4 a, int4 b) {
     return part;
 }
 
-template <int HD, int G, int NW, bool FUSED = false, int CK = 64, bool WT = false>
+template <int HD, int G, int NW, bool FUSED = false, int CK = 64>
 __device__ __forceinline__ void attention_rows(unsigned bid, int tid, const __half* __restrict__ Q, int ldq, const __half* K,
                                                    const __half* V, int ldkv,
                                                    const int* __restrict__ kv_start, const int* __restrict__ kv_len,
@@ -82,7 +81,7 @@ __device__ __forceinline__ void attention_rows(unsigned bid, int tid, const __ha
     __shared__ float cm_s[4][G], cl_s[4][G];
     __shared__ __align__(16) float ca_s[4][G][HD];
     __shared__ __align__(16) __half2 kn[FUSED ? HD / 2 : 1];   // FUSED: the new K row (f16), see the K preload
-    // tid: threadIdx.x (the persistent kernel passes a per-layer opaque copy: see kernels_persist.hip)
+    // tid: threadIdx.x
     const int lane = tid & 63, w = tid >> 6;
     // NW = 4: one workgroup per (row, KV head), its 4 waves take contiguous quarters of the key range and merge
     // their partial softmax states through LDS (long decoder KV ranges).  NW = 1: one wave per (row, KV head)
@@ -158,8 +157,7 @@ __device__ __forceinline__ void attention_rows(unsigned bid, int tid, const __ha
         for (int t = w; t < G + 2; t += 4) {
             if (t >= G && !own) continue;
             const int h = t < G ? kvh * G + t : t == G ? nh + kvh : nh + nkv + kvh;
-            const float2 v = WT ? wt_ldf2(src, (uint32_t)(h * HD + 2 * lane) * 4u)
-                                : *(const float2*)(src + h * HD + 2 * lane);
+            const float2 v = *(const float2*)(src + h * HD + 2 * lane);
             if (t == G + 1) {
                 *(__half2*)(fz.vc + (size_t)sl * kvd + kvh * HD + 2 * lane) = __floats2half2_rn(v.x, v.y);
                 continue;
@@ -542,15 +540,9 @@ __device__ __forceinline__ void attention_rows(unsigned bid, int tid, const __ha
 #pragma unroll
             for (int j = 0; j < PD; j++) qb[j] = amax == 0.f ? 0 : (int)roundf(out[j] / d);
             const float dq = __half2float(f2h(d));
-            if constexpr (WT && PD == 2) {   // the persistent kernel: handed to the O-projection's workgroups (sc1)
-                wt_st16(oq, (uint32_t)(r * D + h * HD + lane * PD), (uint16_t)((qb[0] & 0xff) | ((qb[1] & 0xff) << 8)));
-                if ((lane & (32 / PD - 1)) == 0) wt_stf(od, (uint32_t)(r * (D / 32) + (h * HD + lane * PD) / 32) * 4u, dq);
-            } else {
-                static_assert(!WT || PD == 2, "attention_rows: write-through output for hd 128 only");
 #pragma unroll
-                for (int j = 0; j < PD; j++) oq[(size_t)r * D + h * HD + lane * PD + j] = (int8_t)qb[j];
-                if ((lane & (32 / PD - 1)) == 0) od[(size_t)r * (D / 32) + (h * HD + lane * PD) / 32] = dq;
-            }
+            for (int j = 0; j < PD; j++) oq[(size_t)r * D + h * HD + lane * PD + j] = (int8_t)qb[j];
+            if ((lane & (32 / PD - 1)) == 0) od[(size_t)r * (D / 32) + (h * HD + lane * PD) / 32] = dq;
         }
     }
 }

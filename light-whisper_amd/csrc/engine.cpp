@@ -158,11 +158,8 @@ Session::~Session() {
     if (fix_part_) (void)hipFree(fix_part_);
     if (ec_emb_) (void)hipFree(ec_emb_);
     if (fix_cnt_) (void)hipFree(fix_cnt_);
-    if (d_players_) (void)hipFree(d_players_);
-    if (psync_) (void)hipFree(psync_);
     if (xr_cnt_) (void)hipFree(xr_cnt_);
     if (xr_split_mem_) (void)hipFree(xr_split_mem_);
-    if (pstamps_) (void)hipFree(pstamps_);
     if (pin_) (void)hipHostFree(pin_);
     for (auto& g : graphs_) (void)hipGraphExecDestroy(g.second);
     for (auto& g : draft_graphs_) (void)hipGraphExecDestroy(g.second);
@@ -454,60 +451,6 @@ void Session::ensure_attn_split(int rows) {
     attn_epoch_++;
 }
 
-// one persistent launch at a time per process (kernels_persist.hip: its grid waits need every workgroup resident)
-static std::atomic<int> g_persist_busy{0};
-
-bool Session::persist_prepare() {
-    if (persist_state_ != 0) return persist_state_ > 0;
-    persist_state_ = -1;
-    const qasr_hparams& h = m_->hp;
-    if (!persist_supported(h.txt_h, h.txt_ffn, h.txt_heads, h.txt_kv_heads, h.head_dim)) return false;
-    const int QD = h.txt_heads * h.head_dim, KD = h.txt_kv_heads * h.head_dim;
-    std::vector<PersistLayer> pl(h.txt_layers);
-    for (int l = 0; l < h.txt_layers; l++) {
-        const DecLayer& L = m_->dec[l];
-        if (L.qkv.N != QD + 2 * KD || L.qkv.K != h.txt_h || L.o.N != h.txt_h || L.o.K != QD ||
-            L.gu.N != 2 * h.txt_ffn || L.gu.K != h.txt_h || L.down.N != h.txt_h || L.down.K != h.txt_ffn)
-            return false;
-        pl[l] = PersistLayer{L.qkv.qs, L.o.qs, L.gu.qs, L.down.qs, L.qkv.sc, L.o.sc, L.gu.sc, L.down.sc,
-                             L.attn_norm, L.ffn_norm, L.q_norm, L.k_norm};
-    }
-    pgrid_[0] = persist_grid(h.txt_h, h.txt_ffn, h.txt_heads, h.txt_kv_heads, 16);
-    pgrid_[1] = persist_grid(h.txt_h, h.txt_ffn, h.txt_heads, h.txt_kv_heads, 32);
-    if (pgrid_[0] <= 0 || pgrid_[1] <= 0) return false;
-    QASR_HIP(hipMalloc(&d_players_, pl.size() * sizeof(PersistLayer)));
-    QASR_HIP(hipMemcpy(d_players_, pl.data(), pl.size() * sizeof(PersistLayer), hipMemcpyHostToDevice));
-    QASR_HIP(hipMalloc(&psync_, persist_sync_words() * sizeof(unsigned)));
-    QASR_HIP(hipMemset(psync_, 0, persist_sync_words() * sizeof(unsigned)));
-    if (getenv("QASR_PERSIST_STAMPS")) {
-        const size_t n = (size_t)std::max(pgrid_[0], pgrid_[1]) * kPersistMaxWaits * 2;
-        QASR_HIP(hipMalloc(&pstamps_, n * sizeof(uint64_t)));
-        QASR_HIP(hipMemset(pstamps_, 0, n * sizeof(uint64_t)));
-    }
-    persist_state_ = 1;
-    return true;
-}
-
-// after a decode loop that ran persistent launches: a launch whose grid wait timed out (workgroups not co-resident)
-// left the abort word set and its outputs incomplete — reset the counters and fail the request
-void Session::persist_check_abort() {
-    if (const char* fn = getenv("QASR_PERSIST_STAMPS"); fn && pstamps_) {   // diagnosis: the last launch's stamps
-        const size_t n = (size_t)std::max(pgrid_[0], pgrid_[1]) * kPersistMaxWaits * 2;
-        std::vector<uint64_t> h(n);
-        QASR_HIP(hipMemcpy(h.data(), pstamps_, n * sizeof(uint64_t), hipMemcpyDeviceToHost));
-        if (FILE* f = fopen(fn, "wb")) {
-            fwrite(h.data(), sizeof(uint64_t), n, f);
-            fclose(f);
-        }
-    }
-    unsigned ab = 0;
-    QASR_HIP(hipMemcpy(&ab, psync_ + kPersistAbortWord, sizeof ab, hipMemcpyDeviceToHost));
-    if (ab != 0) {
-        QASR_HIP(hipMemset(psync_, 0, persist_sync_words() * sizeof(unsigned)));
-        throw Error(QASR_E_INTERNAL, "persistent decode: a grid wait timed out (workgroups not co-resident)");
-    }
-}
-
 // the fused-norm residual launches flag a wait that timed out (never with the grid resident) in xr_cnt_[2]
 void Session::xr_check() {
     unsigned e = 0;
@@ -572,49 +515,6 @@ void Session::decoder_layers(float* x, int rows, const int* d_pos, const int* d_
     const bool xr_qkv = xr && rows <= xr_lim[0] && gemm_exact_rows_ok(rows, m_->dec[0].qkv);
     const bool xr_o = xr && rows <= xr_lim[1] && gemm_exact_rows_ok(rows, m_->dec[0].o);
     const bool xr_down = xr && rows <= xr_lim[2] && gemm_exact_rows_ok(rows, m_->dec[0].down);
-    if (persist_run_ && fuse_qk && !rows_share_kv && rows <= kExactRows && !m_->mx()) {
-        // the whole stack in one launch (kernels_persist.hip): every row with the 1-row step's arithmetic
-        PersistArgs a{};
-        a.layers = d_players_;
-        a.n_layers = h.txt_layers;
-        a.H = H;
-        a.F = F;
-        a.nh = nh;
-        a.nkv = nkv;
-        a.R = rows;
-        a.x = x;
-        a.pos = d_pos;
-        a.slot = d_slot;
-        a.kvs = d_kvs;
-        a.kvl = d_kvl;
-        a.kc = kc_;
-        a.vc = vc_;
-        a.layer_kv = (int64_t)layer_kv;
-        a.rope_cs = rope_;
-        a.eps = h.rms_eps;
-        a.scale = scale;
-        a.xq = xq;
-        a.xd = xd;
-        a.qkv = qkv;
-        a.hq = (int8_t*)sc_.get(S_HQ, (size_t)rows * F);
-        a.hd = (float*)sc_.get(S_HD, (size_t)rows * (F / QK) * sizeof(float));
-        const QkFuse dflt{};
-        if (attn_split_ && attn_part_ && rows <= attn_rows_) {   // the 1-row step's key-range split
-            a.apart = attn_part_;
-            a.acnt = attn_cnt_;
-            a.part_rows = attn_rows_;
-        }
-        a.split_min = dflt.split_min;
-        a.split_keys = dflt.split_keys;
-        a.sync = psync_;
-        a.timeout_ticks = 100000000;   // 1 s per grid wait (a decode step takes ~1 ms)
-        a.grid = pgrid_[rows <= 16 ? 0 : 1];
-        a.stamps = pstamps_;
-        static const int fold = getenv("QASR_PERSIST_FOLD") ? atoi(getenv("QASR_PERSIST_FOLD")) : 8;
-        a.fold_rows = fold;
-        decoder_persistent(a, st_);
-        return;
-    }
     // ≤ 32 rows: the exact-row linears as the per-phase launches (xr_linear: weights loaded up front, rows staged in
     // LDS; bit-identical to gemm_exact_rows — tests/test_ops_gpu.py::test_xr_linear_bit_identical_to_exact_rows),
     // faster at 2-32 rows on O / down and from 24 rows on QKV (profiles/r5_xr_cost.log); QASR_NO_XR=1 keeps
@@ -707,7 +607,8 @@ void Session::decoder_layers(float* x, int rows, const int* d_pos, const int* d_
                 dump_rows("h_q", l, rows, hq2, (size_t)rows * F);
                 dump_rows("h_d", l, rows, hd2, (size_t)rows * (F / QK) * sizeof(float));
             }
-            normed = !g_dump && resid_norm(hq2, hd2, L.down, next_norm, xq, xd);
+            // under QASR_DUMP_DIR the launch still runs, only its fused norm is dropped (the dump reads x_in)
+            normed = resid_norm(hq2, hd2, L.down, g_dump ? nullptr : next_norm, xq, xd);
             continue;
         }
         if (gv) {   // O-projection + residual; norm + gate/up + SwiGLU + Q8; down-projection + residual
@@ -1202,22 +1103,6 @@ void Session::run_batch(const float* dpcm, const std::vector<int64_t>& off, cons
     Timer td(st_, times ? &times->decode : nullptr);
     int bound = ((volatile int*)pin_cnt_)[1];
     const bool graphs = !prof_enabled() && !getenv("QASR_NO_GRAPH");
-    // the process's persistent-launch slot for this decode loop (released once the stream has drained)
-    struct PersistSlot {
-        Session* s;
-        bool own = false;
-        ~PersistSlot() {
-            if (!own) return;
-            (void)hipStreamSynchronize(s->st_);
-            s->persist_run_ = false;
-            g_persist_busy.store(0);
-        }
-    } pslot{this};
-    if (persist_ && bound > 0 && !m_->mx() && persist_prepare()) {
-        int z = 0;
-        pslot.own = g_persist_busy.compare_exchange_strong(z, 1);
-    }
-    persist_run_ = pslot.own;
     if (bound > 0) {
         // size every scratch slot for the largest bucket eagerly, before any capture
         const int bmax = row_bucket(bound);
@@ -1234,7 +1119,7 @@ void Session::run_batch(const float* dpcm, const std::vector<int64_t>& off, cons
     // so does a switch of the per-call launch-path variables (QASR_NO_XR / QASR_XR_NORM, read in decoder_layers)
     const uint64_t launch_path = (getenv("QASR_NO_XR") ? 1 : 0) + (getenv("QASR_XR_NORM") ? 2 : 0);
     const uint64_t key[5] = {sc_.epoch, kv_epoch_, m_->precision_gen, deterministic_gen(),
-                             attn_epoch_ * 16 + launch_path * 4 + (batch_inv_ ? 1 : 0) + (persist_run_ ? 2 : 0)};
+                             attn_epoch_ * 16 + launch_path * 4 + (batch_inv_ ? 1 : 0)};
     if (memcmp(key, graph_key_, sizeof key) != 0) {
         for (auto& g : graphs_) (void)hipGraphExecDestroy(g.second);
         graphs_.clear();
@@ -1284,7 +1169,6 @@ void Session::run_batch(const float* dpcm, const std::vector<int64_t>& off, cons
         step++;
     }
     QASR_HIP(hipStreamSynchronize(st_));
-    if (persist_run_) persist_check_abort();
     xr_check();
     if (hist) {
         fprintf(stderr, "decode steps per row bucket:");

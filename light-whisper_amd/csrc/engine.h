@@ -174,26 +174,10 @@ class Session {
         const char* e = getenv("QASR_BATCH_INVARIANT");
         return e && atoi(e) != 0;
     }();
-    // persistent decode (kernels_persist.hip): run_batch's decode steps of ≤ 32 rows as ONE launch of the whole
-    // decoder stack, every row with the 1-row step's arithmetic.  One persistent launch at a time per process (its
-    // grid waits need every workgroup resident): a run takes the process's slot for its decode loop or runs the launch
-    // chain.  QASR_PERSIST=0 disables.
-    bool persist_ = [] {
-        const char* e = getenv("QASR_PERSIST");
-        return e && atoi(e) != 0;
-    }();
-    bool persist_run_ = false;   // this run's decode loop holds the slot
-    int persist_state_ = 0;      // 0 not prepared, 1 ready, -1 unsupported (shapes / occupancy)
-    PersistLayer* d_players_ = nullptr;
-    unsigned* psync_ = nullptr;
-    int pgrid_[2] = {0, 0};      // workgroups for ≤ 16 / ≤ 32 rows
-    uint64_t* pstamps_ = nullptr;   // QASR_PERSIST_STAMPS=<file>: the last launch's grid-wait stamps, written there
-    bool persist_prepare();
     void* xr_split_mem_ = nullptr;   // the xr launches' leaf-split scratch (kernels.h XrSplit)
     XrSplit xr_split_{};
     unsigned* xr_cnt_ = nullptr;   // the residual xr launches' fused-norm counters (3 words, zero between launches)
     void xr_check();
-    void persist_check_abort();
     // split-K fix-up workspace of the decode-step GEMMs (≤ 256 rows; QASR_NO_FIXUP=1: f32 atomics instead): partial
     // tiles + per-tile arrival counters (zeroed once; the kernels leave them zero)
     float* fix_part_ = nullptr;

@@ -21,9 +21,11 @@
 // whose stage failed makes EVERY rank exit non-zero with the failing rank's reason instead of leaving the others
 // blocked in the collective (the reference sees one crashed process, funasr_service.rs:1367-1385).  The stages can be
 // failed on purpose for tests: QASR_FAIL_STAGE=model|vad|asr [QASR_FAIL_RANK=r, default every rank].  At world 1,
-// QASR_LONGFORM_COMM=1 opens a one-rank communicator so the same agreement path runs.  Not covered: a rank that dies
-// inside a collective itself (the launcher's supervisor stops the job then), and a failure before the communicator
-// exists (the unique-id hand-off: rank 0 leaves a ".fail" marker, so the other ranks stop polling at once).
+// QASR_LONGFORM_COMM=1 opens a one-rank communicator so the same agreement path runs.  A rank that never joins the
+// communicator (QASR_FAIL_STAGE=init injects it: the rank exits before qasr_dist_init) or dies inside a collective
+// makes the others fail at the communicator's deadline (qasr_dist_init_deadline, QASR_DIST_TIMEOUT_MS) instead of
+// hanging; a failure before the communicator exists goes through the unique-id hand-off (rank 0 leaves a ".fail"
+// marker, so the other ranks stop polling at once; rank 0 clears a stale marker before it publishes).
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -75,6 +77,21 @@ std::string uid_path() {
            std::to_string(getppid()) + ".bin";
 }
 
+// RCCL prints its version banner on stdout when it first initialises; stdout is this command's JSON channel, so the
+// RCCL calls run with fd 1 pointed at stderr (in the executable, not in the library: qasr.h "Multi-GPU")
+struct StdoutToStderr {
+    int saved = -1;
+    StdoutToStderr() {
+        fflush(stdout);
+        saved = dup(1);
+        if (saved >= 0) dup2(2, 1);
+    }
+    ~StdoutToStderr() {
+        fflush(stdout);
+        if (saved >= 0) dup2(saved, 1), close(saved);
+    }
+};
+
 // rank 0 could not create or publish the id: a marker next to the id file, so the other ranks stop polling at once
 void publish_uid_failure(const std::string& path) {
     if (FILE* f = fopen((path + ".fail").c_str(), "wb")) fclose(f);
@@ -82,6 +99,7 @@ void publish_uid_failure(const std::string& path) {
 
 void exchange_uid(uint8_t id[128], int rank, const std::string& path, double timeout_s) {
     if (rank == 0) {
+        remove((path + ".fail").c_str());   // a stale marker of an earlier launch with the same key
         const std::string tmp = path + "." + std::to_string(getpid()) + ".tmp";
         FILE* f = fopen(tmp.c_str(), "wb");
         if (!f || fwrite(id, 1, 128, f) != 128) throw Fail("unique id: cannot write " + tmp);
@@ -185,7 +203,10 @@ int longform_main(const std::string& engine, const std::string& gguf, int argc, 
             const std::string path = uid_path();
             if (rank == 0) {
                 try {
-                    ck(qasr_dist_unique_id(id, sizeof id), "unique id");
+                    {
+                        StdoutToStderr quiet;
+                        ck(qasr_dist_unique_id(id, sizeof id), "unique id");
+                    }
                     exchange_uid(id, rank, path, 600.0);
                 } catch (...) {
                     publish_uid_failure(path);
@@ -194,8 +215,18 @@ int longform_main(const std::string& engine, const std::string& gguf, int argc, 
             } else {
                 exchange_uid(id, rank, path, 600.0);
             }
-            ck(qasr_dist_init(id, rank, world, local, &comm), "communicator");
-            if (rank == 0) remove(path.c_str());   // every rank has joined: the file has been read
+            const char* inj = getenv("QASR_FAIL_STAGE");
+            const int inj_rank = env_int("QASR_FAIL_RANK", -1);
+            if (inj && strcmp(inj, "init") == 0 && (inj_rank < 0 || inj_rank == rank))
+                throw Fail("injected failure (QASR_FAIL_STAGE=init): this rank never joins the communicator");
+            {
+                StdoutToStderr quiet;   // RCCL's version banner must not reach the JSON channel
+                ck(qasr_dist_init(id, rank, world, local, &comm), "communicator");
+            }
+            if (rank == 0) {   // every rank has joined: the file has been read
+                remove(path.c_str());
+                remove((path + ".fail").c_str());
+            }
         }
         // a stage: run locally, then (with a communicator) agree on every rank's outcome before the next collective
         const char* inject_stage = getenv("QASR_FAIL_STAGE");

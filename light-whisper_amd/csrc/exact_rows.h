@@ -1,6 +1,6 @@
 // The exact-row linear's fragment body: one 16-column fragment of W·Xᵀ for up to 16·RF rows with EXACTLY the
 // arithmetic of k_gemv_wide's 1-row launch (the exact-row contract, engine.cpp), shared by the k_gemm_q8_exact
-// launches (kernels_q8.hip) and the persistent decode kernel (kernels_persist.hip) — one definition, so both give the
+// launches (kernels_q8.hip) and the per-phase xr launches (kernels_xr.hip) — one definition, so both give the
 // same bits.
 //
 // The GEMV's result for output (m, n), K = 1024·T, is: lane ℓ = 2l (l = 0…31) accumulates the blocks b = l + 32t in t
@@ -123,7 +123,7 @@ __device__ __forceinline__ void exact_frag(const int8_t* __restrict__ X, const f
     }
 }
 
-// ---- the persistent kernel's form: weights held in registers (loaded ahead, before a grid wait), activations from an
+// ---- the xr launches' form: weights held in registers (loaded at the workgroup's start), activations from an
 // LDS tile (staged once per phase).  Same lanes, spans, chains and tree as exact_frag: the same bits.
 
 // one wave's weight spans of a 16-column fragment: spans 4w + j + 16t, i = 4t + j (NS = 4T).  XS = 2 (the leaf split
@@ -140,8 +140,7 @@ __device__ __forceinline__ int xr_span(int i, int wv, int half) {
     return XS == 1 ? 4 * wv + (i & 3) + 16 * (i >> 2) : 8 * half + 2 * wv + (i & 1) + 16 * (i >> 1);
 }
 
-// tid: the thread index (the persistent kernel passes a per-layer opaque copy, so per-lane addresses are not hoisted
-// out of its layer loop and kept live across every phase)
+// tid: the thread index
 // spans [I0, I1) only (a caller that loads a matrix in two parts, e.g. half ahead of a grid wait)
 template <int T, int I0 = 0, int I1 = 4 * T, int XS = 1>
 __device__ __forceinline__ void exact_load_w(XWeights<T, XS>& w, const int8_t* __restrict__ W,

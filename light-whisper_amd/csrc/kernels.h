@@ -170,49 +170,7 @@ void attention(const __half* Q, int ldq, const __half* K, const __half* V, int l
                const int* kv_len, int rows, int nh, int nkv, int hd, float scale, float* o, int8_t* oq, float* od,
                hipStream_t s, int64_t total_keys = 0, bool dense = false);
 
-// ---- persistent decode (kernels_persist.hip): the whole decoder stack of a ≤ 32-row decode step in ONE launch of
-// about one workgroup per CU, the layer's stages as phases separated by grid-wide arrival counters, every row with
-// the 1-row step's arithmetic (the same device bodies: rms_row_q8, exact_frag, attention_rows)
-struct PersistLayer {   // one decoder layer's device pointers
-    const int8_t *qkv_q, *o_q, *gu_q, *dn_q;
-    const __half *qkv_s, *o_s, *gu_s, *dn_s;
-    const float *attn_norm, *ffn_norm, *q_norm, *k_norm;
-};
-struct PersistArgs {
-    const PersistLayer* layers;
-    int n_layers, H, F, nh, nkv;   // head dim 128
-    int R;                          // rows (≤ 32; padding rows are the decode plan's dummies)
-    float* x;                       // [R][H] residual stream, in and out
-    const int *pos, *slot, *kvs, *kvl;
-    __half *kc, *vc;                // KV cache (layer stride layer_kv halfs, row stride nkv·128)
-    int64_t layer_kv;
-    const float* rope_cs;
-    float eps, scale;
-    int8_t* xq;                     // [R][max(H, QD)] Q8 rows (+ xd [R][max(H, QD)/32]): norm / attention outputs
-    float* xd;
-    float* qkv;                     // [R][QD + 2·KD] f32
-    int8_t* hq;                     // [R][F] SwiGLU Q8 rows (+ hd [R][F/32])
-    float* hd;
-    float* apart;                   // split attention scratch (nullptr: one piece per row and KV head)
-    int* acnt;
-    int part_rows, split_min, split_keys;
-    unsigned* sync;                 // persist_sync_words() words, zero between launches (the kernel leaves them so)
-    int64_t timeout_ticks;          // 100 MHz ticks a grid wait may take before the launch aborts (sync[abort] = 1)
-    int grid;                       // workgroups (≈ one per CU)
-    int fold_rows;                  // rows up to which the norms run inside the QKV / GU phases
-    uint64_t* stamps;               // diagnosis (QASR_PERSIST_STAMPS): per workgroup and grid wait, s_memrealtime at
-                                    // arrival and at release, [grid][kPersistMaxWaits][2]; nullptr = off
-};
-constexpr int kPersistMaxWaits = 512;
-size_t persist_sync_words();
-constexpr int kPersistAbortWord = 256;   // sync[kPersistAbortWord] != 0: a launch aborted (grid not co-resident)
-// the model dims the persistent kernel is built for (hd 128, 2 query heads per KV head, H / QD / F multiples of 1,024
-// with K/1024 ∈ {1, 2, 3, 6}); 0 if unsupported
-bool persist_supported(int H, int F, int nh, int nkv, int hd);
-// workgroups the persistent launch uses on this device (0: the occupancy check failed)
-int persist_grid(int H, int F, int nh, int nkv, int R);
-void decoder_persistent(const PersistArgs& a, hipStream_t s);
-// the same item bodies as one launch per linear (≤ 32 rows; kernels_persist.hip): exact-row arithmetic, bit-identical
+// ---- the ≤ 32-row decode linears as per-phase launches (kernels_xr.hip): exact-row arithmetic, bit-identical
 // to gemm_exact_rows / the 1-row GEMVs.  src != nullptr (≤ 8 rows, K ≤ 2,048): the input rows are RMSNorm(src)·nw
 // quantised inside the launch (rmsnorm_q8's arithmetic) instead of xq / xd.
 bool xr_ok(int R, int K);

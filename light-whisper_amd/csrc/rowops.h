@@ -35,7 +35,7 @@ __device__ __forceinline__ void quant4_store(float4 v, int c, int lane, int8_t* 
 // rms_row_load (registers) then rms_row_q8_finish, which ends with every thread past one workgroup barrier (part may
 // be reused only after another barrier).  Threads 256+ of a larger workgroup pass active = false (barrier only).
 // WT: the row is read write-through (sc1: it was written by another workgroup of the same launch; xr wave-uniform)
-// (tid < 0: threadIdx.x; the persistent kernel passes its per-layer opaque thread index)
+// (tid < 0: threadIdx.x)
 template <int KC, bool WT = false>
 __device__ __forceinline__ void rms_row_load(const float* __restrict__ xr, int H, const float* __restrict__ w,
                                              float4 (&v)[KC], float4 (&gw)[KC], int tid_ = -1) {

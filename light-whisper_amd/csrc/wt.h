@@ -1,5 +1,5 @@
-// Write-through (sc1) loads and stores for data handed between workgroups of ONE launch (the persistent decode
-// kernel, kernels_persist.hip).  MI355X_MICROARCH.md, inter-workgroup visibility, table row 1: every store of the
+// Write-through (sc1) loads and stores for data handed between workgroups of ONE launch (the xr launches' leaf
+// split and fused-norm tail, kernels_xr.hip).  MI355X_MICROARCH.md, inter-workgroup visibility, table row 1: every store of the
 // handed-off bytes `sc1` (write-through past the XCD's L2), the storing waves' `s_waitcnt vmcnt(0)`, then one lane's
 // agent-scope add; the consumer polls with an `sc1` load, passes a workgroup barrier and reads every byte with `sc1`
 // loads (L1 bypassed, so a line this CU read before the producer's store is never served stale).  Buffer

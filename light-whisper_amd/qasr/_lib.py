@@ -109,6 +109,7 @@ SIGNATURES = {
     "qasr_session_set_batch_invariant": (C.c_int, [P, I32]),
     "qasr_dist_unique_id": (C.c_int, [P, SZ]),
     "qasr_dist_init": (C.c_int, [P, I32, I32, I32, P]),
+    "qasr_dist_init_deadline": (C.c_int, [P, I32, I32, I32, C.c_double, P]),
     "qasr_dist_close": (None, [P]),
     "qasr_dist_broadcast": (C.c_int, [P, P, P, SZ, I32]),
     "qasr_dist_broadcast_weights": (C.c_int, [P, P, I32, P]),

@@ -18,6 +18,7 @@ The reference has no multi-GPU path (SURVEY §8(e) "Reference equivalent: none")
 """
 from __future__ import annotations
 
+import contextlib
 import time
 
 import numpy as np
@@ -209,13 +210,34 @@ def gather_token_streams(streams: list[list[int]], device) -> list[list[list[int
     return out
 
 
+@contextlib.contextmanager
+def stdout_to_stderr():
+    """fd 1 → stderr around RCCL's first initialisation: RCCL prints its version banner on stdout, which is bench.py's
+    JSON channel.  The library itself leaves process-wide descriptors alone (include/qasr.h "Multi-GPU")."""
+    import os
+    import sys
+
+    sys.stdout.flush()
+    saved = os.dup(1)
+    try:
+        os.dup2(2, 1)
+        yield
+    finally:
+        sys.stdout.flush()
+        os.dup2(saved, 1)
+        os.close(saved)
+
+
 class NativeComm:
     """libqasr's RCCL communicator (qasr_dist_*).  Rank 0 creates the unique id; `exchange` (any callable that
     returns rank 0's bytes on every rank, e.g. torch.distributed.broadcast_object_list) distributes it."""
 
-    def __init__(self, rank: int, world: int, device: int, exchange=None, uid: bytes | None = None):
+    def __init__(self, rank: int, world: int, device: int, exchange=None, uid: bytes | None = None,
+                 timeout_ms: float = 0.0):
         """either `exchange` (rank 0 creates the id here and the callable distributes it) or `uid` (the 128 bytes,
-        already on every rank — the caller then agrees on the hand-off before this collective init)"""
+        already on every rank — the caller then agrees on the hand-off before this collective init).  timeout_ms: the
+        communicator's deadline for the init and every collective (qasr_dist_init_deadline; 0 = QASR_DIST_TIMEOUT_MS
+        or 300 s) — a rank that never joins makes this one raise instead of blocking"""
         import ctypes as C
 
         from . import _lib
@@ -227,7 +249,9 @@ class NativeComm:
             got = uid
         uid = (C.c_uint8 * 128).from_buffer_copy(got)
         self._h = C.c_void_p()
-        _lib.check(self._lib.qasr_dist_init(uid, rank, world, device, C.byref(self._h)))
+        with stdout_to_stderr():
+            _lib.check(self._lib.qasr_dist_init_deadline(uid, rank, world, device, C.c_double(timeout_ms),
+                                                         C.byref(self._h)))
         self.rank, self.world = rank, world
 
     @staticmethod
@@ -239,7 +263,8 @@ class NativeComm:
 
         lib = _lib.load()
         uid = (C.c_uint8 * 128)()
-        _lib.check(lib.qasr_dist_unique_id(uid, 128))
+        with stdout_to_stderr():
+            _lib.check(lib.qasr_dist_unique_id(uid, 128))
         return bytes(uid)
 
     def close(self):
@@ -334,6 +359,10 @@ def file_exchange(rank: int, world: int, key: str | None = None, directory: str 
         if world == 1:
             return payload
         if rank == 0:
+            try:   # a stale marker of an earlier launch under the same key
+                os.remove(path + ".fail")
+            except FileNotFoundError:
+                pass
             tmp = f"{path}.{os.getpid()}.tmp"
             with open(tmp, "wb") as f:
                 f.write(payload)

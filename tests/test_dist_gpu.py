@@ -3,6 +3,8 @@ communicator — unique id, comm init, the blob broadcast into a shell (send = t
 shell's: the data movement of a rank-0 → rank-k broadcast), the weight broadcast with its checksum hand-shake, and the
 ragged token gather.  The N = 2/3 orchestration (LPT shards, ragged gathers, empty ranks) is covered on CPU with gloo
 (tests/test_shard_cpu.py); RCCL refuses two ranks on one card, so N > 1 RCCL runs only on the driver's 8-GPU node."""
+import os
+
 import numpy as np
 import pytest
 
@@ -58,3 +60,39 @@ def test_native_rccl_world1(torch_dev, golden):
         m.close()
         comm.close()
     assert _lib.load() is not None
+
+
+def test_native_init_deadline_when_a_rank_never_joins():
+    """qasr_dist_init_deadline: rank 0 of a world-2 communicator whose rank 1 never calls init
+    returns QASR_E_BACKEND at the deadline (non-blocking ncclCommInitRankConfig polled through ncclCommGetAsyncError,
+    then ncclCommAbort) instead of blocking forever.  Run in a child process, so even a hang could not take the
+    test runner with it."""
+    import subprocess
+    import sys
+    import textwrap
+    import time
+
+    code = textwrap.dedent("""
+        import sys, time
+        sys.path.insert(0, %r)
+        from qasr.dist import NativeComm
+        uid = NativeComm.unique_id()
+        t0 = time.monotonic()
+        try:
+            NativeComm(0, 2, 0, uid=uid, timeout_ms=4000)
+        except RuntimeError as e:
+            print("ERR", round(time.monotonic() - t0, 2), str(e).replace(chr(10), " ")[:300])
+            sys.exit(0)
+        print("JOINED")
+        sys.exit(3)
+    """ % os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "light-whisper_amd"))
+    t0 = time.monotonic()
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=150)
+    took = time.monotonic() - t0
+    assert out.returncode == 0, (out.returncode, out.stdout[-500:], out.stderr[-2000:])
+    line = [x for x in out.stdout.splitlines() if x.startswith("ERR")][0]
+    waited = float(line.split()[1])
+    print(line, f"(child {took:.1f} s)")
+    assert 3.5 <= waited <= 60.0, line
+    assert "timed out" in line, line
+

@@ -970,7 +970,7 @@ def test_attention_verify_rows_exact(torch_dev, split, P, R):
     assert np.array_equal(host(od_s), host(od_v))
 
 
-# the ≤ 32-row decode's per-phase launches (kernels_persist.hip xr_*): bit-identical to the exact-row chain
+# the ≤ 32-row decode's per-phase launches (kernels_xr.hip xr_*): bit-identical to the exact-row chain
 @pytest.mark.parametrize("m", [1, 3, 8, 16, 17, 32])
 @pytest.mark.parametrize("n,k,epi", [(4096, 2048, 0), (2048, 2048, 1), (2048, 6144, 1), (1024, 3072, 1), (4096, 1024, 0)])
 def test_xr_linear_bit_identical_to_exact_rows(torch_dev, m, n, k, epi):

@@ -259,3 +259,38 @@ def test_engine_longform_failure_is_agreed(stage, tmp_path):
         ok = subprocess.run(args, capture_output=True, text=True, env=env, timeout=300)
         assert ok.returncode == 0, ok.stderr[-2000:]
         assert json.loads(ok.stdout)["world"] == 1
+
+
+def test_engine_longform_rank_never_joins(tmp_path):
+    """`engine longform` at world 2 where rank 1 fails before it joins the communicator (QASR_FAIL_STAGE=init,
+    QASR_FAIL_RANK=1): rank 1 exits with the injected reason, and rank 0 — blocked in the communicator init — exits
+    non-zero at the communicator's deadline (QASR_DIST_TIMEOUT_MS) instead of hanging (the
+    reference's expectation is a process that exits, funasr_service.rs:1367-1385).  Only rank 0 ever opens RCCL on the
+    card, so one GPU serves both ranks."""
+    import time
+
+    from qasr import _lib
+
+    audio = recording(4.0, 3)
+    wav = tmp_path / "rec.wav"
+    _write_f32_wav(wav, audio)
+    base = {k: val for k, val in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    base.update(QASR_SYNTHETIC="1", HF_HUB_CACHE=str(tmp_path / "hf"), QASR_RDV_KEY=f"nj{os.getpid()}",
+                QASR_RDV_DIR=str(tmp_path), QASR_FAIL_STAGE="init", QASR_FAIL_RANK="1", QASR_DIST_TIMEOUT_MS="6000",
+                WORLD_SIZE="2", LOCAL_RANK="0")
+    args = [_lib.ENGINE_PATH, "longform", "--engine", "qwen3-asr-0.6b", "--force-tps", "8", str(wav)]
+    t0 = time.monotonic()
+    p0 = subprocess.Popen(args, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env={**base, "RANK": "0"})
+    p1 = subprocess.run(args, capture_output=True, text=True, env={**base, "RANK": "1"}, timeout=120)
+    try:
+        out0, err0 = p0.communicate(timeout=150)
+    except subprocess.TimeoutExpired:
+        p0.kill()
+        out0, err0 = p0.communicate()
+        raise AssertionError("rank 0 still blocked 150 s after start: " + err0[-2000:])
+    took = time.monotonic() - t0
+    assert p1.returncode == 1 and "injected failure (QASR_FAIL_STAGE=init)" in p1.stderr, p1.stderr[-2000:]
+    assert p0.returncode == 1 and out0 == "", (p0.returncode, out0[:200], err0[-2000:])
+    assert "timed out" in err0, err0[-2000:]
+    print(f"rank 0 failed after {took:.1f} s: {err0.strip().splitlines()[-1][:300]}")
+    assert took < 120

@@ -22,7 +22,6 @@ CLASSES = [  # (class, kernel-name regex) — first match wins
     ("gemm_q8_prefill", r"k_gemm_q8d<2, 2, 4, 4|k_gemm_q8d<2, 2, 2, 4, 3, 128, 1>|k_gemm_q8d<2, 2, 4, 4, 2, 128"),
     ("gemm_q8_decode", r"k_gemm_q8d<|k_gemm_q8_ks<|k_gemm_q8<"),
     ("gemv_q8", r"k_gemv_q8|k_gemv_wide"),
-    ("persist", r"k_dec_persist"),
     ("xr_linear", r"k_xr_linear|k_xr_gu"),
     ("gemm_q8_exact", r"k_gemm_q8_exact"),
     ("gemm_mx", r"k_gemm_mx"),

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""≤ 32-row decode linears: the per-phase exact launches (qasr_op_xr_linear / qasr_op_xr_gu_swiglu, kernels_persist.hip)
+"""≤ 32-row decode linears: the per-phase exact launches (qasr_op_xr_linear / qasr_op_xr_gu_swiglu, kernels_xr.hip)
 against the exact-row MFMA kernel (qasr_op_gemm_exact_rows [+ swiglu]) and the batched table GEMM (qasr_op_linear_q8
 path 2 / qasr_op_gemm_swiglu_q8), 1.7B decoder shapes, COLD weights (a ring of copies larger than the Infinity Cache).
 The norm is a separate launch in every column (folded variants: fold_*).  GPU.  usage: python tools/xr_cost.py [out.json]"""
