@@ -162,6 +162,15 @@ def class_roofline(name, p):
     gr = graph_replayed(name, p)
     if gr:
         r["graph_replayed"] = gr
+        if gr["matches_build"]:
+            # headline = the graph-replayed figure (the timed steps replay graphs; VERDICT r5: reproducible from the
+            # committed trace as algorithmic_bytes_per_launch / trace avg_launch_us / peak); the eager HIP-event
+            # figure stays beside it
+            r["eager"] = {"achieved": r["achieved"], "frac": r["frac"], "avg_launch_us": r["avg_launch_us"],
+                          "measured_on": base["measured_on"]}
+            r.update(achieved=gr["achieved"], frac=gr["frac"], avg_launch_us=gr["avg_launch_us"],
+                     measured_on="graph-replayed bench steps: " + gr["source"] + " (avg launch time) x this run's "
+                                 "algorithmic work per launch (eager instrumented step)")
     ev = pmc_evidence(name)
     if ev:
         r["committed_pmc"] = ev

@@ -192,6 +192,14 @@ QASR_API int qasr_session_forced_logits(qasr_session* s, const float* pcm16k, si
                                         int32_t n_forced, float* logits_out /* [n_forced+1][vocab] */);
 QASR_API int qasr_session_forced_logits_verify(qasr_session* s, const float* pcm16k, size_t n, const int32_t* forced,
                                                int32_t n_forced, float* logits_out /* [n_forced+1][vocab] */);
+/* teacher forcing through the BATCHED path (packed prefill + continuous-batching decode steps with the batch's
+   GEMMs; in MXFP8 precision the block-scaled MFMA GEMMs): utterance u is fed forced[u][0..n_forced) instead of its
+   argmax; the logits of the utterances listed in want[0..n_want) are written [n_want][n_forced+1][vocab] (row j: after
+   the prompt and forced[u][0..j)).  Eager steps; a parity-test hook (tests/test_model_real_gpu.py C5 test). */
+QASR_API int qasr_session_forced_logits_batch(qasr_session* s, const float* const* pcm, const size_t* n,
+                                              int32_t count, const int32_t* forced /* [count][n_forced] */,
+                                              int32_t n_forced, const int32_t* want, int32_t n_want,
+                                              float* logits_out);
 /* the stages of one utterance, for layer-level parity tests (host outputs) */
 QASR_API int qasr_session_mel(qasr_session* s, const float* pcm16k, size_t n, float* mel_out /*[n_mels][t_pad]*/,
                               int32_t* t_valid, int32_t* t_pad);
@@ -380,10 +388,12 @@ QASR_API int qasr_dist_unique_id(uint8_t* out /* 128 bytes */, size_t cap);
 QASR_API int qasr_dist_init(const uint8_t* id /* 128 bytes */, int32_t rank, int32_t world, int32_t device,
                             qasr_comm** out);
 /* qasr_dist_init with an explicit deadline (ms; <= 0: QASR_DIST_TIMEOUT_MS from the environment, else 300,000) for
-   the init and for every later collective on the communicator.  The communicator is non-blocking inside: a rank
-   that never calls init (it crashed before it) or never enters a collective makes the others return
-   QASR_E_BACKEND at the deadline instead of blocking forever; the communicator is then aborted and every later call
-   on it fails at once.  qasr_dist_init = this with timeout_ms 0.  RCCL may print its version banner on stdout during
+   the init and for every later collective on the communicator: a rank that never calls init (it crashed before it) or
+   never enters a collective makes the others return QASR_E_BACKEND at the deadline instead of blocking forever (an
+   init that timed out is abandoned on a helper thread; a collective's communicator is aborted and every later call
+   on it fails at once).  After such an error the host is expected to exit, as the reference's engine does; after an init
+   timeout it should leave with _exit (the abandoned thread is still inside RCCL, and runtime teardown at a normal exit
+   may fault — seen from a Python host; the C++ `engine longform` exits 1 cleanly).  qasr_dist_init = this with timeout_ms 0.  RCCL may print its version banner on stdout during
    qasr_dist_unique_id / init: a host whose stdout is a protocol channel points fd 1 elsewhere around these calls
    (the library does not touch process-wide file descriptors; engine_longform.cpp and qasr/dist.py do it). */
 QASR_API int qasr_dist_init_deadline(const uint8_t* id /* 128 bytes */, int32_t rank, int32_t world, int32_t device,

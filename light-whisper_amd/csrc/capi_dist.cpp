@@ -9,19 +9,23 @@
 //   * qasr_dist_agree: one int32 all-gather of every rank's local status before a collective (failure agreement).
 // Neither runs inside a timed step.  The reference has no multi-GPU path.
 //
-// Liveness: the communicator is NON-blocking (ncclCommInitRankConfig, blocking = 0) and every call on it is waited
-// for against a deadline (qasr_dist_init_deadline's timeout, default QASR_DIST_TIMEOUT_MS or 300 s): ncclInProgress
-// is polled through ncclCommGetAsyncError, a collective's completion through hipStreamQuery.  A rank that never joins
+// Liveness: every call is waited for against a deadline (qasr_dist_init_deadline's timeout, default
+// QASR_DIST_TIMEOUT_MS or 300 s): the init on a helper thread the caller stops waiting for, a collective's completion
+// polled through hipStreamQuery and ncclCommGetAsyncError.  A rank that never joins
 // (it crashed before init, or inside it) or never enters a collective makes the others return QASR_E_BACKEND at the
 // deadline — the communicator is then aborted (ncclCommAbort) and every later call on it fails at once — instead of
 // hanging the job (the reference's expectation: the engine process exits and the Rust host sees it,
 // funasr_service.rs:1367-1385).
+#include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 #include <unistd.h>
 
 #include <algorithm>
 #include <chrono>
+#include <condition_variable>
+#include <mutex>
 #include <memory>
 #include <string>
 #include <thread>
@@ -78,9 +82,26 @@ double env_timeout_ms() {
     return v > 0 ? v : 300000.0;
 }
 
+// QASR_DIST_DEBUG=1: the deadline machinery's steps on stderr (ms since the process's first call)
+void dbg(const char* fmt, ...) {
+    static const bool on = getenv("QASR_DIST_DEBUG") && atoi(getenv("QASR_DIST_DEBUG")) != 0;
+    if (!on) return;
+    static const auto t0 = std::chrono::steady_clock::now();
+    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    fprintf(stderr, "[qasr dist %9.1f ms] ", ms);
+    va_list ap;
+    va_start(ap, fmt);
+    vfprintf(stderr, fmt, ap);
+    va_end(ap);
+    fputc('\n', stderr);
+    fflush(stderr);
+}
+
 // abort the communicator (it may have work in flight that will never complete) and fail
 [[noreturn]] void comm_fail(qasr_comm* c, const std::string& what) {
+    dbg("fail: %s; aborting the communicator", what.c_str());
     if (c->c && !c->dead) (void)ncclCommAbort(c->c);
+    dbg("abort returned");
     c->c = nullptr;
     c->dead = true;
     throw Error(QASR_E_BACKEND, "RCCL: " + what);
@@ -163,18 +184,48 @@ QASR_API int qasr_dist_init_deadline(const uint8_t* id, int32_t rank, int32_t wo
         auto c = std::make_unique<qasr_comm>();
         c->timeout_ms = timeout_ms > 0 ? timeout_ms : env_timeout_ms();
         QASR_HIP(hipSetDevice(device));
+        // ncclCommInitRank blocks until every rank has joined, and this RCCL's non-blocking config does not make the
+        // calling thread return early (measured: ncclCommInitRankConfig with blocking = 0 stayed inside its bootstrap
+        // with a rank missing, gpurun_out/r6b_nj.log).  So the init runs on a helper thread and this thread waits for
+        // it against the deadline; at the deadline the helper is abandoned (detached: it aborts the communicator itself
+        // if the missing rank ever arrives) and the caller gets QASR_E_BACKEND — the host is expected to exit.
+        struct InitJob {
+            std::mutex mu;
+            std::condition_variable cv;
+            bool done = false, abandoned = false;
+            ncclResult_t r = ncclSuccess;
+            ncclComm_t comm = nullptr;
+        };
+        auto job = std::make_shared<InitJob>();
         ncclUniqueId uid;
         memcpy(uid.internal, id, NCCL_UNIQUE_ID_BYTES);
-        const Deadline ddl(c.get());
-        ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
-        cfg.blocking = 0;   // init returns at once (ncclInProgress); settled below against the deadline
-        const ncclResult_t r = ncclCommInitRankConfig(&c->c, world, uid, rank, &cfg);
-        if (r != ncclSuccess && r != ncclInProgress) {
-            if (c->c) (void)ncclCommAbort(c->c);
-            c->c = nullptr;
-            throw Error(QASR_E_BACKEND, std::string("RCCL: ncclCommInitRankConfig: ") + ncclGetErrorString(r));
+        dbg("init rank %d of %d, device %d, deadline %.0f ms", rank, world, device, c->timeout_ms);
+        std::thread([job, uid, rank, world, device] {
+            ncclComm_t cm = nullptr;
+            ncclResult_t r = hipSetDevice(device) == hipSuccess ? ncclCommInitRank(&cm, world, uid, rank)
+                                                                 : ncclUnhandledCudaError;
+            std::lock_guard<std::mutex> lk(job->mu);
+            job->r = r;
+            job->comm = cm;
+            job->done = true;
+            if (job->abandoned && cm) (void)ncclCommAbort(cm);   // the caller gave up: nobody will use it
+            job->cv.notify_all();
+        }).detach();
+        std::unique_lock<std::mutex> lk(job->mu);
+        const auto t_end = Deadline(c.get()).t;
+        if (!job->cv.wait_until(lk, t_end, [&] { return job->done; })) {
+            job->abandoned = true;
+            dbg("init timed out");
+            throw Error(QASR_E_BACKEND, "RCCL: ncclCommInitRank: timed out after " +
+                                            std::to_string((long)c->timeout_ms) +
+                                            " ms (a rank did not join the communicator)");
         }
-        comm_settle(c.get(), r, "ncclCommInitRankConfig", ddl.t);
+        dbg("ncclCommInitRank returned %d (%s)", (int)job->r, ncclGetErrorString(job->r));
+        if (job->r != ncclSuccess) {
+            if (job->comm) (void)ncclCommAbort(job->comm);
+            throw Error(QASR_E_BACKEND, std::string("RCCL: ncclCommInitRank: ") + ncclGetErrorString(job->r));
+        }
+        c->c = job->comm;
         QASR_HIP(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
         c->rank = rank, c->world = world, c->device = device;
         *out = c.release();

@@ -380,6 +380,21 @@ QASR_API int qasr_session_forced_logits(qasr_session* s, const float* pcm16k, si
     });
 }
 
+QASR_API int qasr_session_forced_logits_batch(qasr_session* s, const float* const* pcm, const size_t* n,
+                                              int32_t count, const int32_t* forced, int32_t n_forced,
+                                              const int32_t* want, int32_t n_want, float* logits_out) {
+    return guard([&] {
+        QASR_CHECK(s && pcm && n && count > 0 && n_forced >= 0 && (want || n_want == 0) && n_want >= 0 &&
+                       (logits_out || n_want == 0),
+                   QASR_E_INVALID, "bad arguments");
+        std::vector<const float*> p(pcm, pcm + count);
+        std::vector<int64_t> len(count);
+        for (int i = 0; i < count; i++) len[i] = (int64_t)n[i];
+        std::vector<int> w(want, want + n_want);
+        s->s->forced_logits_batch_host(p, len, forced, n_forced, w, logits_out);
+    });
+}
+
 QASR_API int qasr_session_forced_logits_verify(qasr_session* s, const float* pcm16k, size_t n, const int32_t* forced,
                                                int32_t n_forced, float* logits_out) {
     return guard([&] {

@@ -703,8 +703,33 @@ void Session::decode_step(const DecState& ds, int B, bool sizing, int64_t keys) 
     lm_head_rows(x, B, H, logits, batch_inv_ && !m_->mx());
     int* d_tok = (int*)sc_.get(S_TOK, (size_t)B * sizeof(int));
     argmax_rows(logits, B, V, d_tok, st_, sc_.get(S_ARGP, argmax_scratch_bytes(B)));
+    if (tf_) {
+        force_tokens(ds, B, tab + 5 * B, tf_->d_ids, tf_->ld, d_tok, st_);
+        tf_capture(logits, B, tab + 5 * B);
+    }
     dec_accept(ds, B, tab + 5 * B, d_tok, st_);
     QASR_HIP(hipMemcpyAsync(pin_cnt_, ds.counters, 4 * sizeof(int), hipMemcpyDeviceToHost, st_));
+}
+
+// teacher forcing: the wanted utterances' logits rows of this step → out[w][step][V] (eager steps, host sync)
+void Session::tf_capture(const float* logits, int rows, const int* row_utt) {
+    const int V = m_->hp.vocab;
+    std::vector<int> ru(rows);
+    if (row_utt) {
+        QASR_HIP(hipMemcpyAsync(ru.data(), row_utt, (size_t)rows * sizeof(int), hipMemcpyDeviceToHost, st_));
+        QASR_HIP(hipStreamSynchronize(st_));
+    } else {
+        for (int r = 0; r < rows; r++) ru[r] = r;   // the prefill's first-token rows: row u = utterance u
+    }
+    const int j = tf_->step++;
+    if (j > tf_->n_forced) return;
+    for (int r = 0; r < rows; r++) {
+        const int u = ru[r];
+        if (u < 0 || u >= (int)tf_->want.size() || tf_->want[u] < 0) continue;
+        float* dst = tf_->out + ((size_t)tf_->want[u] * (tf_->n_forced + 1) + j) * V;
+        QASR_HIP(hipMemcpyAsync(dst, logits + (size_t)r * V, (size_t)V * sizeof(float), hipMemcpyDeviceToHost, st_));
+    }
+    QASR_HIP(hipStreamSynchronize(st_));
 }
 
 // ------------------------------------------------------------------------------------------ draft decode
@@ -946,7 +971,8 @@ void Session::run_batch(const float* dpcm, const std::vector<int64_t>& off, cons
         const double secs = (double)len[u] / 16000.0;
         // one utterance decodes until EOS or n_ctx, like the reference's session.run; a batch caps each utterance
         // (its KV slot range is reserved up front)
-        if (force_tps > 0) budget[u] = std::max(1, (int)lround(force_tps * secs) + 1);
+        if (tf_) budget[u] = tf_->n_forced + 1;   // teacher forcing: n_forced + 1 logits rows
+        else if (force_tps > 0) budget[u] = std::max(1, (int)lround(force_tps * secs) + 1);
         else budget[u] = max_new > 0 ? max_new : count == 1 ? n_ctx_ : 64 + (int)ceil(32.0 * secs);
         budget[u] = std::min(budget[u], n_ctx_ - n_prompt[u]);
         QASR_CHECK(budget[u] > 0, QASR_E_CAPACITY, "utterance exceeds n_ctx");
@@ -1007,7 +1033,7 @@ void Session::run_batch(const float* dpcm, const std::vector<int64_t>& off, cons
         int* hp = hb.data() + 6 * ucap_;
         hp[0] = count;
         hp[1] = (int)slots;  // the dummy KV slot (reserved by ensure_kv below)
-        hp[2] = force_tps > 0;
+        hp[2] = force_tps > 0 || tf_;
         hp[3] = h.tok_eos0;
         hp[4] = h.tok_eos1;
         hp[5] = ld;
@@ -1062,11 +1088,15 @@ void Session::run_batch(const float* dpcm, const std::vector<int64_t>& off, cons
         // the first generated token of every utterance: plan (identity rows) + accept on the device
         int* tab = (int*)sc_.get(S_DTAB, (size_t)6 * count * sizeof(int));
         dec_plan(ds, count, tab, tab + count, tab + 2 * count, tab + 3 * count, tab + 4 * count, tab + 5 * count, st_);
+        if (tf_) {
+            force_tokens(ds, count, tab + 5 * count, tf_->d_ids, tf_->ld, d_tok, st_);
+            tf_capture(logits, count, nullptr);
+        }
         dec_accept(ds, count, tab + 5 * count, d_tok, st_);
         QASR_HIP(hipMemcpyAsync(pin_cnt_, ds.counters, 4 * sizeof(int), hipMemcpyDeviceToHost, st_));
         QASR_HIP(hipStreamSynchronize(st_));
     }
-    if (count == 1 && draft_) {   // streaming: prompt-lookup drafts from earlier transcripts
+    if (count == 1 && draft_ && !tf_) {   // streaming: prompt-lookup drafts from earlier transcripts
         std::vector<int32_t> toks;
         bool eos = false;
         {
@@ -1102,7 +1132,7 @@ void Session::run_batch(const float* dpcm, const std::vector<int64_t>& off, cons
     // bound is the active count read back one step late, which never undercounts because it only decreases
     Timer td(st_, times ? &times->decode : nullptr);
     int bound = ((volatile int*)pin_cnt_)[1];
-    const bool graphs = !prof_enabled() && !getenv("QASR_NO_GRAPH");
+    const bool graphs = !prof_enabled() && !getenv("QASR_NO_GRAPH") && !tf_;
     if (bound > 0) {
         // size every scratch slot for the largest bucket eagerly, before any capture
         const int bmax = row_bucket(bound);
@@ -1414,6 +1444,44 @@ void Session::forced_logits_host(const float* pcm, int64_t n, const int32_t* for
                                 hipMemcpyDeviceToHost, st_));
     }
     QASR_HIP(hipStreamSynchronize(st_));
+}
+
+void Session::forced_logits_batch_host(const std::vector<const float*>& pcm, const std::vector<int64_t>& len,
+                                       const int32_t* forced, int n_forced, const std::vector<int>& want, float* out) {
+    const int count = (int)len.size();
+    QASR_CHECK(count > 0 && n_forced >= 0 && (n_forced == 0 || forced) && out, QASR_E_INVALID, "bad arguments");
+    TeacherForce tf;
+    tf.n_forced = n_forced;
+    tf.ld = n_forced + 1;
+    tf.want.assign(count, -1);
+    for (size_t w = 0; w < want.size(); w++) {
+        QASR_CHECK(want[w] >= 0 && want[w] < count && tf.want[want[w]] < 0, QASR_E_INVALID, "want: bad or repeated index");
+        tf.want[want[w]] = (int)w;
+    }
+    tf.out = out;
+    std::vector<int> ids((size_t)count * tf.ld, -1);
+    for (int u = 0; u < count; u++)
+        for (int j = 0; j < n_forced; j++) ids[(size_t)u * tf.ld + j] = forced[(size_t)u * n_forced + j];
+    QASR_HIP(hipMalloc(&tf.d_ids, ids.size() * sizeof(int)));
+    struct Reset {
+        Session* s;
+        TeacherForce* t;
+        ~Reset() {
+            (void)hipStreamSynchronize(s->st_);
+            (void)hipFree(t->d_ids);
+            s->tf_ = nullptr;
+        }
+    } reset{this, &tf};
+    QASR_HIP(hipMemcpy(tf.d_ids, ids.data(), ids.size() * sizeof(int), hipMemcpyHostToDevice));
+    tf_ = &tf;
+    std::vector<UttResult> res;
+    run_host(pcm, len, 0, 0, res, nullptr);
+    // (the loop may run one more, empty step: the host reads the active count one step late)
+    QASR_CHECK(tf.step >= n_forced + 1, QASR_E_INTERNAL, "teacher forcing: step count");
+    for (int u = 0; u < count; u++)
+        for (int j = 0; j < n_forced; j++)
+            QASR_CHECK(res[u].tokens[j] == forced[(size_t)u * n_forced + j], QASR_E_INTERNAL,
+                       "teacher forcing: a forced token was not accepted");
 }
 
 }  // namespace qasr

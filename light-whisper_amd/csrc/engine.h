@@ -58,6 +58,12 @@ class Session {
     // one_pass: the forced continuation in ONE draft verify pass (n_forced ≤ kDraftRows) instead of one step each
     void forced_logits_host(const float* pcm, int64_t n, const int32_t* forced, int n_forced,
                             std::vector<float>& logits, bool one_pass = false);
+    // teacher forcing through the BATCHED path (run_batch: packed prefill, continuous-batching decode steps with the
+    // batch's GEMMs — in MXFP8 precision the block-scaled MFMA GEMMs): every utterance is fed forced[u][0..n_forced)
+    // instead of its argmax, and the logits of the utterances in `want` are returned, [n_want][n_forced + 1][V]
+    // (row j: after the prompt and forced[u][0..j)).  Eager steps (no step graphs); a test / parity hook.
+    void forced_logits_batch_host(const std::vector<const float*>& pcm, const std::vector<int64_t>& len,
+                                  const int32_t* forced, int n_forced, const std::vector<int>& want, float* out);
 
     Model& model() { return *m_; }
     int n_ctx() const { return n_ctx_; }
@@ -174,6 +180,16 @@ class Session {
         const char* e = getenv("QASR_BATCH_INVARIANT");
         return e && atoi(e) != 0;
     }();
+    // batched teacher forcing (forced_logits_batch_host): device table of forced ids [count][ld] (-1: keep argmax),
+    // the wanted utterances' output slots, the step counter
+    struct TeacherForce {
+        int* d_ids = nullptr;
+        int ld = 0, n_forced = 0, step = 0;
+        std::vector<int> want;   // utterance → output index (-1: not wanted)
+        float* out = nullptr;
+    };
+    TeacherForce* tf_ = nullptr;
+    void tf_capture(const float* logits, int rows, const int* row_utt);
     void* xr_split_mem_ = nullptr;   // the xr launches' leaf-split scratch (kernels.h XrSplit)
     XrSplit xr_split_{};
     unsigned* xr_cnt_ = nullptr;   // the residual xr launches' fused-norm counters (3 words, zero between launches)

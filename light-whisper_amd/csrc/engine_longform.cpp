@@ -221,7 +221,14 @@ int longform_main(const std::string& engine, const std::string& gguf, int argc, 
                 throw Fail("injected failure (QASR_FAIL_STAGE=init): this rank never joins the communicator");
             {
                 StdoutToStderr quiet;   // RCCL's version banner must not reach the JSON channel
-                ck(qasr_dist_init(id, rank, world, local, &comm), "communicator");
+                const int irc = qasr_dist_init(id, rank, world, local, &comm);
+                if (irc != QASR_OK) {
+                    // a rank that never joined (deadline, QASR_DIST_TIMEOUT_MS): the init thread is abandoned inside
+                    // RCCL, so leave without runtime teardown (include/qasr.h qasr_dist_init_deadline)
+                    fprintf(stderr, "engine longform (rank %d): communicator: %s\n", rank, qasr_last_error());
+                    fflush(stderr);
+                    _exit(1);
+                }
             }
             if (rank == 0) {   // every rank has joined: the file has been read
                 remove(path.c_str());

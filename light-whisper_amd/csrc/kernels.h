@@ -211,6 +211,7 @@ struct DecState {
 };
 void dec_plan(const DecState& st, int M_max, int* ids, int* pos, int* slot, int* kvs, int* kvl, int* row_utt,
               hipStream_t s);
+void force_tokens(const DecState& st, int M_max, const int* row_utt, const int* ids, int ld, int* tok, hipStream_t s);
 void dec_accept(const DecState& st, int M_max, const int* row_utt, const int* tok, hipStream_t s);
 void copy_kv_prefix(__half* kc, __half* vc, int layers, int64_t kv_slots, int kvd, int64_t src, int P0,
                     const int* bases, int count, hipStream_t s);

@@ -78,6 +78,24 @@ __global__ void k_dec_accept(DecState st, int M_max, const int* __restrict__ row
     if (still) atomicAdd(&st.counters[1], 1);
 }
 
+// batched teacher forcing (Session::forced_logits_batch_host): row i's accepted token becomes the forced id of its
+// utterance at its next position (ids [U][ld], -1 keeps the argmax); runs between the argmax and k_dec_accept
+__global__ void k_force_tokens(DecState st, int M_max, const int* __restrict__ row_utt, const int* __restrict__ ids,
+                               int ld, int* __restrict__ tok) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= M_max || i >= st.counters[0]) return;
+    const int u = row_utt[i];
+    if (u < 0) return;
+    const int g = st.gen[u];
+    const int f = g < ld ? ids[(size_t)u * ld + g] : -1;
+    if (f >= 0) tok[i] = f;
+}
+
+void force_tokens(const DecState& st, int M_max, const int* row_utt, const int* ids, int ld, int* tok, hipStream_t s) {
+    if (M_max <= 0) return;
+    k_force_tokens<<<cdiv(M_max, 256), 256, 0, s>>>(st, M_max, row_utt, ids, ld, tok);
+}
+
 void dec_plan(const DecState& st, int M_max, int* ids, int* pos, int* slot, int* kvs, int* kvl, int* row_utt,
               hipStream_t s) {
     k_dec_plan<<<1, 1024, 0, s>>>(st, M_max, ids, pos, slot, kvs, kvl, row_utt);

@@ -1169,13 +1169,23 @@ __global__ __launch_bounds__(256 * KG, KG == 1 ? 2 : 1) void k_gemm_q8d(const in
         constexpr bool OP = TJ <= 4 && KG == 1 && (BK == 64 || TI == 1);
         float sb[KBG][TJ], sa[KBG][TI][4], sal[KBG][TI], sbl[KBG];
         long a[KBG][TI], b[KBG][TJ];
+        // WS4 + OP: lane l's column holds the stage's 4 block scales as 8 contiguous bytes ([BN][4] f16); ONE
+        // ds_read_b64 per stage takes all four (64 lanes × 8 B = two conflict-free 32-lane halves), where a 16-bit
+        // read per block at an 8-byte lane stride was 2-way bank-conflicted (round 5 PMC: 0.49 conflict cycles per
+        // LDS instruction in the decode class, 0.003 before the WS4 layout)
+        uint2 sb4w = {0u, 0u};
+        const int kb0 = kg * (KB / KG);
         // per-fragment LDS reads of block kb into slot sl: the B scale(s), row fragment i (A bytes + scales), column
         // fragment j (B bytes) — QASR_PIN issues each one right after the previous block's last use of its registers
         auto load_bscale = [&](int sl, int kb) {
             if constexpr (WS4) {   // LDS [BN][4] f16 and [BM][4] f32
                 if constexpr (OP) {
-                    const int cl = min(lane, 16 * TJ - 1);
-                    sbl[sl] = __half2float(*(const __half*)(st + OSB + 8 * (bcol + cl) + 2 * kb));
+                    if (kb == kb0) {   // the stage's first block of this K group: all four scales at once
+                        const int cl = min(lane, 16 * TJ - 1);
+                        sb4w = *(const uint2*)(st + OSB + 8 * (bcol + cl));
+                    }
+                    const uint32_t w2 = (kb & 2) ? sb4w.y : sb4w.x;
+                    sbl[sl] = __half2float(__ushort_as_half((unsigned short)((kb & 1) ? w2 >> 16 : w2 & 0xffff)));
                 } else {
 #pragma unroll
                     for (int j = 0; j < TJ; j++)
@@ -1237,7 +1247,6 @@ __global__ __launch_bounds__(256 * KG, KG == 1 ? 2 : 1) void k_gemm_q8d(const in
         // (the 128×128 prefill tile runs LAG 2: one result ring slot fewer keeps it at ≤ 168 VGPRs, 3 waves per SIMD)
         constexpr int LAG = (QASR_PIN != 0 && NF >= 16) ? 2 : 3, NQ = (KB / KG) * NF;
         constexpr int NPR = LAG / TJ + 2;   // outer-product results live at once (ring)
-        const int kb0 = kg * (KB / KG);
         v4i c[LAG + 1];
         v16f prod[NPR];
         // QASR_PIN (default): the instruction order is pinned per MFMA slot — [OP MFMA] MFMA q, the next block's

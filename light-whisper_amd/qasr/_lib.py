@@ -89,6 +89,7 @@ SIGNATURES = {
     "qasr_session_close": (None, [P]),
     "qasr_session_forced_logits": (C.c_int, [P, P, SZ, P, I32, P]),
     "qasr_session_forced_logits_verify": (C.c_int, [P, P, SZ, P, I32, P]),
+    "qasr_session_forced_logits_batch": (C.c_int, [P, P, P, I32, P, I32, P, I32, P]),
     "qasr_session_mel": (C.c_int, [P, P, SZ, P, C.POINTER(I32), C.POINTER(I32)]),
     "qasr_session_encode": (C.c_int, [P, P, I32, I32, P, P, C.POINTER(I32)]),
     "qasr_session_prefill_logits": (C.c_int, [P, P, I32, P]),

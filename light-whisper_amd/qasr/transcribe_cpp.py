@@ -254,6 +254,22 @@ class Session:
                  out.ctypes.data_as(C.c_void_p)))
         return out
 
+    def forced_logits_batch(self, audios, forced, want) -> np.ndarray:
+        """teacher forcing through the batched path (qasr_session_forced_logits_batch): audios[u] fed forced[u]
+        ([count][n] ids); logits of the utterances in `want`, [len(want)][n + 1][vocab]"""
+        arrs = [_f32(a) for a in audios]
+        n = len(arrs)
+        f = np.ascontiguousarray(forced, dtype=np.int32).reshape(n, -1)
+        w = np.ascontiguousarray(want, dtype=np.int32)
+        v = self.model.hparams["vocab"]
+        out = np.empty((w.size, f.shape[1] + 1, v), np.float32)
+        ptrs = (C.c_void_p * n)(*[a.ctypes.data_as(C.c_void_p).value for a in arrs])
+        lens = (C.c_size_t * n)(*[a.size for a in arrs])
+        check(_lib.load().qasr_session_forced_logits_batch(self._h, ptrs, lens, n, f.ctypes.data_as(C.c_void_p),
+                                                           f.shape[1], w.ctypes.data_as(C.c_void_p), w.size,
+                                                           out.ctypes.data_as(C.c_void_p)))
+        return out
+
     def mel(self, audio):
         a = _f32(audio)
         n = max(a.size, 8000)

@@ -64,8 +64,8 @@ def test_native_rccl_world1(torch_dev, golden):
 
 def test_native_init_deadline_when_a_rank_never_joins():
     """qasr_dist_init_deadline: rank 0 of a world-2 communicator whose rank 1 never calls init
-    returns QASR_E_BACKEND at the deadline (non-blocking ncclCommInitRankConfig polled through ncclCommGetAsyncError,
-    then ncclCommAbort) instead of blocking forever.  Run in a child process, so even a hang could not take the
+    returns QASR_E_BACKEND at the deadline (the init on a helper thread the caller stops waiting for) instead of
+    blocking forever.  Run in a child process, so even a hang could not take the
     test runner with it."""
     import subprocess
     import sys
@@ -73,7 +73,7 @@ def test_native_init_deadline_when_a_rank_never_joins():
     import time
 
     code = textwrap.dedent("""
-        import sys, time
+        import os, sys, time
         sys.path.insert(0, %r)
         from qasr.dist import NativeComm
         uid = NativeComm.unique_id()
@@ -81,13 +81,13 @@ def test_native_init_deadline_when_a_rank_never_joins():
         try:
             NativeComm(0, 2, 0, uid=uid, timeout_ms=4000)
         except RuntimeError as e:
-            print("ERR", round(time.monotonic() - t0, 2), str(e).replace(chr(10), " ")[:300])
-            sys.exit(0)
-        print("JOINED")
-        sys.exit(3)
+            print("ERR", round(time.monotonic() - t0, 2), str(e).replace(chr(10), " ")[:300], flush=True)
+            os._exit(0)   # the abandoned init thread is still inside RCCL: leave without runtime teardown (qasr.h)
+        print("JOINED", flush=True)
+        os._exit(3)
     """ % os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "light-whisper_amd"))
     t0 = time.monotonic()
-    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=150)
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=90)
     took = time.monotonic() - t0
     assert out.returncode == 0, (out.returncode, out.stdout[-500:], out.stderr[-2000:])
     line = [x for x in out.stdout.splitlines() if x.startswith("ERR")][0]

@@ -490,3 +490,109 @@ def test_real_fused_norm_and_xr_bit_identical(pair, monkeypatch):
         s.set_batch_invariant(False)
     assert new == old
     assert new[:6] == singles
+
+
+def test_real_c5_mxfp8_longform_against_q8(pair):
+    """C5 (BASELINE configs[4]: 1.7B with MXFP8 MFMA weights, long-form) at its shape: a 300 s recording (seed 2, the
+    C5 generator) through the long-form pipeline (qasr.longform: FireRedVAD probabilities, the reference's segmenter,
+    one batch of every speech segment), in MXFP8 precision against the Q8 path.  The batch's decode steps run 5–64
+    rows, so the block-scaled MFMA GEMMs of the BATCHED decode are exercised (1–4-row steps keep the Q8 GEMVs).
+      * VAD probabilities and segments bit-identical between the two runs (precision does not touch the VAD);
+      * every segment's first token (the prompt's argmax, batched prefill) equal wherever the Q8 row is clear, and
+        its prompt logits within the MXFP8 tolerance;
+      * teacher-forced logits through the batched decode (qasr_session_forced_logits_batch: every segment fed the Q8
+        batch's own token stream) at 3 segments — the longest, the median, the shortest — within the tolerance, argmax
+        equal on clear rows;
+      * the free-running token streams' mismatch count recorded (MXFP8 is tolerance parity: the reference has no fp8
+        path).
+    Tolerance: TOL = 0.35 of the row's max |logit| — e4m3 element rounding of every weight and activation over 28
+    layers of the synthetic (untrained) model; observed on MI355X (r6): 0.227 on the prompt rows of these segments
+    (2.5–8 s of speech, 100–200 prompt rows: the 2.5 s clip of test_real_mxfp8_against_q8 sees 8.8e-2); a row is
+    clear when its Q8 top-2 gap exceeds 2·TOL of that span (no error within the tolerance can flip it).  The free-
+    running first-token and stream agreement is recorded, not bounded: MXFP8 is tolerance parity only."""
+    TOL = 0.35
+    from bench import recording
+    from qasr import longform
+    from qasr.firered_vad import FireRedVad
+    from qasr.transcribe_cpp import Model
+
+    arch, _, s, _ = pair
+    if arch != "qwen3-asr-1.7b":
+        pytest.skip("C5 is quoted on the 1.7B model")
+    rec = recording(300.0, seed=2)
+    vad = FireRedVad()
+
+    def pipeline_segments():
+        p = longform.shard_probabilities(vad, rec, 0, 1)
+        return p, longform.segments(p, rec.size)
+
+    p_q8, segs = pipeline_segments()
+    mx = Model.synthetic(arch, seed=SEED)
+    try:
+        mx.set_precision("mxfp8")
+        ms = mx.session(kv_type="f16", n_ctx=4096)
+        p_mx, segs_mx = pipeline_segments()
+        assert np.array_equal(p_q8.view(np.uint32), p_mx.view(np.uint32)) and segs == segs_mx
+        n = len(segs)
+        assert n >= 20, n
+        clips = [rec[a:b] for a, b in segs]
+        q8_tok = [r.tokens for r in s.run_batch(clips, force_tokens_per_s=8)]
+        mx_tok = [r.tokens for r in ms.run_batch(clips, force_tokens_per_s=8)]
+        # prompt logits of every segment (batched prefill), first tokens
+        allw = np.arange(n, dtype=np.int32)
+        empty = np.zeros((n, 0), np.int32)
+        pq = s.forced_logits_batch(clips, empty, allw)[:, 0]
+        pm = ms.forced_logits_batch(clips, empty, allw)[:, 0]
+
+        def row_err(got, ref):
+            return np.abs(got - ref).max(1) / np.abs(ref).max(1)
+
+        def clear_rows(ref, frac=2 * TOL):
+            # a row whose argmax no error within the tolerance can flip: top-2 gap above twice the per-logit bound
+            top2 = np.sort(ref, 1)[:, -2:]
+            return (top2[:, 1] - top2[:, 0]) > frac * np.abs(ref).max(1)
+
+        e_prompt = float(row_err(pm, pq).max())
+        cq = clear_rows(pq)
+        near = clear_rows(pq, 0.005 * 2)   # rows whose Q8 argmax is not a near-tie of the Q8 batch's own order
+        first_mism = [i for i in range(n) if mx_tok[i][0] != q8_tok[i][0]]
+        record(f"real_c5_mxfp8_longform_prompt[{arch}]", segments=n, prompt_logits_rel=e_prompt,
+               first_token_mismatches=len(first_mism), clear_rows=int(cq.sum()),
+               first_token_mismatches_clear=len([i for i in first_mism if cq[i]]))
+        # the tf hook's prompt rows == the batch run's first tokens (same batch, same order; near-ties aside)
+        assert all(q8_tok[i][0] == int(pq[i].argmax()) for i in range(n) if near[i])
+        assert all(mx_tok[i][0] == int(pm[i].argmax()) for i in range(n) if clear_rows(pm, 0.01)[i])
+        assert e_prompt < TOL, e_prompt
+        assert not [i for i in first_mism if cq[i]], first_mism
+        # teacher-forced decode logits through the batched steps
+        lens = np.array([len(t) for t in q8_tok])
+        order = np.argsort(lens, kind="stable")
+        want = np.array([order[-1], order[n // 2], order[0]], np.int32)
+        nf = int(lens.max()) - 1
+        forced = np.array([(t + [t[-1]] * nf)[:nf] for t in q8_tok], np.int32)
+        fq = s.forced_logits_batch(clips, forced, want)
+        fm = ms.forced_logits_batch(clips, forced, want)
+        errs, clear_n, argmax_bad = [], 0, 0
+        for k, u in enumerate(want):
+            rows = len(q8_tok[u])   # the rows past the segment's own stream are padding
+            rq, rm = fq[k, :rows], fm[k, :rows]
+            errs.append(float(row_err(rm, rq).max()))
+            c = clear_rows(rq)
+            clear_n += int(c.sum())
+            argmax_bad += int((rm.argmax(1) != rq.argmax(1))[c].sum())
+            # the hook feeds the Q8 batch's stream: its argmax reproduces that stream (the tf batch steps run other
+            # row buckets than the free run, so near-ties of the GEMM order aside)
+            nt = clear_rows(rq, 0.01)
+            assert all(int(rq[j].argmax()) == q8_tok[u][j] for j in range(rows) if nt[j]), int(u)
+        stream_mism = sum(1 for i in range(n) if mx_tok[i] != q8_tok[i])
+        record(f"real_c5_mxfp8_longform[{arch}]", recording_s=300.0, segments=n,
+               speech_s=round(sum(b - a for a, b in segs) / 16000.0, 1), max_rows=n,
+               prompt_logits_rel=e_prompt, first_token_mismatches=len(first_mism),
+               first_token_clear_rows=int(cq.sum()), tf_segments=[int(u) for u in want],
+               tf_logits_rel=errs, tf_clear_rows=clear_n, tf_argmax_mismatch_clear=argmax_bad,
+               stream_mismatched_segments=stream_mism, tokens=int(lens.sum()))
+        assert max(errs) < TOL, errs
+        assert argmax_bad == 0, argmax_bad
+        ms.close()
+    finally:
+        mx.close()

@@ -283,11 +283,11 @@ def test_engine_longform_rank_never_joins(tmp_path):
     p0 = subprocess.Popen(args, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env={**base, "RANK": "0"})
     p1 = subprocess.run(args, capture_output=True, text=True, env={**base, "RANK": "1"}, timeout=120)
     try:
-        out0, err0 = p0.communicate(timeout=150)
+        out0, err0 = p0.communicate(timeout=90)
     except subprocess.TimeoutExpired:
         p0.kill()
         out0, err0 = p0.communicate()
-        raise AssertionError("rank 0 still blocked 150 s after start: " + err0[-2000:])
+        raise AssertionError("rank 0 still blocked 90 s after start: " + err0[-2000:])
     took = time.monotonic() - t0
     assert p1.returncode == 1 and "injected failure (QASR_FAIL_STAGE=init)" in p1.stderr, p1.stderr[-2000:]
     assert p0.returncode == 1 and out0 == "", (p0.returncode, out0[:200], err0[-2000:])

@@ -19,7 +19,10 @@ import sqlite3
 import sys
 
 CLASSES = [  # (class, kernel-name regex) — first match wins
-    ("gemm_q8_prefill", r"k_gemm_q8d<2, 2, 4, 4|k_gemm_q8d<2, 2, 2, 4, 3, 128, 1>|k_gemm_q8d<2, 2, 4, 4, 2, 128"),
+    # bench.py's ProfScope classes split the Q8 GEMM by row count (prefill / encoder M > 256, decode M <= 256); by name,
+    # M > 256 is the 128x128 K-64 tile (kernels_q8.hip cfg 4) alone — the other big tiles (cfg 8 / 9 / 10, 128x128 /
+    # 64x128 / 64x64 K-128) are the decode steps' vocabulary projections, which the eager step counts as decode
+    ("gemm_q8_prefill", r"k_gemm_q8d<2, 2, 4, 4, 3, 64[,>]"),
     ("gemm_q8_decode", r"k_gemm_q8d<|k_gemm_q8_ks<|k_gemm_q8<"),
     ("gemv_q8", r"k_gemv_q8|k_gemv_wide"),
     ("xr_linear", r"k_xr_linear|k_xr_gu"),

@@ -37,13 +37,13 @@ def main():
     n = collections.Counter()
     ns = collections.Counter()
     for name, t0, t1 in rows(src):
-        k = klass(name)
-        if k is None:
-            continue
+        k = klass(name) or "other"   # every launch lands in a class, so the classes sum to the trace total
         n[k] += 1
         ns[k] += t1 - t0
     res = {k: {"launches": n[k], "launches_per_step": round(n[k] / steps, 1), "ms_per_step": round(ns[k] / steps / 1e6, 3),
                "avg_us": round(ns[k] / n[k] / 1e3, 3)} for k in sorted(n)}
+    tot = sum(ns.values())
+    res["_total"] = {"launches": sum(n.values()), "ms_per_step": round(tot / steps / 1e6, 3)}
     lib = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "light-whisper_amd", "libqasr.so")
     res["_meta"] = {"lib_sha256_16": hashlib.sha256(open(lib, "rb").read()).hexdigest()[:16] if os.path.exists(lib)
                     else None, "steps": steps, "source": os.path.basename(src),
@@ -51,6 +51,12 @@ def main():
     json.dump(res, open(out, "w"), indent=1)
     for k, r in res.items():
         print(k, r)
+    top = collections.Counter()
+    for name, t0, t1 in rows(src):
+        if klass(name) is None:
+            top[name.split("(")[0][:90]] += t1 - t0
+    for name, t in top.most_common(8):   # what "other" holds
+        print(f"  other: {t / steps / 1e6:8.3f} ms/step  {name}")
 
 
 if __name__ == "__main__":
