@@ -237,6 +237,18 @@ QASR_API int qasr_op_gemm_exact_rows(const int8_t* xq, const float* xd, int32_t 
     });
 }
 
+// the xr launches' leaf-split scratch: one process-wide buffer for the op entry points (tests / tools, one stream; every
+// launch leaves its counters zero)
+static const XrSplit& op_xr_split() {
+    static const XrSplit xs = [] {
+        void* mem = nullptr;
+        QASR_HIP(hipMalloc(&mem, xr_split_bytes()));
+        QASR_HIP(hipMemset(mem, 0, xr_split_bytes()));
+        return xr_split_view(mem);
+    }();
+    return xs;
+}
+
 QASR_API int qasr_op_xr_linear(const int8_t* xq, const float* xd, const float* src, const float* nw, float eps,
                                int32_t M, const int8_t* wqs, const void* wsc, int32_t N, int32_t K, float* y,
                                int32_t ldy, int32_t resid, void* stream) {
@@ -247,18 +259,7 @@ QASR_API int qasr_op_xr_linear(const int8_t* xq, const float* xd, const float* s
         W.sc = (__half*)wsc;
         W.N = N;
         W.K = K;
-        // the leaf split's scratch: one process-wide buffer for the op entry points (tests / tools, one stream)
-        static XrSplit xs = [] {
-            XrSplit v;
-            void* mem = nullptr;
-            QASR_HIP(hipMalloc(&mem, xr_split_bytes()));
-            QASR_HIP(hipMemset(mem, 0, xr_split_bytes()));
-            v.part = (float*)mem;
-            v.cnt = (unsigned*)((char*)mem + (size_t)kXrSplitItems * 2 * 2 * 256 * sizeof(float));
-            v.items = kXrSplitItems;
-            return v;
-        }();
-        xr_linear(xq, xd, src, nw, eps, M, W, y, ldy, resid != 0, S(stream), nullptr, &xs);
+        xr_linear(xq, xd, src, nw, eps, M, W, y, ldy, resid != 0, S(stream), nullptr, &op_xr_split());
         launched();
     });
 }

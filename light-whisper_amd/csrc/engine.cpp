@@ -137,9 +137,7 @@ Session::Session(Model* m, int n_ctx) : m_(m), n_ctx_(n_ctx) {
     // the xr launches' leaf split (two workgroups per 16-column fragment): partial trees + arrival counters
     QASR_HIP(hipMalloc(&xr_split_mem_, xr_split_bytes()));
     QASR_HIP(hipMemset(xr_split_mem_, 0, xr_split_bytes()));
-    xr_split_.part = (float*)xr_split_mem_;
-    xr_split_.cnt = (unsigned*)((char*)xr_split_mem_ + (size_t)kXrSplitItems * 2 * 2 * 256 * sizeof(float));
-    xr_split_.items = kXrSplitItems;
+    xr_split_ = xr_split_view(xr_split_mem_);
     const char* nofix = getenv("QASR_NO_FIXUP");
     if (!nofix || atoi(nofix) == 0) {
         fix_floats_ = (size_t)256 * ((widest + 127) / 128 * 128) * kFixSplits;

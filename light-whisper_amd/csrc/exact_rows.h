@@ -126,6 +126,9 @@ __device__ __forceinline__ void exact_frag(const int8_t* __restrict__ X, const f
 // ---- the xr launches' form: weights held in registers (loaded at the workgroup's start), activations from an
 // LDS tile (staged once per phase).  Same lanes, spans, chains and tree as exact_frag: the same bits.
 
+// row stride (floats) of the LDS tile's block scales (exact_frag_lds below)
+__host__ __device__ constexpr int xr_sd_stride(int K) { return K / 32 + 4; }
+
 // one wave's weight spans of a 16-column fragment: spans 4w + j + 16t, i = 4t + j (NS = 4T).  XS = 2 (the leaf split
 // of the per-phase launches): the fragment's 32 leaves are shared by TWO workgroups, half h taking leaves 16h … 16h+15
 // (wave w: leaves 16h + 4w … +3 = O_{4h+w}; spans 8h + 2w + j + 16t, i = 2t + j, NS = 2T); each half's workgroup
@@ -160,7 +163,10 @@ __device__ __forceinline__ void exact_load_w(XWeights<T, XS>& w, const int8_t* _
 }
 
 // sX: the tile's int8 rows (row stride ldx bytes, 16-B aligned, ldx ≡ 16 mod 256 so the 16 rows of a fragment read
-// conflict-free), sXd: its f32 block scales (row stride nb = K/32); rows [0, M) valid (later rows clamped to M − 1)
+// conflict-free), sXd: its f32 block scales (row stride xr_sd_stride(K) = K/32 + 4 floats: the four lane groups of a
+// span's scale read fetch rows 4g + r, which at the unpadded stride (a multiple of 32 floats) sat in one bank — a
+// 4-way conflict on every read, round 6 PMC 2.3–2.8 conflict cycles per LDS instruction in the xr launches; with 4
+// floats of padding the rows start 16 banks apart and 16-B aligned); rows [0, M) valid (later rows clamped to M − 1)
 // XS = 2: this workgroup's half of the leaves (XWeights above); out = H_{2h} + H_{2h+1} of half h
 template <int T, int RF, int XS = 1>
 __device__ __forceinline__ void exact_frag_lds(const XWeights<T, XS>& w, const int8_t* sX, int ldx, const float* sXd,
@@ -169,7 +175,7 @@ __device__ __forceinline__ void exact_frag_lds(const XWeights<T, XS>& w, const i
     constexpr int LW = 8 / XS;   // leaves per wave
     const int lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int fr = lane & 15, g = lane >> 4;
-    constexpr int nb = 32 * T;   // K / 32
+    constexpr int nb = xr_sd_stride(1024 * T);   // K / 32 + 4
     const int8_t* ap[RF];
     const float* dp[RF][4];
 #pragma unroll

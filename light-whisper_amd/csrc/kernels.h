@@ -186,12 +186,14 @@ struct XrNorm {
 // the leaf split's scratch (k_xr_linear XS = 2): two workgroups per 16-column fragment; the second to arrive adds the
 // first's partial tree (write-through, one arrival counter per fragment and row slice, zero between launches)
 struct XrSplit {
-    float* part = nullptr;      // [items][2][RF·256] floats, RF ≤ 2
+    float* part = nullptr;      // [items][kXrSplitPart] floats: [2][RF·256], RF ≤ 2
     unsigned* cnt = nullptr;    // [items]
     int items = 0;
 };
 constexpr int kXrSplitItems = 256;
+constexpr int kXrSplitPart = 2 * 2 * 256;   // floats per item
 size_t xr_split_bytes();        // part + counters for kXrSplitItems items (counters zeroed by the owner)
+XrSplit xr_split_view(void* mem);   // the layout of one xr_split_bytes() allocation
 void xr_linear(const int8_t* xq, const float* xd, const float* src, const float* nw, float eps, int R, const Q8Mat& W,
                float* y, int ldy, bool resid, hipStream_t s, const XrNorm* norm = nullptr,
                const XrSplit* split = nullptr);

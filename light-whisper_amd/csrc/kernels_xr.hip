@@ -34,7 +34,8 @@ __device__ __forceinline__ void stage_tile(const int8_t* X, const float* Xd, int
             }
         }
     }
-    const int nbr = K / QK, t4 = n * nbr / 4;   // float4 chunks of the scales (nbr % 4 == 0)
+    const int nbr = K / QK, t4 = n * nbr / 4, c4 = nbr / 4;   // float4 chunks of the scales (nbr % 4 == 0)
+    const int sds = xr_sd_stride(K);                             // the tile's padded scale row stride
     const uint32_t dbase = (uint32_t)r0 * (uint32_t)nbr * 4u;
     for (int c0 = 0; c0 < t4; c0 += 256 * 4) {
         float4 v[4];
@@ -46,7 +47,10 @@ __device__ __forceinline__ void stage_tile(const int8_t* X, const float* Xd, int
 #pragma unroll
         for (int u = 0; u < 4; u++) {
             const int c = c0 + 256 * u + tid;
-            if (c < t4) *(float4*)(sXd + 4 * c) = v[u];
+            if (c < t4) {
+                const int row = c / c4, col = c - row * c4;
+                *(float4*)(sXd + row * sds + 4 * col) = v[u];
+            }
         }
     }
 }
@@ -64,7 +68,7 @@ __device__ __forceinline__ void norm_tile(const float* x, int H, float eps, int 
 #pragma unroll
         for (int u = 0; u < 8; u++)
             if (r0 + u < R)
-                rms_row_q8_finish<KC, false>(v[u], gw, H, eps, sX + (r0 + u) * ldx, sXd + (r0 + u) * (H / QK), part[u],
+                rms_row_q8_finish<KC, false>(v[u], gw, H, eps, sX + (r0 + u) * ldx, sXd + (r0 + u) * xr_sd_stride(H), part[u],
                                              true, tid);
         __syncthreads();   // part reuse
     }
@@ -151,7 +155,7 @@ __global__ __launch_bounds__(256, 1) void k_xr_linear(const int8_t* X, const flo
                                                       const __half* Ws, int N, float* y, int ldy, XrNorm nm,
                                                       XrSplit xs) {
     constexpr int K = 1024 * T, LX = K + 16;
-    __shared__ __align__(16) int8_t tile[16 * RF * LX + 16 * RF * (K / QK) * 4];
+    __shared__ __align__(16) int8_t tile[16 * RF * LX + 16 * RF * xr_sd_stride(K) * 4];
     __shared__ float hx[4][RF][4][64];
     __shared__ float part[8][4];
     __shared__ unsigned s_prev;
@@ -174,7 +178,7 @@ __global__ __launch_bounds__(256, 1) void k_xr_linear(const int8_t* X, const flo
         // loads and adds the two in half order
         const int lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
         const int item = frag * (int)gridDim.y + (int)blockIdx.y;
-        float* pp = xs.part + (size_t)item * 2 * (RF * 256);
+        float* pp = xs.part + (size_t)item * kXrSplitPart;
         if (wv < RF) {
 #pragma unroll
             for (int r = 0; r < 4; r++) wt_stf(pp, (uint32_t)(((half * RF + wv) * 4 + r) * 64 + lane) * 4u, v[r]);
@@ -207,7 +211,7 @@ __global__ __launch_bounds__(256, 1) void k_xr_gu(const int8_t* X, const float* 
                                                   float eps, int R, const int8_t* Wq, const __half* Ws, int F,
                                                   int8_t* hq, float* hd) {
     constexpr int K = 1024 * T, LX = K + 16;
-    __shared__ __align__(16) int8_t tile[16 * RF * LX + 16 * RF * (K / QK) * 4];
+    __shared__ __align__(16) int8_t tile[16 * RF * LX + 16 * RF * xr_sd_stride(K) * 4];
     __shared__ float hx[4][RF][4][64];
     __shared__ float part[8][4];
     __shared__ float gub[16 * RF][64];
@@ -249,7 +253,15 @@ __global__ __launch_bounds__(256, 1) void k_xr_gu(const int8_t* X, const float* 
 
 bool xr_ok(int R, int K) { return R >= 1 && R <= 32 && (K == 1024 || K == 2048 || K == 3072 || K == 6144); }
 
-size_t xr_split_bytes() { return (size_t)kXrSplitItems * (2 * 2 * 256 * sizeof(float) + sizeof(unsigned)); }
+size_t xr_split_bytes() { return (size_t)kXrSplitItems * (kXrSplitPart * sizeof(float) + sizeof(unsigned)); }
+
+XrSplit xr_split_view(void* mem) {
+    XrSplit v;
+    v.part = (float*)mem;
+    v.cnt = (unsigned*)((char*)mem + (size_t)kXrSplitItems * kXrSplitPart * sizeof(float));
+    v.items = kXrSplitItems;
+    return v;
+}
 
 // QASR_XR_SPLIT=0 turns the leaf split off (A/B)
 static bool xr_split_on() {
@@ -279,7 +291,7 @@ void xr_linear(const int8_t* xq, const float* xd, const float* src, const float*
     // 8 rows — there the hand-off's round trip costs more than the halved weight stream saves (profiles/
     // r5_xr_cost_split.log)
     const int slices = two ? 2 : 1, items = W.N / 16 * slices;
-    const size_t lds = (size_t)16 * rf * (W.K + 16) + (size_t)16 * rf * (W.K / QK) * 4 + 8192;
+    const size_t lds = (size_t)16 * rf * (W.K + 16) + (size_t)16 * rf * xr_sd_stride(W.K) * 4 + 8192;
     const int per_cu = (int)std::min<size_t>(2, 160 * 1024 / lds);
     const bool xs2 = split && split->part && split->cnt && !norm && !fold && W.K > 3072 && items <= split->items &&
                      items < 256 * per_cu && 2 * items <= 256 * per_cu && xr_split_on();
@@ -331,15 +343,20 @@ void xr_gu_swiglu(const int8_t* xq, const float* xd, const float* src, const flo
                "xr_gu_swiglu: rows 1-32 (fold: ≤ 8), K 1,024 / 2,048, interleaved gate/up");
     const int F = W.N / 2;
     const dim3 g(F / 32);
+    // (round 6: a leaf split like k_xr_linear's — two workgroups per h block, half the leaves each, the second adding
+    // the first's values — measured slower at every row count: 17.1 / 29.2 / 30.7 against 15.7 / 19.0 / 19.3 µs at
+    // 16 / 24 / 32 rows, profiles/r6h_xr_cost.log: both halves stage the whole activation tile)
+#define XR_GU(TT, RFF, FF) k_xr_gu<TT, RFF, FF><<<g, 256, 0, s>>>(xq, xd, src, nw, eps, R, W.qs, W.sc, F, hq, hd)
     if (W.K == 1024) {
-        if (fold) k_xr_gu<1, 1, true><<<g, 256, 0, s>>>(xq, xd, src, nw, eps, R, W.qs, W.sc, F, hq, hd);
-        else if (R <= 16) k_xr_gu<1, 1, false><<<g, 256, 0, s>>>(xq, xd, src, nw, eps, R, W.qs, W.sc, F, hq, hd);
-        else k_xr_gu<1, 2, false><<<g, 256, 0, s>>>(xq, xd, src, nw, eps, R, W.qs, W.sc, F, hq, hd);
+        if (fold) XR_GU(1, 1, true);
+        else if (R <= 16) XR_GU(1, 1, false);
+        else XR_GU(1, 2, false);
     } else {
-        if (fold) k_xr_gu<2, 1, true><<<g, 256, 0, s>>>(xq, xd, src, nw, eps, R, W.qs, W.sc, F, hq, hd);
-        else if (R <= 16) k_xr_gu<2, 1, false><<<g, 256, 0, s>>>(xq, xd, src, nw, eps, R, W.qs, W.sc, F, hq, hd);
-        else k_xr_gu<2, 2, false><<<g, 256, 0, s>>>(xq, xd, src, nw, eps, R, W.qs, W.sc, F, hq, hd);
+        if (fold) XR_GU(2, 1, true);
+        else if (R <= 16) XR_GU(2, 1, false);
+        else XR_GU(2, 2, false);
     }
+#undef XR_GU
     QASR_HIP(hipGetLastError());
 }
 

@@ -17,7 +17,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "light-whisper_amd"))
 from qasr import _lib  # noqa: E402
 
-SHAPES = [("qkv", 4096, 2048, 0), ("o", 2048, 2048, 1), ("down", 2048, 6144, 1), ("gu", 12288, 2048, 3)]
+SHAPES = [("qkv", 4096, 2048, 0), ("o", 2048, 2048, 1), ("down", 2048, 6144, 1), ("gu", 12288, 2048, 3),
+          ("lmhead", 151936, 2048, 0)]   # the decode steps' vocabulary projection (SHAPES=lmhead)
 MS = [int(x) for x in os.environ.get("MS", "16,32,64,96,128,160,192,224,256").split(",")]
 CFGS = list(range(4, 31)) + list(range(36, 40))   # 32..35 and 40..48 removed in round 5
 SPLITS = [1, 2, 3, 4, 6, 8]
