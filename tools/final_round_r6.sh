@@ -1,9 +1,9 @@
 #!/bin/bash
-# Round-end evidence on the GPU box (repo root), in two phases so each fits one gpurun call:
-#   tools/final_round_r5.sh <tag> a   graph-replayed kernel trace + per-class trace JSON, PMC passes, the default bench
-#   tools/final_round_r5.sh <tag> b   32 / 64-segment shares (+ kernel trace of the 32-segment share), C3 streams, C2
+# Round-end evidence on the GPU box (repo root), in two phases so each fits one gpurun call (round 6: + the C5 line):
+#   tools/final_round_r6.sh <tag> a   graph-replayed kernel trace + per-class trace JSON, PMC passes, the default bench
+#   tools/final_round_r6.sh <tag> b   32 / 64-segment shares (+ kernel trace of the 32-segment share), C3 streams, C2
 set -o pipefail
-tag=${1:-r5}; phase=${2:-a}
+tag=${1:-r6}; phase=${2:-a}
 root=$(pwd)
 out=$root/gpurun_out
 mkdir -p $out
@@ -37,4 +37,6 @@ else
   echo "c3 done" >> $out/${tag}_progress.log
   timeout -k 10 300 python3 -u tools/latency.py > $out/${tag}_latency.jsonl 2> $out/${tag}_latency.err || exit 1
   echo "c2 done" >> $out/${tag}_progress.log
+  timeout -k 10 400 python3 -u bench.py --workload c5 --no-cpu-baseline > $out/${tag}_c5.log 2>&1 || exit 1
+  echo "c5 done" >> $out/${tag}_progress.log
 fi
