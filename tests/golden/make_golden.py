@@ -428,20 +428,20 @@ def make_hf_tiny():
 REAL_SEED = 7   # tests/test_model_real_gpu.py's synthetic-weight seed
 
 
-def make_hf_06b():
+def make_hf_06b(arch="qwen3-asr-0.6b", fname="hf_06b.npz"):
     """the oracle pinned at the real qwen3-asr-0.6b dimensions (18 encoder layers, d 896, 14 heads; 28
     decoder layers, GQA 16/8, head 128, the 151,936-row tied vocabulary).  transformers' qwen3_asr on the oracle's
     seeded synthetic weights (Q8_0 dequantised), 10 s of speech-like audio: the log-mel, the encoder / projector rows
     (a row subset + float64 sums) and the decoder logits of the chat prompt's last 8 rows, stored compactly (top-64
     values and indices per row + float64 checksums).  tests/test_oracle_cpu.py checks the oracle (float mode) against
-    it."""
+    it.  (make_hf_17b: the same at qwen3-asr-1.7b — the benchmarked model — round 6.)"""
     import torch
     from transformers.models.qwen3_asr.feature_extraction_qwen3_asr import Qwen3ASRFeatureExtractor
 
     import oracle
     from bench import speech_like
 
-    c = oracle.arch_config("qwen3-asr-0.6b")
+    c = oracle.arch_config(arch)
     sp = oracle.QWEN_SPECIAL
     model = hf_model(c, oracle.Model(c, seed=REAL_SEED).export(), sp["tok_audio_pad"])
     audio = speech_like(np.random.default_rng(505), 160000)
@@ -469,8 +469,15 @@ def make_hf_06b():
            "ids": np.array(ids, np.int32), "logit_top_idx": top.astype(np.int32),
            "logit_top_val": np.take_along_axis(logits, top, 1),
            "logit_sum": logits.astype(np.float64).sum(1), "logit_abs_sum": np.abs(logits.astype(np.float64)).sum(1)}
-    np.savez_compressed(os.path.join(HERE, "hf_06b.npz"), **out)
-    print("hf_06b.npz", {k: v.shape for k, v in out.items()})
+    np.savez_compressed(os.path.join(HERE, fname), **out)
+    print(fname, {k: v.shape for k, v in out.items()})
+
+
+def make_hf_17b():
+    """the oracle pinned at the real qwen3-asr-1.7b dimensions (24 encoder layers of d 1,024 / 16 heads; 28 decoder
+    layers of d 2,048, GQA 16/8, FFN 6,144, the tied 151,936-row vocabulary): make_hf_06b's fixture for the model C4
+    and C5 are quoted on"""
+    make_hf_06b("qwen3-asr-1.7b", "hf_17b.npz")
 
 
 # ---------------------------------------------------------------------------------------------- BPE encode

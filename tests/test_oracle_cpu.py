@@ -135,17 +135,19 @@ def test_q8_roundtrip_and_block_dots():
     assert q.shape == (4, 8 * 34)
 
 
-def test_oracle_matches_transformers_at_06b_dims():
+@pytest.mark.parametrize("arch,fixture", [("qwen3-asr-0.6b", "hf_06b.npz"), ("qwen3-asr-1.7b", "hf_17b.npz")])
+def test_oracle_matches_transformers_at_real_dims(arch, fixture):
     """the oracle pinned at the real qwen3-asr-0.6b dimensions (18 encoder layers of d 896 / 14 heads
     with 104-token windows; 28 decoder layers, GQA 16/8, the 151,936-row tied vocabulary) against transformers'
     qwen3_asr on the same seeded synthetic weights (tests/golden/hf_06b.npz, make_golden.py make_hf_06b): log-mel,
     encoder / projector rows and float64 row sums, and the chat prompt's last 8 logit rows (top-64 entries + float64
     sums).  Oracle in float mode (dequantised weights, f32 activations: HF's own arithmetic, f32 summation order
-    aside)."""
+    aside).  Round 6: the same at qwen3-asr-1.7b (24 encoder layers of d 1,024 / 16 heads, decoder d 2,048 / FFN 6,144:
+    tests/golden/hf_17b.npz, make_hf_17b) — the model C4 / C5 are quoted on."""
     import os
 
-    hf = np.load(os.path.join(os.path.dirname(__file__), "golden", "hf_06b.npz"))
-    cfg = oracle.arch_config("qwen3-asr-0.6b")
+    hf = np.load(os.path.join(os.path.dirname(__file__), "golden", fixture))
+    cfg = oracle.arch_config(arch)
     oracle.set_mode(engine=False)
     try:
         m = oracle.Model(cfg, seed=7)
@@ -153,7 +155,7 @@ def test_oracle_matches_transformers_at_06b_dims():
         assert tv == int(hf["t_valid"]) == 1000
         assert np.abs(mel - hf["mel"]).max() < 1e-4
         proj, enc = m.encode(hf["mel"], tv, want_enc=True)
-        assert proj.shape == (130, 1024) and enc.shape == (130, 896)
+        assert proj.shape == (130, cfg["proj_out"]) and enc.shape == (130, cfg["enc_d"])
         rows = hf["enc_rows"]
         e_enc = np.abs(enc[rows] - hf["enc_sel"]).max() / np.abs(hf["enc_sel"]).max()
         e_proj = np.abs(proj[rows] - hf["proj_sel"]).max() / np.abs(hf["proj_sel"]).max()
@@ -168,7 +170,7 @@ def test_oracle_matches_transformers_at_06b_dims():
         span = np.abs(top_v).max()
         e_lg = np.abs(np.take_along_axis(lg, top_i, 1) - top_v).max() / span
         e_lsum = np.abs(lg.astype(np.float64).sum(1) - hf["logit_sum"]).max() / np.abs(hf["logit_abs_sum"]).max()
-        print(f"0.6B dims vs HF: enc {e_enc:.2e} proj {e_proj:.2e} proj-sum {e_sum:.2e} logits {e_lg:.2e} "
+        print(f"{arch} dims vs HF: enc {e_enc:.2e} proj {e_proj:.2e} proj-sum {e_sum:.2e} logits {e_lg:.2e} "
               f"logit-sum {e_lsum:.2e}")
         # observed (r3): enc 6.9e-7, proj 7.8e-7, proj row sums 1.7e-5, logits 2.3e-7 of the span, logit sums 1.2e-8
         # (f32 summation order through 18 + 28 layers); bounds ≈ 10x
