@@ -604,3 +604,32 @@ def test_concurrent_sessions_match_sequential(torch_dev, golden):
     finally:
         _lib.check(_lib.load().qasr_set_deterministic(1))   # the default
         m.close()
+
+
+def test_forced_logits_batch_hook(gpu, golden):
+    """qasr_session_forced_logits_batch (the C5 test's teacher forcing through the batched path) is the batch's own
+    arithmetic with the argmax replaced: (1) one utterance through it == Session.forced_logits (one decode step per
+    token) bit for bit; (2) with batch invariance on, a batch of 6 utterances (decode steps of 6 rows: the exact-row
+    linears, the fixed-chunk attention, the exact vocabulary projection) gives every utterance the bits of its own
+    single-utterance forced logits — prompt row and every forced step — and the prompt-only call (n_forced = 0) the
+    same first rows"""
+    from bench import speech_like
+
+    _, s = gpu
+    clips = [golden[f"{t}__audio"] for t in ("a", "b", "c")]
+    clips += [speech_like(np.random.default_rng(70 + i), int(16000 * (1.2 + 0.7 * i))) for i in range(3)]
+    forced = np.array([[5 + 13 * u + 97 * j for j in range(7)] for u in range(len(clips))], np.int32)
+    one = s.forced_logits(clips[1], forced[1])
+    tf1 = s.forced_logits_batch([clips[1]], forced[1:2], [0])[0]
+    assert tf1.shape == one.shape and np.array_equal(tf1, one)
+    singles = [s.forced_logits(c, f) for c, f in zip(clips, forced)]
+    s.set_batch_invariant(True)
+    try:
+        got = s.forced_logits_batch(clips, forced, list(range(len(clips))))
+        first = s.forced_logits_batch(clips, np.zeros((len(clips), 0), np.int32), [5, 0, 3])
+    finally:
+        s.set_batch_invariant(False)
+    for u in range(len(clips)):
+        assert np.array_equal(got[u], singles[u]), (u, float(np.abs(got[u] - singles[u]).max()))
+    for k, u in enumerate([5, 0, 3]):
+        assert np.array_equal(first[k, 0], singles[u][0]), u
