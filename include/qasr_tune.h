@@ -41,6 +41,11 @@ QASR_API int qasr_op_register_stage_scales(const void* wsc, int32_t N, int32_t K
 QASR_API int qasr_op_xr_linear(const int8_t* xq, const float* xd, const float* src, const float* nw, float eps,
                                int32_t M, const int8_t* wqs, const void* wsc, int32_t N, int32_t K, float* y,
                                int32_t ldy, int32_t resid, void* stream);
+/* the vocabulary projection of 1–16 rows with the exact-row arithmetic (each row the 1-row GEMV's bits): a grid sized
+   by the occupancy query staging the rows once per workgroup and walking the 16-column fragments (kernels_xr.hip
+   k_xr_vocab) */
+QASR_API int qasr_op_xr_vocab(const int8_t* xq, const float* xd, int32_t M, const int8_t* wqs, const void* wsc,
+                             int32_t N, int32_t K, float* y, int32_t ldy, void* stream);
 QASR_API int qasr_op_xr_gu_swiglu(const int8_t* xq, const float* xd, const float* src, const float* nw, float eps,
                                   int32_t M, const int8_t* wqs, const void* wsc, int32_t N, int32_t K, int8_t* hq,
                                   float* hd, void* stream);

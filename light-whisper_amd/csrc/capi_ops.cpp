@@ -264,6 +264,20 @@ QASR_API int qasr_op_xr_linear(const int8_t* xq, const float* xd, const float* s
     });
 }
 
+QASR_API int qasr_op_xr_vocab(const int8_t* xq, const float* xd, int32_t M, const int8_t* wqs, const void* wsc,
+                             int32_t N, int32_t K, float* y, int32_t ldy, void* stream) {
+    return guard([&] {
+        QASR_CHECK(xq && xd && y && N > 0 && ldy >= N, QASR_E_INVALID, "xr_vocab: bad arguments");
+        Q8Mat W;
+        W.qs = (int8_t*)wqs;
+        W.sc = (__half*)wsc;
+        W.N = N;
+        W.K = K;
+        xr_vocab(xq, xd, M, W, y, ldy, S(stream));
+        launched();
+    });
+}
+
 QASR_API int qasr_op_xr_gu_swiglu(const int8_t* xq, const float* xd, const float* src, const float* nw, float eps,
                                   int32_t M, const int8_t* wqs, const void* wsc, int32_t N, int32_t K, int8_t* hq,
                                   float* hd, void* stream) {

@@ -665,7 +665,14 @@ void Session::lm_head_rows(const float* x, int rows, int ldx, float* logits, boo
     mx_ws(rows, h.txt_h);
     // ≤ 4 rows (1-row decode steps) and exact rows (verify passes): the weight-streaming GEMV, one per-row arithmetic
     // for any row count (k_gemv_wide's row groups); more rows: the MFMA GEMM
-    if (exact && rows >= exact_mfma_rows() && gemm_exact_rows_ok(rows, m_->lm_head))
+    // round 6: 5–16 rows — the N = 8 share's later decode steps, short draft verify passes, a small batch's first
+    // tokens — through k_xr_vocab (the 1-row GEMV's bits per row, in default and exact modes alike: 72–74 against the
+    // table's 79–86 µs, profiles/r6n_lmhead_cost.log); QASR_XR_VOCAB=0 restores the table GEMM / exact kernel
+    const bool xv = rows > kGemvRows && !m_->mx() && xr_vocab_ok(rows, h.txt_h, h.vocab) &&
+                    !(getenv("QASR_XR_VOCAB") && atoi(getenv("QASR_XR_VOCAB")) == 0);
+    if (xv)
+        xr_vocab(xq, xd, rows, m_->lm_head, logits, h.vocab, st_);
+    else if (exact && rows >= exact_mfma_rows() && gemm_exact_rows_ok(rows, m_->lm_head))
         gemm_exact_rows(xq, xd, rows, m_->lm_head, nullptr, logits, h.vocab, EPI_STORE, st_);
     else if ((rows <= kGemvRows || exact) && gemv_fused_ok(GV_NONE, rows, h.txt_h))
         gemv_fused(GV_NONE, xq, xd, nullptr, 0, nullptr, 0.f, rows, m_->lm_head, nullptr, logits, h.vocab, EPI_STORE,
@@ -1145,9 +1152,10 @@ void Session::run_batch(const float* dpcm, const std::vector<int64_t>& off, cons
     }
     // captured step graphs hold scratch, KV and weight pointers: any reallocation or precision change retires them;
     // so does a switch of the per-call launch-path variables (QASR_NO_XR / QASR_XR_NORM, read in decoder_layers)
-    const uint64_t launch_path = (getenv("QASR_NO_XR") ? 1 : 0) + (getenv("QASR_XR_NORM") ? 2 : 0);
+    const uint64_t launch_path = (getenv("QASR_NO_XR") ? 1 : 0) + (getenv("QASR_XR_NORM") ? 2 : 0) +
+                                 (getenv("QASR_XR_VOCAB") && atoi(getenv("QASR_XR_VOCAB")) == 0 ? 4 : 0);
     const uint64_t key[5] = {sc_.epoch, kv_epoch_, m_->precision_gen, deterministic_gen(),
-                             attn_epoch_ * 16 + launch_path * 4 + (batch_inv_ ? 1 : 0)};
+                             attn_epoch_ * 64 + launch_path * 4 + (batch_inv_ ? 1 : 0)};
     if (memcmp(key, graph_key_, sizeof key) != 0) {
         for (auto& g : graphs_) (void)hipGraphExecDestroy(g.second);
         graphs_.clear();

@@ -14,6 +14,10 @@
 // on clamped inputs and must not be stored by the caller.
 #pragma once
 #include "kernels.h"
+
+#ifndef QASR_XR_FENCE
+#define QASR_XR_FENCE 2
+#endif
 #include "wt.h"
 
 namespace qasr {
@@ -195,9 +199,9 @@ __device__ __forceinline__ void exact_frag_lds(const XWeights<T, XS>& w, const i
     const xr_v4i zero = {0, 0, 0, 0};
 #pragma unroll
     for (int i = 0; i < 4 * T / XS; i++) {
-        // a scheduling fence every two spans: unfenced, the scheduler hoisted every span's LDS reads (and the weights
-        // of the next fragment) and spilled at 512 registers
-        if (i % 2 == 0) __builtin_amdgcn_sched_barrier(0);
+        // a scheduling fence every QASR_XR_FENCE spans (default 2): unfenced, the scheduler hoisted every span's LDS
+        // reads (and the weights of the next fragment) and spilled at 512 registers
+        if (i % QASR_XR_FENCE == 0) __builtin_amdgcn_sched_barrier(0);
         const int j = i & (4 / XS - 1), s = xr_span<XS>(i, wv, half);
         xr_v4i aq[RF];
         float2 dx[RF][4];

@@ -174,6 +174,10 @@ void attention(const __half* Q, int ldq, const __half* K, const __half* V, int l
 // to gemm_exact_rows / the 1-row GEMVs.  src != nullptr (≤ 8 rows, K ≤ 2,048): the input rows are RMSNorm(src)·nw
 // quantised inside the launch (rmsnorm_q8's arithmetic) instead of xq / xd.
 bool xr_ok(int R, int K);
+// the vocabulary projection of 1–16 rows (K 1,024 / 2,048) with the exact-row arithmetic (the 1-row GEMV's bits per
+// row): a grid of every resident workgroup, each staging the rows once and walking the 16-column fragments
+bool xr_vocab_ok(int R, int K, int N);
+void xr_vocab(const int8_t* xq, const float* xd, int R, const Q8Mat& W, float* y, int ldy, hipStream_t s);
 // norm (residual launches of whole rows, N = H ∈ {1,024, 2,048}): RMSNorm(y)·w → Q8 rows q / d inside the launch
 // (rmsnorm_q8's arithmetic, by the last workgroups to finish); cnt: 3 words, zero between launches
 struct XrNorm {

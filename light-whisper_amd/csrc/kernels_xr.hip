@@ -4,6 +4,8 @@
 //
 // (Round 5 also built the whole ≤ 32-row decoder stack as ONE persistent launch over these bodies; bit-identical but
 // 0.56× the launch chain — DESIGN §10 keeps its measurements — so round 6 removed it from libqasr.)
+#include <algorithm>
+
 #include "exact_rows.h"
 #include "kernels.h"
 #include "rowops.h"
@@ -249,6 +251,84 @@ __global__ __launch_bounds__(256, 1) void k_xr_gu(const int8_t* X, const float* 
         ((int32_t*)(hq + (size_t)m * F + 32 * it))[w4] = ((const int32_t*)hqb[m])[w4];
     }
     if (tid < R) hd[(size_t)tid * (F / QK) + it] = hdb[tid];
+}
+
+// The vocabulary projection of a 5–16-row decode step (N 151,936 at both sizes) with the exact-row arithmetic: a
+// workgroup stages the rows' Q8 activations into LDS ONCE and then walks fragments f, f + G, f + 2G, … (G = the grid,
+// every workgroup resident), the next fragment's weight spans loaded into the other register set while this one's
+// exact_frag runs — one launch streams the 155 MB matrix with every CU busy, where one launch of a workgroup per
+// 16-column fragment re-staged the activation tile 9,496 times (k_gemm_q8_exact 97–111 µs at 5–16 rows) and the table
+// GEMM took 79–86 µs; this: 72–74 µs, the 1-row GEMV's bits per row (profiles/r6n_lmhead_cost.log).  17–32 rows stay on
+// the table / exact kernels: the exact fragment is latency-bound per workgroup, so two 16-row slices per fragment
+// took 136–151 µs against the table's 83–93 (a three-deep weight ring changed nothing: it is not the weight stream).
+__device__ __forceinline__ void vocab_store(const float (&v)[4], int R, int n0, int N, float* y, int ldy, int tid) {
+    const int lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    if (wv == 0) {
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const int row = 4 * (lane >> 4) + r, col = n0 + (lane & 15);
+            if (row < R && col < N) y[(size_t)row * ldy + col] = v[r];
+        }
+    }
+}
+
+template <int T>
+__global__ __launch_bounds__(256) void k_xr_vocab(const int8_t* X, const float* Xd, int R, const int8_t* Wq,
+                                                  const __half* Ws, int N, float* y, int ldy) {
+    constexpr int K = 1024 * T, LX = K + 16;
+    __shared__ __align__(16) int8_t tile[16 * LX + 16 * xr_sd_stride(K) * 4];
+    __shared__ float hx[4][1][4][64];
+    const int tid = threadIdx.x, nfrag = N / 16, G = (int)gridDim.x;
+    float* sXd = (float*)(tile + 16 * LX);
+    XWeights<T> w0, w1;   // alternated by unrolling (a runtime-indexed pair would go to scratch)
+    int f = blockIdx.x;
+    if (f < nfrag) exact_load_w<T>(w0, Wq, Ws, N, K, 16 * f, tid);
+    stage_tile(X, Xd, K, 0, R, tile, LX, sXd, tid);
+    __syncthreads();
+    float v[4];
+    while (f < nfrag) {
+        int fn = f + G;
+        if (fn < nfrag) exact_load_w<T>(w1, Wq, Ws, N, K, 16 * fn, tid);
+        exact_frag_lds<T, 1>(w0, tile, LX, sXd, R, hx, v, tid);
+        vocab_store(v, R, 16 * f, N, y, ldy, tid);
+        __syncthreads();   // hx is reused by the next fragment's exchange
+        f = fn;
+        if (f >= nfrag) break;
+        fn = f + G;
+        if (fn < nfrag) exact_load_w<T>(w0, Wq, Ws, N, K, 16 * fn, tid);
+        exact_frag_lds<T, 1>(w1, tile, LX, sXd, R, hx, v, tid);
+        vocab_store(v, R, 16 * f, N, y, ldy, tid);
+        __syncthreads();
+        f = fn;
+    }
+}
+
+bool xr_vocab_ok(int R, int K, int N) { return R >= 1 && R <= 16 && (K == 1024 || K == 2048) && N % 16 == 0; }
+
+void xr_vocab(const int8_t* xq, const float* xd, int R, const Q8Mat& W, float* y, int ldy, hipStream_t s) {
+    ProfScope ps(s, "xr_vocab", 2.0 * R * W.N * W.K, (double)W.N * W.K * (1.0 + 2.0 / 32) + (double)R * W.K * 1.125 +
+                                                          (double)R * W.N * 4.0);
+    QASR_CHECK(xr_vocab_ok(R, W.K, W.N) && ldy >= W.N, QASR_E_INVALID,
+               "xr_vocab: rows 1-16, K 1,024 / 2,048, N % 16 == 0");
+    typedef void (*VocabKernel)(const int8_t*, const float*, int, const int8_t*, const __half*, int, float*, int);
+    const VocabKernel k = W.K == 1024 ? k_xr_vocab<1> : k_xr_vocab<2>;
+    // the grid: every workgroup resident at once (the occupancy query per instantiation: a persistent walk with more
+    // workgroups than slots would run its second half after the first)
+    static int cus = 0, occ[2] = {0, 0};
+    const int ki = W.K == 1024 ? 0 : 1;
+    if (!cus) {
+        int dev = 0;
+        QASR_HIP(hipGetDevice(&dev));
+        QASR_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    }
+    if (!occ[ki]) {
+        int per_cu = 0;
+        QASR_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(k), 256, 0));
+        occ[ki] = std::max(1, std::min(per_cu, 2));
+    }
+    const int g = std::min(W.N / 16, occ[ki] * cus);
+    hipLaunchKernelGGL(k, dim3(g), dim3(256), 0, s, xq, xd, R, W.qs, W.sc, W.N, y, ldy);
+    QASR_HIP(hipGetLastError());
 }
 
 bool xr_ok(int R, int K) { return R >= 1 && R <= 32 && (K == 1024 || K == 2048 || K == 3072 || K == 6144); }

@@ -139,6 +139,7 @@ SIGNATURES = {
     "qasr_op_set_gemm_fixup": (C.c_int, [P, C.c_int64, P, I32]),
     "qasr_op_gemm_exact_rows": (C.c_int, [P, P, I32, P, P, I32, I32, P, P, I32, I32, P]),
     "qasr_op_swiglu_q8_interleaved": (C.c_int, [P, I32, I32, P, P, P]),
+    "qasr_op_xr_vocab": (C.c_int, [P, P, I32, P, P, I32, I32, P, I32, P]),
     "qasr_op_gemv_fused": (C.c_int, [I32, P, I32, P, F32, I32, P, P, P, P, I32, I32, P, P, I32, I32, P, P, P]),
     "qasr_op_qk_norm_rope": (C.c_int, [P, I32, I32, I32, I32, P, P, P, P, P, F32, P, P, P, P]),
     "qasr_op_q8_to_mx": (C.c_int, [P, P, I32, C.c_int64, P, P, P]),

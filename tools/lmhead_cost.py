@@ -29,6 +29,7 @@ def main():
         xd = torch.rand(M, K // 32, device=dev) * 0.01
         y = torch.zeros(M, N, device=dev)
         y2 = torch.zeros(M, N, device=dev)
+        y3 = torch.zeros(M, N, device=dev)
         paths = {
             "table": lambda i: lib.qasr_op_linear_q8(p(xq), p(xd), M, p(wq[i]), p(ws[i]), N, K, None, None, p(y), N,
                                                      0, 2, None),
@@ -36,6 +37,7 @@ def main():
                                                                 p(y), N, 0, None),
             "gemv_rows": lambda i: lib.qasr_op_gemv_fused(0, None, 0, None, 0.0, M, p(xq), p(xd), p(wq[i]), p(ws[i]),
                                                           N, K, None, p(y2), N, 0, None, None, None),
+            "xr_vocab": lambda i: lib.qasr_op_xr_vocab(p(xq), p(xd), M, p(wq[i]), p(ws[i]), N, K, p(y3), N, None),
         }
         res = {}
         for name, fn in paths.items():
@@ -51,9 +53,15 @@ def main():
             e1.record()
             torch.cuda.synchronize()
             res[name] = e0.elapsed_time(e1) / n * 1e3
+        # the last call of each path used weight copy (n - 1) % copies: recompute all three on copy 0, then compare
+        for name in ("exact_mfma", "gemv_rows", "xr_vocab"):
+            if res.get(name):
+                _lib.check(paths[name](0))
+        torch.cuda.synchronize()
         same = bool(torch.equal(y, y2)) if res.get("exact_mfma") and res.get("gemv_rows") else None
+        same3 = bool(torch.equal(y3, y2)) if res.get("xr_vocab") and res.get("gemv_rows") else None
         print(f"lm_head M={M:3d} " + "  ".join(f"{k} {v:7.1f}us" if v else f"{k} n/a" for k, v in res.items()) +
-              f"  exact==gemv bits: {same}", flush=True)
+              f"  exact==gemv bits: {same}  xr_vocab==gemv bits: {same3}", flush=True)
 
 
 if __name__ == "__main__":
