@@ -1034,3 +1034,24 @@ def test_xr_gu_swiglu_bit_identical(torch_dev, m, f, k):
         _lib.check(L().qasr_op_xr_gu_swiglu(None, None, ptr(src), ptr(nw), C.c_float(1e-6), m, ptr(wq), ptr(ws), 2 * f,
                                             k, ptr(hq), ptr(hd), None))
         assert np.array_equal(host(hq), host(hq_ref)) and np.array_equal(host(hd), host(hd_ref))
+
+
+@pytest.mark.parametrize("m", [1, 5, 9, 16])
+@pytest.mark.parametrize("n,k", [(8224, 2048), (4112, 1024)])
+def test_xr_vocab_bit_identical_to_gemv_rows(torch_dev, m, n, k):
+    """qasr_op_xr_vocab (the 5–16-row vocabulary projection: resident workgroups walking the 16-column fragments, the
+    next fragment's weights loading meanwhile; N chosen so the fragments do not divide the grid evenly) == the
+    weight-streaming GEMV's row groups (qasr_op_gemv_fused) == gemm_exact_rows, bit for bit"""
+    import torch
+
+    rng = np.random.default_rng(m * 31 + n + k)
+    xq = dev(rng.integers(-127, 128, (m, k), dtype=np.int8), torch_dev)
+    xd = dev((rng.random((m, k // 32)) * 0.02).astype(np.float32), torch_dev)
+    xd[0, 1] = 0.0
+    wq, ws = _q8_weights(torch_dev, n, k, 17)
+    y_gv, y_ex, y = (torch.full((m, n), 7.0, dtype=torch.float32, device=torch_dev) for _ in range(3))
+    _lib.check(L().qasr_op_gemv_fused(0, None, 0, None, C.c_float(0.0), m, ptr(xq), ptr(xd), ptr(wq), ptr(ws), n, k,
+                                      None, ptr(y_gv), n, 0, None, None, None))
+    _lib.check(L().qasr_op_gemm_exact_rows(ptr(xq), ptr(xd), m, ptr(wq), ptr(ws), n, k, None, ptr(y_ex), n, 0, None))
+    _lib.check(L().qasr_op_xr_vocab(ptr(xq), ptr(xd), m, ptr(wq), ptr(ws), n, k, ptr(y), n, None))
+    assert np.array_equal(host(y), host(y_gv)) and np.array_equal(host(y), host(y_ex))
