@@ -9,8 +9,12 @@
 //   * FireRedVAD (firered_vad.py:87-111): Kaldi fbank with a per-wave LDS radix-2 FFT (512 points),
 //     DFSMN dense layers (f32), FSMN memory blocks and the sigmoid head.
 #include <math.h>
+#include <stdlib.h>
+
+#include <utility>
 
 #include "kernels_audio.h"
+#include "lds_dma.h"
 
 namespace qasr {
 
@@ -478,13 +482,190 @@ __global__ __launch_bounds__(CV_NT) void k_conv3x3_gelu(const __half* __restrict
     }
 }
 
+// The same implicit GEMM (same tile 256 × 160, same 8 waves of 64×80, same MFMA order → the same bits) with the
+// operands staged global → LDS by LDS-DMA (`global_load_lds_dwordx4`) into a 6-deep ring of K-32 stages instead of
+// through registers and ds_write_b128 into two K-96 buffers, and the fragments in two register sets.  Round 5 PMC of
+// the register-staged kernel: MFMA busy 0.25 with every LDS and fetch rate far below its ceiling — its per-step
+// phases (gathered loads landing, 78 ds_write_b128 per workgroup at 13 cycles each — MI355X_MICROARCH.md §LDS — then
+// the fragment reads after the barrier, then the MFMAs) ran one after another.
+//  * A stage is K = 32 (one tap, 32 input channels): A [256][64 B] (16 pieces of 16 rows × 4 lanes) and B [160][64 B]
+//    (10 pieces); waves 0–7 take A pieces 2w, 2w+1 and B piece w, waves 0–1 also B pieces 8, 9.
+//  * Padding taps and rows past M load 16 zero bytes from `g_conv_zero` (the DMA cannot mask).
+//  * Stage s+1's fragment reads are issued right after stage s's barrier, before stage s's MFMAs (which use the
+//    other register set), so the LDS reads overlap the matrix work.
+//  * LDS image: 64-B rows, 16-B chunk c of row r at chunk c ^ g((r >> 2) & 3), g = {0, 2, 3, 1}: the four 16-lane
+//    groups of every ds_read_b128 fragment read ({0–3,12–15,20–27}, …) then touch 16 distinct 4-bank units
+//    (checked exhaustively for rows 16k + fr); the DMA's lane-linear 1-KB writes are conflict-free by construction.
+constexpr int CD_BK = 32, CD_ROWB = CD_BK * 2, CD_OB = CV_BM * CD_ROWB, CD_STAGE = (CV_BM + CV_BN) * CD_ROWB;
+constexpr int CD_NBUF = 6;   // 6 × 26 KB = 159,744 B of LDS: one workgroup (8 waves, 2 per SIMD) per CU
+static_assert(CD_NBUF * CD_STAGE <= 163840, "conv ring exceeds LDS");
+__device__ __forceinline__ int cd_swz(int row) { return (0x78 >> (2 * ((row >> 2) & 3))) & 3; }
+__device__ __attribute__((aligned(16))) int4 g_conv_zero[1];
+// f(integral_constant<int, U>) for U = 0 … N-1, each call its own code (compile-time ring slot and register set)
+template <int... U, class F>
+__device__ __forceinline__ void cd_unroll(std::integer_sequence<int, U...>, F&& f) {
+    (f(std::integral_constant<int, U>{}), ...);
+}
+
+__global__ __launch_bounds__(CV_NT) void k_conv3x3_gelu_dma(const __half* __restrict__ in, int n_chunks, int Hi,
+                                                          int Wi, const __half* __restrict__ w,
+                                                          const float* __restrict__ bias, int C,
+                                                          void* __restrict__ out, int out_mode) {
+    __shared__ __attribute__((aligned(1024))) char smem[CD_NBUF * CD_STAGE];
+    const int Ho = (Hi + 1) / 2, Wo = (Wi + 1) / 2;
+    const int M = n_chunks * Ho * Wo;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wr = wave >> 1, wc = wave & 1;
+    const int nct = (C + CV_BN - 1) / CV_BN;
+#if QASR_CONV_XCD
+    const int total = gridDim.x, xcd = blockIdx.x % 8, q = total / 8, r8 = total % 8;
+    const int t = xcd * q + min(xcd, r8) + blockIdx.x / 8;
+#else
+    const int t = blockIdx.x;
+#endif
+    const int n0 = (t % nct) * CV_BN, m0 = (t / nct) * CV_BM;
+    const int steps = 9 * (C / CD_BK);
+    // this lane's DMA sources: A pieces 2w, 2w+1 (row 16p + lane/4, 16-B slot lane%4 ← chunk slot ^ swz(row)); the
+    // chunk's base pointer is 64-bit, the in-chunk offset 32-bit
+    const __half* a_ptr[2];
+    int a_iy0[2], a_ix0[2];
+    unsigned a_in[2];
+#pragma unroll
+    for (int u = 0; u < 2; u++) {
+        const int row = 16 * (2 * wave + u) + (lane >> 2), pos = m0 + row;
+        a_in[u] = pos < M;
+        const int rr = min(pos, M - 1), chn = rr / (Ho * Wo), rem = rr % (Ho * Wo);
+        a_iy0[u] = 2 * (rem / Wo) - 1;
+        a_ix0[u] = 2 * (rem % Wo) - 1;
+        a_ptr[u] = in + (size_t)chn * Hi * Wi * C + 8 * ((lane & 3) ^ cd_swz(row));
+    }
+    const int nbp = wave < 2 ? 2 : 1;   // B pieces of this wave (wave-uniform)
+    const __half* b_src[2];
+#pragma unroll
+    for (int u = 0; u < 2; u++) {
+        const int p = u == 0 ? wave : 8 + wave, row = 16 * p + (lane >> 2);
+        const int co = min(n0 + min(row, CV_BN - 1), C - 1);
+        b_src[u] = w + (size_t)co * 9 * C + 8 * ((lane & 3) ^ cd_swz(row));
+    }
+    const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
+    const uint32_t wa = __builtin_amdgcn_readfirstlane(lds0 + 2048 * wave);
+    const uint32_t wb0 = __builtin_amdgcn_readfirstlane(lds0 + CD_OB + 1024 * wave);
+    const uint32_t wb1 = __builtin_amdgcn_readfirstlane(lds0 + CD_OB + 1024 * (8 + (wave & 1)));
+    // stages are issued strictly in order: (tap, ci0) of the next one advance by counters, no division
+    int it_ky = 0, it_kx = 0, it_tap = 0, it_ci = 0;
+    auto issue = [&](int buf) {
+        const uint32_t so = buf * CD_STAGE;
+#pragma unroll
+        for (int u = 0; u < 2; u++) {
+            const int iy = a_iy0[u] + it_ky, ix = a_ix0[u] + it_kx;
+            const unsigned ok = a_in[u] & ((unsigned)iy < (unsigned)Hi) & ((unsigned)ix < (unsigned)Wi);
+            const __half* src = a_ptr[u] + ((iy * Wi + ix) * C + it_ci);
+            dma_lds16(ok ? (const void*)src : (const void*)g_conv_zero, wa + so + 1024 * u);
+        }
+        const int boff = it_tap * C + it_ci;
+        dma_lds16(b_src[0] + boff, wb0 + so);
+        if (nbp == 2) dma_lds16(b_src[1] + boff, wb1 + so);
+        it_ci += CD_BK;
+        if (it_ci == C) {
+            it_ci = 0;
+            it_tap++;
+            it_kx++;
+            if (it_kx == 3) {
+                it_kx = 0;
+                it_ky++;
+            }
+        }
+    };
+    const int fr = lane & 15, kg = lane >> 4;
+    const int fo = 16 * (kg ^ cd_swz(fr));   // fragment rows are fr + multiples of 16
+    v4f acc[4][CV_TJ];
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+#pragma unroll
+        for (int j = 0; j < CV_TJ; j++) acc[i][j] = (v4f){0.f, 0.f, 0.f, 0.f};
+    // (waves whose rows all lie past M compute on the clamped rows too; their results are not stored)
+    v8h fa[2][4], fb[2][CV_TJ];
+    auto frags = [&](int set, int buf) {
+        const char* st = smem + buf * CD_STAGE;
+#pragma unroll
+        for (int i = 0; i < 4; i++) fa[set][i] = *(const v8h*)(st + (wr * 64 + i * 16 + fr) * CD_ROWB + fo);
+#pragma unroll
+        for (int j = 0; j < CV_TJ; j++)
+            fb[set][j] = *(const v8h*)(st + CD_OB + (wc * 16 * CV_TJ + j * 16 + fr) * CD_ROWB + fo);
+    };
+    auto wait_ahead = [&](int ahead) {   // at most `ahead` of this wave's stages still in flight, LDS reads done
+        if (nbp == 2) wait_stages<4, CD_NBUF>(ahead);
+        else wait_stages<3, CD_NBUF>(ahead);
+    };
+    // the ring's NBUF stages are all issued up front; stage s frees its buffer for stage s + NBUF
+#pragma unroll
+    for (int s = 0; s < CD_NBUF; s++)
+        if (s < steps) issue(s);
+    wait_ahead(min(CD_NBUF - 1, steps - 1));
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    frags(0, 0);
+    // one stage: this wave's DMAs of stage s+1 have landed and its reads of stage s are done (lgkmcnt(0)); the barrier
+    // makes both true for every wave — stage s+1 is readable, stage s's buffer is free for stage s + NBUF.  The next
+    // stage's fragment reads are unconditional (past the last stage they re-read a stale buffer, unused): a
+    // conditional read would make the compiler's own lgkmcnt wait before the MFMAs a full drain.
+    auto stage = [&](int s, auto ubc) {
+        constexpr int ub = decltype(ubc)::value;
+        wait_ahead(max(0, min(CD_NBUF - 2, steps - 2 - s)));
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (s + CD_NBUF < steps) issue(ub % CD_NBUF);
+        frags((ub + 1) & 1, (ub + 1) % CD_NBUF);
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+#pragma unroll
+            for (int j = 0; j < CV_TJ; j++)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[ub & 1][i], fb[ub & 1][j], acc[i][j], 0, 0, 0);
+    };
+    // two ring trips per loop trip, so every unrolled stage's ring slot and register set are constants; the last
+    // partial trip is a guarded copy
+    constexpr int TRIP = 2 * CD_NBUF;
+    const int full = steps / TRIP * TRIP;
+    for (int s0 = 0; s0 < full; s0 += TRIP)
+        cd_unroll(std::make_integer_sequence<int, TRIP>{}, [&](auto u) { stage(s0 + u.value, u); });
+    cd_unroll(std::make_integer_sequence<int, TRIP>{}, [&](auto u) {
+        if (full + u.value < steps) stage(full + u.value, u);
+    });
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+#pragma unroll
+        for (int j = 0; j < CV_TJ; j++) {
+            const int col = n0 + wc * 16 * CV_TJ + j * 16 + fr;
+            if (col >= C) continue;
+            const float bv = bias[col];
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const int row = m0 + wr * 64 + i * 16 + 4 * (lane >> 4) + r;
+                if (row >= M) continue;
+                const float v = gelu_f(acc[i][j][r] + bv);
+                if (out_mode == 0) {
+                    ((__half*)out)[(size_t)row * C + col] = f2h(v);
+                } else {
+                    const int ch = row / (Ho * Wo), rem = row % (Ho * Wo), oy = rem / Wo, ox = rem % Wo;
+                    ((float*)out)[(((size_t)ch * Wo + ox) * C + col) * Ho + oy] = v;
+                }
+            }
+        }
+    }
+}
+
 void conv3x3_gelu(const __half* in, int n_chunks, int Hi, int Wi, const __half* w, const float* b, int C, void* out,
                   int out_mode, hipStream_t s) {
     const int M = n_chunks * ((Hi + 1) / 2) * ((Wi + 1) / 2);
     if (M <= 0) return;
     QASR_CHECK(C % 32 == 0, QASR_E_INVALID, "conv channels must be a multiple of 32");
     ProfScope ps(s, "conv3x3_f16", 2.0 * M * C * 9.0 * C, (double)M * 9 * C * 2 / 4 + (double)M * C * 2);
-    if (C % CV_BK == 0) {
+    // QASR_CONV_DMA=0: the register-staged kernel (A/B; same bits)
+    static const bool dma = !(getenv("QASR_CONV_DMA") && atoi(getenv("QASR_CONV_DMA")) == 0);
+    if (C % CV_BK == 0 && dma) {
+        k_conv3x3_gelu_dma<<<cdiv(C, CV_BN) * cdiv(M, CV_BM), CV_NT, 0, s>>>(in, n_chunks, Hi, Wi, w, b, C, out,
+                                                                            out_mode);
+    } else if (C % CV_BK == 0) {
         k_conv3x3_gelu<<<cdiv(C, CV_BN) * cdiv(M, CV_BM), CV_NT, 0, s>>>(in, n_chunks, Hi, Wi, w, b, C, out, out_mode);
     } else {
         dim3 grid(cdiv(C, CT), cdiv(M, CT));
