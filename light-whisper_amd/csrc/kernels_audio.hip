@@ -496,10 +496,13 @@ __global__ __launch_bounds__(CV_NT) void k_conv3x3_gelu(const __half* __restrict
 //  * LDS image: 64-B rows, 16-B chunk c of row r at chunk c ^ g((r >> 2) & 3), g = {0, 2, 3, 1}: the four 16-lane
 //    groups of every ds_read_b128 fragment read ({0–3,12–15,20–27}, …) then touch 16 distinct 4-bank units
 //    (checked exhaustively for rows 16k + fr); the DMA's lane-linear 1-KB writes are conflict-free by construction.
-constexpr int CD_BK = 32, CD_ROWB = CD_BK * 2, CD_OB = CV_BM * CD_ROWB, CD_STAGE = (CV_BM + CV_BN) * CD_ROWB;
-constexpr int CD_NBUF = 6;   // 6 × 26 KB = 159,744 B of LDS: one workgroup (8 waves, 2 per SIMD) per CU
-static_assert(CD_NBUF * CD_STAGE <= 163840, "conv ring exceeds LDS");
-__device__ __forceinline__ int cd_swz(int row) { return (0x78 >> (2 * ((row >> 2) & 3))) & 3; }
+// QASR_CONV_BK=64 (A/B): K-64 stages (128-B rows: whole cache lines per gathered row), a 3-deep ring, both K-32
+// slices of a stage read after its barrier (the second under the first's MFMAs); LDS image 16-B chunk c of row r at
+// c ^ ((r >> 1) & 7), conflict-free for the same fragment reads.
+constexpr int CD_NBUF32 = 6;   // K-32: 6 × 26 KB = 159,744 B of LDS: one workgroup (8 waves, 2 per SIMD) per CU
+constexpr int CD_NBUF64 = 3;   // K-64: 3 × 52 KB
+__device__ __forceinline__ int cd_swz32(int row) { return (0x78 >> (2 * ((row >> 2) & 3))) & 3; }
+__device__ __forceinline__ int cd_swz64(int row) { return (row >> 1) & 7; }
 __device__ __attribute__((aligned(16))) int4 g_conv_zero[1];
 // f(integral_constant<int, U>) for U = 0 … N-1, each call its own code (compile-time ring slot and register set)
 template <int... U, class F>
@@ -507,14 +510,25 @@ __device__ __forceinline__ void cd_unroll(std::integer_sequence<int, U...>, F&& 
     (f(std::integral_constant<int, U>{}), ...);
 }
 
+template <int BK, int NBUF>
 __global__ __launch_bounds__(CV_NT) void k_conv3x3_gelu_dma(const __half* __restrict__ in, int n_chunks, int Hi,
                                                           int Wi, const __half* __restrict__ w,
                                                           const float* __restrict__ bias, int C,
                                                           void* __restrict__ out, int out_mode) {
-    __shared__ __attribute__((aligned(1024))) char smem[CD_NBUF * CD_STAGE];
+    static_assert(BK == 32 || BK == 64, "conv stage K");
+    constexpr int ROWB = BK * 2, OB = CV_BM * ROWB, STAGE = (CV_BM + CV_BN) * ROWB;
+    static_assert(NBUF * STAGE <= 163840, "conv ring exceeds LDS");
+    constexpr int RW = BK / 8, RPP = 64 / RW;            // lanes per row, rows per 1-KB piece
+    constexpr int PA = CV_BM / RPP, PB = CV_BN / RPP;   // pieces per stage: 16 + 10 (K-32), 32 + 20 (K-64)
+    constexpr int AW = PA / 8, BW = PB / 8, BX = PB - 8 * BW;   // per wave: AW A, BW B (+1 for waves < BX)
+    static_assert(AW * 8 == PA && BX < 8, "conv pieces");
+    constexpr int KS = BK / 32;                          // K-32 MFMA slices per stage
+    constexpr bool PIPE = BK == 32;                      // cross-stage fragment prefetch (two register sets)
+    auto swz = [](int r) { return BK == 32 ? cd_swz32(r) : cd_swz64(r); };
+    __shared__ __attribute__((aligned(1024))) char smem[NBUF * STAGE];
     const int Ho = (Hi + 1) / 2, Wo = (Wi + 1) / 2;
     const int M = n_chunks * Ho * Wo;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wr = wave >> 1, wc = wave & 1;
     const int nct = (C + CV_BN - 1) / CV_BN;
 #if QASR_CONV_XCD
@@ -524,48 +538,52 @@ __global__ __launch_bounds__(CV_NT) void k_conv3x3_gelu_dma(const __half* __rest
     const int t = blockIdx.x;
 #endif
     const int n0 = (t % nct) * CV_BN, m0 = (t / nct) * CV_BM;
-    const int steps = 9 * (C / CD_BK);
-    // this lane's DMA sources: A pieces 2w, 2w+1 (row 16p + lane/4, 16-B slot lane%4 ← chunk slot ^ swz(row)); the
+    const int steps = 9 * (C / BK);
+    // this lane's DMA sources: A pieces AW·w + u (row RPP·p + lane/RW, 16-B slot lane%RW ← chunk slot ^ swz(row)); the
     // chunk's base pointer is 64-bit, the in-chunk offset 32-bit
-    const __half* a_ptr[2];
-    int a_iy0[2], a_ix0[2];
-    unsigned a_in[2];
+    const __half* a_ptr[AW];
+    int a_iy0[AW], a_ix0[AW];
+    unsigned a_in[AW];
 #pragma unroll
-    for (int u = 0; u < 2; u++) {
-        const int row = 16 * (2 * wave + u) + (lane >> 2), pos = m0 + row;
+    for (int u = 0; u < AW; u++) {
+        const int row = RPP * (AW * wave + u) + lane / RW, pos = m0 + row;
         a_in[u] = pos < M;
         const int rr = min(pos, M - 1), chn = rr / (Ho * Wo), rem = rr % (Ho * Wo);
         a_iy0[u] = 2 * (rem / Wo) - 1;
         a_ix0[u] = 2 * (rem % Wo) - 1;
-        a_ptr[u] = in + (size_t)chn * Hi * Wi * C + 8 * ((lane & 3) ^ cd_swz(row));
+        a_ptr[u] = in + (size_t)chn * Hi * Wi * C + 8 * ((lane % RW) ^ swz(row));
     }
-    const int nbp = wave < 2 ? 2 : 1;   // B pieces of this wave (wave-uniform)
-    const __half* b_src[2];
+    const bool bx = wave < BX;   // this wave takes an extra B piece (wave-uniform)
+    const __half* b_src[BW + 1];
+    uint32_t b_dst[BW + 1];
 #pragma unroll
-    for (int u = 0; u < 2; u++) {
-        const int p = u == 0 ? wave : 8 + wave, row = 16 * p + (lane >> 2);
-        const int co = min(n0 + min(row, CV_BN - 1), C - 1);
-        b_src[u] = w + (size_t)co * 9 * C + 8 * ((lane & 3) ^ cd_swz(row));
+    for (int u = 0; u <= BW; u++) {
+        const int p = u < BW ? BW * wave + u : min(8 * BW + wave, PB - 1), row = RPP * p + lane / RW;
+        const int co = min(n0 + row, C - 1);
+        b_src[u] = w + (size_t)co * 9 * C + 8 * ((lane % RW) ^ swz(row));
+        b_dst[u] = OB + 1024 * p;
     }
     const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
-    const uint32_t wa = __builtin_amdgcn_readfirstlane(lds0 + 2048 * wave);
-    const uint32_t wb0 = __builtin_amdgcn_readfirstlane(lds0 + CD_OB + 1024 * wave);
-    const uint32_t wb1 = __builtin_amdgcn_readfirstlane(lds0 + CD_OB + 1024 * (8 + (wave & 1)));
+    const uint32_t wa = __builtin_amdgcn_readfirstlane(lds0 + 1024 * AW * wave);
+    uint32_t wb[BW + 1];
+#pragma unroll
+    for (int u = 0; u <= BW; u++) wb[u] = __builtin_amdgcn_readfirstlane(lds0 + b_dst[u]);
     // stages are issued strictly in order: (tap, ci0) of the next one advance by counters, no division
     int it_ky = 0, it_kx = 0, it_tap = 0, it_ci = 0;
-    auto issue = [&](int buf) {
-        const uint32_t so = buf * CD_STAGE;
+    auto issue = [&](int buf) __attribute__((always_inline)) {
+        const uint32_t so = buf * STAGE;
 #pragma unroll
-        for (int u = 0; u < 2; u++) {
+        for (int u = 0; u < AW; u++) {
             const int iy = a_iy0[u] + it_ky, ix = a_ix0[u] + it_kx;
             const unsigned ok = a_in[u] & ((unsigned)iy < (unsigned)Hi) & ((unsigned)ix < (unsigned)Wi);
             const __half* src = a_ptr[u] + ((iy * Wi + ix) * C + it_ci);
             dma_lds16(ok ? (const void*)src : (const void*)g_conv_zero, wa + so + 1024 * u);
         }
         const int boff = it_tap * C + it_ci;
-        dma_lds16(b_src[0] + boff, wb0 + so);
-        if (nbp == 2) dma_lds16(b_src[1] + boff, wb1 + so);
-        it_ci += CD_BK;
+#pragma unroll
+        for (int u = 0; u < BW; u++) dma_lds16(b_src[u] + boff, wb[u] + so);
+        if (BX > 0 && bx) dma_lds16(b_src[BW] + boff, wb[BW] + so);
+        it_ci += BK;
         if (it_ci == C) {
             it_ci = 0;
             it_tap++;
@@ -577,60 +595,90 @@ __global__ __launch_bounds__(CV_NT) void k_conv3x3_gelu_dma(const __half* __rest
         }
     };
     const int fr = lane & 15, kg = lane >> 4;
-    const int fo = 16 * (kg ^ cd_swz(fr));   // fragment rows are fr + multiples of 16
     v4f acc[4][CV_TJ];
 #pragma unroll
     for (int i = 0; i < 4; i++)
 #pragma unroll
         for (int j = 0; j < CV_TJ; j++) acc[i][j] = (v4f){0.f, 0.f, 0.f, 0.f};
     // (waves whose rows all lie past M compute on the clamped rows too; their results are not stored)
-    v8h fa[2][4], fb[2][CV_TJ];
-    auto frags = [&](int set, int buf) {
-        const char* st = smem + buf * CD_STAGE;
+    constexpr int NSET = PIPE ? 2 : KS;
+    v8h fa[NSET][4], fb[NSET][CV_TJ];
+    auto frags = [&](int set, int buf, int ks) __attribute__((always_inline)) {
+        const char* st = smem + buf * STAGE;
+        const int fo = 16 * ((4 * ks + kg) ^ swz(fr));   // fragment rows are fr + multiples of 16
 #pragma unroll
-        for (int i = 0; i < 4; i++) fa[set][i] = *(const v8h*)(st + (wr * 64 + i * 16 + fr) * CD_ROWB + fo);
+        for (int i = 0; i < 4; i++) fa[set][i] = *(const v8h*)(st + (wr * 64 + i * 16 + fr) * ROWB + fo);
 #pragma unroll
         for (int j = 0; j < CV_TJ; j++)
-            fb[set][j] = *(const v8h*)(st + CD_OB + (wc * 16 * CV_TJ + j * 16 + fr) * CD_ROWB + fo);
+            fb[set][j] = *(const v8h*)(st + OB + (wc * 16 * CV_TJ + j * 16 + fr) * ROWB + fo);
     };
-    auto wait_ahead = [&](int ahead) {   // at most `ahead` of this wave's stages still in flight, LDS reads done
-        if (nbp == 2) wait_stages<4, CD_NBUF>(ahead);
-        else wait_stages<3, CD_NBUF>(ahead);
-    };
-    // the ring's NBUF stages are all issued up front; stage s frees its buffer for stage s + NBUF
-#pragma unroll
-    for (int s = 0; s < CD_NBUF; s++)
-        if (s < steps) issue(s);
-    wait_ahead(min(CD_NBUF - 1, steps - 1));
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    frags(0, 0);
-    // one stage: this wave's DMAs of stage s+1 have landed and its reads of stage s are done (lgkmcnt(0)); the barrier
-    // makes both true for every wave — stage s+1 is readable, stage s's buffer is free for stage s + NBUF.  The next
-    // stage's fragment reads are unconditional (past the last stage they re-read a stale buffer, unused): a
-    // conditional read would make the compiler's own lgkmcnt wait before the MFMAs a full drain.
-    auto stage = [&](int s, auto ubc) {
-        constexpr int ub = decltype(ubc)::value;
-        wait_ahead(max(0, min(CD_NBUF - 2, steps - 2 - s)));
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-        if (s + CD_NBUF < steps) issue(ub % CD_NBUF);
-        frags((ub + 1) & 1, (ub + 1) % CD_NBUF);
+    auto mfmas = [&](int set) __attribute__((always_inline)) {
 #pragma unroll
         for (int i = 0; i < 4; i++)
 #pragma unroll
             for (int j = 0; j < CV_TJ; j++)
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[ub & 1][i], fb[ub & 1][j], acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[set][i], fb[set][j], acc[i][j], 0, 0, 0);
     };
-    // two ring trips per loop trip, so every unrolled stage's ring slot and register set are constants; the last
-    // partial trip is a guarded copy
-    constexpr int TRIP = 2 * CD_NBUF;
-    const int full = steps / TRIP * TRIP;
-    for (int s0 = 0; s0 < full; s0 += TRIP)
-        cd_unroll(std::make_integer_sequence<int, TRIP>{}, [&](auto u) { stage(s0 + u.value, u); });
-    cd_unroll(std::make_integer_sequence<int, TRIP>{}, [&](auto u) {
-        if (full + u.value < steps) stage(full + u.value, u);
-    });
+    constexpr int NPW = AW + BW;   // DMAs per wave per stage (+1 on waves < BX)
+    auto wait_ahead = [&](int ahead) __attribute__((always_inline)) {   // at most `ahead` of this wave's stages still in flight, LDS reads done
+        if (BX > 0 && bx) wait_stages<NPW + 1, NBUF>(ahead);
+        else wait_stages<NPW, NBUF>(ahead);
+    };
+    if constexpr (PIPE) {
+        // the ring's NBUF stages are all issued up front; stage s frees its buffer for stage s + NBUF
+#pragma unroll
+        for (int s = 0; s < NBUF; s++)
+            if (s < steps) issue(s);
+        wait_ahead(min(NBUF - 1, steps - 1));
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        frags(0, 0, 0);
+        // one stage: this wave's DMAs of stage s+1 have landed and its reads of stage s are done (lgkmcnt(0)); the
+        // barrier makes both true for every wave — stage s+1 is readable, stage s's buffer is free for stage s + NBUF.
+        // The next stage's fragment reads are unconditional (past the last stage they re-read a stale buffer, unused):
+        // a conditional read would make the compiler's own lgkmcnt wait before the MFMAs a full drain.
+        auto stage = [&](int s, auto ubc) __attribute__((always_inline)) {
+            constexpr int ub = decltype(ubc)::value;
+            wait_ahead(max(0, min(NBUF - 2, steps - 2 - s)));
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+            if (s + NBUF < steps) issue(ub % NBUF);
+            frags((ub + 1) & 1, (ub + 1) % NBUF, 0);
+            mfmas(ub & 1);
+        };
+        // two ring trips per loop trip, so every unrolled stage's ring slot and register set are constants; the last
+        // partial trip is a guarded copy
+        constexpr int TRIP = 2 * NBUF;
+        const int full = steps / TRIP * TRIP;
+        for (int s0 = 0; s0 < full; s0 += TRIP)
+            cd_unroll(std::make_integer_sequence<int, TRIP>{}, [&](auto u) { stage(s0 + u.value, u); });
+        cd_unroll(std::make_integer_sequence<int, TRIP>{}, [&](auto u) {
+            if (full + u.value < steps) stage(full + u.value, u);
+        });
+    } else {
+        // NBUF-1 stages in flight; stage s's barrier frees stage s-1's buffer for stage s + NBUF - 1
+        constexpr int D = NBUF - 1;
+#pragma unroll
+        for (int s = 0; s < D; s++)
+            if (s < steps) issue(s);
+        auto stage = [&](int s, auto ubc) __attribute__((always_inline)) {
+            constexpr int ub = decltype(ubc)::value;
+            wait_ahead(max(0, min(D - 1, steps - 1 - s)));
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+            if (s + D < steps) issue((ub + D) % NBUF);
+#pragma unroll
+            for (int ks = 0; ks < KS; ks++) frags(ks, ub, ks);
+#pragma unroll
+            for (int ks = 0; ks < KS; ks++) mfmas(ks);
+        };
+        const int full = steps / NBUF * NBUF;
+        for (int s0 = 0; s0 < full; s0 += NBUF)
+            cd_unroll(std::make_integer_sequence<int, NBUF>{}, [&](auto u) { stage(s0 + u.value, u); });
+        cd_unroll(std::make_integer_sequence<int, NBUF>{}, [&](auto u) {
+            if (full + u.value < steps) stage(full + u.value, u);
+        });
+    }
 #pragma unroll
     for (int i = 0; i < 4; i++) {
 #pragma unroll
@@ -662,9 +710,12 @@ void conv3x3_gelu(const __half* in, int n_chunks, int Hi, int Wi, const __half* 
     ProfScope ps(s, "conv3x3_f16", 2.0 * M * C * 9.0 * C, (double)M * 9 * C * 2 / 4 + (double)M * C * 2);
     // QASR_CONV_DMA=0: the register-staged kernel (A/B; same bits)
     static const bool dma = !(getenv("QASR_CONV_DMA") && atoi(getenv("QASR_CONV_DMA")) == 0);
-    if (C % CV_BK == 0 && dma) {
-        k_conv3x3_gelu_dma<<<cdiv(C, CV_BN) * cdiv(M, CV_BM), CV_NT, 0, s>>>(in, n_chunks, Hi, Wi, w, b, C, out,
-                                                                            out_mode);
+    static const int bk = getenv("QASR_CONV_BK") ? atoi(getenv("QASR_CONV_BK")) : 32;
+    const int grid = cdiv(C, CV_BN) * cdiv(M, CV_BM);
+    if (C % CV_BK == 0 && dma && bk == 64 && C % 64 == 0) {
+        k_conv3x3_gelu_dma<64, CD_NBUF64><<<grid, CV_NT, 0, s>>>(in, n_chunks, Hi, Wi, w, b, C, out, out_mode);
+    } else if (C % CV_BK == 0 && dma) {
+        k_conv3x3_gelu_dma<32, CD_NBUF32><<<grid, CV_NT, 0, s>>>(in, n_chunks, Hi, Wi, w, b, C, out, out_mode);
     } else if (C % CV_BK == 0) {
         k_conv3x3_gelu<<<cdiv(C, CV_BN) * cdiv(M, CV_BM), CV_NT, 0, s>>>(in, n_chunks, Hi, Wi, w, b, C, out, out_mode);
     } else {
