@@ -510,18 +510,20 @@ __device__ __forceinline__ void cd_unroll(std::integer_sequence<int, U...>, F&& 
     (f(std::integral_constant<int, U>{}), ...);
 }
 
-template <int BK, int NBUF>
-__global__ __launch_bounds__(CV_NT) void k_conv3x3_gelu_dma(const __half* __restrict__ in, int n_chunks, int Hi,
+template <int BK, int NBUF, int NW = 8>
+__global__ __launch_bounds__(NW * 64) void k_conv3x3_gelu_dma(const __half* __restrict__ in, int n_chunks, int Hi,
                                                           int Wi, const __half* __restrict__ w,
                                                           const float* __restrict__ bias, int C,
                                                           void* __restrict__ out, int out_mode) {
     static_assert(BK == 32 || BK == 64, "conv stage K");
-    constexpr int ROWB = BK * 2, OB = CV_BM * ROWB, STAGE = (CV_BM + CV_BN) * ROWB;
+    // NW waves as (NW/2) × 2 of 64×80: BM = 32·NW positions (8 waves: 256, one workgroup per CU; 4 waves: 128, two)
+    constexpr int BM = 32 * NW;
+    constexpr int ROWB = BK * 2, OB = BM * ROWB, STAGE = (BM + CV_BN) * ROWB;
     static_assert(NBUF * STAGE <= 163840, "conv ring exceeds LDS");
     constexpr int RW = BK / 8, RPP = 64 / RW;            // lanes per row, rows per 1-KB piece
-    constexpr int PA = CV_BM / RPP, PB = CV_BN / RPP;   // pieces per stage: 16 + 10 (K-32), 32 + 20 (K-64)
-    constexpr int AW = PA / 8, BW = PB / 8, BX = PB - 8 * BW;   // per wave: AW A, BW B (+1 for waves < BX)
-    static_assert(AW * 8 == PA && BX < 8, "conv pieces");
+    constexpr int PA = BM / RPP, PB = CV_BN / RPP;   // pieces per stage: 16 + 10 (K-32, 8 waves), 32 + 20 (K-64)
+    constexpr int AW = PA / NW, BW = PB / NW, BX = PB - NW * BW;   // per wave: AW A, BW B (+1 for waves < BX)
+    static_assert(AW * NW == PA && BX < NW, "conv pieces");
     constexpr int KS = BK / 32;                          // K-32 MFMA slices per stage
     constexpr bool PIPE = BK == 32;                      // cross-stage fragment prefetch (two register sets)
     auto swz = [](int r) { return BK == 32 ? cd_swz32(r) : cd_swz64(r); };
@@ -537,28 +539,32 @@ __global__ __launch_bounds__(CV_NT) void k_conv3x3_gelu_dma(const __half* __rest
 #else
     const int t = blockIdx.x;
 #endif
-    const int n0 = (t % nct) * CV_BN, m0 = (t / nct) * CV_BM;
+    const int n0 = (t % nct) * CV_BN, m0 = (t / nct) * BM;
     const int steps = 9 * (C / BK);
-    // this lane's DMA sources: A pieces AW·w + u (row RPP·p + lane/RW, 16-B slot lane%RW ← chunk slot ^ swz(row)); the
-    // chunk's base pointer is 64-bit, the in-chunk offset 32-bit
+    // this lane's DMA sources: A pieces AW·w + u (row RPP·p + lane/RW, 16-B slot lane%RW ← chunk slot ^ swz(row)):
+    // the address of its tap-(0, 0) pixel (never read when that tap is padding) and a 9-bit mask of the taps that
+    // are inside the image — a stage then adds one wave-uniform offset and tests one bit
     const __half* a_ptr[AW];
-    int a_iy0[AW], a_ix0[AW];
-    unsigned a_in[AW];
+    unsigned a_ok[AW];
 #pragma unroll
     for (int u = 0; u < AW; u++) {
         const int row = RPP * (AW * wave + u) + lane / RW, pos = m0 + row;
-        a_in[u] = pos < M;
         const int rr = min(pos, M - 1), chn = rr / (Ho * Wo), rem = rr % (Ho * Wo);
-        a_iy0[u] = 2 * (rem / Wo) - 1;
-        a_ix0[u] = 2 * (rem % Wo) - 1;
-        a_ptr[u] = in + (size_t)chn * Hi * Wi * C + 8 * ((lane % RW) ^ swz(row));
+        const int iy0 = 2 * (rem / Wo) - 1, ix0 = 2 * (rem % Wo) - 1;
+        unsigned ok = 0;
+#pragma unroll
+        for (int tp = 0; tp < 9; tp++)
+            ok |= (unsigned)(pos < M && (unsigned)(iy0 + tp / 3) < (unsigned)Hi && (unsigned)(ix0 + tp % 3) < (unsigned)Wi)
+                  << tp;
+        a_ok[u] = ok;
+        a_ptr[u] = in + (size_t)chn * Hi * Wi * C + (ptrdiff_t)(iy0 * Wi + ix0) * C + 8 * ((lane % RW) ^ swz(row));
     }
     const bool bx = wave < BX;   // this wave takes an extra B piece (wave-uniform)
     const __half* b_src[BW + 1];
     uint32_t b_dst[BW + 1];
 #pragma unroll
     for (int u = 0; u <= BW; u++) {
-        const int p = u < BW ? BW * wave + u : min(8 * BW + wave, PB - 1), row = RPP * p + lane / RW;
+        const int p = u < BW ? BW * wave + u : min(NW * BW + wave, PB - 1), row = RPP * p + lane / RW;
         const int co = min(n0 + row, C - 1);
         b_src[u] = w + (size_t)co * 9 * C + 8 * ((lane % RW) ^ swz(row));
         b_dst[u] = OB + 1024 * p;
@@ -570,19 +576,21 @@ __global__ __launch_bounds__(CV_NT) void k_conv3x3_gelu_dma(const __half* __rest
     for (int u = 0; u <= BW; u++) wb[u] = __builtin_amdgcn_readfirstlane(lds0 + b_dst[u]);
     // stages are issued strictly in order: (tap, ci0) of the next one advance by counters, no division
     int it_ky = 0, it_kx = 0, it_tap = 0, it_ci = 0;
-    auto issue = [&](int buf) __attribute__((always_inline)) {
+    // piece q of the next stage's DMAs: q < AW the A pieces, then BW B pieces, then the extra B piece (waves < BX)
+    constexpr int NPQ = AW + BW + (BX > 0 ? 1 : 0);
+    auto issue_piece = [&](int buf, int q) __attribute__((always_inline)) {
         const uint32_t so = buf * STAGE;
-#pragma unroll
-        for (int u = 0; u < AW; u++) {
-            const int iy = a_iy0[u] + it_ky, ix = a_ix0[u] + it_kx;
-            const unsigned ok = a_in[u] & ((unsigned)iy < (unsigned)Hi) & ((unsigned)ix < (unsigned)Wi);
-            const __half* src = a_ptr[u] + ((iy * Wi + ix) * C + it_ci);
-            dma_lds16(ok ? (const void*)src : (const void*)g_conv_zero, wa + so + 1024 * u);
+        if (q < AW) {
+            const int aoff = (it_ky * Wi + it_kx) * C + it_ci;   // wave-uniform
+            const bool ok = (a_ok[q] >> it_tap) & 1u;
+            dma_lds16(ok ? (const void*)(a_ptr[q] + aoff) : (const void*)g_conv_zero, wa + so + 1024 * q);
+        } else if (q < AW + BW) {
+            dma_lds16(b_src[q - AW] + (it_tap * C + it_ci), wb[q - AW] + so);
+        } else if (bx) {
+            dma_lds16(b_src[BW] + (it_tap * C + it_ci), wb[BW] + so);
         }
-        const int boff = it_tap * C + it_ci;
-#pragma unroll
-        for (int u = 0; u < BW; u++) dma_lds16(b_src[u] + boff, wb[u] + so);
-        if (BX > 0 && bx) dma_lds16(b_src[BW] + boff, wb[BW] + so);
+    };
+    auto advance = [&]() __attribute__((always_inline)) {
         it_ci += BK;
         if (it_ci == C) {
             it_ci = 0;
@@ -593,6 +601,11 @@ __global__ __launch_bounds__(CV_NT) void k_conv3x3_gelu_dma(const __half* __rest
                 it_ky++;
             }
         }
+    };
+    auto issue = [&](int buf) __attribute__((always_inline)) {
+#pragma unroll
+        for (int q = 0; q < NPQ; q++) issue_piece(buf, q);
+        advance();
     };
     const int fr = lane & 15, kg = lane >> 4;
     v4f acc[4][CV_TJ];
@@ -642,8 +655,8 @@ __global__ __launch_bounds__(CV_NT) void k_conv3x3_gelu_dma(const __half* __rest
             wait_ahead(max(0, min(NBUF - 2, steps - 2 - s)));
             __builtin_amdgcn_s_barrier();
             asm volatile("" ::: "memory");
-            if (s + NBUF < steps) issue(ub % NBUF);
             frags((ub + 1) & 1, (ub + 1) % NBUF, 0);
+            if (s + NBUF < steps) issue(ub % NBUF);
             mfmas(ub & 1);
         };
         // two ring trips per loop trip, so every unrolled stage's ring slot and register set are constants; the last
@@ -711,8 +724,13 @@ void conv3x3_gelu(const __half* in, int n_chunks, int Hi, int Wi, const __half* 
     // QASR_CONV_DMA=0: the register-staged kernel (A/B; same bits)
     static const bool dma = !(getenv("QASR_CONV_DMA") && atoi(getenv("QASR_CONV_DMA")) == 0);
     static const int bk = getenv("QASR_CONV_BK") ? atoi(getenv("QASR_CONV_BK")) : 32;
+    // QASR_CONV_NW=4: 128-position tiles of 4 waves, two workgroups per CU (A/B)
+    static const int nw = getenv("QASR_CONV_NW") ? atoi(getenv("QASR_CONV_NW")) : 8;
     const int grid = cdiv(C, CV_BN) * cdiv(M, CV_BM);
-    if (C % CV_BK == 0 && dma && bk == 64 && C % 64 == 0) {
+    if (C % CV_BK == 0 && dma && nw == 4) {
+        k_conv3x3_gelu_dma<32, 4, 4><<<cdiv(C, CV_BN) * cdiv(M, 128), 256, 0, s>>>(in, n_chunks, Hi, Wi, w, b, C, out,
+                                                                                 out_mode);
+    } else if (C % CV_BK == 0 && dma && bk == 64 && C % 64 == 0) {
         k_conv3x3_gelu_dma<64, CD_NBUF64><<<grid, CV_NT, 0, s>>>(in, n_chunks, Hi, Wi, w, b, C, out, out_mode);
     } else if (C % CV_BK == 0 && dma) {
         k_conv3x3_gelu_dma<32, CD_NBUF32><<<grid, CV_NT, 0, s>>>(in, n_chunks, Hi, Wi, w, b, C, out, out_mode);
