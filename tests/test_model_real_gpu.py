@@ -596,3 +596,57 @@ def test_real_c5_mxfp8_longform_against_q8(pair):
         ms.close()
     finally:
         mx.close()
+
+
+_DUMP_CHILD = r"""
+import json, os, sys
+import numpy as np
+sys.path.insert(0, os.path.join(sys.argv[1], "light-whisper_amd"))
+sys.path.insert(0, sys.argv[1])
+from qasr.transcribe_cpp import Model
+from bench import speech_like
+secs = json.loads(sys.argv[3])
+clips = [speech_like(np.random.default_rng(600 + i), int(x * 16000)) for i, x in enumerate(secs)]
+m = Model.synthetic(sys.argv[2], seed=7)
+s = m.session(kv_type="f16", n_ctx=4096)
+single = s.run(clips[0], force_tokens_per_s=8).tokens
+s.set_batch_invariant(True)
+batch = [r.tokens for r in s.run_batch(clips, force_tokens_per_s=8)]
+s.close()
+m.close()
+print(json.dumps({"single": list(single), "batch": [list(b) for b in batch]}))
+"""
+
+
+def test_real_dump_mode_same_tokens(pair, tmp_path):
+    """diagnosis dump mode (QASR_DUMP_DIR: every ≤ 32-row decode stage's rows written to files, the fused norms split
+    off) computes the same tokens as a normal run — ADVICE r5: the exact-row path once skipped the down projection
+    under dump.  The dump switch is read once per process, so the dumping run is a child process (eager passes,
+    QASR_NO_GRAPH, as the diagnosis tools run); batch-invariant rows take the exact-row (xm) path"""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    arch, _, s, _ = pair
+    if arch != "qwen3-asr-0.6b":
+        pytest.skip("one architecture is enough for the dump switch")
+    secs = [2.0, 2.6, 3.1]
+    clips = [clip(x, 600 + i) for i, x in enumerate(secs)]
+    single = list(s.run(clips[0], force_tokens_per_s=8).tokens)
+    s.set_batch_invariant(True)
+    try:
+        batch = [list(r.tokens) for r in s.run_batch(clips, force_tokens_per_s=8)]
+    finally:
+        s.set_batch_invariant(False)
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, QASR_DUMP_DIR=str(tmp_path), QASR_NO_GRAPH="1")
+    out = subprocess.run([sys.executable, "-c", _DUMP_CHILD, root, arch, json.dumps(secs)], env=env,
+                         capture_output=True, text=True, timeout=240)
+    assert out.returncode == 0, out.stderr[-2000:]
+    got = json.loads(out.stdout.strip().splitlines()[-1])
+    dumps = len(os.listdir(tmp_path))
+    record(f"real_dump_mode[{arch}]", dump_files=dumps)
+    assert dumps > 0
+    assert got["single"] == single
+    assert got["batch"] == batch
