@@ -516,7 +516,7 @@ __global__ __launch_bounds__(NW * 64) void k_conv3x3_gelu_dma(const __half* __re
                                                           const float* __restrict__ bias, int C,
                                                           void* __restrict__ out, int out_mode) {
     static_assert(BK == 32 || BK == 64, "conv stage K");
-    // NW waves as (NW/2) × 2 of 64×80: BM = 32·NW positions (8 waves: 256, one workgroup per CU; 4 waves: 128, two)
+    // NW waves as (NW/2) × 2 of 64×80: BM = 32·NW positions (8 waves: 256, one workgroup per CU)
     constexpr int BM = 32 * NW;
     constexpr int ROWB = BK * 2, OB = BM * ROWB, STAGE = (BM + CV_BN) * ROWB;
     static_assert(NBUF * STAGE <= 163840, "conv ring exceeds LDS");
@@ -655,8 +655,9 @@ __global__ __launch_bounds__(NW * 64) void k_conv3x3_gelu_dma(const __half* __re
             wait_ahead(max(0, min(NBUF - 2, steps - 2 - s)));
             __builtin_amdgcn_s_barrier();
             asm volatile("" ::: "memory");
-            frags((ub + 1) & 1, (ub + 1) % NBUF, 0);
+            // (this order: the fragment reads after the DMA issue keep the kernel at 205 VGPRs; reads first spilled 5)
             if (s + NBUF < steps) issue(ub % NBUF);
+            frags((ub + 1) & 1, (ub + 1) % NBUF, 0);
             mfmas(ub & 1);
         };
         // two ring trips per loop trip, so every unrolled stage's ring slot and register set are constants; the last
@@ -724,13 +725,8 @@ void conv3x3_gelu(const __half* in, int n_chunks, int Hi, int Wi, const __half* 
     // QASR_CONV_DMA=0: the register-staged kernel (A/B; same bits)
     static const bool dma = !(getenv("QASR_CONV_DMA") && atoi(getenv("QASR_CONV_DMA")) == 0);
     static const int bk = getenv("QASR_CONV_BK") ? atoi(getenv("QASR_CONV_BK")) : 32;
-    // QASR_CONV_NW=4: 128-position tiles of 4 waves, two workgroups per CU (A/B)
-    static const int nw = getenv("QASR_CONV_NW") ? atoi(getenv("QASR_CONV_NW")) : 8;
     const int grid = cdiv(C, CV_BN) * cdiv(M, CV_BM);
-    if (C % CV_BK == 0 && dma && nw == 4) {
-        k_conv3x3_gelu_dma<32, 4, 4><<<cdiv(C, CV_BN) * cdiv(M, 128), 256, 0, s>>>(in, n_chunks, Hi, Wi, w, b, C, out,
-                                                                                 out_mode);
-    } else if (C % CV_BK == 0 && dma && bk == 64 && C % 64 == 0) {
+    if (C % CV_BK == 0 && dma && bk == 64 && C % 64 == 0) {
         k_conv3x3_gelu_dma<64, CD_NBUF64><<<grid, CV_NT, 0, s>>>(in, n_chunks, Hi, Wi, w, b, C, out, out_mode);
     } else if (C % CV_BK == 0 && dma) {
         k_conv3x3_gelu_dma<32, CD_NBUF32><<<grid, CV_NT, 0, s>>>(in, n_chunks, Hi, Wi, w, b, C, out, out_mode);
