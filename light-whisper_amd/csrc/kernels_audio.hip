@@ -137,10 +137,15 @@ __global__ __launch_bounds__(256) void k_mel_frames(const float* __restrict__ pc
     }
     __syncthreads();
     for (int m = threadIdx.x; m < n_mels; m += 256) {
+        // the filter's nonzero band [lo, hi): outside it every term is +0 (finite powers), so summing only the band
+        // gives the same bits as the full 201-bin sum (acc starts at +0 and never turns -0)
+        int lo = 201, hi = 0;
+        for (int kk = 0; kk < 201; kk++)
+            if (filt[kk * n_mels + m] != 0.f) lo = min(lo, kk), hi = kk + 1;
         float lmax = -INFINITY;
         for (int f = 0; f < nf; f++) {
             float acc = 0.f;
-            for (int kk = 0; kk < 201; kk++) acc += filt[kk * n_mels + m] * ps[f][kk];
+            for (int kk = lo; kk < hi; kk++) acc += filt[kk * n_mels + m] * ps[f][kk];
             const float l = log10f(fmaxf(acc, 1e-10f));
             lm[(size_t)(U.frame0 + t0 + f) * n_mels + m] = l;
             lmax = fmaxf(lmax, l);
@@ -207,18 +212,27 @@ __global__ __launch_bounds__(256) void k_conv1_gelu(const float* __restrict__ x,
     }
     __syncthreads();
     __half* yr = y + ((size_t)ch * H1 + oy) * W1 * C;
-    for (int co = threadIdx.x; co < C; co += 256) {
-        float k9[9];
+    // two adjacent channels per thread (C even): one 4-byte store per position instead of two 2-byte ones; each
+    // output's arithmetic is unchanged
+    for (int c2 = threadIdx.x; 2 * c2 < C; c2 += 256) {
+        const int co = 2 * c2;
+        float k9[2][9];
 #pragma unroll
-        for (int t = 0; t < 9; t++) k9[t] = __half2float(w[co * 9 + t]);
-        const float bias = b[co];
+        for (int h = 0; h < 2; h++)
+#pragma unroll
+            for (int t = 0; t < 9; t++) k9[h][t] = __half2float(w[(co + h) * 9 + t]);
+        const float bias0 = b[co], bias1 = b[co + 1];
         for (int ox = 0; ox < W1; ox++) {
-            float acc = 0.f;
+            float acc0 = 0.f, acc1 = 0.f;
 #pragma unroll
             for (int ky = 0; ky < 3; ky++)
 #pragma unroll
-                for (int kx = 0; kx < 3; kx++) acc += k9[ky * 3 + kx] * xs[ky][2 * ox + kx];
-            yr[(size_t)ox * C + co] = f2h(gelu_f(acc + bias));
+                for (int kx = 0; kx < 3; kx++) {
+                    const float xv = xs[ky][2 * ox + kx];
+                    acc0 += k9[0][ky * 3 + kx] * xv;
+                    acc1 += k9[1][ky * 3 + kx] * xv;
+                }
+            *(__half2*)(yr + (size_t)ox * C + co) = __halves2half2(f2h(gelu_f(acc0 + bias0)), f2h(gelu_f(acc1 + bias1)));
         }
     }
 }
@@ -227,6 +241,7 @@ void conv1_gelu(const float* x, int n_chunks, int n_mels, const __half* w, const
                 hipStream_t s) {
     const int64_t n = (int64_t)n_chunks * ((n_mels + 1) / 2) * 50 * C;
     if (n <= 0) return;
+    QASR_CHECK(C % 2 == 0, QASR_E_INVALID, "conv1: channel count must be even");
     ProfScope ps(s, "conv1", (double)n * 18, (double)n * 2);
     k_conv1_gelu<<<dim3((n_mels + 1) / 2, n_chunks), 256, 0, s>>>(x, n_chunks, n_mels, w, b, C, y);
 }
