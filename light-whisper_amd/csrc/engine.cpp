@@ -707,12 +707,16 @@ void Session::decode_step(const DecState& ds, int B, bool sizing, int64_t keys) 
     float* logits = (float*)sc_.get(S_LOGITS, (size_t)B * V * sizeof(float));
     lm_head_rows(x, B, H, logits, batch_inv_ && !m_->mx());
     int* d_tok = (int*)sc_.get(S_TOK, (size_t)B * sizeof(int));
-    argmax_rows(logits, B, V, d_tok, st_, sc_.get(S_ARGP, argmax_scratch_bytes(B)));
+    void* argp = sc_.get(S_ARGP, argmax_scratch_bytes(B));
     if (tf_) {
+        argmax_rows(logits, B, V, d_tok, st_, argp);
         force_tokens(ds, B, tab + 5 * B, tf_->d_ids, tf_->ld, d_tok, st_);
         tf_capture(logits, B, tab + 5 * B);
+        dec_accept(ds, B, tab + 5 * B, d_tok, st_);
+    } else {   // the argmax's final stage and the accept in one launch
+        argmax_rows_partial(logits, B, V, argp, st_);
+        argmax_accept(ds, B, argp, tab + 5 * B, d_tok, st_);
     }
-    dec_accept(ds, B, tab + 5 * B, d_tok, st_);
     QASR_HIP(hipMemcpyAsync(pin_cnt_, ds.counters, 4 * sizeof(int), hipMemcpyDeviceToHost, st_));
 }
 

@@ -128,6 +128,10 @@ void to_f16(const float* x, int rows, int cols, int ldx, __half* y, int ldy, hip
 // argmax per row (lowest index on ties); scratch (argmax_scratch_bytes(M)) selects the two-stage kernel
 void argmax_rows(const float* x, int M, int V, int* out, hipStream_t s, void* scratch = nullptr);
 size_t argmax_scratch_bytes(int M);
+// the first half of argmax_rows (scratch required): kArgParts slice maxima per row as order-preserving 64-bit keys
+// (value bits, then the complement of the index, so ties keep the lowest index); argmax_accept finishes it
+constexpr int kArgParts = 32;
+void argmax_rows_partial(const float* x, int M, int V, void* scratch, hipStream_t s);
 void add_posemb_gather(const float* proj, int n_chunks, int T, int d, const float* pe, const int* valid_idx,
                        int n_out, float* out, hipStream_t s);
 
@@ -219,6 +223,8 @@ void dec_plan(const DecState& st, int M_max, int* ids, int* pos, int* slot, int*
               hipStream_t s);
 void force_tokens(const DecState& st, int M_max, const int* row_utt, const int* ids, int ld, int* tok, hipStream_t s);
 void dec_accept(const DecState& st, int M_max, const int* row_utt, const int* tok, hipStream_t s);
+// argmax_rows' final stage (over argmax_rows_partial's keys) fused with dec_accept: tok[i] as argmax_rows gives it
+void argmax_accept(const DecState& st, int M_max, const void* part, const int* row_utt, int* tok, hipStream_t s);
 void copy_kv_prefix(__half* kc, __half* vc, int layers, int64_t kv_slots, int kvd, int64_t src, int P0,
                     const int* bases, int count, hipStream_t s);
 

@@ -57,12 +57,7 @@ __global__ __launch_bounds__(1024) void k_dec_plan(DecState st, int M_max, int* 
     }
 }
 
-__global__ void k_dec_accept(DecState st, int M_max, const int* __restrict__ row_utt, const int* __restrict__ tok) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= M_max || i >= st.counters[0]) return;
-    const int u = row_utt[i];
-    if (u < 0) return;
-    const int t = tok[i];
+__device__ __forceinline__ void accept_row(const DecState& st, int u, int t) {
     const int forced = st.params[2], eos0 = st.params[3], eos1 = st.params[4], ld = st.params[5];
     int still = 0;
     if (!forced && (t == eos0 || t == eos1)) {
@@ -76,6 +71,40 @@ __global__ void k_dec_accept(DecState st, int M_max, const int* __restrict__ row
         else still = 1;
     }
     if (still) atomicAdd(&st.counters[1], 1);
+}
+
+__global__ void k_dec_accept(DecState st, int M_max, const int* __restrict__ row_utt, const int* __restrict__ tok) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= M_max || i >= st.counters[0]) return;
+    const int u = row_utt[i];
+    if (u < 0) return;
+    accept_row(st, u, tok[i]);
+}
+
+// argmax_rows' second stage fused with k_dec_accept (one launch fewer per decode step): wave i reduces row i's
+// kArgParts keys (max is order-free: the same token as k_argmax_final) and lane 0 stores it and accepts it
+__global__ __launch_bounds__(256) void k_argmax_accept(DecState st, int M_max,
+                                                       const unsigned long long* __restrict__ part,
+                                                       const int* __restrict__ row_utt, int* __restrict__ tok) {
+    const int lane = threadIdx.x & 63, i = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (i >= M_max) return;   // whole wave
+    unsigned long long k = lane < kArgParts ? part[(size_t)i * kArgParts + lane] : 0ull;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const unsigned lo = __shfl_xor((unsigned)k, o), hi = __shfl_xor((unsigned)(k >> 32), o);
+        k = max(k, ((unsigned long long)hi << 32) | lo);
+    }
+    if (lane != 0) return;
+    const int t = (int)(0xFFFFFFFFu - (unsigned)(k & 0xFFFFFFFFull));
+    tok[i] = t;
+    if (i >= st.counters[0]) return;
+    const int u = row_utt[i];
+    if (u >= 0) accept_row(st, u, t);
+}
+
+void argmax_accept(const DecState& st, int M_max, const void* part, const int* row_utt, int* tok, hipStream_t s) {
+    if (M_max <= 0) return;
+    k_argmax_accept<<<cdiv(M_max, 4), 256, 0, s>>>(st, M_max, (const unsigned long long*)part, row_utt, tok);
 }
 
 // batched teacher forcing (Session::forced_logits_batch_host): row i's accepted token becomes the forced id of its

@@ -418,7 +418,7 @@ __global__ __launch_bounds__(256) void k_argmax(const float* __restrict__ x, int
 
 // two-stage argmax: ARG_P workgroups per row each reduce a slice to one 64-bit key (order-preserving float bits
 // high, inverted index low, so the maximum key is the largest value at the lowest index), then one wave per row
-constexpr int ARG_P = 32;
+constexpr int ARG_P = kArgParts;
 
 __device__ __forceinline__ unsigned long long argkey(float v, int i) {
     unsigned u = __float_as_uint(v);
@@ -464,6 +464,12 @@ __global__ __launch_bounds__(64) void k_argmax_final(const unsigned long long* _
 }
 
 size_t argmax_scratch_bytes(int M) { return (size_t)std::max(M, 1) * ARG_P * sizeof(unsigned long long); }
+
+void argmax_rows_partial(const float* x, int M, int V, void* scratch, hipStream_t s) {
+    if (M <= 0) return;
+    const int L = ((cdiv(V, ARG_P) + 3) / 4) * 4;
+    k_argmax_part<<<dim3(ARG_P, M), 256, 0, s>>>(x, V, L, (unsigned long long*)scratch);
+}
 
 void argmax_rows(const float* x, int M, int V, int* out, hipStream_t s, void* scratch) {
     if (M <= 0) return;
