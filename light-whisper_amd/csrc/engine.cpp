@@ -700,9 +700,13 @@ void Session::decode_step(const DecState& ds, int B, bool sizing, int64_t keys) 
     const qasr_hparams& h = m_->hp;
     const int H = h.txt_h, V = h.vocab;
     int* tab = (int*)sc_.get(S_DTAB, (size_t)6 * B * sizeof(int));
-    dec_plan(ds, B, tab, tab + B, tab + 2 * B, tab + 3 * B, tab + 4 * B, tab + 5 * B, st_);
     float* x = (float*)sc_.get(S_X, (size_t)B * H * sizeof(float));
-    embed_rows(tab, B, m_->tok_embd, nullptr, x, st_);
+    if (B <= kPlanEmbedRows) {   // plan + embedding in one launch
+        dec_plan_embed(ds, B, tab, tab + B, tab + 2 * B, tab + 3 * B, tab + 4 * B, tab + 5 * B, m_->tok_embd, x, st_);
+    } else {
+        dec_plan(ds, B, tab, tab + B, tab + 2 * B, tab + 3 * B, tab + 4 * B, tab + 5 * B, st_);
+        embed_rows(tab, B, m_->tok_embd, nullptr, x, st_);
+    }
     decoder_layers(x, B, tab + B, tab + 2 * B, tab + 3 * B, tab + 4 * B, keys);
     float* logits = (float*)sc_.get(S_LOGITS, (size_t)B * V * sizeof(float));
     lm_head_rows(x, B, H, logits, batch_inv_ && !m_->mx());

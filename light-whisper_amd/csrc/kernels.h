@@ -221,6 +221,11 @@ struct DecState {
 };
 void dec_plan(const DecState& st, int M_max, int* ids, int* pos, int* slot, int* kvs, int* kvl, int* row_utt,
               hipStream_t s);
+// dec_plan followed, in the same single-workgroup launch, by embed_rows of the planned ids (no alternative rows) into
+// x [M_max][E.K]: one launch fewer per step (small steps: the one workgroup writes every row)
+void dec_plan_embed(const DecState& st, int M_max, int* ids, int* pos, int* slot, int* kvs, int* kvl, int* row_utt,
+                    const Q8Mat& E, float* x, hipStream_t s);
+constexpr int kPlanEmbedRows = 64;   // decode steps of up to this many rows take dec_plan_embed
 void force_tokens(const DecState& st, int M_max, const int* row_utt, const int* ids, int ld, int* tok, hipStream_t s);
 void dec_accept(const DecState& st, int M_max, const int* row_utt, const int* tok, hipStream_t s);
 // argmax_rows' final stage (over argmax_rows_partial's keys) fused with dec_accept: tok[i] as argmax_rows gives it

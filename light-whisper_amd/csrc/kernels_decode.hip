@@ -3,15 +3,20 @@
 // active, one step late, to pick the next bucket.  Mirrors the host loop of the reference server's
 // session.run (one utterance) for a batch: a row finishes at EOS (natural mode) or when its budget is spent.
 #include "kernels.h"
+#include "rowops.h"
 
 namespace qasr {
 
 // one workgroup: compact the not-done utterances into rows [0, M), pad rows [M, M_max) with a harmless dummy
 // (token 0 at position 0 writing / reading only the dummy KV slot), zero the active counter for accept
+// EMBED (small steps, dec_plan_embed): the same workgroup then writes the step's input rows — token embeddings of
+// the planned ids, k_embed_rows' arithmetic — after a barrier, instead of a second launch
+template <bool EMBED>
 __global__ __launch_bounds__(1024) void k_dec_plan(DecState st, int M_max, int* __restrict__ ids,
                                                    int* __restrict__ pos, int* __restrict__ slot,
                                                    int* __restrict__ kvs, int* __restrict__ kvl,
-                                                   int* __restrict__ row_utt) {
+                                                   int* __restrict__ row_utt, const int8_t* __restrict__ eqs,
+                                                   const __half* __restrict__ esc, int K, float* __restrict__ x) {
     __shared__ int part[1024];
     const int U = st.params[0], dummy = st.params[1];
     const int per = (U + 1023) / 1024;
@@ -54,6 +59,15 @@ __global__ __launch_bounds__(1024) void k_dec_plan(DecState st, int M_max, int* 
         st.counters[0] = min(M, M_max);   // rows of this step
         st.counters[1] = 0;               // active after accept
         if (M > M_max) st.counters[2] = 1;  // bound violated (the host checks)
+    }
+    if constexpr (EMBED) {
+        __threadfence_block();
+        __syncthreads();
+        const int nb = K / QK;
+        for (int i = threadIdx.x; i < M_max * nb; i += 1024) {
+            const int r = i / nb, b = i % nb;
+            dequant_block_q8(eqs, esc, K, ids[r], b, x + (size_t)r * K + b * QK);
+        }
     }
 }
 
@@ -127,7 +141,13 @@ void force_tokens(const DecState& st, int M_max, const int* row_utt, const int* 
 
 void dec_plan(const DecState& st, int M_max, int* ids, int* pos, int* slot, int* kvs, int* kvl, int* row_utt,
               hipStream_t s) {
-    k_dec_plan<<<1, 1024, 0, s>>>(st, M_max, ids, pos, slot, kvs, kvl, row_utt);
+    k_dec_plan<false><<<1, 1024, 0, s>>>(st, M_max, ids, pos, slot, kvs, kvl, row_utt, nullptr, nullptr, 0, nullptr);
+}
+
+void dec_plan_embed(const DecState& st, int M_max, int* ids, int* pos, int* slot, int* kvs, int* kvl, int* row_utt,
+                    const Q8Mat& E, float* x, hipStream_t s) {
+    QASR_CHECK(E.K % QK == 0, QASR_E_INVALID, "dec_plan_embed: embedding width");
+    k_dec_plan<true><<<1, 1024, 0, s>>>(st, M_max, ids, pos, slot, kvs, kvl, row_utt, E.qs, E.sc, E.K, x);
 }
 
 void dec_accept(const DecState& st, int M_max, const int* row_utt, const int* tok, hipStream_t s) {

@@ -2040,18 +2040,7 @@ __global__ void k_embed_rows(const int* __restrict__ ids, int n, const int8_t* _
         for (int j = 0; j < 8; j++) dst[j] = src[j];
         return;
     }
-    const float d = __half2float(sc[(size_t)id * nb + b]);
-    const int4* q4 = (const int4*)(qs + (size_t)id * K + b * QK);
-#pragma unroll
-    for (int h = 0; h < 2; h++) {
-        int4 v = q4[h];
-        int w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            dst[h * 4 + j] = make_float4(d * (float)(int8_t)(w[j] & 0xff), d * (float)(int8_t)((w[j] >> 8) & 0xff),
-                                         d * (float)(int8_t)((w[j] >> 16) & 0xff), d * (float)(int8_t)((w[j] >> 24) & 0xff));
-        }
-    }
+    dequant_block_q8(qs, sc, K, id, b, (float*)dst);
 }
 
 void embed_rows(const int* ids, int n, const Q8Mat& W, const float* alt, float* out, hipStream_t s) {

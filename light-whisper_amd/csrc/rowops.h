@@ -8,6 +8,26 @@
 
 namespace qasr {
 
+// one 32-value block b of Q8 row `id` (qs [..][K] int8, sc [..][K/32] f16) dequantised into dst[0..32): the
+// embedding lookup's arithmetic (k_embed_rows, and the decode step's fused plan + embed)
+__device__ __forceinline__ void dequant_block_q8(const int8_t* __restrict__ qs, const __half* __restrict__ sc, int K,
+                                                 int id, int b, float* __restrict__ dstf) {
+    const int nb = K / QK;
+    float4* dst = (float4*)dstf;
+    const float d = __half2float(sc[(size_t)id * nb + b]);
+    const int4* q4 = (const int4*)(qs + (size_t)id * K + b * QK);
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+        int4 v = q4[h];
+        int w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            dst[h * 4 + j] = make_float4(d * (float)(int8_t)(w[j] & 0xff), d * (float)(int8_t)((w[j] >> 8) & 0xff),
+                                         d * (float)(int8_t)((w[j] >> 16) & 0xff), d * (float)(int8_t)((w[j] >> 24) & 0xff));
+        }
+    }
+}
+
 // one float4 chunk c of a row → 4 int8 of its Q8 block (8 consecutive lanes = one 32-block: amax by three DPP
 // steps); the block's first lane writes the scale.  q / d may point to global memory or LDS.
 // WT: stored write-through (sc1, wt.h: qrow / drow wave-uniform), for a hand-off inside one launch
